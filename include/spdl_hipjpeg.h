@@ -1,0 +1,150 @@
+/*
+ * spdl_hipjpeg.h -- C-ABI of the MI355X (gfx950) JPEG decode stage.
+ *
+ * This is the drop-in boundary that replaces SPDL's nvJPEG/NPP stack:
+ *   Python  spdl.io.decode_image_nvjpeg / load_image_batch_nvjpeg
+ *           (reference src/spdl/io/_core.py:868-915, src/spdl/io/_composite.py:486-524)
+ *   binding src/spdl/io/lib/cuda/decoding_nvjpeg.cpp:39-97 (nanobind, GIL released)
+ *   engine  src/libspdl/cuda/nvjpeg/decoding.cpp:157-255 (decode_image_nvjpeg single/batch)
+ *           src/libspdl/cuda/npp/detail/resize.cpp:36-116 (resize_npp)
+ * and, for the CPU-path-compatible entry points, the FFmpeg image path behind
+ *   spdl.io.load_image_batch (src/spdl/io/_composite.py:358-465).
+ *
+ * Plain C types only: pointers, sizes, ints.  No torch types.  Every function
+ * returns 0 on success or a SPDL_HJ_ERR_* code, and writes a NUL-terminated
+ * message into `err` (when non-NULL) on failure -- the Python layer turns that
+ * into RuntimeError("Failed to decode an image. (...)"), matching the
+ * reference's CHECK_NVJPEG behaviour (src/libspdl/cuda/nvjpeg/detail/utils.h:53-61).
+ *
+ * Threading: a context is used by one thread at a time (the reference keeps
+ * its nvJPEG state thread_local, decoding.cpp:107-112); create one per thread.
+ * Every call is GIL-free (ctypes releases the GIL).
+ */
+#ifndef SPDL_HIPJPEG_H
+#define SPDL_HIPJPEG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPDL_HJ_ABI_VERSION 1
+
+enum spdl_hj_status {
+  SPDL_HJ_OK = 0,
+  SPDL_HJ_ERR_NOT_JPEG = 1,
+  SPDL_HJ_ERR_UNSUPPORTED = 2,  /* progressive, arithmetic, 12-bit, CMYK, multi-scan */
+  SPDL_HJ_ERR_BAD_HEADER = 3,
+  SPDL_HJ_ERR_BAD_HUFFMAN = 4,
+  SPDL_HJ_ERR_TRUNCATED = 5,
+  SPDL_HJ_ERR_BAD_RESTART = 6,
+  SPDL_HJ_ERR_BAD_GEOMETRY = 7,
+  SPDL_HJ_ERR_INVALID_ARG = 8,
+  SPDL_HJ_ERR_HIP = 9,
+  SPDL_HJ_ERR_OOM = 10,
+};
+
+/* output pixel formats (reference nvjpeg/detail/utils.cpp:94-110):
+ * RGB/BGR planar [3,H,W]; RGB24/BGR24 interleaved [H,W,3]; YUV = raw planes. */
+enum spdl_hj_pix_fmt {
+  SPDL_HJ_FMT_RGB = 0,
+  SPDL_HJ_FMT_BGR = 1,
+  SPDL_HJ_FMT_RGB24 = 2,
+  SPDL_HJ_FMT_BGR24 = 3,
+};
+
+enum spdl_hj_aspect { SPDL_HJ_ASPECT_NONE = 0, SPDL_HJ_ASPECT_DECREASE = 1, SPDL_HJ_ASPECT_INCREASE = 2 };
+enum spdl_hj_filter { SPDL_HJ_FILTER_BICUBIC = 0, SPDL_HJ_FILTER_BILINEAR = 1 };
+enum spdl_hj_dtype { SPDL_HJ_DTYPE_U8 = 0, SPDL_HJ_DTYPE_F16 = 1 };
+/* IDCT: FFmpeg simple_idct (the reference CPU path) or IJG islow (libjpeg). */
+enum spdl_hj_idct { SPDL_HJ_IDCT_SIMPLE = 0, SPDL_HJ_IDCT_ISLOW = 1 };
+
+/* Output specification.  resize == 0: full resolution, every image in the
+ * batch must have the same size.  Otherwise the FFmpeg filter chain SPDL
+ * builds (src/spdl/io/_preprocessing.py:214-234) is applied per image:
+ *   scale=w=fit_w:h=fit_h[:force_original_aspect_ratio=decrease|increase]
+ *   [,pad=w=pad_w:h=pad_h:x=-1:y=-1:color=black][,crop=w=crop_w:h=crop_h]
+ * fit_w/fit_h <= 0 mean "input size"; pad/crop <= 0 mean "absent". */
+typedef struct spdl_hj_output {
+  int32_t pix_fmt;      /* spdl_hj_pix_fmt */
+  int32_t dtype;        /* spdl_hj_dtype; F16 applies (x/255 - mean)/std */
+  int32_t idct;         /* spdl_hj_idct */
+  int32_t resize;       /* 0 = none, 1 = apply the chain below */
+  int32_t fit_w, fit_h, aspect;
+  int32_t pad_w, pad_h;
+  int32_t crop_w, crop_h;
+  int32_t filter;       /* spdl_hj_filter */
+  float mean[3], std[3];
+} spdl_hj_output;
+
+typedef struct spdl_hj_image_info {
+  int32_t width, height, ncomp;
+  int32_t h_samp[3], v_samp[3];
+} spdl_hj_image_info;
+
+typedef struct spdl_hj_ctx spdl_hj_ctx;
+
+/* ABI version of the loaded library (== SPDL_HJ_ABI_VERSION). */
+int spdl_hj_abi_version(void);
+
+/* Header probe on the host: SOF fields without decoding.
+ * Replaces nvjpegGetImageInfo (reference nvjpeg/decoding.cpp:114-130). */
+int spdl_hj_get_image_info(const uint8_t* data, size_t size, spdl_hj_image_info* info);
+
+/* Output geometry (width/height of the output image) for an input of w x h
+ * under `out`; lets the caller allocate the output tensor. */
+int spdl_hj_output_size(int32_t w, int32_t h, const spdl_hj_output* out, int32_t* out_w,
+                        int32_t* out_h);
+
+/* Create / destroy a per-thread decoder context bound to `device`.  The
+ * context owns its device workspace (grown on demand) and pinned staging. */
+spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen);
+void spdl_hj_destroy(spdl_hj_ctx* ctx);
+
+/* Decode a batch of host-resident JPEGs into caller-allocated device memory
+ * `out_dev` (out_bytes long) on `stream` (a hipStream_t; NULL = legacy
+ * default stream, (void*)2 = per-thread default, the reference's 0x2 sentinel
+ * in src/libspdl/cuda/types.h:22-39).  The batch is packed into pinned
+ * staging and copied with one hipMemcpyAsync.  Output layout per image is
+ * [3,H,W] (planar) or [H,W,3] (interleaved) at offset i * per-image-size.
+ * status[i] (optional, host) receives the per-image code.  With sync != 0 the
+ * call returns after the stream has drained (reference default sync=true,
+ * decoding.cpp:247-251) and fails if any image failed. */
+int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const size_t* sizes,
+                         int32_t n, const spdl_hj_output* out, void* out_dev, size_t out_bytes,
+                         void* stream, int32_t sync, int32_t* status, char* err, size_t errlen);
+
+/* Device-resident variant: the JPEG bytes are already in HBM, packed in
+ * `dev_data` at host-known offsets (each 256-byte aligned).  `infos` are the
+ * host probes of the same images (spdl_hj_get_image_info).  No H2D copy of
+ * image bytes happens inside the call. */
+int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_t dev_bytes,
+                                const int64_t* offsets, const int64_t* sizes,
+                                const spdl_hj_image_info* infos, int32_t n,
+                                const spdl_hj_output* out, void* out_dev, size_t out_bytes,
+                                void* stream, int32_t sync, int32_t* status, char* err,
+                                size_t errlen);
+
+/* Raw decoded planes (parity surface, the reference's load_image with
+ * filter_desc=None -> yuvj4xxp planes, src/spdl/io/_composite.py:254-295):
+ * plane c of image 0 copied to host buffer planes[c] (comp_w x comp_h bytes,
+ * tightly packed).  Single image. */
+int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, int32_t idct,
+                          uint8_t* const* planes, void* stream, char* err, size_t errlen);
+
+/* Per-kernel timing of the last batch, in microseconds, measured with HIP
+ * events on the decode stream (filled only when enabled). */
+int spdl_hj_set_profiling(spdl_hj_ctx* ctx, int32_t enable);
+int spdl_hj_last_timings(spdl_hj_ctx* ctx, float* us, int32_t cap, int32_t* n_out);
+/* Names of the timed stages in the order spdl_hj_last_timings reports them. */
+const char* spdl_hj_stage_name(int32_t i);
+
+/* Tuning knobs (subsequence size in bits for the parallel Huffman decode). */
+int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

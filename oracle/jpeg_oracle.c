@@ -1,0 +1,1191 @@
+/*
+ * jpeg_oracle.c -- CPU restatement of SPDL's JPEG -> RGB path (test oracle).
+ *
+ * TEST INFRASTRUCTURE ONLY (see jpeg_oracle.h).  Compiled with
+ * -ffp-contract=off so the float steps (resize weights, normalisation) are the
+ * exact IEEE binary32 sequences written here.
+ *
+ * Reference call sites restated (paths relative to the SPDL tree):
+ *   decode:  src/libspdl/core/detail/ffmpeg/decoder.cpp:50-63 -> FFmpeg mjpeg
+ *            (libavcodec/mjpegdec.c decode_block / mjpeg_decode_dc, simple_idct
+ *            template 8-bit: idctRowCondDC, idctSparseColPut).
+ *   convert: src/libspdl/core/detail/ffmpeg/filter_graph.cpp:280-313 ->
+ *            format=pix_fmts=rgb24 (yuvj4xxp -> rgb24, nearest chroma).
+ *   resize:  src/spdl/io/_preprocessing.py:214-234 filter string semantics
+ *            (scale force_original_aspect_ratio, pad x=-1:y=-1, crop).
+ *   norm:    examples/imagenet_classification.py:96-106.
+ */
+#include "jpeg_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+static const uint8_t kNatural[64 + 16] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63,
+    63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+const char* jo_strerror(int code) {
+  switch (code) {
+    case JO_OK: return "ok";
+    case JO_ERR_NOT_JPEG: return "not a JPEG (missing SOI)";
+    case JO_ERR_UNSUPPORTED: return "unsupported JPEG (progressive/arithmetic/12-bit/CMYK/multi-scan)";
+    case JO_ERR_BAD_HEADER: return "corrupt JPEG header";
+    case JO_ERR_BAD_HUFFMAN: return "corrupt entropy-coded data";
+    case JO_ERR_TRUNCATED: return "truncated entropy-coded data";
+    case JO_ERR_BAD_RESTART: return "restart marker mismatch";
+    case JO_ERR_BAD_GEOMETRY: return "invalid resize geometry";
+    default: return "unknown error";
+  }
+}
+
+static int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
+
+/* ------------------------------------------------------------------------ */
+/* Marker parsing (T.81 B.2; FFmpeg ff_mjpeg_decode_{dqt,dht,sof,sos}).       */
+/* ------------------------------------------------------------------------ */
+
+static int check_huff(const uint8_t* bits) {
+  /* canonical code space must not overflow (T.81 C.2) */
+  int code = 0;
+  for (int l = 1; l <= 16; l++) {
+    code += bits[l];
+    if (code > (1 << l)) return 0;
+    code <<= 1;
+  }
+  return 1;
+}
+
+int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
+  memset(info, 0, sizeof(*info));
+  if (size < 4 || d[0] != 0xFF || d[1] != 0xD8) return JO_ERR_NOT_JPEG;
+  int have_sof = 0, qt_have[4] = {0}, dc_have[4] = {0}, ac_have[4] = {0};
+  int comp_id[JO_MAX_COMP] = {0};
+  size_t pos = 2;
+  for (;;) {
+    while (pos < size && d[pos] != 0xFF) pos++; /* skip garbage */
+    while (pos < size && d[pos] == 0xFF) pos++; /* fill bytes */
+    if (pos >= size) return JO_ERR_BAD_HEADER;
+    int m = d[pos++];
+    if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+    if (m == 0xD9) return JO_ERR_BAD_HEADER; /* EOI before SOS */
+    if (pos + 2 > size) return JO_ERR_BAD_HEADER;
+    int len = be16(d + pos);
+    if (len < 2 || pos + (size_t)len > size) return JO_ERR_BAD_HEADER;
+    const uint8_t* s = d + pos + 2;
+    int n = len - 2;
+    pos += (size_t)len;
+    if (m == 0xDB) { /* DQT */
+      while (n > 0) {
+        int pq = s[0] >> 4, tq = s[0] & 15;
+        if (tq > 3 || pq > 1) return JO_ERR_BAD_HEADER;
+        int need = 1 + 64 * (pq + 1);
+        if (n < need) return JO_ERR_BAD_HEADER;
+        for (int i = 0; i < 64; i++)
+          info->qt[tq][i] = pq ? (uint16_t)be16(s + 1 + 2 * i) : s[1 + i];
+        qt_have[tq] = 1;
+        s += need;
+        n -= need;
+      }
+    } else if (m == 0xC4) { /* DHT */
+      while (n > 0) {
+        if (n < 17) return JO_ERR_BAD_HEADER;
+        int tc = s[0] >> 4, th = s[0] & 15;
+        if (tc > 1 || th > 3) return JO_ERR_BAD_HEADER;
+        uint8_t bits[17];
+        bits[0] = 0;
+        int total = 0;
+        for (int l = 1; l <= 16; l++) { bits[l] = s[l]; total += s[l]; }
+        if (total > 256 || n < 17 + total || !check_huff(bits)) return JO_ERR_BAD_HEADER;
+        uint8_t* dbits = tc ? info->ac_bits[th] : info->dc_bits[th];
+        uint8_t* dvals = tc ? info->ac_vals[th] : info->dc_vals[th];
+        memcpy(dbits, bits, 17);
+        memset(dvals, 0, 256);
+        memcpy(dvals, s + 17, (size_t)total);
+        (tc ? ac_have : dc_have)[th] = 1;
+        s += 17 + total;
+        n -= 17 + total;
+      }
+    } else if (m == 0xC0 || m == 0xC1) { /* SOF0 / SOF1 (Huffman, sequential) */
+      if (n < 6) return JO_ERR_BAD_HEADER;
+      if (s[0] != 8) return JO_ERR_UNSUPPORTED;
+      info->height = be16(s + 1);
+      info->width = be16(s + 3);
+      int nf = s[5];
+      if (info->height == 0) return JO_ERR_UNSUPPORTED; /* DNL */
+      if (info->width == 0) return JO_ERR_BAD_HEADER;
+      if (nf != 1 && nf != 3) return JO_ERR_UNSUPPORTED;
+      if (n < 6 + 3 * nf) return JO_ERR_BAD_HEADER;
+      info->ncomp = nf;
+      for (int c = 0; c < nf; c++) {
+        comp_id[c] = s[6 + 3 * c];
+        info->comp_h[c] = s[7 + 3 * c] >> 4;
+        info->comp_v[c] = s[7 + 3 * c] & 15;
+        info->comp_tq[c] = s[8 + 3 * c];
+        if (info->comp_h[c] < 1 || info->comp_h[c] > 4 || info->comp_v[c] < 1 ||
+            info->comp_v[c] > 4 || info->comp_tq[c] > 3)
+          return JO_ERR_BAD_HEADER;
+      }
+      have_sof = 1;
+    } else if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) ||
+               (m >= 0xC9 && m <= 0xCB) || (m >= 0xCD && m <= 0xCF)) {
+      return JO_ERR_UNSUPPORTED; /* progressive, lossless, hierarchical, arithmetic */
+    } else if (m == 0xDD) { /* DRI */
+      if (n < 2) return JO_ERR_BAD_HEADER;
+      info->restart_interval = be16(s);
+    } else if (m == 0xDA) { /* SOS */
+      if (!have_sof) return JO_ERR_BAD_HEADER;
+      int ns = s[0];
+      if (ns != info->ncomp) return JO_ERR_UNSUPPORTED; /* multi-scan sequential */
+      if (n < 1 + 2 * ns + 3) return JO_ERR_BAD_HEADER;
+      int order[JO_MAX_COMP];
+      for (int i = 0; i < ns; i++) {
+        int cs = s[1 + 2 * i], c = -1;
+        for (int k = 0; k < info->ncomp; k++)
+          if (comp_id[k] == cs) c = k;
+        if (c < 0) return JO_ERR_BAD_HEADER;
+        order[i] = c;
+        info->comp_td[c] = s[2 + 2 * i] >> 4;
+        info->comp_ta[c] = s[2 + 2 * i] & 15;
+        if (info->comp_td[c] > 3 || info->comp_ta[c] > 3) return JO_ERR_BAD_HEADER;
+      }
+      int ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahal = s[3 + 2 * ns];
+      if (ss != 0 || se != 63 || ahal != 0) return JO_ERR_UNSUPPORTED;
+      info->scan_start = pos;
+      /* geometry */
+      int hmax = 1, vmax = 1;
+      for (int c = 0; c < info->ncomp; c++) {
+        if (info->comp_h[c] > hmax) hmax = info->comp_h[c];
+        if (info->comp_v[c] > vmax) vmax = info->comp_v[c];
+      }
+      info->hmax = hmax;
+      info->vmax = vmax;
+      for (int c = 0; c < info->ncomp; c++) {
+        if (hmax % info->comp_h[c] || vmax % info->comp_v[c]) return JO_ERR_UNSUPPORTED;
+        if (!qt_have[info->comp_tq[c]] || !dc_have[info->comp_td[c]] ||
+            !ac_have[info->comp_ta[c]])
+          return JO_ERR_BAD_HEADER;
+        info->comp_w[c] = (info->width * info->comp_h[c] + hmax - 1) / hmax;
+        info->comp_h_px[c] = (info->height * info->comp_v[c] + vmax - 1) / vmax;
+      }
+      if (info->ncomp == 1) {
+        info->comp_bw[0] = (info->comp_w[0] + 7) / 8;
+        info->comp_bh[0] = (info->comp_h_px[0] + 7) / 8;
+        info->mcux = info->comp_bw[0];
+        info->mcuy = info->comp_bh[0];
+        info->bpm = 1;
+        info->mcu_comp[0] = 0;
+      } else {
+        info->mcux = (info->width + 8 * hmax - 1) / (8 * hmax);
+        info->mcuy = (info->height + 8 * vmax - 1) / (8 * vmax);
+        int b = 0;
+        for (int i = 0; i < ns; i++) {
+          int c = order[i];
+          info->comp_bw[c] = info->mcux * info->comp_h[c];
+          info->comp_bh[c] = info->mcuy * info->comp_v[c];
+          for (int y = 0; y < info->comp_v[c]; y++)
+            for (int x = 0; x < info->comp_h[c]; x++) {
+              if (b >= JO_MAX_BPM) return JO_ERR_UNSUPPORTED;
+              info->mcu_comp[b] = c;
+              info->mcu_dx[b] = x;
+              info->mcu_dy[b] = y;
+              b++;
+            }
+        }
+        info->bpm = b;
+      }
+      info->nblocks = info->mcux * info->mcuy * info->bpm;
+      return JO_OK;
+    }
+    /* APPn, COM, DHP, EXP, DNL, JPG... : skipped */
+  }
+}
+
+int jo_get_image_info(const uint8_t* d, size_t size, int* w, int* h, int* ncomp) {
+  jo_info info;
+  int rc = jo_parse(d, size, &info);
+  if (rc) return rc;
+  *w = info.width;
+  *h = info.height;
+  *ncomp = info.ncomp;
+  return JO_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Huffman decoding                                                          */
+/* ------------------------------------------------------------------------ */
+
+#define LOOKBITS 9
+typedef struct {
+  int32_t maxcode[18];   /* largest code of length l, -1 if none */
+  int32_t valoff[17];    /* index into vals for first code of length l minus that code */
+  uint8_t vals[256];
+  uint16_t look[1 << LOOKBITS]; /* (len << 8) | sym, 0 when len > LOOKBITS */
+} huff_t;
+
+static void build_huff(const uint8_t* bits, const uint8_t* vals, huff_t* h) {
+  int code = 0, k = 0;
+  memcpy(h->vals, vals, 256);
+  memset(h->look, 0, sizeof(h->look));
+  for (int l = 1; l <= 16; l++) {
+    if (bits[l]) {
+      h->valoff[l] = k - code;
+      for (int i = 0; i < bits[l]; i++) {
+        if (l <= LOOKBITS) {
+          int lo = code << (LOOKBITS - l), cnt = 1 << (LOOKBITS - l);
+          for (int j = 0; j < cnt; j++) h->look[lo + j] = (uint16_t)((l << 8) | vals[k]);
+        }
+        code++;
+        k++;
+      }
+      h->maxcode[l] = code - 1;
+    } else {
+      h->maxcode[l] = -1;
+      h->valoff[l] = 0;
+    }
+    code <<= 1;
+  }
+  h->maxcode[17] = 0x7FFFFFFF;
+}
+
+typedef struct {
+  const uint8_t* d;
+  size_t size, pos;
+  uint64_t buf;
+  int cnt;
+  int hit_marker;
+  int64_t real_bits;   /* bits loaded from actual data */
+  int64_t used_bits;   /* bits consumed */
+} bitrd_t;
+
+static void br_fill(bitrd_t* b) {
+  while (b->cnt <= 56) {
+    unsigned byte = 0;
+    if (!b->hit_marker) {
+      if (b->pos >= b->size) {
+        b->hit_marker = 1;
+      } else {
+        unsigned c = b->d[b->pos];
+        if (c == 0xFF) {
+          unsigned nx = b->pos + 1 < b->size ? b->d[b->pos + 1] : 0xD9;
+          if (nx == 0x00) {
+            b->pos += 2;
+            byte = 0xFF;
+            b->real_bits += 8;
+          } else {
+            b->hit_marker = 1;
+          }
+        } else {
+          b->pos++;
+          byte = c;
+          b->real_bits += 8;
+        }
+      }
+    }
+    b->buf |= (uint64_t)byte << (56 - b->cnt);
+    b->cnt += 8;
+  }
+}
+
+static inline unsigned br_peek16(bitrd_t* b) {
+  if (b->cnt < 32) br_fill(b);
+  return (unsigned)(b->buf >> 48);
+}
+static inline void br_skip(bitrd_t* b, int n) {
+  b->buf <<= n;
+  b->cnt -= n;
+  b->used_bits += n;
+}
+static inline unsigned br_get(bitrd_t* b, int n) {
+  if (n == 0) return 0;
+  if (b->cnt < 32) br_fill(b);
+  unsigned v = (unsigned)(b->buf >> (64 - n));
+  br_skip(b, n);
+  return v;
+}
+
+/* returns symbol or -1 for an invalid code */
+static int huff_decode(bitrd_t* b, const huff_t* h) {
+  unsigned w = br_peek16(b);
+  unsigned e = h->look[w >> (16 - LOOKBITS)];
+  if (e) {
+    br_skip(b, (int)(e >> 8));
+    return (int)(e & 0xFF);
+  }
+  for (int l = LOOKBITS + 1; l <= 16; l++) {
+    int code = (int)(w >> (16 - l));
+    if (code <= h->maxcode[l]) {
+      br_skip(b, l);
+      return h->vals[h->valoff[l] + code];
+    }
+  }
+  return -1;
+}
+
+static inline int extend(unsigned v, int s) {
+  return (v < (1u << (s - 1))) ? (int)v - ((1 << s) - 1) : (int)v;
+}
+
+static inline int16_t clip16(int32_t v) {
+  return v < -32768 ? -32768 : v > 32767 ? 32767 : (int16_t)v;
+}
+
+int jo_decode_coefs(const uint8_t* d, size_t size, const jo_info* info, int16_t* coefs,
+                    int16_t* levels) {
+  huff_t dct[4], act[4];
+  for (int t = 0; t < 4; t++) {
+    build_huff(info->dc_bits[t], info->dc_vals[t], &dct[t]);
+    build_huff(info->ac_bits[t], info->ac_vals[t], &act[t]);
+  }
+  size_t lvl_off[JO_MAX_COMP] = {0};
+  {
+    size_t o = 0;
+    for (int c = 0; c < info->ncomp; c++) {
+      lvl_off[c] = o;
+      o += (size_t)info->comp_bw[c] * info->comp_bh[c] * 64;
+    }
+  }
+  memset(coefs, 0, (size_t)info->nblocks * 64 * sizeof(int16_t));
+  if (levels) {
+    size_t tot = 0;
+    for (int c = 0; c < info->ncomp; c++) tot += (size_t)info->comp_bw[c] * info->comp_bh[c] * 64;
+    memset(levels, 0, tot * sizeof(int16_t));
+  }
+  bitrd_t br;
+  memset(&br, 0, sizeof(br));
+  br.d = d;
+  br.size = size;
+  br.pos = info->scan_start;
+  /* FFmpeg mjpegdec initialises (and resets at each RSTn) the dequantised DC
+   * predictor to 4 << bits = 1024: the +128 level shift lives in block[0]. */
+  int32_t pred[JO_MAX_COMP] = {0};  /* sum of DC diffs (quantised) */
+  uint32_t last_dc[JO_MAX_COMP] = {JO_DC_BIAS, JO_DC_BIAS, JO_DC_BIAS};
+  int nmcu = info->mcux * info->mcuy;
+  int ri = info->restart_interval;
+  for (int mcu = 0; mcu < nmcu; mcu++) {
+    if (ri && mcu && mcu % ri == 0) {
+      /* restart: check the consumed bits were real, drop padding, eat RSTn */
+      if (br.used_bits > br.real_bits) return JO_ERR_TRUNCATED;
+      /* a segment is the byte run between markers: leftover bits of this
+       * interval are ignored, decoding resumes after the next marker, which
+       * must be RSTn (same segmentation as the device destuff pass). */
+      size_t p = br.pos;
+      for (;;) {
+        if (p >= size) return JO_ERR_BAD_RESTART;
+        if (d[p] == 0xFF && p + 1 < size && d[p + 1] == 0x00) {
+          p += 2;
+          continue;
+        }
+        if (d[p] == 0xFF) break;
+        p++;
+      }
+      while (p < size && d[p] == 0xFF) p++;
+      if (p >= size || d[p] < 0xD0 || d[p] > 0xD7) return JO_ERR_BAD_RESTART;
+      br.pos = p + 1;
+      br.buf = 0;
+      br.cnt = 0;
+      br.hit_marker = 0;
+      br.real_bits = br.used_bits = 0;
+      for (int c = 0; c < JO_MAX_COMP; c++) pred[c] = 0, last_dc[c] = JO_DC_BIAS;
+    }
+    int mx = mcu % info->mcux, my = mcu / info->mcux;
+    for (int b = 0; b < info->bpm; b++) {
+      int c = info->mcu_comp[b];
+      const uint16_t* q = info->qt[info->comp_tq[c]];
+      int16_t* blk = coefs + ((size_t)mcu * info->bpm + b) * 64;
+      int bx, by;
+      if (info->ncomp == 1) {
+        bx = mx;
+        by = my;
+      } else {
+        bx = mx * info->comp_h[c] + info->mcu_dx[b];
+        by = my * info->comp_v[c] + info->mcu_dy[b];
+      }
+      int16_t* lv = levels ? levels + lvl_off[c] + ((size_t)by * info->comp_bw[c] + bx) * 64 : NULL;
+      /* DC */
+      int s = huff_decode(&br, &dct[info->comp_td[c]]);
+      if (s < 0 || s > 15) return JO_ERR_BAD_HUFFMAN;
+      int diff = s ? extend(br_get(&br, s), s) : 0;
+      pred[c] += diff;
+      last_dc[c] = (uint32_t)diff * (uint32_t)q[0] + last_dc[c];
+      blk[0] = clip16((int32_t)last_dc[c]);
+      if (lv) lv[0] = (int16_t)pred[c];
+      /* AC */
+      const huff_t* ah = &act[info->comp_ta[c]];
+      for (int k = 1; k < 64;) {
+        int rs = huff_decode(&br, ah);
+        if (rs < 0) return JO_ERR_BAD_HUFFMAN;
+        int r = rs >> 4;
+        s = rs & 15;
+        if (s == 0) {
+          if (r == 15) {
+            k += 16;
+            continue;
+          }
+          if (r != 0) return JO_ERR_BAD_HUFFMAN;
+          break; /* EOB */
+        }
+        k += r;
+        if (k > 63) return JO_ERR_BAD_HUFFMAN;
+        int v = extend(br_get(&br, s), s);
+        blk[kNatural[k]] = (int16_t)(v * (int)q[k]);
+        if (lv) lv[kNatural[k]] = (int16_t)v;
+        k++;
+      }
+    }
+  }
+  if (br.used_bits > br.real_bits) return JO_ERR_TRUNCATED;
+  return JO_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* IDCTs                                                                     */
+/* ------------------------------------------------------------------------ */
+
+/* FFmpeg simple_idct, 8-bit (libavcodec/simple_idct_template.c, BIT_DEPTH 8,
+ * extra_shift 0): W_i = round(cos(i*pi/16)*sqrt(2)*2^14), ROW_SHIFT 11,
+ * COL_SHIFT 20, DC-only row shortcut (row[0] << 3, kept as int16).  The
+ * "SUINT" arithmetic is emulated with uint32 and an int cast before the
+ * arithmetic shift. */
+#define SW1 22725
+#define SW2 21407
+#define SW3 19266
+#define SW4 16383
+#define SW5 12873
+#define SW6 8867
+#define SW7 4520
+#define SROW_SHIFT 11
+#define SCOL_SHIFT 20
+
+static void simple_row(int16_t* row) {
+  if (!(row[1] | row[2] | row[3] | row[4] | row[5] | row[6] | row[7])) {
+    int16_t t = (int16_t)(uint16_t)((uint32_t)(int32_t)row[0] << 3);
+    for (int i = 0; i < 8; i++) row[i] = t;
+    return;
+  }
+  uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+  a0 = (uint32_t)SW4 * (uint32_t)(int32_t)row[0] + (1u << (SROW_SHIFT - 1));
+  a1 = a0;
+  a2 = a0;
+  a3 = a0;
+  a0 += (uint32_t)SW2 * (uint32_t)(int32_t)row[2];
+  a1 += (uint32_t)SW6 * (uint32_t)(int32_t)row[2];
+  a2 -= (uint32_t)SW6 * (uint32_t)(int32_t)row[2];
+  a3 -= (uint32_t)SW2 * (uint32_t)(int32_t)row[2];
+
+  b0 = (uint32_t)(SW1 * row[1]);
+  b0 += (uint32_t)SW3 * (uint32_t)(int32_t)row[3];
+  b1 = (uint32_t)(SW3 * row[1]);
+  b1 += (uint32_t)(-SW7) * (uint32_t)(int32_t)row[3];
+  b2 = (uint32_t)(SW5 * row[1]);
+  b2 += (uint32_t)(-SW1) * (uint32_t)(int32_t)row[3];
+  b3 = (uint32_t)(SW7 * row[1]);
+  b3 += (uint32_t)(-SW5) * (uint32_t)(int32_t)row[3];
+
+  if (row[4] | row[5] | row[6] | row[7]) {
+    a0 += (uint32_t)SW4 * (uint32_t)(int32_t)row[4] + (uint32_t)SW6 * (uint32_t)(int32_t)row[6];
+    a1 += (uint32_t)(-SW4) * (uint32_t)(int32_t)row[4] - (uint32_t)SW2 * (uint32_t)(int32_t)row[6];
+    a2 += (uint32_t)(-SW4) * (uint32_t)(int32_t)row[4] + (uint32_t)SW2 * (uint32_t)(int32_t)row[6];
+    a3 += (uint32_t)SW4 * (uint32_t)(int32_t)row[4] - (uint32_t)SW6 * (uint32_t)(int32_t)row[6];
+    b0 += (uint32_t)SW5 * (uint32_t)(int32_t)row[5];
+    b0 += (uint32_t)SW7 * (uint32_t)(int32_t)row[7];
+    b1 += (uint32_t)(-SW1) * (uint32_t)(int32_t)row[5];
+    b1 += (uint32_t)(-SW5) * (uint32_t)(int32_t)row[7];
+    b2 += (uint32_t)SW7 * (uint32_t)(int32_t)row[5];
+    b2 += (uint32_t)SW3 * (uint32_t)(int32_t)row[7];
+    b3 += (uint32_t)SW3 * (uint32_t)(int32_t)row[5];
+    b3 += (uint32_t)(-SW1) * (uint32_t)(int32_t)row[7];
+  }
+  row[0] = (int16_t)((int32_t)(a0 + b0) >> SROW_SHIFT);
+  row[7] = (int16_t)((int32_t)(a0 - b0) >> SROW_SHIFT);
+  row[1] = (int16_t)((int32_t)(a1 + b1) >> SROW_SHIFT);
+  row[6] = (int16_t)((int32_t)(a1 - b1) >> SROW_SHIFT);
+  row[2] = (int16_t)((int32_t)(a2 + b2) >> SROW_SHIFT);
+  row[5] = (int16_t)((int32_t)(a2 - b2) >> SROW_SHIFT);
+  row[3] = (int16_t)((int32_t)(a3 + b3) >> SROW_SHIFT);
+  row[4] = (int16_t)((int32_t)(a3 - b3) >> SROW_SHIFT);
+}
+
+static inline uint8_t clip_u8(int32_t v) { return v < 0 ? 0 : v > 255 ? 255 : (uint8_t)v; }
+
+static void simple_col_put(uint8_t* dst, int stride, const int16_t* col) {
+  uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+  a0 = (uint32_t)SW4 * (uint32_t)(col[8 * 0] + ((1 << (SCOL_SHIFT - 1)) / SW4));
+  a1 = a0;
+  a2 = a0;
+  a3 = a0;
+  a0 += (uint32_t)SW2 * (uint32_t)(int32_t)col[8 * 2];
+  a1 += (uint32_t)SW6 * (uint32_t)(int32_t)col[8 * 2];
+  a2 += (uint32_t)(-SW6) * (uint32_t)(int32_t)col[8 * 2];
+  a3 += (uint32_t)(-SW2) * (uint32_t)(int32_t)col[8 * 2];
+  b0 = (uint32_t)(SW1 * col[8 * 1]);
+  b1 = (uint32_t)(SW3 * col[8 * 1]);
+  b2 = (uint32_t)(SW5 * col[8 * 1]);
+  b3 = (uint32_t)(SW7 * col[8 * 1]);
+  b0 += (uint32_t)SW3 * (uint32_t)(int32_t)col[8 * 3];
+  b1 += (uint32_t)(-SW7) * (uint32_t)(int32_t)col[8 * 3];
+  b2 += (uint32_t)(-SW1) * (uint32_t)(int32_t)col[8 * 3];
+  b3 += (uint32_t)(-SW5) * (uint32_t)(int32_t)col[8 * 3];
+  /* the sparse "if (col[8*k])" tests in FFmpeg only skip additions of zero */
+  a0 += (uint32_t)SW4 * (uint32_t)(int32_t)col[8 * 4];
+  a1 += (uint32_t)(-SW4) * (uint32_t)(int32_t)col[8 * 4];
+  a2 += (uint32_t)(-SW4) * (uint32_t)(int32_t)col[8 * 4];
+  a3 += (uint32_t)SW4 * (uint32_t)(int32_t)col[8 * 4];
+  b0 += (uint32_t)SW5 * (uint32_t)(int32_t)col[8 * 5];
+  b1 += (uint32_t)(-SW1) * (uint32_t)(int32_t)col[8 * 5];
+  b2 += (uint32_t)SW7 * (uint32_t)(int32_t)col[8 * 5];
+  b3 += (uint32_t)SW3 * (uint32_t)(int32_t)col[8 * 5];
+  a0 += (uint32_t)SW6 * (uint32_t)(int32_t)col[8 * 6];
+  a1 += (uint32_t)(-SW2) * (uint32_t)(int32_t)col[8 * 6];
+  a2 += (uint32_t)SW2 * (uint32_t)(int32_t)col[8 * 6];
+  a3 += (uint32_t)(-SW6) * (uint32_t)(int32_t)col[8 * 6];
+  b0 += (uint32_t)SW7 * (uint32_t)(int32_t)col[8 * 7];
+  b1 += (uint32_t)(-SW5) * (uint32_t)(int32_t)col[8 * 7];
+  b2 += (uint32_t)SW3 * (uint32_t)(int32_t)col[8 * 7];
+  b3 += (uint32_t)(-SW1) * (uint32_t)(int32_t)col[8 * 7];
+  dst[0 * stride] = clip_u8((int32_t)(a0 + b0) >> SCOL_SHIFT);
+  dst[1 * stride] = clip_u8((int32_t)(a1 + b1) >> SCOL_SHIFT);
+  dst[2 * stride] = clip_u8((int32_t)(a2 + b2) >> SCOL_SHIFT);
+  dst[3 * stride] = clip_u8((int32_t)(a3 + b3) >> SCOL_SHIFT);
+  dst[4 * stride] = clip_u8((int32_t)(a3 - b3) >> SCOL_SHIFT);
+  dst[5 * stride] = clip_u8((int32_t)(a2 - b2) >> SCOL_SHIFT);
+  dst[6 * stride] = clip_u8((int32_t)(a1 - b1) >> SCOL_SHIFT);
+  dst[7 * stride] = clip_u8((int32_t)(a0 - b0) >> SCOL_SHIFT);
+}
+
+void jo_idct_simple(const int16_t* in, uint8_t* out, int stride) {
+  int16_t blk[64];
+  memcpy(blk, in, sizeof(blk));
+  for (int i = 0; i < 8; i++) simple_row(blk + 8 * i);
+  for (int i = 0; i < 8; i++) simple_col_put(out + i, stride, blk + i);
+}
+
+/* IJG jidctint.c jpeg_idct_islow (libjpeg 9): CONST_BITS 13, PASS1_BITS 2,
+ * columns first, zero-AC shortcuts in both passes (exact), output through the
+ * range-limit table: sample = limit[(x >> 18) & 1023] with the range centre
+ * (512 << 5) folded into the row-pass DC term. */
+#define CB 13
+#define P1 2
+#define F0298 2446
+#define F0390 3196
+#define F0541 4433
+#define F0765 6270
+#define F0899 7373
+#define F1175 9633
+#define F1501 12299
+#define F1847 15137
+#define F1961 16069
+#define F2053 16819
+#define F2562 20995
+#define F3072 25172
+
+static inline uint8_t islow_limit(int32_t x) {
+  int t = (int)(x & 1023); /* index into IDCT_range_limit */
+  int v = t - 384;         /* sample_range_limit index */
+  return v < 0 ? 0 : v > 255 ? 255 : (uint8_t)v;
+}
+
+void jo_idct_islow(const int16_t* in_biased, uint8_t* out, int stride) {
+  /* coefficients carry FFmpeg's DC bias (1024); libjpeg's DC does not */
+  int16_t in[64];
+  memcpy(in, in_biased, sizeof(in));
+  in[0] = (int16_t)(in[0] - JO_DC_BIAS);
+  int32_t ws[64];
+  for (int c = 0; c < 8; c++) {
+    const int16_t* p = in + c;
+    if (!(p[8] | p[16] | p[24] | p[32] | p[40] | p[48] | p[56])) {
+      int32_t dc = (int32_t)p[0] * (1 << P1);
+      for (int r = 0; r < 8; r++) ws[r * 8 + c] = dc;
+      continue;
+    }
+    int32_t z1, z2, z3, t0, t1, t2, t3, t10, t11, t12, t13;
+    z2 = p[0];
+    z3 = p[32];
+    z2 *= (1 << CB);
+    z3 *= (1 << CB);
+    z2 += 1 << (CB - P1 - 1);
+    t0 = z2 + z3;
+    t1 = z2 - z3;
+    z2 = p[16];
+    z3 = p[48];
+    z1 = (z2 + z3) * F0541;
+    t2 = z1 + z2 * F0765;
+    t3 = z1 - z3 * F1847;
+    t10 = t0 + t2;
+    t13 = t0 - t2;
+    t11 = t1 + t3;
+    t12 = t1 - t3;
+    t0 = p[56];
+    t1 = p[40];
+    t2 = p[24];
+    t3 = p[8];
+    z2 = t0 + t2;
+    z3 = t1 + t3;
+    z1 = (z2 + z3) * F1175;
+    z2 = z2 * -F1961;
+    z3 = z3 * -F0390;
+    z2 += z1;
+    z3 += z1;
+    z1 = (t0 + t3) * -F0899;
+    t0 = t0 * F0298;
+    t3 = t3 * F1501;
+    t0 += z1 + z2;
+    t3 += z1 + z3;
+    z1 = (t1 + t2) * -F2562;
+    t1 = t1 * F2053;
+    t2 = t2 * F3072;
+    t1 += z1 + z3;
+    t2 += z1 + z2;
+    ws[0 * 8 + c] = (t10 + t3) >> (CB - P1);
+    ws[7 * 8 + c] = (t10 - t3) >> (CB - P1);
+    ws[1 * 8 + c] = (t11 + t2) >> (CB - P1);
+    ws[6 * 8 + c] = (t11 - t2) >> (CB - P1);
+    ws[2 * 8 + c] = (t12 + t1) >> (CB - P1);
+    ws[5 * 8 + c] = (t12 - t1) >> (CB - P1);
+    ws[3 * 8 + c] = (t13 + t0) >> (CB - P1);
+    ws[4 * 8 + c] = (t13 - t0) >> (CB - P1);
+  }
+  for (int r = 0; r < 8; r++) {
+    const int32_t* w = ws + r * 8;
+    uint8_t* o = out + r * stride;
+    int32_t z1, z2, z3, t0, t1, t2, t3, t10, t11, t12, t13;
+    z2 = w[0] + ((512 << (P1 + 3)) + (1 << (P1 + 2)));
+    if (!(w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7])) {
+      uint8_t v = islow_limit(z2 >> (P1 + 3));
+      for (int i = 0; i < 8; i++) o[i] = v;
+      continue;
+    }
+    z3 = w[4];
+    t0 = (z2 + z3) * (1 << CB);
+    t1 = (z2 - z3) * (1 << CB);
+    z2 = w[2];
+    z3 = w[6];
+    z1 = (z2 + z3) * F0541;
+    t2 = z1 + z2 * F0765;
+    t3 = z1 - z3 * F1847;
+    t10 = t0 + t2;
+    t13 = t0 - t2;
+    t11 = t1 + t3;
+    t12 = t1 - t3;
+    t0 = w[7];
+    t1 = w[5];
+    t2 = w[3];
+    t3 = w[1];
+    z2 = t0 + t2;
+    z3 = t1 + t3;
+    z1 = (z2 + z3) * F1175;
+    z2 = z2 * -F1961;
+    z3 = z3 * -F0390;
+    z2 += z1;
+    z3 += z1;
+    z1 = (t0 + t3) * -F0899;
+    t0 = t0 * F0298;
+    t3 = t3 * F1501;
+    t0 += z1 + z2;
+    t3 += z1 + z3;
+    z1 = (t1 + t2) * -F2562;
+    t1 = t1 * F2053;
+    t2 = t2 * F3072;
+    t1 += z1 + z3;
+    t2 += z1 + z2;
+    const int sh = CB + P1 + 3;
+    o[0] = islow_limit((t10 + t3) >> sh);
+    o[7] = islow_limit((t10 - t3) >> sh);
+    o[1] = islow_limit((t11 + t2) >> sh);
+    o[6] = islow_limit((t11 - t2) >> sh);
+    o[2] = islow_limit((t12 + t1) >> sh);
+    o[5] = islow_limit((t12 - t1) >> sh);
+    o[3] = islow_limit((t13 + t0) >> sh);
+    o[4] = islow_limit((t13 - t0) >> sh);
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Planes, colour                                                            */
+/* ------------------------------------------------------------------------ */
+
+size_t jo_planes_size(const jo_info* info) {
+  size_t t = 0;
+  for (int c = 0; c < info->ncomp; c++) t += (size_t)info->comp_bw[c] * info->comp_bh[c] * 64;
+  return t;
+}
+
+static void plane_ptrs(const jo_info* info, const uint8_t* planes, const uint8_t** p, int* stride) {
+  size_t o = 0;
+  for (int c = 0; c < info->ncomp; c++) {
+    p[c] = planes + o;
+    stride[c] = info->comp_bw[c] * 8;
+    o += (size_t)info->comp_bw[c] * info->comp_bh[c] * 64;
+  }
+}
+
+static int decode_planes_info(const uint8_t* d, size_t size, const jo_info* info, int idct,
+                              uint8_t* planes) {
+  int16_t* coefs = (int16_t*)malloc((size_t)info->nblocks * 64 * sizeof(int16_t));
+  if (!coefs) return JO_ERR_BAD_HEADER;
+  int rc = jo_decode_coefs(d, size, info, coefs, NULL);
+  if (rc) {
+    free(coefs);
+    return rc;
+  }
+  const uint8_t* pc[JO_MAX_COMP];
+  int st[JO_MAX_COMP];
+  plane_ptrs(info, planes, pc, st);
+  int nmcu = info->mcux * info->mcuy;
+  for (int mcu = 0; mcu < nmcu; mcu++) {
+    int mx = mcu % info->mcux, my = mcu / info->mcux;
+    for (int b = 0; b < info->bpm; b++) {
+      int c = info->mcu_comp[b];
+      int bx = info->ncomp == 1 ? mx : mx * info->comp_h[c] + info->mcu_dx[b];
+      int by = info->ncomp == 1 ? my : my * info->comp_v[c] + info->mcu_dy[b];
+      uint8_t* dst = (uint8_t*)pc[c] + (size_t)by * 8 * st[c] + (size_t)bx * 8;
+      const int16_t* blk = coefs + ((size_t)mcu * info->bpm + b) * 64;
+      if (idct == JO_IDCT_ISLOW)
+        jo_idct_islow(blk, dst, st[c]);
+      else
+        jo_idct_simple(blk, dst, st[c]);
+    }
+  }
+  free(coefs);
+  return JO_OK;
+}
+
+int jo_decode_planes(const uint8_t* d, size_t size, int idct, uint8_t* planes) {
+  jo_info info;
+  int rc = jo_parse(d, size, &info);
+  if (rc) return rc;
+  return decode_planes_info(d, size, &info, idct, planes);
+}
+
+/* JFIF YCbCr -> RGB, integer tables as IJG jdcolor.c / jdmerge.c
+ * (SCALEBITS 16, FIX(x) = (int)(x * 65536 + 0.5)). */
+#define SCB 16
+#define FIXC(x) ((int32_t)((x) * (1L << SCB) + 0.5))
+typedef struct {
+  int32_t cr_r[256], cb_b[256], cr_g[256], cb_g[256];
+} csc_t;
+
+static void build_csc(csc_t* t) {
+  for (int i = 0; i < 256; i++) {
+    int32_t x = i - 128;
+    t->cr_r[i] = (FIXC(1.402) * x + (1 << (SCB - 1))) >> SCB;
+    t->cb_b[i] = (FIXC(1.772) * x + (1 << (SCB - 1))) >> SCB;
+    t->cr_g[i] = -FIXC(0.714136286) * x;
+    t->cb_g[i] = -FIXC(0.344136286) * x + (1 << (SCB - 1));
+  }
+}
+
+static inline void csc_px(const csc_t* t, int y, int cb, int cr, uint8_t* rgb) {
+  rgb[0] = clip_u8(y + t->cr_r[cr]);
+  rgb[1] = clip_u8(y + ((t->cb_g[cb] + t->cr_g[cr]) >> SCB));
+  rgb[2] = clip_u8(y + t->cb_b[cb]);
+}
+
+static void store_px(uint8_t* out, int fmt, int ow, int oh, int x, int y, const uint8_t* rgb) {
+  int swap = (fmt == JO_FMT_BGR || fmt == JO_FMT_BGR24);
+  uint8_t c0 = swap ? rgb[2] : rgb[0], c1 = rgb[1], c2 = swap ? rgb[0] : rgb[2];
+  if (fmt == JO_FMT_RGB || fmt == JO_FMT_BGR) {
+    size_t pl = (size_t)ow * oh, o = (size_t)y * ow + x;
+    out[o] = c0;
+    out[pl + o] = c1;
+    out[2 * pl + o] = c2;
+  } else {
+    size_t o = ((size_t)y * ow + x) * 3;
+    out[o] = c0;
+    out[o + 1] = c1;
+    out[o + 2] = c2;
+  }
+}
+
+static int planes_to_rgb(const jo_info* info, const uint8_t* planes, int fmt, uint8_t* out) {
+  const uint8_t* pc[JO_MAX_COMP];
+  int st[JO_MAX_COMP];
+  plane_ptrs(info, planes, pc, st);
+  csc_t t;
+  build_csc(&t);
+  int W = info->width, H = info->height;
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      uint8_t rgb[3];
+      int yv = pc[0][(size_t)y * st[0] + x];
+      if (info->ncomp == 1) {
+        rgb[0] = rgb[1] = rgb[2] = (uint8_t)yv;
+      } else {
+        int cx1 = x * info->comp_h[1] / info->hmax, cy1 = y * info->comp_v[1] / info->vmax;
+        int cx2 = x * info->comp_h[2] / info->hmax, cy2 = y * info->comp_v[2] / info->vmax;
+        int cb = pc[1][(size_t)cy1 * st[1] + cx1];
+        int cr = pc[2][(size_t)cy2 * st[2] + cx2];
+        csc_px(&t, yv, cb, cr, rgb);
+      }
+      store_px(out, fmt, W, H, x, y, rgb);
+    }
+  return JO_OK;
+}
+
+int jo_decode_rgb(const uint8_t* d, size_t size, int idct, int fmt, uint8_t* out) {
+  jo_info info;
+  int rc = jo_parse(d, size, &info);
+  if (rc) return rc;
+  uint8_t* planes = (uint8_t*)malloc(jo_planes_size(&info));
+  if (!planes) return JO_ERR_BAD_HEADER;
+  rc = decode_planes_info(d, size, &info, idct, planes);
+  if (!rc) rc = planes_to_rgb(&info, planes, fmt, out);
+  free(planes);
+  return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Resize geometry (FFmpeg scale_eval.c ff_scale_adjust_dimensions semantics: */
+/* av_rescale rounds to nearest; vf_pad x=-1 -> (W-w)/2; vf_crop centre).     */
+/* ------------------------------------------------------------------------ */
+
+static int64_t rescale_rnd(int64_t a, int64_t b, int64_t c) { return (a * b + c / 2) / c; }
+
+int jo_geometry(int w, int h, const jo_resize* rs, jo_geom* g) {
+  if (w <= 0 || h <= 0) return JO_ERR_BAD_GEOMETRY;
+  int64_t fw = rs->fit_w > 0 ? rs->fit_w : w;
+  int64_t fh = rs->fit_h > 0 ? rs->fit_h : h;
+  int64_t sw = fw, sh = fh;
+  if (rs->aspect != JO_ASPECT_NONE) {
+    int64_t tw = rescale_rnd(fh, w, h), th = rescale_rnd(fw, h, w);
+    if (rs->aspect == JO_ASPECT_DECREASE) {
+      sw = tw < fw ? tw : fw;
+      sh = th < fh ? th : fh;
+    } else {
+      sw = tw > fw ? tw : fw;
+      sh = th > fh ? th : fh;
+    }
+  }
+  if (sw < 1) sw = 1;
+  if (sh < 1) sh = 1;
+  int64_t cw = sw, ch = sh, px = 0, py = 0;
+  if (rs->pad_w > 0 && rs->pad_h > 0) {
+    cw = rs->pad_w;
+    ch = rs->pad_h;
+    if (cw < sw || ch < sh) return JO_ERR_BAD_GEOMETRY;
+    px = (cw - sw) / 2;
+    py = (ch - sh) / 2;
+  }
+  int64_t ow = cw, oh = ch, cx = 0, cy = 0;
+  if (rs->crop_w > 0 && rs->crop_h > 0) {
+    ow = rs->crop_w;
+    oh = rs->crop_h;
+    if (ow > cw || oh > ch) return JO_ERR_BAD_GEOMETRY;
+    cx = (cw - ow) / 2;
+    cy = (ch - oh) / 2;
+  }
+  if (sw > 65535 || sh > 65535 || ow > 65535 || oh > 65535) return JO_ERR_BAD_GEOMETRY;
+  g->sw = (int)sw;
+  g->sh = (int)sh;
+  g->dx = (int)(px - cx);
+  g->dy = (int)(py - cy);
+  g->ow = (int)ow;
+  g->oh = (int)oh;
+  return JO_OK;
+}
+
+/* Resampling kernel: Keys cubic with a = -0.6 (the B=0, C=0.6 member of the
+ * family swscale's SWS_BICUBIC uses), support widened by the downscale factor
+ * (anti-aliased); or a triangle (bilinear).  Every float step is one IEEE op. */
+static float kernel_eval(int filter, float x) {
+  float t = fabsf(x);
+  if (filter == JO_FILTER_BILINEAR) return t < 1.0f ? 1.0f - t : 0.0f;
+  float t2 = t * t;
+  float t3 = t2 * t;
+  if (t <= 1.0f) {
+    float a = 1.4f * t3;
+    float b = 2.4f * t2;
+    return (a - b) + 1.0f;
+  }
+  if (t < 2.0f) {
+    float a = -0.6f * t3;
+    float b = 3.0f * t2;
+    float c = 4.8f * t;
+    return ((a + b) - c) + 2.4f;
+  }
+  return 0.0f;
+}
+
+static float filter_radius(int filter) { return filter == JO_FILTER_BILINEAR ? 1.0f : 2.0f; }
+
+int jo_max_taps(int src_len, int dst_len, int filter) {
+  float scale = (float)src_len / (float)dst_len;
+  float fscale = scale > 1.0f ? scale : 1.0f;
+  float support = filter_radius(filter) * fscale;
+  return (int)ceilf(2.0f * support) + 1;
+}
+
+int jo_axis_weights(int src_len, int dst_len, int filter, int maxtaps, int32_t* first, int16_t* w) {
+  float scale = (float)src_len / (float)dst_len;
+  float fscale = scale > 1.0f ? scale : 1.0f;
+  float support = filter_radius(filter) * fscale;
+  int used = 0;
+  float wf[1024];
+  int wq[1024];
+  for (int i = 0; i < dst_len; i++) {
+    float center = ((float)i + 0.5f) * scale;
+    center = center - 0.5f;
+    int lo = (int)ceilf(center - support);
+    int hi = (int)floorf(center + support);
+    int n = hi - lo + 1;
+    if (n > maxtaps || n > 1024) return -1;
+    if (n > used) used = n;
+    float sum = 0.0f;
+    for (int t = 0; t < n; t++) {
+      float x = ((float)(lo + t) - center) / fscale;
+      wf[t] = kernel_eval(filter, x);
+      sum = sum + wf[t];
+    }
+    int qs = 0, am = 0;
+    for (int t = 0; t < n; t++) {
+      float q = wf[t] / sum;
+      q = q * 16384.0f;
+      q = q + 0.5f;
+      wq[t] = (int)floorf(q);
+      qs += wq[t];
+      if (wq[t] > wq[am]) am = t;
+    }
+    wq[am] += 16384 - qs;
+    first[i] = lo;
+    for (int t = 0; t < maxtaps; t++) w[(size_t)i * maxtaps + t] = (int16_t)(t < n ? wq[t] : 0);
+  }
+  return used;
+}
+
+uint16_t jo_f32_to_f16(float f) {
+  uint32_t x;
+  memcpy(&x, &f, 4);
+  uint32_t sign = (x >> 16) & 0x8000;
+  uint32_t exp = (x >> 23) & 0xFF;
+  uint32_t man = x & 0x7FFFFF;
+  if (exp == 0xFF) return (uint16_t)(sign | 0x7C00 | (man ? 0x200 : 0));
+  int e = (int)exp - 127 + 15;
+  if (e >= 31) return (uint16_t)(sign | 0x7C00);
+  if (e <= 0) {
+    if (e < -10) return (uint16_t)sign;
+    man |= 0x800000;
+    int shift = 14 - e;
+    uint32_t h = man >> shift;
+    uint32_t rem = man & ((1u << shift) - 1), half = 1u << (shift - 1);
+    if (rem > half || (rem == half && (h & 1))) h++;
+    return (uint16_t)(sign | h);
+  }
+  uint32_t h = ((uint32_t)e << 10) | (man >> 13);
+  uint32_t rem = man & 0x1FFF;
+  if (rem > 0x1000 || (rem == 0x1000 && (h & 1))) h++;
+  return (uint16_t)(sign | h);
+}
+
+/* resize one plane (true dims pw x ph, stride st) to sw x sh:
+ * horizontal Q14 taps -> Q6 intermediate ((acc + 128) >> 8), then vertical Q14
+ * -> (acc + 2^19) >> 20, clamp u8. */
+static int resize_plane(const uint8_t* src, int pw, int ph, int st, int sw, int sh, int filter,
+                        uint8_t* dst) {
+  int mtx = jo_max_taps(pw, sw, filter), mty = jo_max_taps(ph, sh, filter);
+  int32_t* fx = (int32_t*)malloc(sizeof(int32_t) * sw);
+  int16_t* wx = (int16_t*)malloc(sizeof(int16_t) * (size_t)sw * mtx);
+  int32_t* fy = (int32_t*)malloc(sizeof(int32_t) * sh);
+  int16_t* wy = (int16_t*)malloc(sizeof(int16_t) * (size_t)sh * mty);
+  int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * (size_t)ph * sw);
+  int rc = JO_OK;
+  if (!fx || !wx || !fy || !wy || !tmp) {
+    rc = JO_ERR_BAD_GEOMETRY;
+    goto done;
+  }
+  if (jo_axis_weights(pw, sw, filter, mtx, fx, wx) < 0 ||
+      jo_axis_weights(ph, sh, filter, mty, fy, wy) < 0) {
+    rc = JO_ERR_BAD_GEOMETRY;
+    goto done;
+  }
+  for (int r = 0; r < ph; r++) {
+    const uint8_t* row = src + (size_t)r * st;
+    for (int x = 0; x < sw; x++) {
+      int32_t acc = 0;
+      for (int t = 0; t < mtx; t++) {
+        int k = fx[x] + t;
+        k = k < 0 ? 0 : k >= pw ? pw - 1 : k;
+        acc += (int32_t)wx[(size_t)x * mtx + t] * row[k];
+      }
+      tmp[(size_t)r * sw + x] = (acc + 128) >> 8;
+    }
+  }
+  for (int y = 0; y < sh; y++)
+    for (int x = 0; x < sw; x++) {
+      int32_t acc = 0;
+      for (int t = 0; t < mty; t++) {
+        int k = fy[y] + t;
+        k = k < 0 ? 0 : k >= ph ? ph - 1 : k;
+        acc += (int32_t)wy[(size_t)y * mty + t] * tmp[(size_t)k * sw + x];
+      }
+      dst[(size_t)y * sw + x] = clip_u8((acc + (1 << 19)) >> 20);
+    }
+done:
+  free(fx);
+  free(wx);
+  free(fy);
+  free(wy);
+  free(tmp);
+  return rc;
+}
+
+int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize* rs, int fmt,
+                     int dtype, const float* mean, const float* stdv, void* out,
+                     jo_geom* geom_out) {
+  jo_geom g;
+  int rc = jo_geometry(info->width, info->height, rs, &g);
+  if (rc) return rc;
+  if (geom_out) *geom_out = g;
+  const uint8_t* pc[JO_MAX_COMP];
+  int st[JO_MAX_COMP];
+  plane_ptrs(info, planes, pc, st);
+  uint8_t* rp[JO_MAX_COMP] = {0};
+  for (int c = 0; c < info->ncomp; c++) {
+    rp[c] = (uint8_t*)malloc((size_t)g.sw * g.sh);
+    if (!rp[c] || (rc = resize_plane(pc[c], info->comp_w[c], info->comp_h_px[c], st[c], g.sw,
+                                     g.sh, rs->filter, rp[c]))) {
+      if (!rc) rc = JO_ERR_BAD_GEOMETRY;
+      for (int k = 0; k <= c; k++) free(rp[k]);
+      return rc;
+    }
+  }
+  csc_t t;
+  build_csc(&t);
+  int planar = (fmt == JO_FMT_RGB || fmt == JO_FMT_BGR);
+  int swap = (fmt == JO_FMT_BGR || fmt == JO_FMT_BGR24);
+  size_t pl = (size_t)g.ow * g.oh;
+  for (int y = 0; y < g.oh; y++)
+    for (int x = 0; x < g.ow; x++) {
+      int cx = x - g.dx, cy = y - g.dy;
+      uint8_t rgb[3] = {0, 0, 0};
+      if (cx >= 0 && cx < g.sw && cy >= 0 && cy < g.sh) {
+        size_t o = (size_t)cy * g.sw + cx;
+        if (info->ncomp == 1)
+          rgb[0] = rgb[1] = rgb[2] = rp[0][o];
+        else
+          csc_px(&t, rp[0][o], rp[1][o], rp[2][o], rgb);
+      }
+      for (int ch = 0; ch < 3; ch++) {
+        int src_ch = swap ? 2 - ch : ch;
+        size_t oi = planar ? (size_t)ch * pl + (size_t)y * g.ow + x : ((size_t)y * g.ow + x) * 3 + ch;
+        if (dtype == JO_DTYPE_U8) {
+          ((uint8_t*)out)[oi] = rgb[src_ch];
+        } else {
+          float v = (float)rgb[src_ch] / 255.0f;
+          v = v - mean[ch];
+          v = v / stdv[ch];
+          ((uint16_t*)out)[oi] = jo_f32_to_f16(v);
+        }
+      }
+    }
+  for (int c = 0; c < info->ncomp; c++) free(rp[c]);
+  return JO_OK;
+}
+
+int jo_decode_resize(const uint8_t* d, size_t size, int idct, const jo_resize* rs, int fmt,
+                     int dtype, const float* mean, const float* stdv, void* out,
+                     jo_geom* geom_out) {
+  jo_info info;
+  int rc = jo_parse(d, size, &info);
+  if (rc) return rc;
+  uint8_t* planes = (uint8_t*)malloc(jo_planes_size(&info));
+  if (!planes) return JO_ERR_BAD_HEADER;
+  rc = decode_planes_info(d, size, &info, idct, planes);
+  if (!rc) rc = jo_resize_planes(&info, planes, rs, fmt, dtype, mean, stdv, out, geom_out);
+  free(planes);
+  return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Threaded batch drivers (CPU baseline: one decoder per thread, images     */
+/* striped across threads, as examples/image_dataloading.py's workers).      */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+  const uint8_t* const* data;
+  const size_t* sizes;
+  int n, tid, nthreads, idct, fmt, dtype, resize;
+  const jo_resize* rs;
+  const float *mean, *stdv;
+  uint8_t* out;
+  size_t out_stride;
+  int* status;
+  int failed;
+} job_t;
+
+static void* worker(void* arg) {
+  job_t* j = (job_t*)arg;
+  for (int i = j->tid; i < j->n; i += j->nthreads) {
+    int rc;
+    if (j->resize)
+      rc = jo_decode_resize(j->data[i], j->sizes[i], j->idct, j->rs, j->fmt, j->dtype, j->mean,
+                            j->stdv, j->out + (size_t)i * j->out_stride, NULL);
+    else
+      rc = jo_decode_rgb(j->data[i], j->sizes[i], j->idct, j->fmt,
+                         j->out + (size_t)i * j->out_stride);
+    if (j->status) j->status[i] = rc;
+    if (rc) j->failed++;
+  }
+  return NULL;
+}
+
+static int run_batch(job_t* proto, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  job_t jobs[256];
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = *proto;
+    jobs[t].tid = t;
+    jobs[t].nthreads = nthreads;
+    jobs[t].failed = 0;
+    if (nthreads > 1) pthread_create(&th[t], NULL, worker, &jobs[t]);
+  }
+  if (nthreads == 1) worker(&jobs[0]);
+  int failed = 0;
+  for (int t = 0; t < nthreads; t++) {
+    if (nthreads > 1) pthread_join(th[t], NULL);
+    failed += jobs[t].failed;
+  }
+  return failed;
+}
+
+int jo_decode_resize_batch(const uint8_t* const* data, const size_t* sizes, int n, int idct,
+                           const jo_resize* rs, int fmt, int dtype, const float* mean,
+                           const float* stdv, uint8_t* out, size_t out_stride, int nthreads,
+                           int* status) {
+  job_t j;
+  memset(&j, 0, sizeof(j));
+  j.data = data;
+  j.sizes = sizes;
+  j.n = n;
+  j.idct = idct;
+  j.fmt = fmt;
+  j.dtype = dtype;
+  j.resize = 1;
+  j.rs = rs;
+  j.mean = mean;
+  j.stdv = stdv;
+  j.out = out;
+  j.out_stride = out_stride;
+  j.status = status;
+  return run_batch(&j, nthreads);
+}
+
+int jo_decode_rgb_batch(const uint8_t* const* data, const size_t* sizes, int n, int idct, int fmt,
+                        uint8_t* out, size_t out_stride, int nthreads, int* status) {
+  job_t j;
+  memset(&j, 0, sizeof(j));
+  j.data = data;
+  j.sizes = sizes;
+  j.n = n;
+  j.idct = idct;
+  j.fmt = fmt;
+  j.out = out;
+  j.out_stride = out_stride;
+  j.status = status;
+  return run_batch(&j, nthreads);
+}

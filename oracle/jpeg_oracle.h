@@ -1,0 +1,163 @@
+/*
+ * jpeg_oracle.h -- CPU restatement of SPDL's JPEG -> RGB path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * (or as the timed CPU baseline).  The product path (spdl_amd) never links,
+ * loads or calls it.
+ *
+ * What it restates (citations relative to the SPDL reference tree):
+ *   - demux + FFmpeg `mjpeg` decode called from
+ *       src/libspdl/core/detail/ffmpeg/decoder.cpp:50-63 (avcodec_send_packet /
+ *       avcodec_receive_frame) with threads=1 (ctx_utils.cpp:180-183);
+ *     the arithmetic is FFmpeg's (third-party, not vendored in the reference,
+ *     CI pin conda-forge ffmpeg==8.0, .github/workflows/_build_linux.yml:127):
+ *       marker parse, baseline Huffman decode with DC prediction, dequant
+ *       (block[j] = level * qtab[i]), 8-bit `simple_idct` (idctRowCondDC +
+ *       idctSparseColPut), clamp to u8, planes in yuvj4xxp.
+ *   - the filter graph of load_image_batch (src/spdl/io/_composite.py:438-443,
+ *     src/spdl/io/_preprocessing.py:214-234): scale (force_original_aspect_ratio
+ *     decrease|increase) + centred pad / crop + format=rgb24.
+ *   - the ImageNet normalisation epilogue (examples/imagenet_classification.py:
+ *     96-106): x.float()/255, (x-mean)/std.
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - entropy decode + dequant: pinned bit-exact against IJG libjpeg 9d
+ *     (jpeg_read_coefficients), tests/golden/ coefficient fixtures.
+ *   - JO_IDCT_ISLOW + nearest chroma + JFIF integer colour conversion: pinned
+ *     bit-exact end-to-end against libjpeg 9d (dct_method=JDCT_ISLOW,
+ *     do_fancy_upsampling=FALSE).
+ *   - JO_IDCT_SIMPLE (FFmpeg simple_idct) and the resize filter: parity
+ *     UNPINNED against FFmpeg (no FFmpeg in this image); restated from the
+ *     published algorithm.
+ */
+#ifndef SPDL_JPEG_ORACLE_H
+#define SPDL_JPEG_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  JO_OK = 0,
+  JO_ERR_NOT_JPEG = 1,
+  JO_ERR_UNSUPPORTED = 2,   /* progressive / arithmetic / 12-bit / CMYK ... */
+  JO_ERR_BAD_HEADER = 3,
+  JO_ERR_BAD_HUFFMAN = 4,   /* invalid code / run past coefficient 63     */
+  JO_ERR_TRUNCATED = 5,     /* entropy data ended before the last MCU      */
+  JO_ERR_BAD_RESTART = 6,
+  JO_ERR_BAD_GEOMETRY = 7,
+};
+
+enum { JO_IDCT_SIMPLE = 0, JO_IDCT_ISLOW = 1 };
+
+/* pixel formats: planar (CHW) vs interleaved (HWC), channel order */
+enum { JO_FMT_RGB = 0, JO_FMT_BGR = 1, JO_FMT_RGB24 = 2, JO_FMT_BGR24 = 3 };
+
+enum { JO_ASPECT_NONE = 0, JO_ASPECT_DECREASE = 1, JO_ASPECT_INCREASE = 2 };
+enum { JO_FILTER_BICUBIC = 0, JO_FILTER_BILINEAR = 1 };
+enum { JO_DTYPE_U8 = 0, JO_DTYPE_F16 = 1 };
+
+#define JO_MAX_COMP 3
+#define JO_MAX_BPM 10
+/* dequantised DC predictor start value (FFmpeg mjpegdec: 4 << bits) */
+#define JO_DC_BIAS 1024
+
+typedef struct {
+  int width, height;
+  int ncomp;                 /* 1 or 3 */
+  int hmax, vmax;
+  int mcux, mcuy;            /* MCUs per row / column */
+  int bpm;                   /* blocks per MCU */
+  int nblocks;               /* mcux * mcuy * bpm */
+  int restart_interval;      /* MCUs per restart interval, 0 = none */
+  int comp_h[JO_MAX_COMP], comp_v[JO_MAX_COMP], comp_tq[JO_MAX_COMP];
+  int comp_td[JO_MAX_COMP], comp_ta[JO_MAX_COMP];
+  int comp_bw[JO_MAX_COMP], comp_bh[JO_MAX_COMP];   /* blocks per row / col */
+  int comp_w[JO_MAX_COMP], comp_h_px[JO_MAX_COMP];  /* true plane dims     */
+  int mcu_comp[JO_MAX_BPM], mcu_dx[JO_MAX_BPM], mcu_dy[JO_MAX_BPM];
+  uint16_t qt[4][64];        /* zig-zag order, as in the stream */
+  uint8_t dc_bits[4][17], dc_vals[4][256];
+  uint8_t ac_bits[4][17], ac_vals[4][256];
+  size_t scan_start;         /* byte offset of the entropy-coded data */
+} jo_info;
+
+typedef struct {
+  int fit_w, fit_h;          /* scale box; <=0 means "input size" */
+  int aspect;                /* JO_ASPECT_* */
+  int pad_w, pad_h;          /* canvas; <=0 means no pad */
+  int crop_w, crop_h;        /* centre crop; <=0 means no crop */
+  int filter;                /* JO_FILTER_* */
+} jo_resize;
+
+typedef struct {
+  int sw, sh;                /* scaled content size */
+  int dx, dy;                /* out(x,y) = content(x-dx, y-dy) */
+  int ow, oh;                /* output size */
+} jo_geom;
+
+const char* jo_strerror(int code);
+
+int jo_parse(const uint8_t* data, size_t size, jo_info* info);
+
+/* Quick SOF probe: width/height/ncomp without full validation. */
+int jo_get_image_info(const uint8_t* data, size_t size, int* w, int* h, int* ncomp);
+
+/* Entropy decode + dequant.  coefs: nblocks*64 int16, natural order, MCU order,
+ * dequantised FFmpeg-style (DC carries the +1024 level-shift bias).  levels (optional): quantised levels laid out per
+ * component in block-raster order (comp 0 first), natural order -- the layout
+ * libjpeg's jpeg_read_coefficients exposes, used for pinning. */
+int jo_decode_coefs(const uint8_t* data, size_t size, const jo_info* info,
+                    int16_t* coefs, int16_t* levels);
+
+void jo_idct_simple(const int16_t* in, uint8_t* out, int stride);
+void jo_idct_islow(const int16_t* in, uint8_t* out, int stride);
+
+/* Decoded planes, padded to whole blocks: plane c is comp_bw[c]*8 wide and
+ * comp_bh[c]*8 tall, stored back to back. */
+size_t jo_planes_size(const jo_info* info);
+int jo_decode_planes(const uint8_t* data, size_t size, int idct, uint8_t* planes);
+
+/* Full-resolution RGB (nearest chroma replication, JFIF integer CSC). */
+int jo_decode_rgb(const uint8_t* data, size_t size, int idct, int fmt, uint8_t* out);
+
+int jo_geometry(int w, int h, const jo_resize* rs, jo_geom* g);
+
+/* 1-D resampling table: for each dst index i, first[i] and taps weights
+ * (Q14, sum == 16384) in w[i*maxtaps ...]; returns ntaps used (<= maxtaps) or -1. */
+int jo_axis_weights(int src_len, int dst_len, int filter, int maxtaps,
+                    int32_t* first, int16_t* w);
+int jo_max_taps(int src_len, int dst_len, int filter);
+
+/* Decode + resize + csc + pad/crop (+ normalise when dtype == F16).
+ * out is ow*oh*3 elements (u8 or IEEE fp16 bits). */
+int jo_decode_resize(const uint8_t* data, size_t size, int idct, const jo_resize* rs,
+                     int fmt, int dtype, const float* mean, const float* stdv,
+                     void* out, jo_geom* geom_out);
+
+/* Same, starting from already-decoded planes (used by tests to isolate the
+ * resize stage). */
+int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize* rs,
+                     int fmt, int dtype, const float* mean, const float* stdv,
+                     void* out, jo_geom* geom_out);
+
+uint16_t jo_f32_to_f16(float f);
+
+/* Multi-threaded batch (CPU baseline).  Image i goes to out + i*out_stride
+ * bytes.  status[i] receives the per-image code.  Returns #failed. */
+int jo_decode_resize_batch(const uint8_t* const* data, const size_t* sizes, int n,
+                           int idct, const jo_resize* rs, int fmt, int dtype,
+                           const float* mean, const float* stdv,
+                           uint8_t* out, size_t out_stride, int nthreads, int* status);
+
+int jo_decode_rgb_batch(const uint8_t* const* data, const size_t* sizes, int n,
+                        int idct, int fmt, uint8_t* out, size_t out_stride,
+                        int nthreads, int* status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

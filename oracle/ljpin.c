@@ -1,0 +1,141 @@
+/*
+ * ljpin.c -- pins the oracle against IJG libjpeg 9d (/opt/conda/lib/libjpeg.so.9).
+ *
+ * TEST INFRASTRUCTURE ONLY: used by tests/gen_golden.py (and the pin tests
+ * when the library is present) to produce independent golden vectors:
+ *   - lj_read_coefs: quantised coefficients via jpeg_read_coefficients(), the
+ *     entropy-decode + DC-prediction ground truth (natural order, per
+ *     component, block rows padded to the sampling factor).
+ *   - lj_decode_rgb: full decode with dct_method = JDCT_ISLOW and
+ *     do_fancy_upsampling = FALSE (nearest chroma), out_color_space = JCS_RGB.
+ * libjpeg is a third-party implementation of T.81, not SPDL; see DESIGN.md.
+ */
+#include <setjmp.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "jpeglib.h"
+
+typedef struct {
+  struct jpeg_error_mgr pub;
+  jmp_buf jb;
+} err_t;
+
+static void on_error(j_common_ptr c) {
+  err_t* e = (err_t*)c->err;
+  longjmp(e->jb, 1);
+}
+static void on_message(j_common_ptr c, int lvl) { (void)c; (void)lvl; }
+
+static void mem_src_init(j_decompress_ptr c) { (void)c; }
+static boolean mem_fill(j_decompress_ptr c) {
+  static const JOCTET eoi[2] = {0xFF, 0xD9};
+  c->src->next_input_byte = eoi;
+  c->src->bytes_in_buffer = 2;
+  return TRUE;
+}
+static void mem_skip(j_decompress_ptr c, long n) {
+  if (n <= 0) return;
+  if ((size_t)n > c->src->bytes_in_buffer) n = (long)c->src->bytes_in_buffer;
+  c->src->next_input_byte += n;
+  c->src->bytes_in_buffer -= (size_t)n;
+}
+static void mem_term(j_decompress_ptr c) { (void)c; }
+
+static void set_src(j_decompress_ptr c, struct jpeg_source_mgr* s, const uint8_t* d, size_t n) {
+  s->init_source = mem_src_init;
+  s->fill_input_buffer = mem_fill;
+  s->skip_input_data = mem_skip;
+  s->resync_to_restart = jpeg_resync_to_restart;
+  s->term_source = mem_term;
+  s->next_input_byte = d;
+  s->bytes_in_buffer = n;
+  c->src = s;
+}
+
+/* info[0..]: width, height, ncomp, then per comp: bw, bh, h, v ; qt: 4x64 natural */
+int lj_read_coefs(const uint8_t* d, size_t n, int* info, int16_t* out, size_t out_cap,
+                  uint16_t* qt) {
+  struct jpeg_decompress_struct c;
+  err_t e;
+  struct jpeg_source_mgr src;
+  c.err = jpeg_std_error(&e.pub);
+  e.pub.error_exit = on_error;
+  e.pub.emit_message = on_message;
+  if (setjmp(e.jb)) {
+    jpeg_destroy_decompress(&c);
+    return -1;
+  }
+  jpeg_create_decompress(&c);
+  set_src(&c, &src, d, n);
+  jpeg_read_header(&c, TRUE);
+  jvirt_barray_ptr* arr = jpeg_read_coefficients(&c);
+  info[0] = (int)c.image_width;
+  info[1] = (int)c.image_height;
+  info[2] = c.num_components;
+  size_t o = 0;
+  for (int ci = 0; ci < c.num_components; ci++) {
+    jpeg_component_info* cp = &c.comp_info[ci];
+    int bw = (int)cp->width_in_blocks, bh = (int)cp->height_in_blocks;
+    if (c.num_components > 1) {
+      bw = (bw + cp->h_samp_factor - 1) / cp->h_samp_factor * cp->h_samp_factor;
+      bh = (bh + cp->v_samp_factor - 1) / cp->v_samp_factor * cp->v_samp_factor;
+    }
+    info[3 + 4 * ci] = bw;
+    info[4 + 4 * ci] = bh;
+    info[5 + 4 * ci] = cp->h_samp_factor;
+    info[6 + 4 * ci] = cp->v_samp_factor;
+    for (int r = 0; r < bh; r++) {
+      JBLOCKARRAY row = (*c.mem->access_virt_barray)((j_common_ptr)&c, arr[ci], (JDIMENSION)r, 1, FALSE);
+      for (int b = 0; b < bw; b++) {
+        if (o + 64 > out_cap) {
+          jpeg_destroy_decompress(&c);
+          return -2;
+        }
+        for (int k = 0; k < 64; k++) out[o + k] = row[0][b][k];
+        o += 64;
+      }
+    }
+    if (cp->quant_table && cp->quant_tbl_no < 4)
+      for (int k = 0; k < 64; k++) qt[cp->quant_tbl_no * 64 + k] = cp->quant_table->quantval[k];
+  }
+  jpeg_finish_decompress(&c);
+  jpeg_destroy_decompress(&c);
+  return (int)(o / 64);
+}
+
+int lj_decode_rgb(const uint8_t* d, size_t n, uint8_t* out, size_t cap, int* w, int* h) {
+  struct jpeg_decompress_struct c;
+  err_t e;
+  struct jpeg_source_mgr src;
+  c.err = jpeg_std_error(&e.pub);
+  e.pub.error_exit = on_error;
+  e.pub.emit_message = on_message;
+  if (setjmp(e.jb)) {
+    jpeg_destroy_decompress(&c);
+    return -1;
+  }
+  jpeg_create_decompress(&c);
+  set_src(&c, &src, d, n);
+  jpeg_read_header(&c, TRUE);
+  c.out_color_space = JCS_RGB;
+  c.dct_method = JDCT_ISLOW;
+  c.do_fancy_upsampling = FALSE;
+  c.do_block_smoothing = FALSE;
+  jpeg_start_decompress(&c);
+  *w = (int)c.output_width;
+  *h = (int)c.output_height;
+  size_t stride = (size_t)c.output_width * 3;
+  if (stride * c.output_height > cap) {
+    jpeg_destroy_decompress(&c);
+    return -2;
+  }
+  while (c.output_scanline < c.output_height) {
+    JSAMPROW row = out + stride * c.output_scanline;
+    jpeg_read_scanlines(&c, &row, 1);
+  }
+  jpeg_finish_decompress(&c);
+  jpeg_destroy_decompress(&c);
+  return 0;
+}

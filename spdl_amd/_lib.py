@@ -1,0 +1,323 @@
+"""ctypes binding of the gfx950 decode stage (``include/spdl_hipjpeg.h``).
+
+The product path: every public operator in :mod:`spdl_amd.io` ends here, in
+``spdl_amd/lib/libspdl_hipjpeg.so``.  There is no CPU fallback: a missing
+library or a missing GPU raises immediately.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from dataclasses import dataclass, field
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libspdl_hipjpeg.so")
+
+ABI_VERSION = 1
+
+# enums (mirror include/spdl_hipjpeg.h)
+PIX_FMTS = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
+ASPECT = {None: 0, "none": 0, "decrease": 1, "increase": 2}
+FILTERS = {"bicubic": 0, "bilinear": 1}
+IDCT = {"simple": 0, "islow": 1}
+DTYPE_U8, DTYPE_F16 = 0, 1
+
+EXPORTED = (
+    "spdl_hj_abi_version",
+    "spdl_hj_get_image_info",
+    "spdl_hj_output_size",
+    "spdl_hj_create",
+    "spdl_hj_destroy",
+    "spdl_hj_decode_batch",
+    "spdl_hj_decode_batch_device",
+    "spdl_hj_decode_planes",
+    "spdl_hj_set_profiling",
+    "spdl_hj_last_timings",
+    "spdl_hj_stage_name",
+    "spdl_hj_set_param",
+)
+
+
+class ImageInfo(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("ncomp", ctypes.c_int32),
+        ("h_samp", ctypes.c_int32 * 3),
+        ("v_samp", ctypes.c_int32 * 3),
+    ]
+
+
+class OutputSpec(ctypes.Structure):
+    _fields_ = [
+        ("pix_fmt", ctypes.c_int32),
+        ("dtype", ctypes.c_int32),
+        ("idct", ctypes.c_int32),
+        ("resize", ctypes.c_int32),
+        ("fit_w", ctypes.c_int32),
+        ("fit_h", ctypes.c_int32),
+        ("aspect", ctypes.c_int32),
+        ("pad_w", ctypes.c_int32),
+        ("pad_h", ctypes.c_int32),
+        ("crop_w", ctypes.c_int32),
+        ("crop_h", ctypes.c_int32),
+        ("filter", ctypes.c_int32),
+        ("mean", ctypes.c_float * 3),
+        ("std", ctypes.c_float * 3),
+    ]
+
+
+@dataclass(frozen=True)
+class Output:
+    """What the decoder produces for every image of a batch.
+
+    ``resize=False`` keeps the full resolution.  Otherwise the FFmpeg filter
+    chain SPDL builds is applied (src/spdl/io/_preprocessing.py:214-234)::
+
+        scale=w=fit_w:h=fit_h[:force_original_aspect_ratio=aspect]
+        [,pad=w=pad_w:h=pad_h:x=-1:y=-1:color=black][,crop=w=crop_w:h=crop_h]
+    """
+
+    pix_fmt: str = "rgb"
+    normalize: bool = False  # -> fp16 (x/255 - mean)/std
+    idct: str = "simple"
+    resize: bool = False
+    fit_w: int = 0
+    fit_h: int = 0
+    aspect: str | None = None
+    pad_w: int = 0
+    pad_h: int = 0
+    crop_w: int = 0
+    crop_h: int = 0
+    filter: str = "bicubic"
+    mean: tuple = (0.485, 0.456, 0.406)
+    std: tuple = (0.229, 0.224, 0.225)
+
+    def to_c(self) -> OutputSpec:
+        if self.pix_fmt not in PIX_FMTS:
+            raise RuntimeError(f"Unexpected pix_fmt: {self.pix_fmt}")
+        return OutputSpec(
+            PIX_FMTS[self.pix_fmt],
+            DTYPE_F16 if self.normalize else DTYPE_U8,
+            IDCT[self.idct],
+            int(bool(self.resize)),
+            int(self.fit_w),
+            int(self.fit_h),
+            ASPECT[self.aspect],
+            int(self.pad_w),
+            int(self.pad_h),
+            int(self.crop_w),
+            int(self.crop_h),
+            FILTERS[self.filter],
+            (ctypes.c_float * 3)(*self.mean),
+            (ctypes.c_float * 3)(*self.std),
+        )
+
+    @property
+    def planar(self) -> bool:
+        return self.pix_fmt in ("rgb", "bgr")
+
+
+_LIB = None
+_LIB_LOCK = threading.Lock()
+
+
+def lib() -> ctypes.CDLL:
+    """Load the native library (raises if it has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LIB_LOCK:
+        if _LIB is not None:
+            return _LIB
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"spdl_amd native library not found at {LIB_PATH}; "
+                "build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(make -C spdl_amd/csrc)"
+            )
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32
+        cp = ctypes.c_char_p
+        L.spdl_hj_abi_version.restype = ctypes.c_int
+        L.spdl_hj_get_image_info.argtypes = [vp, sz, ctypes.POINTER(ImageInfo)]
+        L.spdl_hj_output_size.argtypes = [
+            i32, i32, ctypes.POINTER(OutputSpec), ctypes.POINTER(i32), ctypes.POINTER(i32)
+        ]
+        L.spdl_hj_create.argtypes = [ctypes.c_int, cp, sz]
+        L.spdl_hj_create.restype = vp
+        L.spdl_hj_destroy.argtypes = [vp]
+        L.spdl_hj_destroy.restype = None
+        L.spdl_hj_decode_batch.argtypes = [
+            vp, vp, vp, i32, ctypes.POINTER(OutputSpec), vp, sz, vp, i32, vp, cp, sz
+        ]
+        L.spdl_hj_decode_batch_device.argtypes = [
+            vp, vp, sz, vp, vp, vp, i32, ctypes.POINTER(OutputSpec), vp, sz, vp, i32, vp, cp, sz
+        ]
+        L.spdl_hj_decode_planes.argtypes = [vp, vp, sz, i32, vp, vp, cp, sz]
+        L.spdl_hj_set_profiling.argtypes = [vp, i32]
+        L.spdl_hj_last_timings.argtypes = [vp, vp, i32, ctypes.POINTER(i32)]
+        L.spdl_hj_stage_name.argtypes = [i32]
+        L.spdl_hj_stage_name.restype = ctypes.c_char_p
+        L.spdl_hj_set_param.argtypes = [vp, cp, ctypes.c_int64]
+        ver = L.spdl_hj_abi_version()
+        if ver != ABI_VERSION:
+            raise RuntimeError(f"libspdl_hipjpeg ABI {ver} != expected {ABI_VERSION}")
+        _LIB = L
+    return _LIB
+
+
+def get_image_info(data) -> ImageInfo:
+    """Host SOF probe (width, height, components, sampling factors)."""
+    mv = memoryview(data).cast("B")
+    buf = (ctypes.c_char * len(mv)).from_buffer_copy(mv) if mv.readonly else (
+        ctypes.c_char * len(mv)).from_buffer(mv)
+    info = ImageInfo()
+    rc = lib().spdl_hj_get_image_info(ctypes.addressof(buf), len(mv), ctypes.byref(info))
+    if rc:
+        raise RuntimeError(f"Failed to decode an image. (header probe: status {rc})")
+    return info
+
+
+def output_size(width: int, height: int, out: Output) -> tuple[int, int]:
+    ow, oh = ctypes.c_int32(), ctypes.c_int32()
+    spec = out.to_c()
+    rc = lib().spdl_hj_output_size(width, height, ctypes.byref(spec), ctypes.byref(ow),
+                                   ctypes.byref(oh))
+    if rc:
+        raise RuntimeError(f"invalid output geometry for {width}x{height} ({rc})")
+    return ow.value, oh.value
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)
+
+
+class Decoder:
+    """One native context (device workspace + pinned staging) bound to a
+    device.  Not thread-safe: use :func:`thread_decoder` for a per-thread one
+    (the reference keeps its nvJPEG state thread_local,
+    src/libspdl/cuda/nvjpeg/decoding.cpp:107-112)."""
+
+    def __init__(self, device_index: int = 0):
+        err = ctypes.create_string_buffer(512)
+        h = lib().spdl_hj_create(int(device_index), err, 512)
+        if not h:
+            raise RuntimeError(f"spdl_amd: cannot create decoder: {err.value.decode()}")
+        self._h = h
+        self.device_index = int(device_index)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().spdl_hj_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_param(self, name: str, value: int) -> None:
+        rc = lib().spdl_hj_set_param(self._h, name.encode(), int(value))
+        if rc:
+            raise ValueError(f"invalid decoder parameter {name}={value}")
+
+    def set_profiling(self, enable: bool) -> None:
+        lib().spdl_hj_set_profiling(self._h, int(bool(enable)))
+
+    def last_timings(self) -> dict:
+        buf = (ctypes.c_float * 16)()
+        n = ctypes.c_int32()
+        lib().spdl_hj_last_timings(self._h, buf, 16, ctypes.byref(n))
+        return {lib().spdl_hj_stage_name(i).decode(): buf[i] for i in range(n.value)}
+
+    def decode_batch(self, datas, out: Output, out_ptr: int, out_bytes: int, stream=None,
+                     sync: bool = True) -> list[int]:
+        n = len(datas)
+        if n == 0:
+            raise RuntimeError("Failed to decode an image. (the batch is empty)")
+        keep = []
+        ptrs = (ctypes.c_void_p * n)()
+        sizes = (ctypes.c_size_t * n)()
+        for i, d in enumerate(datas):
+            mv = memoryview(d).cast("B")
+            if mv.readonly:
+                b = (ctypes.c_char * len(mv)).from_buffer_copy(mv)
+            else:
+                b = (ctypes.c_char * len(mv)).from_buffer(mv)
+            keep.append(b)
+            ptrs[i] = ctypes.addressof(b)
+            sizes[i] = len(mv)
+        status = (ctypes.c_int32 * n)()
+        err = ctypes.create_string_buffer(1024)
+        spec = out.to_c()
+        rc = lib().spdl_hj_decode_batch(
+            self._h, ptrs, sizes, n, ctypes.byref(spec), out_ptr, out_bytes,
+            _stream_handle(stream), int(bool(sync)), status, err, 1024,
+        )
+        if rc:
+            raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
+        return list(status)
+
+    def decode_batch_device(self, dev_ptr: int, dev_bytes: int, offsets, sizes, infos,
+                            out: Output, out_ptr: int, out_bytes: int, stream=None,
+                            sync: bool = True) -> list[int]:
+        n = len(offsets)
+        offs = (ctypes.c_int64 * n)(*offsets)
+        szs = (ctypes.c_int64 * n)(*sizes)
+        inf = (ImageInfo * n)(*infos)
+        status = (ctypes.c_int32 * n)()
+        err = ctypes.create_string_buffer(1024)
+        spec = out.to_c()
+        rc = lib().spdl_hj_decode_batch_device(
+            self._h, dev_ptr, dev_bytes, offs, szs, inf, n, ctypes.byref(spec), out_ptr,
+            out_bytes, _stream_handle(stream), int(bool(sync)), status, err, 1024,
+        )
+        if rc:
+            raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
+        return list(status)
+
+    def decode_planes(self, data, idct: str = "simple", stream=None):
+        import numpy as np
+
+        info = get_image_info(data)
+        hmax = max(info.h_samp[c] for c in range(info.ncomp))
+        vmax = max(info.v_samp[c] for c in range(info.ncomp))
+        planes = []
+        for c in range(info.ncomp):
+            if info.ncomp == 1:
+                w, h = info.width, info.height
+            else:
+                w = -(-info.width * info.h_samp[c] // hmax)
+                h = -(-info.height * info.v_samp[c] // vmax)
+            planes.append(np.zeros((h, w), np.uint8))
+        ptrs = (ctypes.c_void_p * 3)(*([p.ctypes.data for p in planes] + [None] * (3 - len(planes))))
+        mv = memoryview(data).cast("B")
+        b = (ctypes.c_char * len(mv)).from_buffer_copy(mv)
+        err = ctypes.create_string_buffer(1024)
+        rc = lib().spdl_hj_decode_planes(self._h, ctypes.addressof(b), len(mv), IDCT[idct],
+                                         ptrs, _stream_handle(stream), err, 1024)
+        if rc:
+            raise RuntimeError(err.value.decode())
+        return planes
+
+
+_TLS = threading.local()
+
+
+def thread_decoder(device_index: int) -> Decoder:
+    """The calling thread's decoder for `device_index` (created on first use)."""
+    d = getattr(_TLS, "decoders", None)
+    if d is None:
+        d = _TLS.decoders = {}
+    dec = d.get(device_index)
+    if dec is None:
+        dec = d[device_index] = Decoder(device_index)
+    return dec

@@ -1,0 +1,94 @@
+// hj_common.h -- layouts shared by the host driver and the gfx950 kernels.
+//
+// HBM layout of one batch (all offsets are per-image, computed on the host
+// from the SOF probe, so every buffer is a flat allocation reused across
+// batches):
+//   bytes   : packed JPEG files, each at a 256-B aligned offset
+//   clean   : destuffed entropy-coded bytes, same offsets as `bytes`
+//   segs    : restart-segment start offsets (bytes into clean), seg_cap each
+//   info    : ImageInfo (device parse result + status)
+//   luts    : HuffTable[8] per image (DC0..3, AC0..3)
+//   coefs   : int16 [nblocks][64] per image, natural order, MCU order
+//   planes  : u8 component planes padded to whole blocks
+//   weights : resize tables (first index + Q14 taps) per image/plane/axis
+#pragma once
+#include <stdint.h>
+
+namespace hj {
+
+constexpr int kMaxComp = 3;
+constexpr int kMaxBpm = 10;
+constexpr int kLutBits = 10;
+constexpr int kLutSize = 1 << kLutBits;
+constexpr int kDcBias = 1024;  // FFmpeg mjpegdec last_dc start value (4 << bits)
+constexpr int kMaxTaps = 128;
+
+// LUT entry (u32): [0:5) nbits consumed, [5:7) kind, [8:16) symbol,
+// [16:32) value (int16, kind==2 only)
+constexpr uint32_t kKindSlow = 0;  // code longer than kLutBits (or invalid)
+constexpr uint32_t kKindCode = 1;  // code resolved, value bits follow
+constexpr uint32_t kKindFull = 2;  // code + value resolved
+
+struct HuffTable {
+  uint32_t lut[kLutSize];
+  int32_t maxcode[18];  // max code of length l (-1 if none), [17] sentinel
+  int32_t valoff[17];
+  uint8_t vals[256];
+};
+
+struct ImageDesc {      // host-filled per image
+  int64_t in_off;       // offset into bytes/clean
+  int64_t in_size;
+  int64_t coef_off;     // in blocks
+  int64_t plane_off[kMaxComp];
+  int64_t seg_off;      // entries into segs
+  int64_t out_off;      // elements into the output
+  int64_t wt_off;       // entries into the weights pool (int32 units)
+  int32_t seg_cap;
+  int32_t width, height, ncomp;
+  int32_t h_samp[kMaxComp], v_samp[kMaxComp];
+  int32_t nblocks;
+  int32_t plane_stride[kMaxComp];
+  // resize geometry (host computed from the probe; device recomputes nothing)
+  int32_t sw, sh, dx, dy, ow, oh;
+  int32_t taps_x[kMaxComp], taps_y[kMaxComp];
+  int32_t pad_;
+};
+
+struct ImageInfo {      // device-filled by the parse kernel
+  int32_t status;
+  int32_t width, height, ncomp, hmax, vmax, mcux, mcuy, bpm, nblocks, ri;
+  int32_t scan_start;
+  int32_t comp_h[kMaxComp], comp_v[kMaxComp];
+  int32_t comp_bw[kMaxComp], comp_bh[kMaxComp];
+  int32_t comp_w[kMaxComp], comp_hpx[kMaxComp];
+  int32_t mcu_comp[kMaxBpm], mcu_dx[kMaxBpm], mcu_dy[kMaxBpm];
+  int32_t dc_tab[kMaxComp], ac_tab[kMaxComp];  // table slot 0..7
+  uint16_t qt[kMaxComp][64];                    // zig-zag order
+  int32_t nseg;         // restart segments found by destuff
+  int32_t clean_len;    // destuffed bytes
+  int32_t sync_rounds;  // diagnostics: rounds the Huffman sync took
+  int32_t pad_;
+};
+
+struct BatchParams {
+  int32_t n;
+  int32_t pix_fmt, dtype, idct;
+  int32_t resize, filter;
+  int32_t out_w, out_h;  // full-res mode: common size
+  int32_t sub_bits;      // Huffman subsequence size (bits, multiple of 32)
+  float mean[3], std[3];
+};
+
+enum Status {
+  kOk = 0,
+  kErrNotJpeg = 1,
+  kErrUnsupported = 2,
+  kErrBadHeader = 3,
+  kErrBadHuffman = 4,
+  kErrTruncated = 5,
+  kErrBadRestart = 6,
+  kErrBadGeometry = 7,
+};
+
+}  // namespace hj

@@ -1,0 +1,703 @@
+// hj_host.cpp -- host driver behind include/spdl_hipjpeg.h.
+//
+// Replaces src/libspdl/cuda/nvjpeg/decoding.cpp (decode_image_nvjpeg single
+// :157-202 and batch :204-255) and src/libspdl/cuda/npp/detail/resize.cpp.
+// Differences by design: the whole batch goes through one kernel
+// sequence instead of a per-image nvjpegDecode + 3x nppiResize loop; the
+// header probe replaces nvjpegGetImageInfo; bytes travel to HBM in one
+// hipMemcpyAsync from pinned staging.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/spdl_hipjpeg.h"
+#include "hj_common.h"
+
+namespace hj {
+hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageInfo*, HuffTable*, int, hipStream_t);
+hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, uint8_t*, uint32_t*, int,
+                          hipStream_t);
+hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
+                          const HuffTable*, int16_t*, int, int, hipStream_t);
+hipError_t launch_idct(const int16_t*, const ImageDesc*, const ImageInfo*, uint8_t*, int, int, int,
+                       hipStream_t);
+hipError_t launch_weights(const ImageDesc*, const ImageInfo*, int32_t*, int, int, int,
+                          hipStream_t);
+hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
+                      const BatchParams&, int64_t, int, hipStream_t);
+hipError_t launch_resize(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*, void*,
+                         const BatchParams&, int64_t, int, hipStream_t);
+}  // namespace hj
+
+using namespace hj;
+
+namespace {
+
+constexpr int kStages = 8;
+const char* kStageNames[kStages] = {"h2d",   "parse", "destuff", "entropy",
+                                    "idct",  "weights", "output", "d2h_status"};
+
+void set_err(char* err, size_t errlen, const char* fmt, ...) {
+  if (!err || !errlen) return;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(err, errlen, fmt, ap);
+  va_end(ap);
+}
+
+const char* status_str(int s) {
+  switch (s) {
+    case SPDL_HJ_OK: return "OK";
+    case SPDL_HJ_ERR_NOT_JPEG: return "not a JPEG";
+    case SPDL_HJ_ERR_UNSUPPORTED: return "unsupported JPEG (progressive, arithmetic, 12-bit, CMYK or multi-scan)";
+    case SPDL_HJ_ERR_BAD_HEADER: return "corrupt JPEG header";
+    case SPDL_HJ_ERR_BAD_HUFFMAN: return "corrupt entropy-coded data";
+    case SPDL_HJ_ERR_TRUNCATED: return "truncated entropy-coded data";
+    case SPDL_HJ_ERR_BAD_RESTART: return "restart marker mismatch";
+    case SPDL_HJ_ERR_BAD_GEOMETRY: return "invalid resize geometry";
+    case SPDL_HJ_ERR_INVALID_ARG: return "invalid argument";
+    case SPDL_HJ_ERR_HIP: return "HIP runtime error";
+    case SPDL_HJ_ERR_OOM: return "out of device memory";
+    default: return "unknown error";
+  }
+}
+
+inline int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n + n / 4 + 4096;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n + n / 4 + 4096;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// ---- host SOF probe (replaces nvjpegGetImageInfo) --------------------------
+int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
+  memset(info, 0, sizeof(*info));
+  if (!d || size < 4 || d[0] != 0xFF || d[1] != 0xD8) return SPDL_HJ_ERR_NOT_JPEG;
+  size_t pos = 2;
+  for (;;) {
+    while (pos < size && d[pos] != 0xFF) pos++;
+    while (pos < size && d[pos] == 0xFF) pos++;
+    if (pos >= size) return SPDL_HJ_ERR_BAD_HEADER;
+    int m = d[pos++];
+    if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+    if (m == 0xD9 || m == 0xDA) return SPDL_HJ_ERR_BAD_HEADER;  // no SOF before scan
+    if (pos + 2 > size) return SPDL_HJ_ERR_BAD_HEADER;
+    int len = (d[pos] << 8) | d[pos + 1];
+    if (len < 2 || pos + (size_t)len > size) return SPDL_HJ_ERR_BAD_HEADER;
+    const uint8_t* s = d + pos + 2;
+    pos += (size_t)len;
+    if (m == 0xC0 || m == 0xC1) {
+      if (len < 8) return SPDL_HJ_ERR_BAD_HEADER;
+      if (s[0] != 8) return SPDL_HJ_ERR_UNSUPPORTED;
+      info->height = (s[1] << 8) | s[2];
+      info->width = (s[3] << 8) | s[4];
+      info->ncomp = s[5];
+      if (info->height == 0) return SPDL_HJ_ERR_UNSUPPORTED;
+      if (info->width == 0) return SPDL_HJ_ERR_BAD_HEADER;
+      if (info->ncomp != 1 && info->ncomp != 3) return SPDL_HJ_ERR_UNSUPPORTED;
+      if (len < 8 + 3 * info->ncomp) return SPDL_HJ_ERR_BAD_HEADER;
+      for (int c = 0; c < info->ncomp; c++) {
+        info->h_samp[c] = s[7 + 3 * c] >> 4;
+        info->v_samp[c] = s[7 + 3 * c] & 15;
+        if (info->h_samp[c] < 1 || info->h_samp[c] > 4 || info->v_samp[c] < 1 ||
+            info->v_samp[c] > 4)
+          return SPDL_HJ_ERR_BAD_HEADER;
+      }
+      return SPDL_HJ_OK;
+    }
+    if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
+        (m >= 0xCD && m <= 0xCF))
+      return SPDL_HJ_ERR_UNSUPPORTED;
+  }
+}
+
+// ---- geometry (FFmpeg scale/pad/crop semantics; see oracle jo_geometry) ----
+int64_t rescale_rnd(int64_t a, int64_t b, int64_t c) { return (a * b + c / 2) / c; }
+
+struct Geom {
+  int sw, sh, dx, dy, ow, oh;
+};
+
+int geometry(int w, int h, const spdl_hj_output* o, Geom* g) {
+  if (w <= 0 || h <= 0) return SPDL_HJ_ERR_BAD_GEOMETRY;
+  if (!o->resize) {
+    *g = {w, h, 0, 0, w, h};
+    return SPDL_HJ_OK;
+  }
+  int64_t fw = o->fit_w > 0 ? o->fit_w : w, fh = o->fit_h > 0 ? o->fit_h : h;
+  int64_t sw = fw, sh = fh;
+  if (o->aspect != SPDL_HJ_ASPECT_NONE) {
+    int64_t tw = rescale_rnd(fh, w, h), th = rescale_rnd(fw, h, w);
+    if (o->aspect == SPDL_HJ_ASPECT_DECREASE) {
+      sw = tw < fw ? tw : fw;
+      sh = th < fh ? th : fh;
+    } else {
+      sw = tw > fw ? tw : fw;
+      sh = th > fh ? th : fh;
+    }
+  }
+  if (sw < 1) sw = 1;
+  if (sh < 1) sh = 1;
+  int64_t cw = sw, ch = sh, px = 0, py = 0;
+  if (o->pad_w > 0 && o->pad_h > 0) {
+    cw = o->pad_w;
+    ch = o->pad_h;
+    if (cw < sw || ch < sh) return SPDL_HJ_ERR_BAD_GEOMETRY;
+    px = (cw - sw) / 2;
+    py = (ch - sh) / 2;
+  }
+  int64_t ow = cw, oh = ch, cx = 0, cy = 0;
+  if (o->crop_w > 0 && o->crop_h > 0) {
+    ow = o->crop_w;
+    oh = o->crop_h;
+    if (ow > cw || oh > ch) return SPDL_HJ_ERR_BAD_GEOMETRY;
+    cx = (cw - ow) / 2;
+    cy = (ch - oh) / 2;
+  }
+  if (sw > 65535 || sh > 65535 || ow > 65535 || oh > 65535) return SPDL_HJ_ERR_BAD_GEOMETRY;
+  *g = {(int)sw, (int)sh, (int)(px - cx), (int)(py - cy), (int)ow, (int)oh};
+  return SPDL_HJ_OK;
+}
+
+int max_taps(int src_len, int dst_len, int filter) {
+  float scale = (float)src_len / (float)dst_len;
+  float fscale = scale > 1.0f ? scale : 1.0f;
+  float support = (filter == SPDL_HJ_FILTER_BILINEAR ? 1.0f : 2.0f) * fscale;
+  return (int)ceilf(2.0f * support) + 1;
+}
+
+struct Layout {
+  std::vector<ImageDesc> desc;
+  int64_t total_blocks = 0, total_planes = 0, total_segs = 0, total_wts = 0;
+  int64_t out_elems_per_image = 0;
+  int max_blocks = 0, max_len = 0;
+  int64_t max_px = 0;
+  int ow = 0, oh = 0;
+};
+
+int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_image_info* infos,
+                 int n, const spdl_hj_output* out, Layout& L, int32_t* status, char* err,
+                 size_t errlen) {
+  L.desc.assign(n, ImageDesc{});
+  for (int i = 0; i < n; i++) {
+    ImageDesc& d = L.desc[i];
+    const spdl_hj_image_info& p = infos[i];
+    d.in_off = offsets[i];
+    d.in_size = sizes[i];
+    d.width = p.width;
+    d.height = p.height;
+    d.ncomp = p.ncomp;
+    int hmax = 1, vmax = 1;
+    for (int c = 0; c < p.ncomp; c++) {
+      d.h_samp[c] = p.h_samp[c];
+      d.v_samp[c] = p.v_samp[c];
+      hmax = p.h_samp[c] > hmax ? p.h_samp[c] : hmax;
+      vmax = p.v_samp[c] > vmax ? p.v_samp[c] : vmax;
+    }
+    int bw[3] = {0, 0, 0}, bh[3] = {0, 0, 0}, cw[3] = {0, 0, 0}, chh[3] = {0, 0, 0};
+    int64_t nblocks;
+    if (p.ncomp == 1) {
+      cw[0] = p.width;
+      chh[0] = p.height;
+      bw[0] = (p.width + 7) / 8;
+      bh[0] = (p.height + 7) / 8;
+      nblocks = (int64_t)bw[0] * bh[0];
+    } else {
+      int mcux = (p.width + 8 * hmax - 1) / (8 * hmax), mcuy = (p.height + 8 * vmax - 1) / (8 * vmax);
+      int bpm = 0;
+      for (int c = 0; c < p.ncomp; c++) {
+        if (hmax % p.h_samp[c] || vmax % p.v_samp[c]) {
+          if (status) status[i] = SPDL_HJ_ERR_UNSUPPORTED;
+          set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i,
+                  status_str(SPDL_HJ_ERR_UNSUPPORTED));
+          return SPDL_HJ_ERR_UNSUPPORTED;
+        }
+        bw[c] = mcux * p.h_samp[c];
+        bh[c] = mcuy * p.v_samp[c];
+        cw[c] = (p.width * p.h_samp[c] + hmax - 1) / hmax;
+        chh[c] = (p.height * p.v_samp[c] + vmax - 1) / vmax;
+        bpm += p.h_samp[c] * p.v_samp[c];
+      }
+      if (bpm > kMaxBpm) {
+        if (status) status[i] = SPDL_HJ_ERR_UNSUPPORTED;
+        set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i,
+                status_str(SPDL_HJ_ERR_UNSUPPORTED));
+        return SPDL_HJ_ERR_UNSUPPORTED;
+      }
+      nblocks = (int64_t)mcux * mcuy * bpm;
+    }
+    if (nblocks > (1 << 30)) {
+      set_err(err, errlen, "image %d too large", i);
+      return SPDL_HJ_ERR_UNSUPPORTED;
+    }
+    d.nblocks = (int)nblocks;
+    d.coef_off = L.total_blocks;
+    L.total_blocks += nblocks;
+    if (d.nblocks > L.max_blocks) L.max_blocks = d.nblocks;
+    for (int c = 0; c < p.ncomp; c++) {
+      d.plane_stride[c] = bw[c] * 8;
+      d.plane_off[c] = L.total_planes;
+      L.total_planes += round_up((int64_t)bw[c] * 8 * bh[c] * 8, 256);
+    }
+    d.seg_cap = (int32_t)(sizes[i] / 2 + 2);
+    d.seg_off = L.total_segs;
+    L.total_segs += d.seg_cap;
+    Geom g;
+    int rc = geometry(p.width, p.height, out, &g);
+    if (rc) {
+      if (status) status[i] = rc;
+      set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, status_str(rc));
+      return rc;
+    }
+    d.sw = g.sw;
+    d.sh = g.sh;
+    d.dx = g.dx;
+    d.dy = g.dy;
+    d.ow = g.ow;
+    d.oh = g.oh;
+    if (i == 0) {
+      L.ow = g.ow;
+      L.oh = g.oh;
+    } else if (g.ow != L.ow || g.oh != L.oh) {
+      set_err(err, errlen,
+              "all images of a batch must produce the same output size "
+              "(image 0: %dx%d, image %d: %dx%d); pass a resize target",
+              L.ow, L.oh, i, g.ow, g.oh);
+      return SPDL_HJ_ERR_INVALID_ARG;
+    }
+    d.wt_off = L.total_wts;
+    if (out->resize) {
+      for (int c = 0; c < p.ncomp; c++) {
+        d.taps_x[c] = max_taps(cw[c], g.sw, out->filter);
+        d.taps_y[c] = max_taps(chh[c], g.sh, out->filter);
+        if (d.taps_x[c] > kMaxTaps || d.taps_y[c] > kMaxTaps) {
+          if (status) status[i] = SPDL_HJ_ERR_BAD_GEOMETRY;
+          set_err(err, errlen,
+                  "Failed to decode an image. (image %d: downscale factor too large: %dx%d -> "
+                  "%dx%d)",
+                  i, p.width, p.height, g.sw, g.sh);
+          return SPDL_HJ_ERR_BAD_GEOMETRY;
+        }
+        L.total_wts += (int64_t)g.sw * (1 + (d.taps_x[c] + 1) / 2) +
+                       (int64_t)g.sh * (1 + (d.taps_y[c] + 1) / 2);
+      }
+      int ml = g.sw > g.sh ? g.sw : g.sh;
+      if (ml > L.max_len) L.max_len = ml;
+    }
+    int64_t px = (int64_t)g.ow * g.oh;
+    if (px > L.max_px) L.max_px = px;
+  }
+  L.out_elems_per_image = (int64_t)L.ow * L.oh * 3;
+  for (int i = 0; i < n; i++) L.desc[i].out_off = (int64_t)i * L.out_elems_per_image;
+  return SPDL_HJ_OK;
+}
+
+}  // namespace
+
+struct spdl_hj_ctx {
+  int device = 0;
+  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts;
+  PinBuf pin_in, pin_desc, pin_status;
+  hipEvent_t staging_free = nullptr;  // host staging may be rewritten after this
+  hipEvent_t batch_done = nullptr;    // device workspace free after this
+  hipEvent_t ev[kStages + 1] = {};
+  bool profiling = false;
+  float timings[kStages] = {};
+  int ntimings = 0;
+  int sub_bits = 512;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+#define HJ_HIP(expr)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) {                                                              \
+      set_err(err, errlen, "HIP error %s at %s:%d (%s)", hipGetErrorString(e_), __FILE__, \
+              __LINE__, #expr);                                                          \
+      return e_ == hipErrorOutOfMemory ? SPDL_HJ_ERR_OOM : SPDL_HJ_ERR_HIP;             \
+    }                                                                                    \
+  } while (0)
+
+inline void mark(spdl_hj_ctx* c, int i, hipStream_t st) {
+  if (c->profiling) (void)hipEventRecord(c->ev[i], st);
+}
+
+// device pipeline over bytes already in HBM
+int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, const Layout& L,
+                 int n, const spdl_hj_output* out, void* out_dev, size_t out_bytes,
+                 hipStream_t st, int sync, int32_t* status, char* err, size_t errlen,
+                 bool planes_only) {
+  const size_t esz = out->dtype == SPDL_HJ_DTYPE_F16 ? 2 : 1;
+  if (!planes_only && (size_t)L.out_elems_per_image * n * esz > out_bytes) {
+    set_err(err, errlen, "output buffer too small: need %lld bytes, have %zu",
+            (long long)(L.out_elems_per_image * n * esz), out_bytes);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  int64_t max_end = 0;
+  for (int i = 0; i < n; i++) {
+    if (L.desc[i].in_off % 256) {
+      set_err(err, errlen, "image %d offset %lld is not 256-byte aligned", i,
+              (long long)L.desc[i].in_off);
+      return SPDL_HJ_ERR_INVALID_ARG;
+    }
+    int64_t e = L.desc[i].in_off + L.desc[i].in_size;
+    if ((size_t)e > bytes_len) {
+      set_err(err, errlen, "image %d extends past the input buffer", i);
+      return SPDL_HJ_ERR_INVALID_ARG;
+    }
+    if (e > max_end) max_end = e;
+  }
+  // the previous batch may still be using the workspace (async call)
+  HJ_HIP(hipStreamWaitEvent(st, ctx->batch_done, 0));
+  HJ_HIP(ctx->clean.ensure((size_t)max_end + 512));
+  HJ_HIP(ctx->segs.ensure((size_t)L.total_segs * 4 + 64));
+  HJ_HIP(ctx->desc.ensure(sizeof(ImageDesc) * n));
+  HJ_HIP(ctx->info.ensure(sizeof(ImageInfo) * n));
+  HJ_HIP(ctx->luts.ensure(sizeof(HuffTable) * 8 * n));
+  HJ_HIP(ctx->coefs.ensure((size_t)L.total_blocks * 128 + 256));
+  HJ_HIP(ctx->planes.ensure((size_t)L.total_planes + 256));
+  if (out->resize) HJ_HIP(ctx->wts.ensure((size_t)L.total_wts * 4 + 256));
+  HJ_HIP(ctx->pin_desc.ensure(sizeof(ImageDesc) * n));
+  HJ_HIP(ctx->pin_status.ensure(sizeof(int32_t) * n));
+  HJ_HIP(hipEventSynchronize(ctx->staging_free));
+  memcpy(ctx->pin_desc.p, L.desc.data(), sizeof(ImageDesc) * n);
+  HJ_HIP(hipMemcpyAsync(ctx->desc.p, ctx->pin_desc.p, sizeof(ImageDesc) * n,
+                        hipMemcpyHostToDevice, st));
+  HJ_HIP(hipMemsetAsync(ctx->coefs.p, 0, (size_t)L.total_blocks * 128, st));
+  mark(ctx, 1, st);
+  auto* desc = static_cast<const ImageDesc*>(ctx->desc.p);
+  auto* infos = static_cast<ImageInfo*>(ctx->info.p);
+  HJ_HIP(launch_parse(d_bytes, desc, infos, static_cast<HuffTable*>(ctx->luts.p), n, st));
+  mark(ctx, 2, st);
+  HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<uint8_t*>(ctx->clean.p),
+                        static_cast<uint32_t*>(ctx->segs.p), n, st));
+  mark(ctx, 3, st);
+  HJ_HIP(launch_entropy(static_cast<const uint8_t*>(ctx->clean.p),
+                        static_cast<const uint32_t*>(ctx->segs.p), desc, infos,
+                        static_cast<const HuffTable*>(ctx->luts.p),
+                        static_cast<int16_t*>(ctx->coefs.p), ctx->sub_bits, n, st));
+  mark(ctx, 4, st);
+  HJ_HIP(launch_idct(static_cast<const int16_t*>(ctx->coefs.p), desc, infos,
+                     static_cast<uint8_t*>(ctx->planes.p), out->idct, L.max_blocks, n, st));
+  mark(ctx, 5, st);
+  BatchParams bp{};
+  bp.n = n;
+  bp.pix_fmt = out->pix_fmt;
+  bp.dtype = out->dtype;
+  bp.idct = out->idct;
+  bp.resize = out->resize;
+  bp.filter = out->filter;
+  bp.out_w = L.ow;
+  bp.out_h = L.oh;
+  bp.sub_bits = ctx->sub_bits;
+  for (int c = 0; c < 3; c++) {
+    bp.mean[c] = out->mean[c];
+    bp.std[c] = out->std[c];
+  }
+  if (!planes_only) {
+    if (out->resize) {
+      HJ_HIP(launch_weights(desc, infos, static_cast<int32_t*>(ctx->wts.p), out->filter, L.max_len,
+                            n, st));
+      mark(ctx, 6, st);
+      HJ_HIP(launch_resize(static_cast<const uint8_t*>(ctx->planes.p), desc, infos,
+                           static_cast<const int32_t*>(ctx->wts.p), out_dev, bp, L.max_px, n, st));
+    } else {
+      mark(ctx, 6, st);
+      HJ_HIP(launch_csc(static_cast<const uint8_t*>(ctx->planes.p), desc, infos, out_dev, bp,
+                        L.max_px, n, st));
+    }
+  } else {
+    mark(ctx, 6, st);
+  }
+  mark(ctx, 7, st);
+  // per-image status: strided D2H of ImageInfo::status
+  HJ_HIP(hipMemcpy2DAsync(ctx->pin_status.p, sizeof(int32_t), ctx->info.p, sizeof(ImageInfo),
+                          sizeof(int32_t), n, hipMemcpyDeviceToHost, st));
+  mark(ctx, 8, st);
+  HJ_HIP(hipEventRecord(ctx->batch_done, st));
+  HJ_HIP(hipEventRecord(ctx->staging_free, st));
+  if (!sync) return SPDL_HJ_OK;
+  HJ_HIP(hipStreamSynchronize(st));
+  if (ctx->profiling) {
+    ctx->ntimings = kStages;
+    for (int i = 0; i < kStages; i++) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) != hipSuccess) ms = -1.f;
+      ctx->timings[i] = ms * 1000.f;
+    }
+  }
+  const int32_t* stv = static_cast<const int32_t*>(ctx->pin_status.p);
+  int first_bad = -1;
+  for (int i = 0; i < n; i++) {
+    if (status) status[i] = stv[i];
+    if (stv[i] != SPDL_HJ_OK && first_bad < 0) first_bad = i;
+  }
+  if (first_bad >= 0) {
+    set_err(err, errlen, "Failed to decode an image. (image %d: %s)", first_bad,
+            status_str(stv[first_bad]));
+    return stv[first_bad];
+  }
+  return SPDL_HJ_OK;
+}
+
+bool valid_output(const spdl_hj_output* o) {
+  return o && o->pix_fmt >= 0 && o->pix_fmt <= 3 && (o->dtype == 0 || o->dtype == 1) &&
+         (o->idct == 0 || o->idct == 1) && (o->filter == 0 || o->filter == 1) &&
+         o->aspect >= 0 && o->aspect <= 2;
+}
+
+}  // namespace
+
+extern "C" {
+
+int spdl_hj_abi_version(void) { return SPDL_HJ_ABI_VERSION; }
+
+int spdl_hj_get_image_info(const uint8_t* data, size_t size, spdl_hj_image_info* info) {
+  if (!info) return SPDL_HJ_ERR_INVALID_ARG;
+  return probe(data, size, info);
+}
+
+int spdl_hj_output_size(int32_t w, int32_t h, const spdl_hj_output* out, int32_t* out_w,
+                        int32_t* out_h) {
+  if (!valid_output(out) || !out_w || !out_h) return SPDL_HJ_ERR_INVALID_ARG;
+  Geom g;
+  int rc = geometry(w, h, out, &g);
+  if (rc) return rc;
+  *out_w = g.ow;
+  *out_h = g.oh;
+  return SPDL_HJ_OK;
+}
+
+spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) {
+    set_err(err, errlen, "no HIP device available (%s)", hipGetErrorString(e));
+    return nullptr;
+  }
+  if (device < 0 || device >= count) {
+    set_err(err, errlen, "device index %d out of range (%d devices)", device, count);
+    return nullptr;
+  }
+  DeviceGuard g(device);
+  auto* c = new spdl_hj_ctx();
+  c->device = device;
+  bool ok = hipEventCreateWithFlags(&c->staging_free, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->batch_done, hipEventDisableTiming) == hipSuccess;
+  for (int i = 0; ok && i <= kStages; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+  if (!ok) {
+    set_err(err, errlen, "hipEventCreate failed");
+    spdl_hj_destroy(c);
+    return nullptr;
+  }
+  return c;
+}
+
+void spdl_hj_destroy(spdl_hj_ctx* c) {
+  if (!c) return;
+  DeviceGuard g(c->device);
+  if (c->batch_done) (void)hipEventSynchronize(c->batch_done);
+  DevBuf* bufs[] = {&c->bytes, &c->clean, &c->segs, &c->desc, &c->info,
+                    &c->luts,  &c->coefs, &c->planes, &c->wts};
+  for (DevBuf* b : bufs) b->release();
+  c->pin_in.release();
+  c->pin_desc.release();
+  c->pin_status.release();
+  if (c->staging_free) (void)hipEventDestroy(c->staging_free);
+  if (c->batch_done) (void)hipEventDestroy(c->batch_done);
+  for (int i = 0; i <= kStages; i++)
+    if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  delete c;
+}
+
+int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const size_t* sizes,
+                         int32_t n, const spdl_hj_output* out, void* out_dev, size_t out_bytes,
+                         void* stream, int32_t sync, int32_t* status, char* err, size_t errlen) {
+  if (!ctx || !data || !sizes || n <= 0 || !valid_output(out) || !out_dev) {
+    set_err(err, errlen, n <= 0 ? "the batch is empty" : "invalid argument");
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(ctx->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  std::vector<spdl_hj_image_info> infos(n);
+  std::vector<int64_t> offs(n), szs(n);
+  int64_t total = 0;
+  for (int i = 0; i < n; i++) {
+    int rc = probe(data[i], sizes[i], &infos[i]);
+    if (status) status[i] = rc;
+    if (rc) {
+      set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, status_str(rc));
+      return rc;
+    }
+    offs[i] = total;
+    szs[i] = (int64_t)sizes[i];
+    total += round_up((int64_t)sizes[i] + 64, 256);
+  }
+  Layout L;
+  int rc = build_layout(offs.data(), szs.data(), infos.data(), n, out, L, status, err, errlen);
+  if (rc) return rc;
+  HJ_HIP(ctx->pin_in.ensure((size_t)total));
+  HJ_HIP(ctx->bytes.ensure((size_t)total));
+  HJ_HIP(hipStreamWaitEvent(st, ctx->batch_done, 0));
+  HJ_HIP(hipEventSynchronize(ctx->staging_free));
+  auto* pin = static_cast<uint8_t*>(ctx->pin_in.p);
+  for (int i = 0; i < n; i++) {
+    memcpy(pin + offs[i], data[i], sizes[i]);
+    memset(pin + offs[i] + sizes[i], 0, (size_t)(round_up((int64_t)sizes[i] + 64, 256) - (int64_t)sizes[i]));
+  }
+  mark(ctx, 0, st);
+  HJ_HIP(hipMemcpyAsync(ctx->bytes.p, pin, (size_t)total, hipMemcpyHostToDevice, st));
+  return run_pipeline(ctx, static_cast<const uint8_t*>(ctx->bytes.p), (size_t)total, L, n, out,
+                      out_dev, out_bytes, st, sync, status, err, errlen, false);
+}
+
+int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_t dev_bytes,
+                                const int64_t* offsets, const int64_t* sizes,
+                                const spdl_hj_image_info* infos, int32_t n,
+                                const spdl_hj_output* out, void* out_dev, size_t out_bytes,
+                                void* stream, int32_t sync, int32_t* status, char* err,
+                                size_t errlen) {
+  if (!ctx || !dev_data || !offsets || !sizes || !infos || n <= 0 || !valid_output(out) ||
+      !out_dev) {
+    set_err(err, errlen, n <= 0 ? "the batch is empty" : "invalid argument");
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(ctx->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Layout L;
+  int rc = build_layout(offsets, sizes, infos, n, out, L, status, err, errlen);
+  if (rc) return rc;
+  mark(ctx, 0, st);
+  return run_pipeline(ctx, dev_data, dev_bytes, L, n, out, out_dev, out_bytes, st, sync, status,
+                      err, errlen, false);
+}
+
+int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, int32_t idct,
+                          uint8_t* const* planes, void* stream, char* err, size_t errlen) {
+  if (!ctx || !data || !planes || (idct != 0 && idct != 1)) {
+    set_err(err, errlen, "invalid argument");
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(ctx->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  spdl_hj_image_info info;
+  int rc = probe(data, size, &info);
+  if (rc) {
+    set_err(err, errlen, "Failed to decode an image. (%s)", status_str(rc));
+    return rc;
+  }
+  spdl_hj_output o{};
+  o.idct = idct;
+  int64_t off = 0, sz = (int64_t)size, total = round_up(sz + 64, 256);
+  Layout L;
+  rc = build_layout(&off, &sz, &info, 1, &o, L, nullptr, err, errlen);
+  if (rc) return rc;
+  HJ_HIP(ctx->pin_in.ensure((size_t)total));
+  HJ_HIP(ctx->bytes.ensure((size_t)total));
+  HJ_HIP(hipStreamWaitEvent(st, ctx->batch_done, 0));
+  HJ_HIP(hipEventSynchronize(ctx->staging_free));
+  memcpy(ctx->pin_in.p, data, size);
+  memset(static_cast<uint8_t*>(ctx->pin_in.p) + size, 0, (size_t)(total - sz));
+  HJ_HIP(hipMemcpyAsync(ctx->bytes.p, ctx->pin_in.p, (size_t)total, hipMemcpyHostToDevice, st));
+  rc = run_pipeline(ctx, static_cast<const uint8_t*>(ctx->bytes.p), (size_t)total, L, 1, &o,
+                    nullptr, 0, st, 1, nullptr, err, errlen, true);
+  if (rc) return rc;
+  const ImageDesc& d = L.desc[0];
+  int hmax = 1, vmax = 1;
+  for (int c = 0; c < info.ncomp; c++) {
+    hmax = info.h_samp[c] > hmax ? info.h_samp[c] : hmax;
+    vmax = info.v_samp[c] > vmax ? info.v_samp[c] : vmax;
+  }
+  for (int c = 0; c < info.ncomp; c++) {
+    int w = info.ncomp == 1 ? info.width : (info.width * info.h_samp[c] + hmax - 1) / hmax;
+    int h = info.ncomp == 1 ? info.height : (info.height * info.v_samp[c] + vmax - 1) / vmax;
+    HJ_HIP(hipMemcpy2DAsync(planes[c], (size_t)w,
+                            static_cast<const uint8_t*>(ctx->planes.p) + d.plane_off[c],
+                            (size_t)d.plane_stride[c], (size_t)w, (size_t)h,
+                            hipMemcpyDeviceToHost, st));
+  }
+  HJ_HIP(hipStreamSynchronize(st));
+  return SPDL_HJ_OK;
+}
+
+int spdl_hj_set_profiling(spdl_hj_ctx* ctx, int32_t enable) {
+  if (!ctx) return SPDL_HJ_ERR_INVALID_ARG;
+  ctx->profiling = enable != 0;
+  return SPDL_HJ_OK;
+}
+
+int spdl_hj_last_timings(spdl_hj_ctx* ctx, float* us, int32_t cap, int32_t* n_out) {
+  if (!ctx || !us || !n_out) return SPDL_HJ_ERR_INVALID_ARG;
+  int k = ctx->ntimings < cap ? ctx->ntimings : cap;
+  for (int i = 0; i < k; i++) us[i] = ctx->timings[i];
+  *n_out = k;
+  return SPDL_HJ_OK;
+}
+
+const char* spdl_hj_stage_name(int32_t i) {
+  return (i >= 0 && i < kStages) ? kStageNames[i] : "";
+}
+
+int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
+  if (!ctx || !name) return SPDL_HJ_ERR_INVALID_ARG;
+  if (!strcmp(name, "sub_bits")) {
+    if (value < 32 || value > (1 << 24) || value % 32) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->sub_bits = (int)value;
+    return SPDL_HJ_OK;
+  }
+  return SPDL_HJ_ERR_INVALID_ARG;
+}
+
+}  // extern "C"

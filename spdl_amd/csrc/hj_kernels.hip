@@ -1,0 +1,1399 @@
+// hj_kernels.hip -- gfx950 kernels of the JPEG -> RGB decode stage.
+//
+// Pipeline (one launch each, all on the caller's stream):
+//   parse_kernel    one workgroup per image: marker walk (T.81 B.2) and the
+//                   10-bit Huffman lookup tables (code+value fused entries).
+//   destuff_kernel  one workgroup per image: removes 0xFF00 stuffing, splits
+//                   restart segments (RSTn), block-wide prefix sums.
+//   entropy_kernel  one workgroup per image: self-synchronising parallel
+//                   Huffman decode.  The segment bitstream is cut into
+//                   subsequences ("slots"); each thread owns a contiguous run
+//                   of slots, decodes it from a guessed state, and runs are
+//                   re-decoded from their left neighbour's end state until
+//                   every slot start state is consistent (slot boundaries are
+//                   checkpoints: a re-decode stops where it merges with the
+//                   previous trajectory).  A segmented prefix sum over runs
+//                   then gives every run its absolute block index and DC
+//                   predictors, and a final pass writes dequantised
+//                   coefficients.
+//   idct_kernel     8x8 IDCT (FFmpeg simple_idct or IJG islow), block -> plane.
+//   weights_kernel  per-image resampling tables (Q14), resize mode only.
+//   csc_kernel / resize_kernel   planes -> RGB (nearest chroma, JFIF integer
+//                   colour conversion), resize/pad/crop, optional
+//                   (x/255-mean)/std -> fp16, planar or interleaved.
+//
+// Semantics follow oracle/jpeg_oracle.c line for line (the CPU restatement of
+// SPDL's FFmpeg path); the two are compared bit-exactly by tests/.
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include "hj_common.h"
+
+namespace hj {
+
+__constant__ uint8_t kNat[80] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33,
+    40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36,
+    29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
+    47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+// ---------------------------------------------------------------------------
+// parse_kernel
+// ---------------------------------------------------------------------------
+
+struct ParseScratch {
+  ImageInfo info;
+  uint16_t qt[4][64];
+  uint8_t bits[8][17];   // 0..3 DC, 4..7 AC
+  uint8_t vals[8][256];
+  int32_t have[8];
+  int32_t qhave[4];
+  int32_t maxcode[8][18];
+  int32_t valoff[8][17];
+};
+
+__device__ static int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
+
+__device__ static int parse_headers(const uint8_t* d, int size, ParseScratch& s) {
+  ImageInfo& in = s.info;
+  if (size < 4 || d[0] != 0xFF || d[1] != 0xD8) return kErrNotJpeg;
+  int have_sof = 0;
+  int comp_id[kMaxComp] = {0, 0, 0};
+  int comp_tq[kMaxComp] = {0, 0, 0};
+  int pos = 2;
+  for (;;) {
+    while (pos < size && d[pos] != 0xFF) pos++;
+    while (pos < size && d[pos] == 0xFF) pos++;
+    if (pos >= size) return kErrBadHeader;
+    int m = d[pos++];
+    if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+    if (m == 0xD9) return kErrBadHeader;
+    if (pos + 2 > size) return kErrBadHeader;
+    int len = be16(d + pos);
+    if (len < 2 || pos + len > size) return kErrBadHeader;
+    const uint8_t* p = d + pos + 2;
+    int n = len - 2;
+    pos += len;
+    if (m == 0xDB) {
+      while (n > 0) {
+        int pq = p[0] >> 4, tq = p[0] & 15;
+        if (tq > 3 || pq > 1) return kErrBadHeader;
+        int need = 1 + 64 * (pq + 1);
+        if (n < need) return kErrBadHeader;
+        for (int i = 0; i < 64; i++) s.qt[tq][i] = pq ? (uint16_t)be16(p + 1 + 2 * i) : p[1 + i];
+        s.qhave[tq] = 1;
+        p += need;
+        n -= need;
+      }
+    } else if (m == 0xC4) {
+      while (n > 0) {
+        if (n < 17) return kErrBadHeader;
+        int tc = p[0] >> 4, th = p[0] & 15;
+        if (tc > 1 || th > 3) return kErrBadHeader;
+        int slot = tc * 4 + th, total = 0, code = 0;
+        s.bits[slot][0] = 0;
+        for (int l = 1; l <= 16; l++) {
+          s.bits[slot][l] = p[l];
+          total += p[l];
+          code += p[l];
+          if (code > (1 << l)) return kErrBadHeader;
+          code <<= 1;
+        }
+        if (total > 256 || n < 17 + total) return kErrBadHeader;
+        for (int i = 0; i < 256; i++) s.vals[slot][i] = i < total ? p[17 + i] : 0;
+        s.have[slot] = 1;
+        p += 17 + total;
+        n -= 17 + total;
+      }
+    } else if (m == 0xC0 || m == 0xC1) {
+      if (n < 6) return kErrBadHeader;
+      if (p[0] != 8) return kErrUnsupported;
+      in.height = be16(p + 1);
+      in.width = be16(p + 3);
+      int nf = p[5];
+      if (in.height == 0) return kErrUnsupported;
+      if (in.width == 0) return kErrBadHeader;
+      if (nf != 1 && nf != 3) return kErrUnsupported;
+      if (n < 6 + 3 * nf) return kErrBadHeader;
+      in.ncomp = nf;
+      for (int c = 0; c < nf; c++) {
+        comp_id[c] = p[6 + 3 * c];
+        in.comp_h[c] = p[7 + 3 * c] >> 4;
+        in.comp_v[c] = p[7 + 3 * c] & 15;
+        comp_tq[c] = p[8 + 3 * c];
+        if (in.comp_h[c] < 1 || in.comp_h[c] > 4 || in.comp_v[c] < 1 || in.comp_v[c] > 4 ||
+            comp_tq[c] > 3)
+          return kErrBadHeader;
+      }
+      have_sof = 1;
+    } else if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) ||
+               (m >= 0xC9 && m <= 0xCB) || (m >= 0xCD && m <= 0xCF)) {
+      return kErrUnsupported;
+    } else if (m == 0xDD) {
+      if (n < 2) return kErrBadHeader;
+      in.ri = be16(p);
+    } else if (m == 0xDA) {
+      if (!have_sof) return kErrBadHeader;
+      int ns = p[0];
+      if (ns != in.ncomp) return kErrUnsupported;
+      if (n < 1 + 2 * ns + 3) return kErrBadHeader;
+      int order[kMaxComp] = {0, 0, 0};
+      for (int i = 0; i < ns; i++) {
+        int cs = p[1 + 2 * i], c = -1;
+        for (int k = 0; k < in.ncomp; k++)
+          if (comp_id[k] == cs) c = k;
+        if (c < 0) return kErrBadHeader;
+        order[i] = c;
+        in.dc_tab[c] = p[2 + 2 * i] >> 4;
+        in.ac_tab[c] = p[2 + 2 * i] & 15;
+        if (in.dc_tab[c] > 3 || in.ac_tab[c] > 3) return kErrBadHeader;
+      }
+      int ss = p[1 + 2 * ns], se = p[2 + 2 * ns], ahal = p[3 + 2 * ns];
+      if (ss != 0 || se != 63 || ahal != 0) return kErrUnsupported;
+      in.scan_start = pos;
+      int hmax = 1, vmax = 1;
+      for (int c = 0; c < in.ncomp; c++) {
+        hmax = max(hmax, in.comp_h[c]);
+        vmax = max(vmax, in.comp_v[c]);
+      }
+      in.hmax = hmax;
+      in.vmax = vmax;
+      for (int c = 0; c < in.ncomp; c++) {
+        if (hmax % in.comp_h[c] || vmax % in.comp_v[c]) return kErrUnsupported;
+        if (!s.qhave[comp_tq[c]] || !s.have[in.dc_tab[c]] || !s.have[4 + in.ac_tab[c]])
+          return kErrBadHeader;
+        in.comp_w[c] = (in.width * in.comp_h[c] + hmax - 1) / hmax;
+        in.comp_hpx[c] = (in.height * in.comp_v[c] + vmax - 1) / vmax;
+        for (int i = 0; i < 64; i++) in.qt[c][i] = s.qt[comp_tq[c]][i];
+      }
+      if (in.ncomp == 1) {
+        in.comp_bw[0] = (in.comp_w[0] + 7) / 8;
+        in.comp_bh[0] = (in.comp_hpx[0] + 7) / 8;
+        in.mcux = in.comp_bw[0];
+        in.mcuy = in.comp_bh[0];
+        in.bpm = 1;
+        in.mcu_comp[0] = 0;
+        in.mcu_dx[0] = in.mcu_dy[0] = 0;
+      } else {
+        in.mcux = (in.width + 8 * hmax - 1) / (8 * hmax);
+        in.mcuy = (in.height + 8 * vmax - 1) / (8 * vmax);
+        int b = 0;
+        for (int i = 0; i < ns; i++) {
+          int c = order[i];
+          in.comp_bw[c] = in.mcux * in.comp_h[c];
+          in.comp_bh[c] = in.mcuy * in.comp_v[c];
+          for (int y = 0; y < in.comp_v[c]; y++)
+            for (int x = 0; x < in.comp_h[c]; x++) {
+              if (b >= kMaxBpm) return kErrUnsupported;
+              in.mcu_comp[b] = c;
+              in.mcu_dx[b] = x;
+              in.mcu_dy[b] = y;
+              b++;
+            }
+        }
+        in.bpm = b;
+      }
+      in.nblocks = in.mcux * in.mcuy * in.bpm;
+      return kOk;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) parse_kernel(const uint8_t* __restrict__ bytes,
+                                                    const ImageDesc* __restrict__ desc,
+                                                    ImageInfo* __restrict__ infos,
+                                                    HuffTable* __restrict__ luts) {
+  __shared__ ParseScratch s;
+  __shared__ int st;
+  const int img = blockIdx.x, tid = threadIdx.x;
+  const ImageDesc dd = desc[img];
+  {
+    int* z = reinterpret_cast<int*>(&s);
+    for (int i = tid; i < (int)(sizeof(ParseScratch) / 4); i += blockDim.x) z[i] = 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int rc = parse_headers(bytes + dd.in_off, (int)dd.in_size, s);
+    if (rc == kOk) {
+      // the host probe sized every buffer; it must agree with the device parse
+      if (s.info.width != dd.width || s.info.height != dd.height || s.info.ncomp != dd.ncomp ||
+          s.info.nblocks != dd.nblocks)
+        rc = kErrBadHeader;
+      for (int c = 0; c < s.info.ncomp && rc == kOk; c++)
+        if (s.info.comp_h[c] != dd.h_samp[c] || s.info.comp_v[c] != dd.v_samp[c])
+          rc = kErrBadHeader;
+      if (rc == kOk && s.info.ri > 0 &&
+          (s.info.mcux * s.info.mcuy + s.info.ri - 1) / s.info.ri > dd.seg_cap)
+        rc = kErrBadRestart;
+    }
+    s.info.status = rc;
+    // canonical-code decode arrays (T.81 F.2.2.3 / libjpeg jdhuff.c)
+    for (int t = 0; t < 8 && rc == kOk; t++) {
+      if (!s.have[t]) continue;
+      int code = 0, k = 0;
+      for (int l = 1; l <= 16; l++) {
+        if (s.bits[t][l]) {
+          s.valoff[t][l] = k - code;
+          code += s.bits[t][l];
+          k += s.bits[t][l];
+          s.maxcode[t][l] = code - 1;
+        } else {
+          s.maxcode[t][l] = -1;
+          s.valoff[t][l] = 0;
+        }
+        code <<= 1;
+      }
+      s.maxcode[t][17] = 0x7FFFFFFF;
+    }
+    st = rc;
+  }
+  __syncthreads();
+  if (st != kOk) {
+    if (tid == 0) infos[img] = s.info;
+    return;
+  }
+  HuffTable* tabs = luts + (size_t)img * 8;
+  for (int t = 0; t < 8; t++) {
+    if (!s.have[t]) continue;
+    const bool is_dc = t < 4;
+    for (int idx = tid; idx < kLutSize; idx += blockDim.x) {
+      uint32_t e = 0;  // kKindSlow
+      for (int l = 1; l <= kLutBits; l++) {
+        int code = idx >> (kLutBits - l);
+        if (code <= s.maxcode[t][l]) {
+          int sym = s.vals[t][s.valoff[t][l] + code];
+          int sz = is_dc ? sym : (sym & 15);
+          if (is_dc && sym > 15) {
+            e = (uint32_t)l | (kKindCode << 5) | ((uint32_t)sym << 8);
+          } else if (l + sz <= kLutBits) {
+            int v = 0;
+            if (sz) {
+              int raw = (idx >> (kLutBits - l - sz)) & ((1 << sz) - 1);
+              v = raw < (1 << (sz - 1)) ? raw - ((1 << sz) - 1) : raw;
+            }
+            e = (uint32_t)(l + sz) | (kKindFull << 5) | ((uint32_t)sym << 8) |
+                ((uint32_t)(uint16_t)(int16_t)v << 16);
+          } else {
+            e = (uint32_t)l | (kKindCode << 5) | ((uint32_t)sym << 8);
+          }
+          break;
+        }
+      }
+      tabs[t].lut[idx] = e;
+    }
+    for (int i = tid; i < 18; i += blockDim.x) tabs[t].maxcode[i] = s.maxcode[t][i];
+    for (int i = tid; i < 17; i += blockDim.x) tabs[t].valoff[i] = s.valoff[t][i];
+    for (int i = tid; i < 256; i += blockDim.x) tabs[t].vals[i] = s.vals[t][i];
+  }
+  if (tid == 0) infos[img] = s.info;
+}
+
+// ---------------------------------------------------------------------------
+// destuff_kernel
+// ---------------------------------------------------------------------------
+
+constexpr int kDsThreads = 256;
+constexpr int kDsPer = 16;
+constexpr int kDsTile = kDsThreads * kDsPer;
+
+// block-wide exclusive scan of two counters (keep bytes, RST markers)
+__device__ static void block_scan2(int a, int b, int& ea, int& eb, int& ta, int& tb, int* sa,
+                                   int* sb) {
+  const int tid = threadIdx.x;
+  sa[tid] = a;
+  sb[tid] = b;
+  __syncthreads();
+  for (int off = 1; off < kDsThreads; off <<= 1) {
+    int va = tid >= off ? sa[tid - off] : 0, vb = tid >= off ? sb[tid - off] : 0;
+    __syncthreads();
+    sa[tid] += va;
+    sb[tid] += vb;
+    __syncthreads();
+  }
+  ea = sa[tid] - a;
+  eb = sb[tid] - b;
+  ta = sa[kDsThreads - 1];
+  tb = sb[kDsThreads - 1];
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kDsThreads) destuff_kernel(const uint8_t* __restrict__ bytes,
+                                                             const ImageDesc* __restrict__ desc,
+                                                             ImageInfo* __restrict__ infos,
+                                                             uint8_t* __restrict__ clean,
+                                                             uint32_t* __restrict__ segs) {
+  __shared__ int sa[kDsThreads], sb[kDsThreads];
+  __shared__ int term;
+  const int img = blockIdx.x, tid = threadIdx.x;
+  if (infos[img].status != kOk) return;
+  const ImageDesc dd = desc[img];
+  const uint8_t* d = bytes + dd.in_off;
+  const int size = (int)dd.in_size;
+  const int start = infos[img].scan_start;
+  uint8_t* out = clean + dd.in_off;
+  uint32_t* sg = segs + dd.seg_off;
+  int carry_keep = 0, carry_rst = 0;
+  bool overflow = false;
+  if (tid == 0) sg[0] = 0;
+  for (int base = start;; base += kDsTile) {
+    if (tid == 0) term = 0x7FFFFFFF;
+    __syncthreads();
+    const int j0 = base + tid * kDsPer;
+    // pass 1: find the first terminating marker in the tile
+    for (int j = j0; j < j0 + kDsPer && j < size; j++) {
+      if (d[j] != 0xFF) continue;
+      if (j > start && d[j - 1] == 0xFF) continue;  // fill byte of a marker run
+      if (j + 1 < size && d[j + 1] == 0x00) continue; // stuffed data 0xFF
+      int k = j + 1;
+      while (k < size && d[k] == 0xFF) k++;
+      if (!(k < size && d[k] >= 0xD0 && d[k] <= 0xD7)) {
+        atomicMin(&term, j);
+        break;
+      }
+    }
+    if (tid == 0 && base + kDsTile >= size) atomicMin(&term, size);
+    __syncthreads();
+    const int lim = term;
+    // pass 2: counts
+    int keep = 0, rst = 0;
+    for (int j = j0; j < j0 + kDsPer && j < lim; j++) {
+      const int c = d[j];
+      const bool prev_ff = j > start && d[j - 1] == 0xFF;
+      if (c != 0xFF) {
+        keep += !prev_ff;
+      } else if (!prev_ff) {
+        if (j + 1 < size && d[j + 1] == 0x00) keep++;
+        else rst++;  // before `lim`, a marker start is always RSTn
+      }
+    }
+    int ek, er, tk, tr;
+    block_scan2(keep, rst, ek, er, tk, tr, sa, sb);
+    // pass 3: scatter
+    int o = carry_keep + ek, r = carry_rst + er;
+    for (int j = j0; j < j0 + kDsPer && j < lim; j++) {
+      const int c = d[j];
+      const bool prev_ff = j > start && d[j - 1] == 0xFF;
+      if (c != 0xFF) {
+        if (!prev_ff) out[o++] = (uint8_t)c;
+      } else if (!prev_ff) {
+        if (j + 1 < size && d[j + 1] == 0x00) {
+          out[o++] = 0xFF;
+        } else {
+          r++;
+          if (r < dd.seg_cap) sg[r] = (uint32_t)o;
+          else overflow = true;
+        }
+      }
+    }
+    carry_keep += tk;
+    carry_rst += tr;
+    if (lim < base + kDsTile) break;
+  }
+  // zero padding so the bit reader never sees stale bytes past the data
+  if (tid < 16) out[carry_keep + tid] = 0;
+  if (overflow) infos[img].status = kErrBadRestart;
+  if (tid == 0) {
+    infos[img].clean_len = carry_keep;
+    infos[img].nseg = min(carry_rst + 1, dd.seg_cap);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// entropy_kernel
+// ---------------------------------------------------------------------------
+
+constexpr int kEnThreads = 256;
+constexpr int kMaxSlots = 2048;
+constexpr int kMaxLds = 6;  // distinct tables held in LDS
+
+struct EntShared {
+  uint32_t lut[kMaxLds][kLutSize];
+  int32_t maxcode[kMaxLds][18];
+  int32_t valoff[kMaxLds][17];
+  uint8_t vals[kMaxLds][256];
+  uint32_t s_pos[kMaxSlots];
+  uint32_t s_zb[kMaxSlots];   // z | b << 8
+  int32_t s_nblk[kMaxSlots];
+  int32_t s_dc[kMaxSlots][kMaxComp];
+  uint32_t run_pos[kEnThreads];
+  uint32_t run_zb[kEnThreads];
+  int32_t scan_flag[kEnThreads];
+  int32_t scan_v[kEnThreads][4];  // blk, dc0, dc1, dc2
+  uint16_t qt[kMaxComp][64];
+  int32_t tdc[kMaxBpm], tac[kMaxBpm], bcomp[kMaxBpm];
+  int32_t red[kEnThreads];
+  int32_t flag;
+  int32_t err;
+};
+
+struct BitReader {
+  const uint32_t* w;
+  uint64_t buf;
+  uint32_t wi;
+  int cnt;
+  uint32_t pos;
+  __device__ __forceinline__ void init(const uint32_t* words, uint32_t p) {
+    w = words;
+    wi = p >> 5;
+    const uint64_t hi = __builtin_bswap32(w[wi]), lo = __builtin_bswap32(w[wi + 1]);
+    buf = ((hi << 32) | lo) << (p & 31);
+    cnt = 64 - (int)(p & 31);
+    wi += 2;
+    pos = p;
+  }
+  __device__ __forceinline__ void refill() {
+    if (cnt <= 32) {
+      buf |= (uint64_t)__builtin_bswap32(w[wi++]) << (32 - cnt);
+      cnt += 32;
+    }
+  }
+  __device__ __forceinline__ uint32_t peek(int n) const { return (uint32_t)(buf >> (64 - n)); }
+  __device__ __forceinline__ void skip(int n) {
+    buf <<= n;
+    cnt -= n;
+    pos += (uint32_t)n;
+  }
+};
+
+// Decode one Huffman symbol with table t; returns symbol, sets nbits consumed
+// through the fused value path: on kind==Full, `fullv` receives the value
+// and `consumed` includes the value bits.  Returns -1 for an invalid code
+// (nothing consumed).
+__device__ __forceinline__ int huff_sym(const EntShared& S, int t, BitReader& br, int& vbits,
+                                        int& fullv, bool& full) {
+  const uint32_t e = S.lut[t][br.peek(kLutBits)];
+  const uint32_t kind = (e >> 5) & 3;
+  if (kind == kKindFull) {
+    full = true;
+    fullv = (int)e >> 16;
+    vbits = 0;
+    br.skip((int)(e & 31));
+    return (int)((e >> 8) & 0xFF);
+  }
+  full = false;
+  if (kind == kKindCode) {
+    br.skip((int)(e & 31));
+    return (int)((e >> 8) & 0xFF);
+  }
+  const uint32_t w16 = br.peek(16);
+  for (int l = kLutBits + 1; l <= 16; l++) {
+    const int code = (int)(w16 >> (16 - l));
+    if (code <= S.maxcode[t][l]) {
+      br.skip(l);
+      return S.vals[t][S.valoff[t][l] + code];
+    }
+  }
+  return -1;
+}
+
+__device__ __forceinline__ int extend_bits(uint32_t v, int s) {
+  return (v < (1u << (s - 1))) ? (int)v - ((1 << s) - 1) : (int)v;
+}
+
+struct WriteCtx {
+  int16_t* coef;      // image coefficient base
+  int32_t nb;         // next block index to start
+  int32_t dc[kMaxComp];
+  int32_t seg_end_blk;
+  uint32_t seg_end_bits;
+};
+
+// Decode every symbol that starts in [br.pos, end).  Sync mode (WRITE=false)
+// is total: invalid codes consume one bit, out-of-range runs end the block,
+// so any bit position yields a deterministic trajectory.  Write mode stops at
+// the segment's last block and reports corruption.
+template <bool WRITE>
+__device__ int decode_range(const EntShared& S, BitReader& br, int& z, int& b, const int bpm,
+                            const uint32_t end, int& nblk, int* dcs, WriteCtx* wc) {
+  while (br.pos < end) {
+    if (WRITE && z == 0 && wc->nb >= wc->seg_end_blk) return kOk;
+    br.refill();
+    const int c = S.bcomp[b];
+    int vb, fv;
+    bool full;
+    if (z == 0) {
+      const int s = huff_sym(S, S.tdc[b], br, vb, fv, full);
+      if (s < 0 || s > 15) {
+        if (WRITE) return kErrBadHuffman;
+        br.skip(1);
+        continue;
+      }
+      int diff = 0;
+      if (full) {
+        diff = fv;
+      } else if (s) {
+        diff = extend_bits(br.peek(s), s);
+        br.skip(s);
+      }
+      if (WRITE) {
+        const int blk = wc->nb++;
+        wc->dc[c] += diff;
+        const uint32_t v = (uint32_t)kDcBias + (uint32_t)S.qt[c][0] * (uint32_t)wc->dc[c];
+        const int32_t vi = (int32_t)v;
+        wc->coef[(size_t)blk * 64] = (int16_t)(vi < -32768 ? -32768 : vi > 32767 ? 32767 : vi);
+      } else {
+        nblk++;
+        dcs[c] += diff;
+      }
+      z = 1;
+    } else {
+      const int rs = huff_sym(S, S.tac[b], br, vb, fv, full);
+      if (rs < 0) {
+        if (WRITE) return kErrBadHuffman;
+        br.skip(1);
+        continue;
+      }
+      const int r = rs >> 4, s = rs & 15;
+      if (s == 0) {
+        if (r == 15) {
+          z += 16;
+        } else {
+          if (WRITE && r != 0) return kErrBadHuffman;
+          z = 64;
+        }
+      } else {
+        z += r;
+        int v = fv;
+        if (!full) {
+          v = extend_bits(br.peek(s), s);
+          br.skip(s);
+        }
+        if (z > 63) {
+          if (WRITE) return kErrBadHuffman;
+          z = 64;
+        } else {
+          if (WRITE)
+            wc->coef[(size_t)(wc->nb - 1) * 64 + kNat[z]] = (int16_t)(v * (int)S.qt[c][z]);
+          z++;
+        }
+      }
+      if (z >= 64) {
+        z = 0;
+        b = (b + 1 == bpm) ? 0 : b + 1;
+      }
+    }
+    if (WRITE && br.pos > wc->seg_end_bits) return kErrTruncated;
+  }
+  return kOk;
+}
+
+__global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __restrict__ clean,
+                                                             const uint32_t* __restrict__ segs,
+                                                             const ImageDesc* __restrict__ desc,
+                                                             ImageInfo* __restrict__ infos,
+                                                             const HuffTable* __restrict__ luts,
+                                                             int16_t* __restrict__ coefs,
+                                                             const int sub_bits_param) {
+  __shared__ EntShared S;
+  const int img = blockIdx.x, tid = threadIdx.x;
+  if (infos[img].status != kOk) return;
+  const ImageDesc dd = desc[img];
+  const ImageInfo& in = infos[img];
+  const int bpm = in.bpm, ri = in.ri, nmcu = in.mcux * in.mcuy;
+  const int nblocks = in.nblocks;
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(clean + dd.in_off);
+  const uint32_t* sg = segs + dd.seg_off;
+  const int clean_len = in.clean_len;
+  const int nseg_found = in.nseg;
+  const int nseg = ri > 0 ? (nmcu + ri - 1) / ri : 1;
+
+  // ---- tables into LDS (dedup table slots per component) ----
+  int ldc[kMaxComp], lac[kMaxComp];
+  {
+    int slots[kMaxLds], ns = 0;
+    for (int c = 0; c < in.ncomp; c++) {
+      int want[2] = {in.dc_tab[c], 4 + in.ac_tab[c]};
+      for (int k = 0; k < 2; k++) {
+        int f = -1;
+        for (int i = 0; i < ns; i++)
+          if (slots[i] == want[k]) f = i;
+        if (f < 0) {
+          f = ns;
+          slots[ns++] = want[k];
+        }
+        (k == 0 ? ldc : lac)[c] = f;
+      }
+    }
+    const HuffTable* tabs = luts + (size_t)img * 8;
+    for (int i = 0; i < ns; i++) {
+      const HuffTable& T = tabs[slots[i]];
+      for (int k = tid; k < kLutSize; k += kEnThreads) S.lut[i][k] = T.lut[k];
+      if (tid < 18) S.maxcode[i][tid] = T.maxcode[tid];
+      if (tid < 17) S.valoff[i][tid] = T.valoff[tid];
+      S.vals[i][tid] = T.vals[tid];
+    }
+    for (int k = tid; k < kMaxComp * 64; k += kEnThreads) S.qt[k / 64][k % 64] = in.qt[k / 64][k % 64];
+    if (tid < bpm) {
+      const int c = in.mcu_comp[tid];
+      S.bcomp[tid] = c;
+      S.tdc[tid] = ldc[c];
+      S.tac[tid] = lac[c];
+    }
+    if (tid == 0) S.err = kOk;
+  }
+  if (nseg_found < nseg) {
+    if (tid == 0) infos[img].status = kErrBadRestart;
+    return;
+  }
+  __syncthreads();
+
+  auto seg_start_bits = [&](int s) -> uint32_t { return sg[s] * 8u; };
+  auto seg_end_bits = [&](int s) -> uint32_t {
+    return (s + 1 < nseg_found ? sg[s + 1] : (uint32_t)clean_len) * 8u;
+  };
+
+  // ---- subsequence size: keep every segment within kMaxSlots slots ----
+  uint32_t maxbits = 0;
+  for (int s = tid; s < nseg; s += kEnThreads) {
+    uint32_t a = seg_start_bits(s), e = seg_end_bits(s);
+    maxbits = max(maxbits, e > a ? e - a : 0u);
+  }
+  S.red[tid] = (int32_t)maxbits;
+  __syncthreads();
+  for (int off = kEnThreads / 2; off > 0; off >>= 1) {
+    if (tid < off) S.red[tid] = max(S.red[tid], S.red[tid + off]);
+    __syncthreads();
+  }
+  maxbits = (uint32_t)S.red[0];
+  __syncthreads();
+  uint32_t N = (uint32_t)sub_bits_param;
+  {
+    uint32_t need = (maxbits + kMaxSlots - 1) / kMaxSlots;
+    need = (need + 31) & ~31u;
+    if (need > N) N = need;
+  }
+  const int cmax = max(1, (int)((maxbits + N - 1) / N));
+  const int seg_per_chunk = max(1, kMaxSlots / cmax);
+  int16_t* coef_img = coefs + (size_t)dd.coef_off * 64;
+  int rounds_total = 0;
+
+  for (int seg_lo = 0; seg_lo < nseg; seg_lo += seg_per_chunk) {
+    const int nsc = min(seg_per_chunk, nseg - seg_lo);
+    const int nslots = nsc * cmax;
+    const int K = (nslots + kEnThreads - 1) / kEnThreads;
+    const int r0 = min(tid * K, nslots), r1 = min(r0 + K, nslots);
+    // slot geometry helpers
+    auto slot_seg = [&](int k) { return seg_lo + k / cmax; };
+    auto slot_j = [&](int k) { return k % cmax; };
+    auto slot_start = [&](int k) { return seg_start_bits(slot_seg(k)) + (uint32_t)slot_j(k) * N; };
+    auto slot_end = [&](int k) {
+      const uint32_t a = slot_start(k) + N, e = seg_end_bits(slot_seg(k));
+      return a < e ? a : e;
+    };
+    auto slot_empty = [&](int k) {
+      return slot_j(k) > 0 && slot_start(k) >= seg_end_bits(slot_seg(k));
+    };
+    auto slot_known = [&](int k) { return slot_j(k) == 0; };
+
+    // ---- round 0: every run from a guess at its first slot ----
+    {
+      BitReader br;
+      int z = 0, b = 0;
+      bool have = false;
+      for (int k = r0; k < r1; k++) {
+        if (slot_empty(k)) {
+          have = false;
+          continue;
+        }
+        if (slot_known(k) || !have) {
+          z = 0;
+          b = 0;
+          br.init(words, slot_start(k));
+        }
+        S.s_pos[k] = br.pos;
+        S.s_zb[k] = (uint32_t)z | ((uint32_t)b << 8);
+        int nblk = 0, dcs[kMaxComp] = {0, 0, 0};
+        decode_range<false>(S, br, z, b, bpm, slot_end(k), nblk, dcs, nullptr);
+        S.s_nblk[k] = nblk;
+        for (int c = 0; c < kMaxComp; c++) S.s_dc[k][c] = dcs[c];
+        have = true;
+      }
+      S.run_pos[tid] = br.pos;
+      S.run_zb[tid] = have ? ((uint32_t)z | ((uint32_t)b << 8)) : 0xFFFFFFFFu;
+      if (r0 >= r1) S.run_zb[tid] = 0xFFFFFFFFu;
+    }
+    // ---- sync rounds ----
+    int rounds = 0;
+    for (;;) {
+      if (tid == 0) S.flag = 0;
+      __syncthreads();
+      bool redo = false;
+      uint32_t npos = 0, nzb = 0;
+      if (tid > 0 && r0 < r1 && !slot_known(r0) && !slot_empty(r0)) {
+        npos = S.run_pos[tid - 1];
+        nzb = S.run_zb[tid - 1];
+        if (nzb != 0xFFFFFFFFu && (npos != S.s_pos[r0] || nzb != S.s_zb[r0])) redo = true;
+      }
+      __syncthreads();
+      if (redo) {
+        BitReader br;
+        br.init(words, npos);
+        int z = (int)(nzb & 0xFF), b = (int)(nzb >> 8);
+        bool merged = false;
+        for (int k = r0; k < r1; k++) {
+          if (slot_empty(k) || slot_known(k)) {
+            merged = true;
+            break;
+          }
+          const uint32_t zb = (uint32_t)z | ((uint32_t)b << 8);
+          if (k > r0 && S.s_pos[k] == br.pos && S.s_zb[k] == zb) {
+            merged = true;
+            break;
+          }
+          S.s_pos[k] = br.pos;
+          S.s_zb[k] = zb;
+          int nblk = 0, dcs[kMaxComp] = {0, 0, 0};
+          decode_range<false>(S, br, z, b, bpm, slot_end(k), nblk, dcs, nullptr);
+          S.s_nblk[k] = nblk;
+          for (int c = 0; c < kMaxComp; c++) S.s_dc[k][c] = dcs[c];
+        }
+        if (!merged) {
+          const uint32_t zb = (uint32_t)z | ((uint32_t)b << 8);
+          if (S.run_pos[tid] != br.pos || S.run_zb[tid] != zb) {
+            S.run_pos[tid] = br.pos;
+            S.run_zb[tid] = zb;
+            S.flag = 1;
+          }
+        }
+      }
+      __syncthreads();
+      const int again = S.flag;
+      rounds++;
+      __syncthreads();
+      if (!again || rounds > kEnThreads + 2) break;
+    }
+    rounds_total += rounds;
+
+    // ---- segmented exclusive scan over runs: (absolute next block, DC preds) ----
+    {
+      int flag = 0, v[4] = {0, 0, 0, 0};
+      for (int k = r0; k < r1; k++) {
+        if (slot_empty(k)) continue;
+        if (slot_known(k)) {
+          flag = 1;
+          v[0] = ri > 0 ? slot_seg(k) * ri * bpm : 0;
+          v[1] = v[2] = v[3] = 0;
+        }
+        v[0] += S.s_nblk[k];
+        for (int c = 0; c < kMaxComp; c++) v[1 + c] += S.s_dc[k][c];
+      }
+      S.scan_flag[tid] = flag;
+      for (int i = 0; i < 4; i++) S.scan_v[tid][i] = v[i];
+      __syncthreads();
+      // inclusive Hillis-Steele segmented scan
+      for (int off = 1; off < kEnThreads; off <<= 1) {
+        int pf = 0, pv[4] = {0, 0, 0, 0};
+        const bool take = tid >= off;
+        if (take) {
+          pf = S.scan_flag[tid - off];
+          for (int i = 0; i < 4; i++) pv[i] = S.scan_v[tid - off][i];
+        }
+        __syncthreads();
+        if (take && !S.scan_flag[tid]) {
+          for (int i = 0; i < 4; i++) S.scan_v[tid][i] += pv[i];
+          S.scan_flag[tid] = pf;
+        }
+        __syncthreads();
+      }
+    }
+    // ---- write pass ----
+    {
+      WriteCtx wc;
+      wc.coef = coef_img;
+      wc.nb = 0;
+      wc.dc[0] = wc.dc[1] = wc.dc[2] = 0;
+      if (tid > 0) {
+        wc.nb = S.scan_v[tid - 1][0];
+        for (int c = 0; c < kMaxComp; c++) wc.dc[c] = S.scan_v[tid - 1][1 + c];
+      }
+      BitReader br;
+      int z = 0, b = 0;
+      bool have = false;
+      int rc = kOk;
+      for (int k = r0; k < r1 && rc == kOk; k++) {
+        if (slot_empty(k)) continue;
+        const int s = slot_seg(k);
+        if (slot_known(k)) {
+          z = 0;
+          b = 0;
+          br.init(words, slot_start(k));
+          wc.nb = ri > 0 ? s * ri * bpm : 0;
+          wc.dc[0] = wc.dc[1] = wc.dc[2] = 0;
+        } else if (!have) {
+          const uint32_t zb = S.s_zb[k];
+          br.init(words, S.s_pos[k]);
+          z = (int)(zb & 0xFF);
+          b = (int)(zb >> 8);
+        }
+        have = true;
+        wc.seg_end_blk = ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks;
+        wc.seg_end_bits = seg_end_bits(s);
+        int dummy = 0;
+        rc = decode_range<true>(S, br, z, b, bpm, slot_end(k), dummy, nullptr, &wc);
+        // last slot of its segment: every block of the segment must be done
+        const bool last = (k + 1 >= nslots) || slot_j(k + 1) == 0 || slot_empty(k + 1);
+        // (nb beyond the segment only happens for garbage after its last block)
+        if (rc == kOk && last && (wc.nb < wc.seg_end_blk || (wc.nb == wc.seg_end_blk && z != 0)))
+          rc = kErrTruncated;
+      }
+      if (rc != kOk) atomicCAS(&S.err, kOk, rc);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (S.err != kOk) infos[img].status = S.err;
+    infos[img].sync_rounds = rounds_total;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// idct_kernel
+// ---------------------------------------------------------------------------
+
+constexpr int kW1 = 22725, kW2 = 21407, kW3 = 19266, kW4 = 16383, kW5 = 12873, kW6 = 8867,
+              kW7 = 4520;
+
+__device__ __forceinline__ uint8_t clip_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
+
+// FFmpeg simple_idct 8-bit (see oracle/jpeg_oracle.c simple_row / simple_col_put)
+__device__ __forceinline__ void simple_row(int16_t* r) {
+  if (!(r[1] | r[2] | r[3] | r[4] | r[5] | r[6] | r[7])) {
+    const int16_t t = (int16_t)(uint16_t)((uint32_t)(int32_t)r[0] << 3);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r[i] = t;
+    return;
+  }
+  uint32_t a0 = (uint32_t)kW4 * (uint32_t)(int32_t)r[0] + (1u << 10);
+  uint32_t a1 = a0, a2 = a0, a3 = a0;
+  a0 += (uint32_t)kW2 * (uint32_t)(int32_t)r[2];
+  a1 += (uint32_t)kW6 * (uint32_t)(int32_t)r[2];
+  a2 -= (uint32_t)kW6 * (uint32_t)(int32_t)r[2];
+  a3 -= (uint32_t)kW2 * (uint32_t)(int32_t)r[2];
+  uint32_t b0 = (uint32_t)(kW1 * r[1]) + (uint32_t)kW3 * (uint32_t)(int32_t)r[3];
+  uint32_t b1 = (uint32_t)(kW3 * r[1]) + (uint32_t)(-kW7) * (uint32_t)(int32_t)r[3];
+  uint32_t b2 = (uint32_t)(kW5 * r[1]) + (uint32_t)(-kW1) * (uint32_t)(int32_t)r[3];
+  uint32_t b3 = (uint32_t)(kW7 * r[1]) + (uint32_t)(-kW5) * (uint32_t)(int32_t)r[3];
+  if (r[4] | r[5] | r[6] | r[7]) {
+    a0 += (uint32_t)kW4 * (uint32_t)(int32_t)r[4] + (uint32_t)kW6 * (uint32_t)(int32_t)r[6];
+    a1 += (uint32_t)(-kW4) * (uint32_t)(int32_t)r[4] - (uint32_t)kW2 * (uint32_t)(int32_t)r[6];
+    a2 += (uint32_t)(-kW4) * (uint32_t)(int32_t)r[4] + (uint32_t)kW2 * (uint32_t)(int32_t)r[6];
+    a3 += (uint32_t)kW4 * (uint32_t)(int32_t)r[4] - (uint32_t)kW6 * (uint32_t)(int32_t)r[6];
+    b0 += (uint32_t)kW5 * (uint32_t)(int32_t)r[5] + (uint32_t)kW7 * (uint32_t)(int32_t)r[7];
+    b1 += (uint32_t)(-kW1) * (uint32_t)(int32_t)r[5] + (uint32_t)(-kW5) * (uint32_t)(int32_t)r[7];
+    b2 += (uint32_t)kW7 * (uint32_t)(int32_t)r[5] + (uint32_t)kW3 * (uint32_t)(int32_t)r[7];
+    b3 += (uint32_t)kW3 * (uint32_t)(int32_t)r[5] + (uint32_t)(-kW1) * (uint32_t)(int32_t)r[7];
+  }
+  r[0] = (int16_t)((int32_t)(a0 + b0) >> 11);
+  r[7] = (int16_t)((int32_t)(a0 - b0) >> 11);
+  r[1] = (int16_t)((int32_t)(a1 + b1) >> 11);
+  r[6] = (int16_t)((int32_t)(a1 - b1) >> 11);
+  r[2] = (int16_t)((int32_t)(a2 + b2) >> 11);
+  r[5] = (int16_t)((int32_t)(a2 - b2) >> 11);
+  r[3] = (int16_t)((int32_t)(a3 + b3) >> 11);
+  r[4] = (int16_t)((int32_t)(a3 - b3) >> 11);
+}
+
+__device__ __forceinline__ void simple_col(const int16_t* c, uint8_t* o /* 8 rows, stride 8 */) {
+  uint32_t a0 = (uint32_t)kW4 * (uint32_t)(c[0] + ((1 << 19) / kW4));
+  uint32_t a1 = a0, a2 = a0, a3 = a0;
+  a0 += (uint32_t)kW2 * (uint32_t)(int32_t)c[16];
+  a1 += (uint32_t)kW6 * (uint32_t)(int32_t)c[16];
+  a2 += (uint32_t)(-kW6) * (uint32_t)(int32_t)c[16];
+  a3 += (uint32_t)(-kW2) * (uint32_t)(int32_t)c[16];
+  uint32_t b0 = (uint32_t)(kW1 * c[8]) + (uint32_t)kW3 * (uint32_t)(int32_t)c[24];
+  uint32_t b1 = (uint32_t)(kW3 * c[8]) + (uint32_t)(-kW7) * (uint32_t)(int32_t)c[24];
+  uint32_t b2 = (uint32_t)(kW5 * c[8]) + (uint32_t)(-kW1) * (uint32_t)(int32_t)c[24];
+  uint32_t b3 = (uint32_t)(kW7 * c[8]) + (uint32_t)(-kW5) * (uint32_t)(int32_t)c[24];
+  a0 += (uint32_t)kW4 * (uint32_t)(int32_t)c[32];
+  a1 += (uint32_t)(-kW4) * (uint32_t)(int32_t)c[32];
+  a2 += (uint32_t)(-kW4) * (uint32_t)(int32_t)c[32];
+  a3 += (uint32_t)kW4 * (uint32_t)(int32_t)c[32];
+  b0 += (uint32_t)kW5 * (uint32_t)(int32_t)c[40];
+  b1 += (uint32_t)(-kW1) * (uint32_t)(int32_t)c[40];
+  b2 += (uint32_t)kW7 * (uint32_t)(int32_t)c[40];
+  b3 += (uint32_t)kW3 * (uint32_t)(int32_t)c[40];
+  a0 += (uint32_t)kW6 * (uint32_t)(int32_t)c[48];
+  a1 += (uint32_t)(-kW2) * (uint32_t)(int32_t)c[48];
+  a2 += (uint32_t)kW2 * (uint32_t)(int32_t)c[48];
+  a3 += (uint32_t)(-kW6) * (uint32_t)(int32_t)c[48];
+  b0 += (uint32_t)kW7 * (uint32_t)(int32_t)c[56];
+  b1 += (uint32_t)(-kW5) * (uint32_t)(int32_t)c[56];
+  b2 += (uint32_t)kW3 * (uint32_t)(int32_t)c[56];
+  b3 += (uint32_t)(-kW1) * (uint32_t)(int32_t)c[56];
+  o[0] = clip_u8((int32_t)(a0 + b0) >> 20);
+  o[8] = clip_u8((int32_t)(a1 + b1) >> 20);
+  o[16] = clip_u8((int32_t)(a2 + b2) >> 20);
+  o[24] = clip_u8((int32_t)(a3 + b3) >> 20);
+  o[32] = clip_u8((int32_t)(a3 - b3) >> 20);
+  o[40] = clip_u8((int32_t)(a2 - b2) >> 20);
+  o[48] = clip_u8((int32_t)(a1 - b1) >> 20);
+  o[56] = clip_u8((int32_t)(a0 - b0) >> 20);
+}
+
+// IJG islow (see oracle/jpeg_oracle.c jo_idct_islow)
+constexpr int F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373,
+              F1175 = 9633, F1501 = 12299, F1847 = 15137, F1961 = 16069, F2053 = 16819,
+              F2562 = 20995, F3072 = 25172;
+
+__device__ __forceinline__ uint8_t islow_limit(int32_t x) {
+  const int v = (int)(x & 1023) - 384;
+  return (uint8_t)min(max(v, 0), 255);
+}
+
+__device__ __forceinline__ void islow_block(int16_t* in, uint8_t* out) {
+  int32_t ws[64];
+  in[0] = (int16_t)(in[0] - kDcBias);
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    const int16_t* p = in + c;
+    if (!(p[8] | p[16] | p[24] | p[32] | p[40] | p[48] | p[56])) {
+      const int32_t dc = (int32_t)p[0] * 4;
+#pragma unroll
+      for (int r = 0; r < 8; r++) ws[r * 8 + c] = dc;
+      continue;
+    }
+    int32_t z1, z2, z3, t0, t1, t2, t3, t10, t11, t12, t13;
+    z2 = (int32_t)p[0] * 8192 + (1 << 10);
+    z3 = (int32_t)p[32] * 8192;
+    t0 = z2 + z3;
+    t1 = z2 - z3;
+    z2 = p[16];
+    z3 = p[48];
+    z1 = (z2 + z3) * F0541;
+    t2 = z1 + z2 * F0765;
+    t3 = z1 - z3 * F1847;
+    t10 = t0 + t2;
+    t13 = t0 - t2;
+    t11 = t1 + t3;
+    t12 = t1 - t3;
+    t0 = p[56];
+    t1 = p[40];
+    t2 = p[24];
+    t3 = p[8];
+    z2 = t0 + t2;
+    z3 = t1 + t3;
+    z1 = (z2 + z3) * F1175;
+    z2 = z2 * -F1961 + z1;
+    z3 = z3 * -F0390 + z1;
+    z1 = (t0 + t3) * -F0899;
+    t0 = t0 * F0298 + z1 + z2;
+    t3 = t3 * F1501 + z1 + z3;
+    z1 = (t1 + t2) * -F2562;
+    t1 = t1 * F2053 + z1 + z3;
+    t2 = t2 * F3072 + z1 + z2;
+    ws[0 * 8 + c] = (t10 + t3) >> 11;
+    ws[7 * 8 + c] = (t10 - t3) >> 11;
+    ws[1 * 8 + c] = (t11 + t2) >> 11;
+    ws[6 * 8 + c] = (t11 - t2) >> 11;
+    ws[2 * 8 + c] = (t12 + t1) >> 11;
+    ws[5 * 8 + c] = (t12 - t1) >> 11;
+    ws[3 * 8 + c] = (t13 + t0) >> 11;
+    ws[4 * 8 + c] = (t13 - t0) >> 11;
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int32_t* w = ws + r * 8;
+    uint8_t* o = out + r * 8;
+    int32_t z1, z2, z3, t0, t1, t2, t3, t10, t11, t12, t13;
+    z2 = w[0] + ((512 << 5) + (1 << 4));
+    if (!(w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7])) {
+      const uint8_t v = islow_limit(z2 >> 5);
+#pragma unroll
+      for (int i = 0; i < 8; i++) o[i] = v;
+      continue;
+    }
+    z3 = w[4];
+    t0 = (z2 + z3) * 8192;
+    t1 = (z2 - z3) * 8192;
+    z2 = w[2];
+    z3 = w[6];
+    z1 = (z2 + z3) * F0541;
+    t2 = z1 + z2 * F0765;
+    t3 = z1 - z3 * F1847;
+    t10 = t0 + t2;
+    t13 = t0 - t2;
+    t11 = t1 + t3;
+    t12 = t1 - t3;
+    t0 = w[7];
+    t1 = w[5];
+    t2 = w[3];
+    t3 = w[1];
+    z2 = t0 + t2;
+    z3 = t1 + t3;
+    z1 = (z2 + z3) * F1175;
+    z2 = z2 * -F1961 + z1;
+    z3 = z3 * -F0390 + z1;
+    z1 = (t0 + t3) * -F0899;
+    t0 = t0 * F0298 + z1 + z2;
+    t3 = t3 * F1501 + z1 + z3;
+    z1 = (t1 + t2) * -F2562;
+    t1 = t1 * F2053 + z1 + z3;
+    t2 = t2 * F3072 + z1 + z2;
+    o[0] = islow_limit((t10 + t3) >> 18);
+    o[7] = islow_limit((t10 - t3) >> 18);
+    o[1] = islow_limit((t11 + t2) >> 18);
+    o[6] = islow_limit((t11 - t2) >> 18);
+    o[2] = islow_limit((t12 + t1) >> 18);
+    o[5] = islow_limit((t12 - t1) >> 18);
+    o[3] = islow_limit((t13 + t0) >> 18);
+    o[4] = islow_limit((t13 - t0) >> 18);
+  }
+}
+
+template <int IDCT>
+__global__ void __launch_bounds__(256) idct_kernel(const int16_t* __restrict__ coefs,
+                                                   const ImageDesc* __restrict__ desc,
+                                                   const ImageInfo* __restrict__ infos,
+                                                   uint8_t* __restrict__ planes) {
+  const int img = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const ImageInfo& in = infos[img];
+  if (in.status != kOk || j >= in.nblocks) return;
+  const ImageDesc& dd = desc[img];
+  const int bpm = in.bpm;
+  const int mcu = j / bpm, b = j - mcu * bpm;
+  const int c = in.mcu_comp[b];
+  const int mx = mcu % in.mcux, my = mcu / in.mcux;
+  int bx, by;
+  if (in.ncomp == 1) {
+    bx = mx;
+    by = my;
+  } else {
+    bx = mx * in.comp_h[c] + in.mcu_dx[b];
+    by = my * in.comp_v[c] + in.mcu_dy[b];
+  }
+  int16_t blk[64];
+  const uint4* src = reinterpret_cast<const uint4*>(coefs + ((size_t)dd.coef_off + j) * 64);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint4 q = src[i];
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      blk[8 * i + 2 * k] = (int16_t)(w[k] & 0xFFFF);
+      blk[8 * i + 2 * k + 1] = (int16_t)(w[k] >> 16);
+    }
+  }
+  uint8_t px[64];
+  if (IDCT == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) simple_row(blk + 8 * i);
+#pragma unroll
+    for (int i = 0; i < 8; i++) simple_col(blk + i, px + i);
+  } else {
+    islow_block(blk, px);
+  }
+  const int stride = dd.plane_stride[c];
+  uint8_t* dst = planes + dd.plane_off[c] + (size_t)by * 8 * stride + bx * 8;
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    uint2 v;
+    v.x = (uint32_t)px[8 * r] | ((uint32_t)px[8 * r + 1] << 8) | ((uint32_t)px[8 * r + 2] << 16) |
+          ((uint32_t)px[8 * r + 3] << 24);
+    v.y = (uint32_t)px[8 * r + 4] | ((uint32_t)px[8 * r + 5] << 8) |
+          ((uint32_t)px[8 * r + 6] << 16) | ((uint32_t)px[8 * r + 7] << 24);
+    *reinterpret_cast<uint2*>(dst + (size_t)r * stride) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// colour conversion (IJG jdcolor.c / jdmerge.c integer tables, SCALEBITS 16)
+// ---------------------------------------------------------------------------
+
+constexpr int32_t kFix1402 = 91881, kFix1772 = 116130, kFix0714 = 46802, kFix0344 = 22554;
+
+__device__ __forceinline__ void ycc_rgb(int y, int cb, int cr, int* rgb) {
+  const int32_t x_cb = cb - 128, x_cr = cr - 128;
+  const int32_t cr_r = (kFix1402 * x_cr + 32768) >> 16;
+  const int32_t cb_b = (kFix1772 * x_cb + 32768) >> 16;
+  const int32_t g = ((-kFix0344 * x_cb + 32768) + (-kFix0714 * x_cr)) >> 16;
+  rgb[0] = clip_u8(y + cr_r);
+  rgb[1] = clip_u8(y + g);
+  rgb[2] = clip_u8(y + cb_b);
+}
+
+__device__ __forceinline__ void store_rgb(void* out, int64_t base, int fmt, int dtype, int ow,
+                                          int oh, int x, int y, const int* rgb,
+                                          const BatchParams& p) {
+  const bool planar = fmt == 0 || fmt == 1;
+  const bool swap = fmt == 1 || fmt == 3;
+  const int64_t pl = (int64_t)ow * oh;
+#pragma unroll
+  for (int ch = 0; ch < 3; ch++) {
+    const int v = rgb[swap ? 2 - ch : ch];
+    const int64_t oi = base + (planar ? ch * pl + (int64_t)y * ow + x : ((int64_t)y * ow + x) * 3 + ch);
+    if (dtype == 0) {
+      static_cast<uint8_t*>(out)[oi] = (uint8_t)v;
+    } else {
+      float f = __fdiv_rn((float)v, 255.0f);
+      f = __fsub_rn(f, p.mean[ch]);
+      f = __fdiv_rn(f, p.std[ch]);
+      static_cast<__half*>(out)[oi] = __float2half_rn(f);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) csc_kernel(const uint8_t* __restrict__ planes,
+                                                  const ImageDesc* __restrict__ desc,
+                                                  const ImageInfo* __restrict__ infos,
+                                                  void* __restrict__ out, const BatchParams p) {
+  const int img = blockIdx.y;
+  const ImageInfo& in = infos[img];
+  if (in.status != kOk) return;
+  const ImageDesc& dd = desc[img];
+  const int W = in.width, H = in.height;
+  const int64_t npx = (int64_t)W * H;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int y = (int)(i / W), x = (int)(i - (int64_t)y * W);
+    const int yv = planes[dd.plane_off[0] + (int64_t)y * dd.plane_stride[0] + x];
+    int rgb[3];
+    if (in.ncomp == 1) {
+      rgb[0] = rgb[1] = rgb[2] = yv;
+    } else {
+      const int cx1 = x * in.comp_h[1] / in.hmax, cy1 = y * in.comp_v[1] / in.vmax;
+      const int cx2 = x * in.comp_h[2] / in.hmax, cy2 = y * in.comp_v[2] / in.vmax;
+      const int cb = planes[dd.plane_off[1] + (int64_t)cy1 * dd.plane_stride[1] + cx1];
+      const int cr = planes[dd.plane_off[2] + (int64_t)cy2 * dd.plane_stride[2] + cx2];
+      ycc_rgb(yv, cb, cr, rgb);
+    }
+    store_rgb(out, dd.out_off, p.pix_fmt, p.dtype, W, H, x, y, rgb, p);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// resize: weights + fused resize/csc/pad/normalise
+// ---------------------------------------------------------------------------
+
+#pragma clang fp contract(off)
+__device__ float kernel_eval(int filter, float x) {
+  const float t = fabsf(x);
+  if (filter == 1) return t < 1.0f ? 1.0f - t : 0.0f;
+  const float t2 = t * t;
+  const float t3 = t2 * t;
+  if (t <= 1.0f) {
+    const float a = 1.4f * t3;
+    const float b = 2.4f * t2;
+    return (a - b) + 1.0f;
+  }
+  if (t < 2.0f) {
+    const float a = -0.6f * t3;
+    const float b = 3.0f * t2;
+    const float c = 4.8f * t;
+    return ((a + b) - c) + 2.4f;
+  }
+  return 0.0f;
+}
+
+// Weight table for one (image, plane, axis): entry i holds first tap index
+// (int32) then `taps` Q14 weights (int16, padded with zero).  Layout in the
+// int32 pool: [first x dst_len][ceil(taps/2) x dst_len] (weights packed 2/int32).
+__global__ void __launch_bounds__(256) weights_kernel(const ImageDesc* __restrict__ desc,
+                                                      const ImageInfo* __restrict__ infos,
+                                                      int32_t* __restrict__ pool,
+                                                      const int filter) {
+  const int img = blockIdx.z, which = blockIdx.y;  // which = plane*2 + axis
+  const ImageInfo& in = infos[img];
+  if (in.status != kOk) return;
+  const ImageDesc& dd = desc[img];
+  const int c = which >> 1, axis = which & 1;
+  if (c >= dd.ncomp) return;
+  const int src_len = axis == 0 ? in.comp_w[c] : in.comp_hpx[c];
+  const int dst_len = axis == 0 ? dd.sw : dd.sh;
+  const int taps = axis == 0 ? dd.taps_x[c] : dd.taps_y[c];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= dst_len) return;
+  // table offset inside the image's region
+  int64_t off = dd.wt_off;
+  for (int k = 0; k < which; k++) {
+    const int kc = k >> 1, ka = k & 1;
+    if (kc >= dd.ncomp) break;
+    const int dl = ka == 0 ? dd.sw : dd.sh, tp = ka == 0 ? dd.taps_x[kc] : dd.taps_y[kc];
+    off += (int64_t)dl * (1 + (tp + 1) / 2);
+  }
+  int32_t* first = pool + off;
+  int16_t* w = reinterpret_cast<int16_t*>(pool + off + dst_len) + (int64_t)i * ((taps + 1) / 2) * 2;
+  const float scale = __fdiv_rn((float)src_len, (float)dst_len);
+  const float fscale = scale > 1.0f ? scale : 1.0f;
+  const float support = (filter == 1 ? 1.0f : 2.0f) * fscale;
+  float center = ((float)i + 0.5f) * scale;
+  center = center - 0.5f;
+  const int lo = (int)ceilf(center - support);
+  const int hi = (int)floorf(center + support);
+  const int n = hi - lo + 1;
+  float wf[kMaxTaps];
+  int wq[kMaxTaps];
+  float sum = 0.0f;
+  for (int t = 0; t < n && t < kMaxTaps; t++) {
+    const float x = __fdiv_rn((float)(lo + t) - center, fscale);
+    wf[t] = kernel_eval(filter, x);
+    sum = sum + wf[t];
+  }
+  int qs = 0, am = 0;
+  for (int t = 0; t < n && t < kMaxTaps; t++) {
+    float q = __fdiv_rn(wf[t], sum);
+    q = q * 16384.0f;
+    q = q + 0.5f;
+    wq[t] = (int)floorf(q);
+    qs += wq[t];
+    if (wq[t] > wq[am]) am = t;
+  }
+  wq[am] += 16384 - qs;
+  first[i] = lo;
+  const int tp2 = ((taps + 1) / 2) * 2;
+  for (int t = 0; t < tp2; t++) w[t] = (int16_t)(t < n ? wq[t] : 0);
+}
+#pragma clang fp contract(on)
+
+__device__ __forceinline__ int resize_plane_px(const uint8_t* __restrict__ src, int pw, int ph,
+                                               int stride, const int32_t* fx, const int16_t* wx,
+                                               int tx, const int32_t* fy, const int16_t* wy,
+                                               int ty, int cx, int cy) {
+  const int x0 = fx[cx], y0 = fy[cy];
+  const int16_t* wxr = wx + (int64_t)cx * tx;
+  const int16_t* wyr = wy + (int64_t)cy * ty;
+  int32_t acc = 0;
+  for (int a = 0; a < ty; a++) {
+    int r = y0 + a;
+    r = r < 0 ? 0 : (r >= ph ? ph - 1 : r);
+    const uint8_t* row = src + (int64_t)r * stride;
+    int32_t h = 0;
+    for (int t = 0; t < tx; t++) {
+      int k = x0 + t;
+      k = k < 0 ? 0 : (k >= pw ? pw - 1 : k);
+      h += (int32_t)wxr[t] * row[k];
+    }
+    acc += (int32_t)wyr[a] * ((h + 128) >> 8);
+  }
+  return clip_u8((acc + (1 << 19)) >> 20);
+}
+
+__global__ void __launch_bounds__(256) resize_kernel(const uint8_t* __restrict__ planes,
+                                                     const ImageDesc* __restrict__ desc,
+                                                     const ImageInfo* __restrict__ infos,
+                                                     const int32_t* __restrict__ pool,
+                                                     void* __restrict__ out, const BatchParams p) {
+  const int img = blockIdx.y;
+  const ImageInfo& in = infos[img];
+  if (in.status != kOk) return;
+  const ImageDesc& dd = desc[img];
+  const int ow = dd.ow, oh = dd.oh;
+  const int64_t npx = (int64_t)ow * oh;
+  // table pointers
+  const int32_t* fxp[kMaxComp];
+  const int16_t* wxp[kMaxComp];
+  const int32_t* fyp[kMaxComp];
+  const int16_t* wyp[kMaxComp];
+  int txs[kMaxComp], tys[kMaxComp];
+  int64_t off = dd.wt_off;
+  for (int c = 0; c < dd.ncomp; c++) {
+    txs[c] = ((dd.taps_x[c] + 1) / 2) * 2;
+    tys[c] = ((dd.taps_y[c] + 1) / 2) * 2;
+    fxp[c] = pool + off;
+    wxp[c] = reinterpret_cast<const int16_t*>(pool + off + dd.sw);
+    off += (int64_t)dd.sw * (1 + txs[c] / 2);
+    fyp[c] = pool + off;
+    wyp[c] = reinterpret_cast<const int16_t*>(pool + off + dd.sh);
+    off += (int64_t)dd.sh * (1 + tys[c] / 2);
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int y = (int)(i / ow), x = (int)(i - (int64_t)y * ow);
+    const int cx = x - dd.dx, cy = y - dd.dy;
+    int rgb[3] = {0, 0, 0};
+    if (cx >= 0 && cx < dd.sw && cy >= 0 && cy < dd.sh) {
+      int v[kMaxComp];
+      for (int c = 0; c < dd.ncomp; c++)
+        v[c] = resize_plane_px(planes + dd.plane_off[c], in.comp_w[c], in.comp_hpx[c],
+                               dd.plane_stride[c], fxp[c], wxp[c], txs[c], fyp[c], wyp[c], tys[c],
+                               cx, cy);
+      if (dd.ncomp == 1)
+        rgb[0] = rgb[1] = rgb[2] = v[0];
+      else
+        ycc_rgb(v[0], v[1], v[2], rgb);
+    }
+    store_rgb(out, dd.out_off, p.pix_fmt, p.dtype, ow, oh, x, y, rgb, p);
+  }
+}
+
+// raw planes (parity surface): copy plane c cropped to its true size
+__global__ void planes_copy_kernel(const uint8_t* __restrict__ planes,
+                                   const ImageDesc* __restrict__ desc,
+                                   const ImageInfo* __restrict__ infos, uint8_t* __restrict__ out,
+                                   int64_t off1, int64_t off2) {
+  const ImageInfo& in = infos[0];
+  if (in.status != kOk) return;
+  const ImageDesc& dd = desc[0];
+  const int64_t offs[3] = {0, off1, off2};
+  for (int c = 0; c < in.ncomp; c++) {
+    const int w = in.comp_w[c], h = in.comp_hpx[c];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)w * h;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const int y = (int)(i / w), x = (int)(i - (int64_t)y * w);
+      out[offs[c] + i] = planes[dd.plane_off[c] + (int64_t)y * dd.plane_stride[c] + x];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers (host side, same TU)
+// ---------------------------------------------------------------------------
+
+hipError_t launch_parse(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
+                        HuffTable* luts, int n, hipStream_t st) {
+  hipLaunchKernelGGL(parse_kernel, dim3(n), dim3(256), 0, st, bytes, desc, infos, luts);
+  return hipGetLastError();
+}
+hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
+                          uint8_t* clean, uint32_t* segs, int n, hipStream_t st) {
+  hipLaunchKernelGGL(destuff_kernel, dim3(n), dim3(kDsThreads), 0, st, bytes, desc, infos, clean,
+                     segs);
+  return hipGetLastError();
+}
+hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
+                          ImageInfo* infos, const HuffTable* luts, int16_t* coefs, int sub_bits,
+                          int n, hipStream_t st) {
+  hipLaunchKernelGGL(entropy_kernel, dim3(n), dim3(kEnThreads), 0, st, clean, segs, desc, infos,
+                     luts, coefs, sub_bits);
+  return hipGetLastError();
+}
+hipError_t launch_idct(const int16_t* coefs, const ImageDesc* desc, const ImageInfo* infos,
+                       uint8_t* planes, int idct, int max_blocks, int n, hipStream_t st) {
+  dim3 grid((max_blocks + 255) / 256, n);
+  if (idct == 1)
+    hipLaunchKernelGGL(idct_kernel<1>, grid, dim3(256), 0, st, coefs, desc, infos, planes);
+  else
+    hipLaunchKernelGGL(idct_kernel<0>, grid, dim3(256), 0, st, coefs, desc, infos, planes);
+  return hipGetLastError();
+}
+hipError_t launch_weights(const ImageDesc* desc, const ImageInfo* infos, int32_t* pool,
+                          int filter, int max_len, int n, hipStream_t st) {
+  dim3 grid((max_len + 255) / 256, 6, n);
+  hipLaunchKernelGGL(weights_kernel, grid, dim3(256), 0, st, desc, infos, pool, filter);
+  return hipGetLastError();
+}
+hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
+                      void* out, const BatchParams& p, int64_t max_px, int n, hipStream_t st) {
+  int64_t gx64 = (max_px + 255) / 256;
+  int gx = (int)(gx64 < 4096 ? gx64 : 4096);
+  hipLaunchKernelGGL(csc_kernel, dim3(gx, n), dim3(256), 0, st, planes, desc, infos, out, p);
+  return hipGetLastError();
+}
+hipError_t launch_resize(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
+                         const int32_t* pool, void* out, const BatchParams& p, int64_t max_px,
+                         int n, hipStream_t st) {
+  int64_t gx64 = (max_px + 255) / 256;
+  int gx = (int)(gx64 < 4096 ? gx64 : 4096);
+  hipLaunchKernelGGL(resize_kernel, dim3(gx, n), dim3(256), 0, st, planes, desc, infos, pool, out,
+                     p);
+  return hipGetLastError();
+}
+hipError_t launch_planes_copy(const uint8_t* planes, const ImageDesc* desc,
+                              const ImageInfo* infos, uint8_t* out, int64_t off1, int64_t off2,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(planes_copy_kernel, dim3(256), dim3(256), 0, st, planes, desc, infos, out,
+                     off1, off2);
+  return hipGetLastError();
+}
+
+}  // namespace hj

@@ -1,0 +1,34 @@
+"""Drop-in image operator surface (mirror of ``spdl.io``'s image API,
+reference src/spdl/io/__init__.py:20-86), backed by gfx950 HIP kernels."""
+
+from ._buffer import CPUBuffer, CUDABuffer
+from ._config import CUDAConfig, cuda_config
+from ._convert import to_numpy, to_torch
+from ._image import (
+    decode_image_nvjpeg,
+    load_image,
+    load_image_batch,
+    load_image_batch_nvjpeg,
+)
+from ._preprocessing import get_video_filter_desc, parse_image_filter
+
+# HIP-named aliases: same functions, named for the hardware they run on.
+decode_image_hip = decode_image_nvjpeg
+load_image_batch_hip = load_image_batch_nvjpeg
+
+__all__ = [
+    "CPUBuffer",
+    "CUDABuffer",
+    "CUDAConfig",
+    "cuda_config",
+    "decode_image_hip",
+    "decode_image_nvjpeg",
+    "get_video_filter_desc",
+    "load_image",
+    "load_image_batch",
+    "load_image_batch_hip",
+    "load_image_batch_nvjpeg",
+    "parse_image_filter",
+    "to_numpy",
+    "to_torch",
+]

@@ -1,0 +1,60 @@
+"""Deterministic synthetic JPEG workload (BASELINE.md §2 / SURVEY.md §8(d)).
+
+Seeded numpy image: per channel six random sinusoids (amplitude 10-40,
+frequency 0.002-0.05 cycles/px) + 128 + N(0, 6) noise, clipped to u8, encoded
+by Pillow (baseline, 4:2:0 by default, no restart markers).  At 480x640 q90
+this is ~110 KB per image, the size BASELINE.md's roofline accounting uses.
+"""
+
+from __future__ import annotations
+
+import io
+
+import numpy as np
+
+
+def synthetic_pixels(seed: int, height: int = 480, width: int = 640) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:height, 0:width].astype(np.float32)
+    img = np.empty((height, width, 3), np.float32)
+    for c in range(3):
+        acc = np.full((height, width), 128.0, np.float32)
+        for _ in range(6):
+            amp = rng.uniform(10, 40)
+            fx, fy = rng.uniform(0.002, 0.05, size=2)
+            ph = rng.uniform(0, 2 * np.pi)
+            acc += amp * np.sin(2 * np.pi * (fx * xx + fy * yy) + ph).astype(np.float32)
+        acc += rng.normal(0, 6, size=(height, width)).astype(np.float32)
+        img[..., c] = acc
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def encode_jpeg(
+    pixels: np.ndarray, quality: int = 90, subsampling: int = 2, optimize: bool = False
+) -> bytes:
+    """Pillow baseline JPEG. subsampling: 0=4:4:4, 1=4:2:2, 2=4:2:0."""
+    from PIL import Image
+
+    mode = "L" if pixels.ndim == 2 else "RGB"
+    buf = io.BytesIO()
+    kw = dict(quality=quality, optimize=optimize, progressive=False)
+    if mode == "RGB":
+        kw["subsampling"] = subsampling
+    Image.fromarray(pixels, mode).save(buf, format="JPEG", **kw)
+    return buf.getvalue()
+
+
+def synthetic_jpeg(
+    seed: int,
+    height: int = 480,
+    width: int = 640,
+    quality: int = 90,
+    subsampling: int = 2,
+) -> bytes:
+    return encode_jpeg(synthetic_pixels(seed, height, width), quality, subsampling)
+
+
+def synthetic_batch(n: int, distinct: int = 32, **kw) -> list[bytes]:
+    """n JPEGs cycling through `distinct` seeded images."""
+    base = [synthetic_jpeg(1000 + i, **kw) for i in range(min(n, distinct))]
+    return [base[i % len(base)] for i in range(n)]

@@ -1,0 +1,96 @@
+"""Deterministic JPEG test inputs (generated with Pillow from seeded pixels).
+
+Covers the edge cases the reference tests exercise (tests/io/image_decoding_test.py:
+yuvj420p / 422 / 444 / gray, odd sizes) plus restart intervals, quality extremes,
+noise (long codes, many 0xFF00 stuffings) and a tiny image.
+"""
+
+from __future__ import annotations
+
+import functools
+import io
+
+import numpy as np
+from PIL import Image
+
+from spdl_amd.synthetic import synthetic_pixels
+
+
+def _enc(px, **kw) -> bytes:
+    b = io.BytesIO()
+    mode = "L" if px.ndim == 2 else "RGB"
+    Image.fromarray(px, mode).save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def _noise(seed, h, w, c=3):
+    rng = np.random.default_rng(seed)
+    shape = (h, w) if c == 1 else (h, w, c)
+    return rng.integers(0, 256, size=shape, dtype=np.uint8)
+
+
+@functools.lru_cache(maxsize=None)
+def case(name: str) -> bytes:
+    if name == "q90_420":
+        return _enc(synthetic_pixels(1), quality=90, subsampling=2)
+    if name == "q75_420":
+        return _enc(synthetic_pixels(2), quality=75, subsampling=2)
+    if name == "q95_420":
+        return _enc(synthetic_pixels(3), quality=95, subsampling=2)
+    if name == "q90_444":
+        return _enc(synthetic_pixels(4, 240, 320), quality=90, subsampling=0)
+    if name == "q90_422":
+        return _enc(synthetic_pixels(5, 240, 320), quality=90, subsampling=1)
+    if name == "odd_227x333":
+        return _enc(synthetic_pixels(6, 227, 333), quality=90, subsampling=2)
+    if name == "odd_444_101x67":
+        return _enc(synthetic_pixels(7, 101, 67), quality=85, subsampling=0)
+    if name == "gray":
+        return _enc(synthetic_pixels(8, 200, 300)[..., 0], quality=90)
+    if name == "gray_odd":
+        return _enc(synthetic_pixels(9, 77, 131)[..., 1], quality=80)
+    if name == "noise_420":
+        return _enc(_noise(10, 240, 320), quality=90, subsampling=2)
+    if name == "noise_q100":
+        return _enc(_noise(11, 120, 160), quality=100, subsampling=0)
+    if name == "restart_rows":
+        return _enc(synthetic_pixels(12, 240, 320), quality=90, restart_marker_rows=1)
+    if name == "restart_blocks":
+        return _enc(synthetic_pixels(13, 227, 333), quality=90, restart_marker_blocks=7)
+    if name == "restart_every_mcu":
+        return _enc(synthetic_pixels(14, 64, 96), quality=90, restart_marker_blocks=1)
+    if name == "tiny_8x8":
+        return _enc(synthetic_pixels(15, 8, 8), quality=90)
+    if name == "tiny_1x1":
+        return _enc(synthetic_pixels(16, 1, 1), quality=90)
+    if name == "optimized":
+        return _enc(synthetic_pixels(17, 240, 320), quality=90, optimize=True)
+    if name == "large_1080p":
+        return _enc(synthetic_pixels(18, 1080, 1920), quality=90, subsampling=2)
+    raise KeyError(name)
+
+
+VALID = [
+    "q90_420", "q75_420", "q95_420", "q90_444", "q90_422", "odd_227x333", "odd_444_101x67",
+    "gray", "gray_odd", "noise_420", "noise_q100", "restart_rows", "restart_blocks",
+    "restart_every_mcu", "tiny_8x8", "tiny_1x1", "optimized", "large_1080p",
+]
+
+
+def progressive() -> bytes:
+    return _enc(synthetic_pixels(20, 64, 64), quality=90, progressive=True)
+
+
+def truncated() -> bytes:
+    d = case("q90_420")
+    return d[: len(d) // 2]
+
+
+def corrupt_scan(seed: int = 0) -> bytes:
+    d = bytearray(case("q75_420"))
+    start = d.index(b"\xff\xda") + 20
+    rng = np.random.default_rng(seed)
+    pos = rng.integers(start, len(d) - 100, size=40)
+    for p in pos:
+        d[p] = int(rng.integers(0, 255))
+    return bytes(d)

@@ -1,0 +1,189 @@
+"""GPU parity: the gfx950 decode stage vs the CPU oracle, through the C-ABI.
+
+Bar (north_star): bit-exact for the integer stages (planes, rgb after the
+integer colour conversion, resize in fixed point); normalised fp16 output
+bit-exact as well (same IEEE op sequence), tolerance 0.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from spdl_amd._lib import Output
+from tests import cases
+
+pytestmark = pytest.mark.gpu
+
+
+def _decode(decoder, datas, out: Output, shape, dtype=torch.uint8):
+    t = torch.empty((len(datas),) + tuple(shape), dtype=dtype, device="cuda:0")
+    status = decoder.decode_batch(datas, out, t.data_ptr(), t.numel() * t.element_size(),
+                                  stream=torch.cuda.current_stream())
+    assert all(s == 0 for s in status)
+    return t.cpu()
+
+
+@pytest.mark.parametrize("name", cases.VALID)
+@pytest.mark.parametrize("idct", ["simple", "islow"])
+def test_planes_bit_exact(decoder, oracle, name, idct):
+    d = cases.case(name)
+    hyp = decoder.decode_planes(d, idct=idct)
+    ref = oracle.decode_planes(d, idct=oracle.IDCT_ISLOW if idct == "islow" else oracle.IDCT_SIMPLE)
+    assert len(hyp) == len(ref)
+    for h, r in zip(hyp, ref):
+        np.testing.assert_array_equal(h, r, strict=True)
+
+
+@pytest.mark.parametrize("name", cases.VALID)
+@pytest.mark.parametrize("pix_fmt", ["rgb", "rgb24", "bgr", "bgr24"])
+def test_fullres_rgb_bit_exact(decoder, oracle, name, pix_fmt):
+    d = cases.case(name)
+    info = oracle.parse(d)
+    W, H = info.width, info.height
+    shape = (3, H, W) if pix_fmt in ("rgb", "bgr") else (H, W, 3)
+    hyp = _decode(decoder, [d], Output(pix_fmt=pix_fmt), shape)[0].numpy()
+    ref = oracle.decode_rgb(d, oracle.IDCT_SIMPLE, pix_fmt)
+    np.testing.assert_array_equal(hyp, ref, strict=True)
+
+
+@pytest.mark.parametrize("name", ["q90_420", "odd_227x333", "gray", "restart_blocks", "noise_420"])
+def test_islow_matches_libjpeg_fixture(decoder, oracle, name):
+    """islow mode end-to-end vs libjpeg 9d when the pin helper is present."""
+    d = cases.case(name)
+    if oracle.ljpin() is None:
+        pytest.skip("libjpeg 9 not available on this host")
+    info = oracle.parse(d)
+    hyp = _decode(decoder, [d], Output(pix_fmt="rgb24", idct="islow"), (info.height, info.width, 3))
+    ref = oracle.lj_decode_rgb(d)
+    np.testing.assert_array_equal(hyp[0].numpy(), ref, strict=True)
+
+
+RESIZES = {
+    "pad224": dict(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224),
+    "crop224": dict(fit_w=224, fit_h=224, aspect="increase", crop_w=224, crop_h=224),
+    "stretch160x120": dict(fit_w=160, fit_h=120),
+    "imagenet": dict(fit_w=256, fit_h=256, aspect="decrease", pad_w=256, pad_h=256, crop_w=224,
+                     crop_h=224),
+    "upscale": dict(fit_w=700, fit_h=500),
+}
+
+
+@pytest.mark.parametrize("name", ["q90_420", "odd_227x333", "gray", "q90_444", "restart_rows",
+                                  "large_1080p", "tiny_8x8"])
+@pytest.mark.parametrize("rk", list(RESIZES))
+@pytest.mark.parametrize("filt", ["bicubic", "bilinear"])
+def test_resize_bit_exact(decoder, oracle, name, rk, filt):
+    d = cases.case(name)
+    kw = RESIZES[rk]
+    rs = oracle.Resize(filter=filt, **kw)
+    ref = oracle.decode_resize(d, rs, pix_fmt="rgb")
+    out = Output(pix_fmt="rgb", resize=True, filter=filt, **kw)
+    hyp = _decode(decoder, [d], out, ref.shape)[0].numpy()
+    np.testing.assert_array_equal(hyp, ref, strict=True)
+
+
+@pytest.mark.parametrize("pix_fmt", ["rgb", "rgb24"])
+def test_normalize_fp16_bit_exact(decoder, oracle, pix_fmt):
+    d = cases.case("q90_420")
+    kw = RESIZES["pad224"]
+    ref = oracle.decode_resize(d, oracle.Resize(**kw), pix_fmt=pix_fmt, normalize=True)
+    out = Output(pix_fmt=pix_fmt, resize=True, normalize=True, **kw)
+    hyp = _decode(decoder, [d], out, ref.shape, dtype=torch.float16)[0].numpy()
+    np.testing.assert_array_equal(hyp.view(np.uint16), ref.view(np.uint16), strict=True)
+
+
+def test_batch_mixed_sizes_resize(decoder, oracle):
+    names = ["q90_420", "odd_227x333", "gray", "restart_blocks", "q90_444", "noise_420",
+             "large_1080p", "optimized"]
+    datas = [cases.case(n) for n in names]
+    kw = RESIZES["pad224"]
+    out = Output(pix_fmt="rgb24", resize=True, **kw)
+    hyp = _decode(decoder, datas, out, (224, 224, 3)).numpy()
+    for i, d in enumerate(datas):
+        ref = oracle.decode_resize(d, oracle.Resize(**kw), pix_fmt="rgb24")
+        np.testing.assert_array_equal(hyp[i], ref, strict=True)
+
+
+def test_batch_256_fullres(decoder, oracle):
+    from spdl_amd.synthetic import synthetic_batch
+
+    datas = synthetic_batch(256, distinct=8)
+    hyp = _decode(decoder, datas, Output(pix_fmt="rgb24"), (480, 640, 3)).numpy()
+    refs = {}
+    for i, d in enumerate(datas):
+        if d not in refs:
+            refs[d] = oracle.decode_rgb(d, oracle.IDCT_SIMPLE, "rgb24")
+        np.testing.assert_array_equal(hyp[i], refs[d], strict=True)
+
+
+@pytest.mark.parametrize("bad", ["progressive", "truncated", "not_jpeg", "corrupt"])
+def test_errors_then_recover(decoder, oracle, bad):
+    """Rubbish raises RuntimeError and later calls still work
+    (reference tests/cuda/nvjpeg_decode_test.py:51-78)."""
+    if bad == "progressive":
+        d = cases.progressive()
+    elif bad == "truncated":
+        d = cases.truncated()
+    elif bad == "not_jpeg":
+        d = bytes(np.random.default_rng(0).integers(0, 256, 5000, dtype=np.uint8))
+    else:
+        d = cases.corrupt_scan(3)
+    ok_ref = True
+    try:
+        oracle.decode_rgb(d)
+    except oracle.OracleError:
+        ok_ref = False
+    if bad != "corrupt":
+        assert not ok_ref
+    info_ok = True
+    try:
+        info = oracle.parse(d)
+    except oracle.OracleError:
+        info_ok = False
+    if info_ok:
+        shape = (info.height, info.width, 3)
+    else:
+        shape = (8, 8, 3)
+    t = torch.empty(shape, dtype=torch.uint8, device="cuda:0")
+    if ok_ref:
+        decoder.decode_batch([d], Output(pix_fmt="rgb24"), t.data_ptr(), t.numel())
+        np.testing.assert_array_equal(t.cpu().numpy(), oracle.decode_rgb(d, 0, "rgb24"))
+    else:
+        with pytest.raises(RuntimeError, match="Failed to decode an image"):
+            decoder.decode_batch([d], Output(pix_fmt="rgb24"), t.data_ptr(), t.numel())
+    # recovery
+    good = cases.case("q90_444")
+    hyp = _decode(decoder, [good], Output(pix_fmt="rgb24"), (240, 320, 3))[0].numpy()
+    np.testing.assert_array_equal(hyp, oracle.decode_rgb(good, 0, "rgb24"))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_corrupt_streams_agree_with_oracle(decoder, oracle, seed):
+    d = cases.corrupt_scan(seed)
+    try:
+        ref = oracle.decode_rgb(d, 0, "rgb24")
+    except oracle.OracleError:
+        ref = None
+    info = oracle.parse(d)
+    t = torch.empty((info.height, info.width, 3), dtype=torch.uint8, device="cuda:0")
+    if ref is None:
+        with pytest.raises(RuntimeError):
+            decoder.decode_batch([d], Output(pix_fmt="rgb24"), t.data_ptr(), t.numel())
+    else:
+        decoder.decode_batch([d], Output(pix_fmt="rgb24"), t.data_ptr(), t.numel())
+        np.testing.assert_array_equal(t.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("sub_bits", [32, 64, 256, 1024, 8192])
+def test_subsequence_sizes(oracle, sub_bits):
+    """The sync result must not depend on the subsequence size."""
+    from spdl_amd._lib import Decoder
+
+    dec = Decoder(0)
+    dec.set_param("sub_bits", sub_bits)
+    for name in ["q90_420", "restart_blocks", "noise_420", "gray_odd"]:
+        d = cases.case(name)
+        info = oracle.parse(d)
+        hyp = _decode(dec, [d], Output(pix_fmt="rgb24"), (info.height, info.width, 3))[0].numpy()
+        np.testing.assert_array_equal(hyp, oracle.decode_rgb(d, 0, "rgb24"))
+    dec.close()
