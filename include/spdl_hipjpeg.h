@@ -134,6 +134,14 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
 int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, int32_t idct,
                           uint8_t* const* planes, void* stream, char* err, size_t errlen);
 
+/* Debug/parity surface: run parse + destuff + entropy decode of one image
+ * and copy back the dequantised coefficients (nblocks x 64 int16, natural
+ * order, MCU order, DC carries the FFmpeg +1024 bias), the destuffed scan
+ * bytes, and diagnostics diag[0..3] = {status, clean_len, nseg, sync_rounds}. */
+int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, int16_t* coefs,
+                          size_t coef_cap, uint8_t* clean, size_t clean_cap, int32_t* diag,
+                          char* err, size_t errlen);
+
 /* Per-kernel timing of the last batch, in microseconds, measured with HIP
  * events on the decode stream (filled only when enabled). */
 int spdl_hj_set_profiling(spdl_hj_ctx* ctx, int32_t enable);

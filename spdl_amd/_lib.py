@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libspdl_hipjpeg.so")
@@ -37,6 +37,7 @@ EXPORTED = (
     "spdl_hj_last_timings",
     "spdl_hj_stage_name",
     "spdl_hj_set_param",
+    "spdl_hj_debug_entropy",
 )
 
 
@@ -162,6 +163,7 @@ def lib() -> ctypes.CDLL:
         L.spdl_hj_stage_name.argtypes = [i32]
         L.spdl_hj_stage_name.restype = ctypes.c_char_p
         L.spdl_hj_set_param.argtypes = [vp, cp, ctypes.c_int64]
+        L.spdl_hj_debug_entropy.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, cp, sz]
         ver = L.spdl_hj_abi_version()
         if ver != ABI_VERSION:
             raise RuntimeError(f"libspdl_hipjpeg ABI {ver} != expected {ABI_VERSION}")
@@ -283,6 +285,25 @@ class Decoder:
         if rc:
             raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
         return list(status)
+
+    def debug_entropy(self, data, nblocks: int):
+        """Coefficients / destuffed bytes / diagnostics of one image (tests)."""
+        import numpy as np
+
+        mv = memoryview(data).cast("B")
+        b = (ctypes.c_char * len(mv)).from_buffer_copy(mv)
+        coefs = np.zeros((nblocks, 64), np.int16)
+        clean = np.zeros(len(mv), np.uint8)
+        diag = np.zeros(4, np.int32)
+        err = ctypes.create_string_buffer(1024)
+        rc = lib().spdl_hj_debug_entropy(self._h, ctypes.addressof(b), len(mv), coefs.ctypes.data,
+                                         coefs.size, clean.ctypes.data, clean.size,
+                                         diag.ctypes.data, err, 1024)
+        if rc:
+            raise RuntimeError(err.value.decode())
+        return coefs, clean[: max(int(diag[1]), 0)], {
+            "status": int(diag[0]), "clean_len": int(diag[1]), "nseg": int(diag[2]),
+            "sync_rounds": int(diag[3])}
 
     def decode_planes(self, data, idct: str = "simple", stream=None):
         import numpy as np

@@ -672,6 +672,50 @@ int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   return SPDL_HJ_OK;
 }
 
+int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, int16_t* coefs,
+                          size_t coef_cap, uint8_t* clean, size_t clean_cap, int32_t* diag,
+                          char* err, size_t errlen) {
+  if (!ctx || !data || !diag) {
+    set_err(err, errlen, "invalid argument");
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(ctx->device);
+  hipStream_t st = nullptr;
+  spdl_hj_image_info info;
+  int rc = probe(data, size, &info);
+  if (rc) {
+    set_err(err, errlen, "probe failed (%s)", status_str(rc));
+    return rc;
+  }
+  spdl_hj_output o{};
+  int64_t off = 0, sz = (int64_t)size, total = round_up(sz + 64, 256);
+  Layout L;
+  rc = build_layout(&off, &sz, &info, 1, &o, L, nullptr, err, errlen);
+  if (rc) return rc;
+  HJ_HIP(ctx->pin_in.ensure((size_t)total));
+  HJ_HIP(ctx->bytes.ensure((size_t)total));
+  HJ_HIP(hipEventSynchronize(ctx->batch_done));
+  memcpy(ctx->pin_in.p, data, size);
+  memset(static_cast<uint8_t*>(ctx->pin_in.p) + size, 0, (size_t)(total - sz));
+  HJ_HIP(hipMemcpyAsync(ctx->bytes.p, ctx->pin_in.p, (size_t)total, hipMemcpyHostToDevice, st));
+  (void)run_pipeline(ctx, static_cast<const uint8_t*>(ctx->bytes.p), (size_t)total, L, 1, &o,
+                     nullptr, 0, st, 1, nullptr, err, errlen, true);
+  ImageInfo hi;
+  HJ_HIP(hipMemcpy(&hi, ctx->info.p, sizeof(ImageInfo), hipMemcpyDeviceToHost));
+  diag[0] = hi.status;
+  diag[1] = hi.clean_len;
+  diag[2] = hi.nseg;
+  diag[3] = hi.sync_rounds;
+  size_t nc = (size_t)L.desc[0].nblocks * 64;
+  if (coefs) HJ_HIP(hipMemcpy(coefs, ctx->coefs.p, 2 * (nc < coef_cap ? nc : coef_cap),
+                              hipMemcpyDeviceToHost));
+  if (clean && hi.clean_len > 0) {
+    size_t n = (size_t)hi.clean_len < clean_cap ? (size_t)hi.clean_len : clean_cap;
+    HJ_HIP(hipMemcpy(clean, ctx->clean.p, n, hipMemcpyDeviceToHost));
+  }
+  return SPDL_HJ_OK;
+}
+
 int spdl_hj_set_profiling(spdl_hj_ctx* ctx, int32_t enable) {
   if (!ctx) return SPDL_HJ_ERR_INVALID_ARG;
   ctx->profiling = enable != 0;

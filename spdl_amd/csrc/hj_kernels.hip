@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include "hj_common.h"
+#include "hj_idct.h"
 
 namespace hj {
 
@@ -850,196 +851,6 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
 // idct_kernel
 // ---------------------------------------------------------------------------
 
-constexpr int kW1 = 22725, kW2 = 21407, kW3 = 19266, kW4 = 16383, kW5 = 12873, kW6 = 8867,
-              kW7 = 4520;
-
-__device__ __forceinline__ uint8_t clip_u8(int v) { return (uint8_t)min(max(v, 0), 255); }
-
-// FFmpeg simple_idct 8-bit (see oracle/jpeg_oracle.c simple_row / simple_col_put)
-__device__ __forceinline__ void simple_row(int16_t* r) {
-  if (!(r[1] | r[2] | r[3] | r[4] | r[5] | r[6] | r[7])) {
-    const int16_t t = (int16_t)(uint16_t)((uint32_t)(int32_t)r[0] << 3);
-#pragma unroll
-    for (int i = 0; i < 8; i++) r[i] = t;
-    return;
-  }
-  uint32_t a0 = (uint32_t)kW4 * (uint32_t)(int32_t)r[0] + (1u << 10);
-  uint32_t a1 = a0, a2 = a0, a3 = a0;
-  a0 += (uint32_t)kW2 * (uint32_t)(int32_t)r[2];
-  a1 += (uint32_t)kW6 * (uint32_t)(int32_t)r[2];
-  a2 -= (uint32_t)kW6 * (uint32_t)(int32_t)r[2];
-  a3 -= (uint32_t)kW2 * (uint32_t)(int32_t)r[2];
-  uint32_t b0 = (uint32_t)(kW1 * r[1]) + (uint32_t)kW3 * (uint32_t)(int32_t)r[3];
-  uint32_t b1 = (uint32_t)(kW3 * r[1]) + (uint32_t)(-kW7) * (uint32_t)(int32_t)r[3];
-  uint32_t b2 = (uint32_t)(kW5 * r[1]) + (uint32_t)(-kW1) * (uint32_t)(int32_t)r[3];
-  uint32_t b3 = (uint32_t)(kW7 * r[1]) + (uint32_t)(-kW5) * (uint32_t)(int32_t)r[3];
-  if (r[4] | r[5] | r[6] | r[7]) {
-    a0 += (uint32_t)kW4 * (uint32_t)(int32_t)r[4] + (uint32_t)kW6 * (uint32_t)(int32_t)r[6];
-    a1 += (uint32_t)(-kW4) * (uint32_t)(int32_t)r[4] - (uint32_t)kW2 * (uint32_t)(int32_t)r[6];
-    a2 += (uint32_t)(-kW4) * (uint32_t)(int32_t)r[4] + (uint32_t)kW2 * (uint32_t)(int32_t)r[6];
-    a3 += (uint32_t)kW4 * (uint32_t)(int32_t)r[4] - (uint32_t)kW6 * (uint32_t)(int32_t)r[6];
-    b0 += (uint32_t)kW5 * (uint32_t)(int32_t)r[5] + (uint32_t)kW7 * (uint32_t)(int32_t)r[7];
-    b1 += (uint32_t)(-kW1) * (uint32_t)(int32_t)r[5] + (uint32_t)(-kW5) * (uint32_t)(int32_t)r[7];
-    b2 += (uint32_t)kW7 * (uint32_t)(int32_t)r[5] + (uint32_t)kW3 * (uint32_t)(int32_t)r[7];
-    b3 += (uint32_t)kW3 * (uint32_t)(int32_t)r[5] + (uint32_t)(-kW1) * (uint32_t)(int32_t)r[7];
-  }
-  r[0] = (int16_t)((int32_t)(a0 + b0) >> 11);
-  r[7] = (int16_t)((int32_t)(a0 - b0) >> 11);
-  r[1] = (int16_t)((int32_t)(a1 + b1) >> 11);
-  r[6] = (int16_t)((int32_t)(a1 - b1) >> 11);
-  r[2] = (int16_t)((int32_t)(a2 + b2) >> 11);
-  r[5] = (int16_t)((int32_t)(a2 - b2) >> 11);
-  r[3] = (int16_t)((int32_t)(a3 + b3) >> 11);
-  r[4] = (int16_t)((int32_t)(a3 - b3) >> 11);
-}
-
-__device__ __forceinline__ void simple_col(const int16_t* c, uint8_t* o /* 8 rows, stride 8 */) {
-  uint32_t a0 = (uint32_t)kW4 * (uint32_t)(c[0] + ((1 << 19) / kW4));
-  uint32_t a1 = a0, a2 = a0, a3 = a0;
-  a0 += (uint32_t)kW2 * (uint32_t)(int32_t)c[16];
-  a1 += (uint32_t)kW6 * (uint32_t)(int32_t)c[16];
-  a2 += (uint32_t)(-kW6) * (uint32_t)(int32_t)c[16];
-  a3 += (uint32_t)(-kW2) * (uint32_t)(int32_t)c[16];
-  uint32_t b0 = (uint32_t)(kW1 * c[8]) + (uint32_t)kW3 * (uint32_t)(int32_t)c[24];
-  uint32_t b1 = (uint32_t)(kW3 * c[8]) + (uint32_t)(-kW7) * (uint32_t)(int32_t)c[24];
-  uint32_t b2 = (uint32_t)(kW5 * c[8]) + (uint32_t)(-kW1) * (uint32_t)(int32_t)c[24];
-  uint32_t b3 = (uint32_t)(kW7 * c[8]) + (uint32_t)(-kW5) * (uint32_t)(int32_t)c[24];
-  a0 += (uint32_t)kW4 * (uint32_t)(int32_t)c[32];
-  a1 += (uint32_t)(-kW4) * (uint32_t)(int32_t)c[32];
-  a2 += (uint32_t)(-kW4) * (uint32_t)(int32_t)c[32];
-  a3 += (uint32_t)kW4 * (uint32_t)(int32_t)c[32];
-  b0 += (uint32_t)kW5 * (uint32_t)(int32_t)c[40];
-  b1 += (uint32_t)(-kW1) * (uint32_t)(int32_t)c[40];
-  b2 += (uint32_t)kW7 * (uint32_t)(int32_t)c[40];
-  b3 += (uint32_t)kW3 * (uint32_t)(int32_t)c[40];
-  a0 += (uint32_t)kW6 * (uint32_t)(int32_t)c[48];
-  a1 += (uint32_t)(-kW2) * (uint32_t)(int32_t)c[48];
-  a2 += (uint32_t)kW2 * (uint32_t)(int32_t)c[48];
-  a3 += (uint32_t)(-kW6) * (uint32_t)(int32_t)c[48];
-  b0 += (uint32_t)kW7 * (uint32_t)(int32_t)c[56];
-  b1 += (uint32_t)(-kW5) * (uint32_t)(int32_t)c[56];
-  b2 += (uint32_t)kW3 * (uint32_t)(int32_t)c[56];
-  b3 += (uint32_t)(-kW1) * (uint32_t)(int32_t)c[56];
-  o[0] = clip_u8((int32_t)(a0 + b0) >> 20);
-  o[8] = clip_u8((int32_t)(a1 + b1) >> 20);
-  o[16] = clip_u8((int32_t)(a2 + b2) >> 20);
-  o[24] = clip_u8((int32_t)(a3 + b3) >> 20);
-  o[32] = clip_u8((int32_t)(a3 - b3) >> 20);
-  o[40] = clip_u8((int32_t)(a2 - b2) >> 20);
-  o[48] = clip_u8((int32_t)(a1 - b1) >> 20);
-  o[56] = clip_u8((int32_t)(a0 - b0) >> 20);
-}
-
-// IJG islow (see oracle/jpeg_oracle.c jo_idct_islow)
-constexpr int F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 = 7373,
-              F1175 = 9633, F1501 = 12299, F1847 = 15137, F1961 = 16069, F2053 = 16819,
-              F2562 = 20995, F3072 = 25172;
-
-__device__ __forceinline__ uint8_t islow_limit(int32_t x) {
-  const int v = (int)(x & 1023) - 384;
-  return (uint8_t)min(max(v, 0), 255);
-}
-
-__device__ __forceinline__ void islow_block(int16_t* in, uint8_t* out) {
-  int32_t ws[64];
-  in[0] = (int16_t)(in[0] - kDcBias);
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    const int16_t* p = in + c;
-    if (!(p[8] | p[16] | p[24] | p[32] | p[40] | p[48] | p[56])) {
-      const int32_t dc = (int32_t)p[0] * 4;
-#pragma unroll
-      for (int r = 0; r < 8; r++) ws[r * 8 + c] = dc;
-      continue;
-    }
-    int32_t z1, z2, z3, t0, t1, t2, t3, t10, t11, t12, t13;
-    z2 = (int32_t)p[0] * 8192 + (1 << 10);
-    z3 = (int32_t)p[32] * 8192;
-    t0 = z2 + z3;
-    t1 = z2 - z3;
-    z2 = p[16];
-    z3 = p[48];
-    z1 = (z2 + z3) * F0541;
-    t2 = z1 + z2 * F0765;
-    t3 = z1 - z3 * F1847;
-    t10 = t0 + t2;
-    t13 = t0 - t2;
-    t11 = t1 + t3;
-    t12 = t1 - t3;
-    t0 = p[56];
-    t1 = p[40];
-    t2 = p[24];
-    t3 = p[8];
-    z2 = t0 + t2;
-    z3 = t1 + t3;
-    z1 = (z2 + z3) * F1175;
-    z2 = z2 * -F1961 + z1;
-    z3 = z3 * -F0390 + z1;
-    z1 = (t0 + t3) * -F0899;
-    t0 = t0 * F0298 + z1 + z2;
-    t3 = t3 * F1501 + z1 + z3;
-    z1 = (t1 + t2) * -F2562;
-    t1 = t1 * F2053 + z1 + z3;
-    t2 = t2 * F3072 + z1 + z2;
-    ws[0 * 8 + c] = (t10 + t3) >> 11;
-    ws[7 * 8 + c] = (t10 - t3) >> 11;
-    ws[1 * 8 + c] = (t11 + t2) >> 11;
-    ws[6 * 8 + c] = (t11 - t2) >> 11;
-    ws[2 * 8 + c] = (t12 + t1) >> 11;
-    ws[5 * 8 + c] = (t12 - t1) >> 11;
-    ws[3 * 8 + c] = (t13 + t0) >> 11;
-    ws[4 * 8 + c] = (t13 - t0) >> 11;
-  }
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-    const int32_t* w = ws + r * 8;
-    uint8_t* o = out + r * 8;
-    int32_t z1, z2, z3, t0, t1, t2, t3, t10, t11, t12, t13;
-    z2 = w[0] + ((512 << 5) + (1 << 4));
-    if (!(w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7])) {
-      const uint8_t v = islow_limit(z2 >> 5);
-#pragma unroll
-      for (int i = 0; i < 8; i++) o[i] = v;
-      continue;
-    }
-    z3 = w[4];
-    t0 = (z2 + z3) * 8192;
-    t1 = (z2 - z3) * 8192;
-    z2 = w[2];
-    z3 = w[6];
-    z1 = (z2 + z3) * F0541;
-    t2 = z1 + z2 * F0765;
-    t3 = z1 - z3 * F1847;
-    t10 = t0 + t2;
-    t13 = t0 - t2;
-    t11 = t1 + t3;
-    t12 = t1 - t3;
-    t0 = w[7];
-    t1 = w[5];
-    t2 = w[3];
-    t3 = w[1];
-    z2 = t0 + t2;
-    z3 = t1 + t3;
-    z1 = (z2 + z3) * F1175;
-    z2 = z2 * -F1961 + z1;
-    z3 = z3 * -F0390 + z1;
-    z1 = (t0 + t3) * -F0899;
-    t0 = t0 * F0298 + z1 + z2;
-    t3 = t3 * F1501 + z1 + z3;
-    z1 = (t1 + t2) * -F2562;
-    t1 = t1 * F2053 + z1 + z3;
-    t2 = t2 * F3072 + z1 + z2;
-    o[0] = islow_limit((t10 + t3) >> 18);
-    o[7] = islow_limit((t10 - t3) >> 18);
-    o[1] = islow_limit((t11 + t2) >> 18);
-    o[6] = islow_limit((t11 - t2) >> 18);
-    o[2] = islow_limit((t12 + t1) >> 18);
-    o[5] = islow_limit((t12 - t1) >> 18);
-    o[3] = islow_limit((t13 + t0) >> 18);
-    o[4] = islow_limit((t13 - t0) >> 18);
-  }
-}
-
 template <int IDCT>
 __global__ void __launch_bounds__(256) idct_kernel(const int16_t* __restrict__ coefs,
                                                    const ImageDesc* __restrict__ desc,
@@ -1062,7 +873,7 @@ __global__ void __launch_bounds__(256) idct_kernel(const int16_t* __restrict__ c
     bx = mx * in.comp_h[c] + in.mcu_dx[b];
     by = my * in.comp_v[c] + in.mcu_dy[b];
   }
-  int16_t blk[64];
+  int32_t blk[64];
   const uint4* src = reinterpret_cast<const uint4*>(coefs + ((size_t)dd.coef_off + j) * 64);
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -1070,11 +881,11 @@ __global__ void __launch_bounds__(256) idct_kernel(const int16_t* __restrict__ c
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      blk[8 * i + 2 * k] = (int16_t)(w[k] & 0xFFFF);
-      blk[8 * i + 2 * k + 1] = (int16_t)(w[k] >> 16);
+      blk[8 * i + 2 * k] = sext16(w[k]);
+      blk[8 * i + 2 * k + 1] = sext16(w[k] >> 16);
     }
   }
-  uint8_t px[64];
+  int32_t px[64];
   if (IDCT == 0) {
 #pragma unroll
     for (int i = 0; i < 8; i++) simple_row(blk + 8 * i);
@@ -1100,7 +911,7 @@ __global__ void __launch_bounds__(256) idct_kernel(const int16_t* __restrict__ c
 // colour conversion (IJG jdcolor.c / jdmerge.c integer tables, SCALEBITS 16)
 // ---------------------------------------------------------------------------
 
-constexpr int32_t kFix1402 = 91881, kFix1772 = 116130, kFix0714 = 46802, kFix0344 = 22554;
+constexpr int32_t kFix1402 = 91881, kFix1772 = 116130, kFix0714 = 46802, kFix0344 = 22553;
 
 __device__ __forceinline__ void ycc_rgb(int y, int cb, int cr, int* rgb) {
   const int32_t x_cb = cb - 128, x_cr = cr - 128;
