@@ -22,6 +22,20 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* Per-thread grow-only scratch buffers: the batch driver decodes many images
+ * per thread, and fresh multi-MB mallocs per image page-fault under the
+ * process-wide mm lock, which serialises the threads. */
+static __thread void* tl_buf[12];
+static __thread size_t tl_cap[12];
+static void* scratch(int slot, size_t n) {
+  if (tl_cap[slot] < n) {
+    free(tl_buf[slot]);
+    tl_buf[slot] = malloc(n);
+    tl_cap[slot] = tl_buf[slot] ? n : 0;
+  }
+  return tl_buf[slot];
+}
+
 static const uint8_t kNatural[64 + 16] = {
     0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
     12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
@@ -725,13 +739,10 @@ static void plane_ptrs(const jo_info* info, const uint8_t* planes, const uint8_t
 
 static int decode_planes_info(const uint8_t* d, size_t size, const jo_info* info, int idct,
                               uint8_t* planes) {
-  int16_t* coefs = (int16_t*)malloc((size_t)info->nblocks * 64 * sizeof(int16_t));
+  int16_t* coefs = (int16_t*)scratch(0, (size_t)info->nblocks * 64 * sizeof(int16_t));
   if (!coefs) return JO_ERR_BAD_HEADER;
   int rc = jo_decode_coefs(d, size, info, coefs, NULL);
-  if (rc) {
-    free(coefs);
-    return rc;
-  }
+  if (rc) return rc;
   const uint8_t* pc[JO_MAX_COMP];
   int st[JO_MAX_COMP];
   plane_ptrs(info, planes, pc, st);
@@ -750,7 +761,6 @@ static int decode_planes_info(const uint8_t* d, size_t size, const jo_info* info
         jo_idct_simple(blk, dst, st[c]);
     }
   }
-  free(coefs);
   return JO_OK;
 }
 
@@ -830,11 +840,10 @@ int jo_decode_rgb(const uint8_t* d, size_t size, int idct, int fmt, uint8_t* out
   jo_info info;
   int rc = jo_parse(d, size, &info);
   if (rc) return rc;
-  uint8_t* planes = (uint8_t*)malloc(jo_planes_size(&info));
+  uint8_t* planes = (uint8_t*)scratch(1, jo_planes_size(&info));
   if (!planes) return JO_ERR_BAD_HEADER;
   rc = decode_planes_info(d, size, &info, idct, planes);
   if (!rc) rc = planes_to_rgb(&info, planes, fmt, out);
-  free(planes);
   return rc;
 }
 
@@ -986,11 +995,11 @@ uint16_t jo_f32_to_f16(float f) {
 static int resize_plane(const uint8_t* src, int pw, int ph, int st, int sw, int sh, int filter,
                         uint8_t* dst) {
   int mtx = jo_max_taps(pw, sw, filter), mty = jo_max_taps(ph, sh, filter);
-  int32_t* fx = (int32_t*)malloc(sizeof(int32_t) * sw);
-  int16_t* wx = (int16_t*)malloc(sizeof(int16_t) * (size_t)sw * mtx);
-  int32_t* fy = (int32_t*)malloc(sizeof(int32_t) * sh);
-  int16_t* wy = (int16_t*)malloc(sizeof(int16_t) * (size_t)sh * mty);
-  int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * (size_t)ph * sw);
+  int32_t* fx = (int32_t*)scratch(2, sizeof(int32_t) * sw);
+  int16_t* wx = (int16_t*)scratch(3, sizeof(int16_t) * (size_t)sw * mtx);
+  int32_t* fy = (int32_t*)scratch(4, sizeof(int32_t) * sh);
+  int16_t* wy = (int16_t*)scratch(5, sizeof(int16_t) * (size_t)sh * mty);
+  int32_t* tmp = (int32_t*)scratch(6, sizeof(int32_t) * (size_t)ph * sw);
   int rc = JO_OK;
   if (!fx || !wx || !fy || !wy || !tmp) {
     rc = JO_ERR_BAD_GEOMETRY;
@@ -1024,11 +1033,6 @@ static int resize_plane(const uint8_t* src, int pw, int ph, int st, int sw, int 
       dst[(size_t)y * sw + x] = clip_u8((acc + (1 << 19)) >> 20);
     }
 done:
-  free(fx);
-  free(wx);
-  free(fy);
-  free(wy);
-  free(tmp);
   return rc;
 }
 
@@ -1044,11 +1048,10 @@ int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize
   plane_ptrs(info, planes, pc, st);
   uint8_t* rp[JO_MAX_COMP] = {0};
   for (int c = 0; c < info->ncomp; c++) {
-    rp[c] = (uint8_t*)malloc((size_t)g.sw * g.sh);
+    rp[c] = (uint8_t*)scratch(7 + c, (size_t)g.sw * g.sh);
     if (!rp[c] || (rc = resize_plane(pc[c], info->comp_w[c], info->comp_h_px[c], st[c], g.sw,
                                      g.sh, rs->filter, rp[c]))) {
       if (!rc) rc = JO_ERR_BAD_GEOMETRY;
-      for (int k = 0; k <= c; k++) free(rp[k]);
       return rc;
     }
   }
@@ -1081,7 +1084,6 @@ int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize
         }
       }
     }
-  for (int c = 0; c < info->ncomp; c++) free(rp[c]);
   return JO_OK;
 }
 
@@ -1091,11 +1093,10 @@ int jo_decode_resize(const uint8_t* d, size_t size, int idct, const jo_resize* r
   jo_info info;
   int rc = jo_parse(d, size, &info);
   if (rc) return rc;
-  uint8_t* planes = (uint8_t*)malloc(jo_planes_size(&info));
+  uint8_t* planes = (uint8_t*)scratch(1, jo_planes_size(&info));
   if (!planes) return JO_ERR_BAD_HEADER;
   rc = decode_planes_info(d, size, &info, idct, planes);
   if (!rc) rc = jo_resize_planes(&info, planes, rs, fmt, dtype, mean, stdv, out, geom_out);
-  free(planes);
   return rc;
 }
 
