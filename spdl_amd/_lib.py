@@ -294,7 +294,7 @@ class Decoder:
         b = (ctypes.c_char * len(mv)).from_buffer_copy(mv)
         coefs = np.zeros((nblocks, 64), np.int16)
         clean = np.zeros(len(mv), np.uint8)
-        diag = np.zeros(4, np.int32)
+        diag = np.zeros(12, np.int32)
         err = ctypes.create_string_buffer(1024)
         rc = lib().spdl_hj_debug_entropy(self._h, ctypes.addressof(b), len(mv), coefs.ctypes.data,
                                          coefs.size, clean.ctypes.data, clean.size,
@@ -303,7 +303,9 @@ class Decoder:
             raise RuntimeError(err.value.decode())
         return coefs, clean[: max(int(diag[1]), 0)], {
             "status": int(diag[0]), "clean_len": int(diag[1]), "nseg": int(diag[2]),
-            "sync_rounds": int(diag[3])}
+            "sync_rounds": int(diag[3]),
+            "phase_us": [round(int(x) / 100.0, 1) for x in diag[4:8]],
+            "dbg": [int(x) for x in diag[8:12]]}
 
     def decode_planes(self, data, idct: str = "simple", stream=None):
         import numpy as np

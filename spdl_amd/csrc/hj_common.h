@@ -24,13 +24,18 @@ constexpr int kDcBias = 1024;  // FFmpeg mjpegdec last_dc start value (4 << bits
 constexpr int kMaxTaps = 128;
 
 // LUT entry (u32): [0:5) nbits consumed, [5:7) kind, [8:16) symbol,
-// [16:32) value (int16, kind==2 only)
-constexpr uint32_t kKindSlow = 0;  // code longer than kLutBits (or invalid)
+// [16:32) value (int16, kind==Full) or sub-table index (kind==Sub)
+constexpr uint32_t kKindSlow = 0;  // invalid, or a sub-table that did not fit
 constexpr uint32_t kKindCode = 1;  // code resolved, value bits follow
 constexpr uint32_t kKindFull = 2;  // code + value resolved
+constexpr uint32_t kKindSub = 3;   // code longer than kLutBits: look up sub[idx][next 6 bits]
+constexpr int kSubBits = 16 - kLutBits;
+constexpr int kMaxSub = 16;        // 64-entry sub-tables per Huffman table
 
 struct HuffTable {
   uint32_t lut[kLutSize];
+  uint32_t sub[kMaxSub << kSubBits];  // second level for codes of 11..16 bits
+  int32_t nsub;
   int32_t maxcode[18];  // max code of length l (-1 if none), [17] sentinel
   int32_t valoff[17];
   uint8_t vals[256];
@@ -69,6 +74,8 @@ struct ImageInfo {      // device-filled by the parse kernel
   int32_t clean_len;    // destuffed bytes
   int32_t sync_rounds;  // diagnostics: rounds the Huffman sync took
   int32_t pad_;
+  int64_t tphase[4];    // diagnostics: wall_clock64 ticks of the entropy phases
+  int64_t dbg[4];       // diagnostics: symbols (round 0), wave iterations, shader clocks, rt ticks
 };
 
 struct BatchParams {

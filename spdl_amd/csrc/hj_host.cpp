@@ -706,6 +706,8 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   diag[1] = hi.clean_len;
   diag[2] = hi.nseg;
   diag[3] = hi.sync_rounds;
+  for (int i = 0; i < 4; i++) diag[4 + i] = (int32_t)hi.tphase[i];
+  for (int i = 0; i < 4; i++) diag[8 + i] = (int32_t)hi.dbg[i];
   size_t nc = (size_t)L.desc[0].nblocks * 64;
   if (coefs) HJ_HIP(hipMemcpy(coefs, ctx->coefs.p, 2 * (nc < coef_cap ? nc : coef_cap),
                               hipMemcpyDeviceToHost));

@@ -257,31 +257,58 @@ __global__ void __launch_bounds__(256) parse_kernel(const uint8_t* __restrict__ 
   for (int t = 0; t < 8; t++) {
     if (!s.have[t]) continue;
     const bool is_dc = t < 4;
-    for (int idx = tid; idx < kLutSize; idx += blockDim.x) {
-      uint32_t e = 0;  // kKindSlow
-      for (int l = 1; l <= kLutBits; l++) {
-        int code = idx >> (kLutBits - l);
+    // canonical codes are consecutive: the 10-bit prefixes of all codes longer
+    // than kLutBits form one contiguous range [p_lo, p_hi]
+    int p_lo = kLutSize, p_hi = -1;
+    for (int l = kLutBits + 1; l <= 16; l++) {
+      if (s.bits[t][l] == 0) continue;
+      const int first = s.maxcode[t][l] - s.bits[t][l] + 1;
+      p_lo = min(p_lo, first >> (l - kLutBits));
+      p_hi = max(p_hi, s.maxcode[t][l] >> (l - kLutBits));
+    }
+    const int nsub = p_hi >= p_lo ? p_hi - p_lo + 1 : 0;
+    const bool sub_ok = nsub <= kMaxSub;
+    // one 16-bit window -> entry (levels share this)
+    auto entry16 = [&](uint32_t w16, int max_len) -> uint32_t {
+      for (int l = 1; l <= max_len; l++) {
+        const int code = (int)(w16 >> (16 - l));
         if (code <= s.maxcode[t][l]) {
-          int sym = s.vals[t][s.valoff[t][l] + code];
-          int sz = is_dc ? sym : (sym & 15);
-          if (is_dc && sym > 15) {
-            e = (uint32_t)l | (kKindCode << 5) | ((uint32_t)sym << 8);
-          } else if (l + sz <= kLutBits) {
+          const int sym = s.vals[t][s.valoff[t][l] + code];
+          const int sz = is_dc ? sym : (sym & 15);
+          if (is_dc && sym > 15) return 0u;  // invalid size -> slow path reports it
+          if (l + sz <= 16) {
             int v = 0;
             if (sz) {
-              int raw = (idx >> (kLutBits - l - sz)) & ((1 << sz) - 1);
+              const int raw = (int)((w16 >> (16 - l - sz)) & ((1u << sz) - 1));
               v = raw < (1 << (sz - 1)) ? raw - ((1 << sz) - 1) : raw;
             }
-            e = (uint32_t)(l + sz) | (kKindFull << 5) | ((uint32_t)sym << 8) |
-                ((uint32_t)(uint16_t)(int16_t)v << 16);
-          } else {
-            e = (uint32_t)l | (kKindCode << 5) | ((uint32_t)sym << 8);
+            return (uint32_t)(l + sz) | (kKindFull << 5) | ((uint32_t)sym << 8) |
+                   ((uint32_t)(uint16_t)(int16_t)v << 16);
           }
-          break;
+          return (uint32_t)l | (kKindCode << 5) | ((uint32_t)sym << 8);
         }
       }
+      return 0u;
+    };
+    for (int idx = tid; idx < kLutSize; idx += blockDim.x) {
+      // level 1 resolves codes (and code+value) that fit in kLutBits
+      uint32_t e = entry16((uint32_t)idx << kSubBits, kLutBits);
+      if ((e >> 5 & 3) == kKindFull && (e & 31) > kLutBits) {
+        // value bits beyond the level-1 window: keep the code, read the value later
+        const uint32_t sym = (e >> 8) & 0xFF;
+        const int sz = is_dc ? (int)sym : (int)(sym & 15);
+        e = (uint32_t)((e & 31) - sz) | (kKindCode << 5) | (sym << 8);
+      }
+      if (e == 0u && idx >= p_lo && idx <= p_hi)
+        e = sub_ok ? ((kKindSub << 5) | ((uint32_t)(idx - p_lo) << 16)) : 0u;
       tabs[t].lut[idx] = e;
     }
+    if (sub_ok)
+      for (int i = tid; i < nsub << kSubBits; i += blockDim.x)
+        tabs[t].sub[i] = entry16(((uint32_t)(p_lo + (i >> kSubBits)) << kSubBits) |
+                                     (uint32_t)(i & ((1 << kSubBits) - 1)),
+                                 16);
+    if (tid == 0) tabs[t].nsub = sub_ok ? nsub : 0;
     for (int i = tid; i < 18; i += blockDim.x) tabs[t].maxcode[i] = s.maxcode[t][i];
     for (int i = tid; i < 17; i += blockDim.x) tabs[t].valoff[i] = s.valoff[t][i];
     for (int i = tid; i < 256; i += blockDim.x) tabs[t].vals[i] = s.vals[t][i];
@@ -407,8 +434,11 @@ constexpr int kEnThreads = 256;
 constexpr int kMaxSlots = 2048;
 constexpr int kMaxLds = 6;  // distinct tables held in LDS
 
+constexpr int kSubPool = 2048;  // LDS entries for second-level tables of all tables
+
 struct EntShared {
   uint32_t lut[kMaxLds][kLutSize];
+  uint32_t sub[kSubPool];
   int32_t maxcode[kMaxLds][18];
   int32_t valoff[kMaxLds][17];
   uint8_t vals[kMaxLds][256];
@@ -421,74 +451,68 @@ struct EntShared {
   int32_t scan_flag[kEnThreads];
   int32_t scan_v[kEnThreads][4];  // blk, dc0, dc1, dc2
   uint16_t qt[kMaxComp][64];
+  uint8_t nat[64];
   int32_t tdc[kMaxBpm], tac[kMaxBpm], bcomp[kMaxBpm];
   int32_t red[kEnThreads];
   int32_t flag;
   int32_t err;
 };
 
-struct BitReader {
+// Per-thread bit reader over the destuffed stream (big-endian bytes read as
+// 32-bit words).  `buf` holds the next 33..64 bits MSB-first; `nxt` is the
+// following word, loaded one refill ahead so its latency overlaps ~5 symbols.
+struct Dec {
   const uint32_t* w;
   uint64_t buf;
+  uint32_t nxt;
   uint32_t wi;
   int cnt;
-  uint32_t pos;
-  __device__ __forceinline__ void init(const uint32_t* words, uint32_t p) {
-    w = words;
-    wi = p >> 5;
-    const uint64_t hi = __builtin_bswap32(w[wi]), lo = __builtin_bswap32(w[wi + 1]);
-    buf = ((hi << 32) | lo) << (p & 31);
-    cnt = 64 - (int)(p & 31);
-    wi += 2;
-    pos = p;
-  }
-  __device__ __forceinline__ void refill() {
-    if (cnt <= 32) {
-      buf |= (uint64_t)__builtin_bswap32(w[wi++]) << (32 - cnt);
-      cnt += 32;
-    }
-  }
-  __device__ __forceinline__ uint32_t peek(int n) const { return (uint32_t)(buf >> (64 - n)); }
-  __device__ __forceinline__ void skip(int n) {
-    buf <<= n;
-    cnt -= n;
-    pos += (uint32_t)n;
-  }
+  uint32_t pos;  // absolute bit position of buf's MSB
+  int z, b;      // next coefficient index (0 = DC), block-in-MCU
 };
 
-// Decode one Huffman symbol with table t; returns symbol, sets nbits consumed
-// through the fused value path: on kind==Full, `fullv` receives the value
-// and `consumed` includes the value bits.  Returns -1 for an invalid code
-// (nothing consumed).
-__device__ __forceinline__ int huff_sym(const EntShared& S, int t, BitReader& br, int& vbits,
-                                        int& fullv, bool& full) {
-  const uint32_t e = S.lut[t][br.peek(kLutBits)];
-  const uint32_t kind = (e >> 5) & 3;
-  if (kind == kKindFull) {
-    full = true;
-    fullv = (int)e >> 16;
-    vbits = 0;
-    br.skip((int)(e & 31));
-    return (int)((e >> 8) & 0xFF);
-  }
-  full = false;
-  if (kind == kKindCode) {
-    br.skip((int)(e & 31));
-    return (int)((e >> 8) & 0xFF);
-  }
-  const uint32_t w16 = br.peek(16);
-  for (int l = kLutBits + 1; l <= 16; l++) {
-    const int code = (int)(w16 >> (16 - l));
-    if (code <= S.maxcode[t][l]) {
-      br.skip(l);
-      return S.vals[t][S.valoff[t][l] + code];
-    }
-  }
-  return -1;
+__device__ __forceinline__ void dec_init(Dec& d, const uint32_t* words, uint32_t p, int z, int b) {
+  d.w = words;
+  const uint32_t wi = p >> 5;
+  const uint64_t hi = __builtin_bswap32(words[wi]), lo = __builtin_bswap32(words[wi + 1]);
+  d.buf = ((hi << 32) | lo) << (p & 31);
+  d.cnt = 64 - (int)(p & 31);
+  d.nxt = words[wi + 2];
+  d.wi = wi + 3;
+  d.pos = p;
+  d.z = z;
+  d.b = b;
 }
 
-__device__ __forceinline__ int extend_bits(uint32_t v, int s) {
-  return (v < (1u << (s - 1))) ? (int)v - ((1 << s) - 1) : (int)v;
+__device__ __forceinline__ void dec_refill(Dec& d) {
+  if (d.cnt <= 32) {
+    d.buf |= (uint64_t)__builtin_bswap32(d.nxt) << (32 - d.cnt);
+    d.cnt += 32;
+    d.nxt = d.w[d.wi++];
+  }
+}
+
+// block-in-MCU -> (dc table, ac table, component), packed 8 bits per block in
+// three wave-uniform words
+__device__ __forceinline__ uint32_t binfo(int b, uint32_t w0, uint32_t w1, uint32_t w2) {
+  const uint32_t w = b < 4 ? w0 : (b < 8 ? w1 : w2);
+  return (w >> ((b & 3) * 8)) & 0xFF;
+}
+
+// Canonical decode of a code that is not fully resolved by the LUT (longer
+// than kLutBits, or a DC size > 15): returns a kKindCode entry, 0 if invalid.
+__device__ __attribute__((noinline)) uint32_t slow_symbol(const EntShared& S, int t, uint64_t buf,
+                                                          bool is_dc) {
+  const uint32_t w16 = (uint32_t)(buf >> 48);
+  for (int l = 1; l <= 16; l++) {
+    const int code = (int)(w16 >> (16 - l));
+    if (code <= S.maxcode[t][l]) {
+      const int sym = S.vals[t][S.valoff[t][l] + code];
+      if (is_dc && sym > 15) return 0;
+      return (uint32_t)l | (kKindCode << 5) | ((uint32_t)sym << 8);
+    }
+  }
+  return 0;
 }
 
 struct WriteCtx {
@@ -499,81 +523,87 @@ struct WriteCtx {
   uint32_t seg_end_bits;
 };
 
-// Decode every symbol that starts in [br.pos, end).  Sync mode (WRITE=false)
-// is total: invalid codes consume one bit, out-of-range runs end the block,
-// so any bit position yields a deterministic trajectory.  Write mode stops at
-// the segment's last block and reports corruption.
+// Decode every symbol that starts in [d.pos, end).  One path for DC and AC
+// symbols (selects instead of branches: lanes of a wave decode different
+// streams, so any branch is paid by the whole wave).  Sync mode
+// (WRITE=false) is total -- invalid codes consume one bit, runs past
+// coefficient 63 end the block -- so every bit position yields one
+// deterministic trajectory; it accumulates blocks started and DC diffs.
+// Write mode stores dequantised coefficients, stops after the segment's last
+// block and reports corruption.
 template <bool WRITE>
-__device__ int decode_range(const EntShared& S, BitReader& br, int& z, int& b, const int bpm,
-                            const uint32_t end, int& nblk, int* dcs, WriteCtx* wc) {
-  while (br.pos < end) {
-    if (WRITE && z == 0 && wc->nb >= wc->seg_end_blk) return kOk;
-    br.refill();
-    const int c = S.bcomp[b];
-    int vb, fv;
-    bool full;
-    if (z == 0) {
-      const int s = huff_sym(S, S.tdc[b], br, vb, fv, full);
-      if (s < 0 || s > 15) {
+__device__ int decode_range(const EntShared& S, Dec& d, const uint32_t bw0, const uint32_t bw1,
+                            const uint32_t bw2, const int bpm, const uint32_t end, int& nblk,
+                            int& dc0, int& dc1, int& dc2, WriteCtx* wc, int* nsym = nullptr) {
+  uint32_t info = binfo(d.b, bw0, bw1, bw2);
+  while (d.pos < end) {
+    if (nsym) (*nsym)++;
+    if (WRITE && d.z == 0 && wc->nb >= wc->seg_end_blk) return kOk;
+    dec_refill(d);
+    const bool is_dc = d.z == 0;
+    const int t = is_dc ? (int)(info & 7) : (int)((info >> 3) & 7);
+    const int c = (int)(info >> 6);
+    uint32_t e = S.lut[t][(uint32_t)(d.buf >> (64 - kLutBits))];
+    if (((e >> 5) & 3) == kKindSub)
+      e = S.sub[((e >> 16) << kSubBits) + (uint32_t)((d.buf >> (48)) & ((1u << kSubBits) - 1))];
+    if (((e >> 5) & 3) == kKindSlow) {
+      e = slow_symbol(S, t, d.buf, is_dc);
+      if (e == 0) {
         if (WRITE) return kErrBadHuffman;
-        br.skip(1);
+        d.buf <<= 1;
+        d.cnt -= 1;
+        d.pos += 1;
         continue;
-      }
-      int diff = 0;
-      if (full) {
-        diff = fv;
-      } else if (s) {
-        diff = extend_bits(br.peek(s), s);
-        br.skip(s);
-      }
-      if (WRITE) {
-        const int blk = wc->nb++;
-        wc->dc[c] += diff;
-        const uint32_t v = (uint32_t)kDcBias + (uint32_t)S.qt[c][0] * (uint32_t)wc->dc[c];
-        const int32_t vi = (int32_t)v;
-        wc->coef[(size_t)blk * 64] = (int16_t)(vi < -32768 ? -32768 : vi > 32767 ? 32767 : vi);
-      } else {
-        nblk++;
-        dcs[c] += diff;
-      }
-      z = 1;
-    } else {
-      const int rs = huff_sym(S, S.tac[b], br, vb, fv, full);
-      if (rs < 0) {
-        if (WRITE) return kErrBadHuffman;
-        br.skip(1);
-        continue;
-      }
-      const int r = rs >> 4, s = rs & 15;
-      if (s == 0) {
-        if (r == 15) {
-          z += 16;
-        } else {
-          if (WRITE && r != 0) return kErrBadHuffman;
-          z = 64;
-        }
-      } else {
-        z += r;
-        int v = fv;
-        if (!full) {
-          v = extend_bits(br.peek(s), s);
-          br.skip(s);
-        }
-        if (z > 63) {
-          if (WRITE) return kErrBadHuffman;
-          z = 64;
-        } else {
-          if (WRITE)
-            wc->coef[(size_t)(wc->nb - 1) * 64 + kNat[z]] = (int16_t)(v * (int)S.qt[c][z]);
-          z++;
-        }
-      }
-      if (z >= 64) {
-        z = 0;
-        b = (b + 1 == bpm) ? 0 : b + 1;
       }
     }
-    if (WRITE && br.pos > wc->seg_end_bits) return kErrTruncated;
+    const uint32_t len = e & 31, sym = (e >> 8) & 0xFF;
+    const bool full = ((e >> 5) & 3) == kKindFull;
+    const uint32_t sz = full ? 0u : (is_dc ? sym : (sym & 15u));
+    const uint64_t rest = d.buf << len;
+    const uint32_t raw = (uint32_t)((rest >> 1) >> (63 - sz));  // top sz bits, 0 if sz==0
+    const uint32_t half = (1u << sz) >> 1;
+    const int vx = (int)raw - (raw < half ? (int)((1u << sz) - 1u) : 0);
+    const int v = full ? (int)(int16_t)(e >> 16) : vx;
+    const uint32_t nbits = len + sz;
+    d.buf <<= nbits;
+    d.cnt -= (int)nbits;
+    d.pos += nbits;
+    const int r = is_dc ? 0 : (int)(sym >> 4);
+    const bool coef = is_dc || (sym & 15u) != 0;
+    const int zpos = d.z + r;
+    const bool bad_run = coef && zpos > 63;
+    int zn = coef ? zpos + 1 : (r == 15 ? d.z + 16 : 64);
+    zn = bad_run ? 64 : zn;
+    if (WRITE) {
+      if (bad_run || (!coef && r != 0 && r != 15)) return kErrBadHuffman;
+      const int zp = zpos & 63;
+      const int qv = S.qt[c][zp];
+      const int cur = c == 0 ? wc->dc[0] : (c == 1 ? wc->dc[1] : wc->dc[2]);
+      const int ndc = cur + v;
+      const uint32_t dq = (uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc;
+      const int32_t dqi = (int32_t)dq;
+      const int16_t val = is_dc ? (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi))
+                                : (int16_t)(v * qv);
+      const int blk = is_dc ? wc->nb : wc->nb - 1;
+      if (coef) wc->coef[(size_t)blk * 64 + S.nat[zp]] = val;
+      if (is_dc) {
+        wc->nb++;
+        if (c == 0) wc->dc[0] = ndc;
+        else if (c == 1) wc->dc[1] = ndc;
+        else wc->dc[2] = ndc;
+      }
+    } else {
+      nblk += is_dc ? 1 : 0;
+      dc0 += (is_dc && c == 0) ? v : 0;
+      dc1 += (is_dc && c == 1) ? v : 0;
+      dc2 += (is_dc && c == 2) ? v : 0;
+    }
+    const bool bend = zn >= 64;
+    const int bn = (d.b + 1 == bpm) ? 0 : d.b + 1;
+    d.z = bend ? 0 : zn;
+    d.b = bend ? bn : d.b;
+    info = binfo(d.b, bw0, bw1, bw2);
+    if (WRITE && d.pos > wc->seg_end_bits) return kErrTruncated;
   }
   return kOk;
 }
@@ -599,11 +629,11 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
   const int nseg = ri > 0 ? (nmcu + ri - 1) / ri : 1;
 
   // ---- tables into LDS (dedup table slots per component) ----
-  int ldc[kMaxComp], lac[kMaxComp];
+  uint32_t bw[3] = {0, 0, 0};
   {
-    int slots[kMaxLds], ns = 0;
+    int slots[kMaxLds], ns = 0, ldc[kMaxComp] = {0, 0, 0}, lac[kMaxComp] = {0, 0, 0};
     for (int c = 0; c < in.ncomp; c++) {
-      int want[2] = {in.dc_tab[c], 4 + in.ac_tab[c]};
+      const int want[2] = {in.dc_tab[c], 4 + in.ac_tab[c]};
       for (int k = 0; k < 2; k++) {
         int f = -1;
         for (int i = 0; i < ns; i++)
@@ -616,19 +646,31 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       }
     }
     const HuffTable* tabs = luts + (size_t)img * 8;
+    int pool = 0;  // in units of 64-entry sub-tables
     for (int i = 0; i < ns; i++) {
       const HuffTable& T = tabs[slots[i]];
-      for (int k = tid; k < kLutSize; k += kEnThreads) S.lut[i][k] = T.lut[k];
+      const int nsub = T.nsub;
+      const bool fits = (pool + nsub) << kSubBits <= kSubPool;
+      const int base = pool;
+      if (fits) pool += nsub;
+      for (int k = tid; k < kLutSize; k += kEnThreads) {
+        uint32_t e = T.lut[k];
+        if ((e >> 5 & 3) == kKindSub) e = fits ? e + ((uint32_t)base << 16) : 0u;
+        S.lut[i][k] = e;
+      }
+      if (fits)
+        for (int k = tid; k < nsub << kSubBits; k += kEnThreads)
+          S.sub[(base << kSubBits) + k] = T.sub[k];
       if (tid < 18) S.maxcode[i][tid] = T.maxcode[tid];
       if (tid < 17) S.valoff[i][tid] = T.valoff[tid];
       S.vals[i][tid] = T.vals[tid];
     }
     for (int k = tid; k < kMaxComp * 64; k += kEnThreads) S.qt[k / 64][k % 64] = in.qt[k / 64][k % 64];
-    if (tid < bpm) {
-      const int c = in.mcu_comp[tid];
-      S.bcomp[tid] = c;
-      S.tdc[tid] = ldc[c];
-      S.tac[tid] = lac[c];
+    if (tid < 64) S.nat[tid] = kNat[tid];
+    for (int b = 0; b < bpm; b++) {
+      const int c = in.mcu_comp[b];
+      const uint32_t v = (uint32_t)ldc[c] | ((uint32_t)lac[c] << 3) | ((uint32_t)c << 6);
+      bw[b >> 2] |= v << ((b & 3) * 8);
     }
     if (tid == 0) S.err = kOk;
   }
@@ -646,7 +688,7 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
   // ---- subsequence size: keep every segment within kMaxSlots slots ----
   uint32_t maxbits = 0;
   for (int s = tid; s < nseg; s += kEnThreads) {
-    uint32_t a = seg_start_bits(s), e = seg_end_bits(s);
+    const uint32_t a = seg_start_bits(s), e = seg_end_bits(s);
     maxbits = max(maxbits, e > a ? e - a : 0u);
   }
   S.red[tid] = (int32_t)maxbits;
@@ -667,13 +709,18 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
   const int seg_per_chunk = max(1, kMaxSlots / cmax);
   int16_t* coef_img = coefs + (size_t)dd.coef_off * 64;
   int rounds_total = 0;
+  __shared__ int dbg_sh[2];
+  int64_t dbg_acc[4] = {0, 0, 0, 0};
+  if (tid < 2) dbg_sh[tid] = 0;
+  __syncthreads();
+  int64_t tph[4] = {0, 0, 0, 0};
+  int64_t tstamp = wall_clock64();
 
   for (int seg_lo = 0; seg_lo < nseg; seg_lo += seg_per_chunk) {
     const int nsc = min(seg_per_chunk, nseg - seg_lo);
     const int nslots = nsc * cmax;
     const int K = (nslots + kEnThreads - 1) / kEnThreads;
     const int r0 = min(tid * K, nslots), r1 = min(r0 + K, nslots);
-    // slot geometry helpers
     auto slot_seg = [&](int k) { return seg_lo + k / cmax; };
     auto slot_j = [&](int k) { return k % cmax; };
     auto slot_start = [&](int k) { return seg_start_bits(slot_seg(k)) + (uint32_t)slot_j(k) * N; };
@@ -687,33 +734,52 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
     auto slot_known = [&](int k) { return slot_j(k) == 0; };
 
     // ---- round 0: every run from a guess at its first slot ----
+    int nsym0 = 0;
+    const int64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = wall_clock64();
     {
-      BitReader br;
-      int z = 0, b = 0;
+      Dec d;
+      d.pos = 0;
+      d.z = d.b = 0;
       bool have = false;
       for (int k = r0; k < r1; k++) {
         if (slot_empty(k)) {
           have = false;
           continue;
         }
-        if (slot_known(k) || !have) {
-          z = 0;
-          b = 0;
-          br.init(words, slot_start(k));
-        }
-        S.s_pos[k] = br.pos;
-        S.s_zb[k] = (uint32_t)z | ((uint32_t)b << 8);
-        int nblk = 0, dcs[kMaxComp] = {0, 0, 0};
-        decode_range<false>(S, br, z, b, bpm, slot_end(k), nblk, dcs, nullptr);
+        if (slot_known(k) || !have) dec_init(d, words, slot_start(k), 0, 0);
+        S.s_pos[k] = d.pos;
+        S.s_zb[k] = (uint32_t)d.z | ((uint32_t)d.b << 8);
+        int nblk = 0, c0 = 0, c1 = 0, c2 = 0;
+        decode_range<false>(S, d, bw[0], bw[1], bw[2], bpm, slot_end(k), nblk, c0, c1, c2, nullptr,
+                            &nsym0);
         S.s_nblk[k] = nblk;
-        for (int c = 0; c < kMaxComp; c++) S.s_dc[k][c] = dcs[c];
+        S.s_dc[k][0] = c0;
+        S.s_dc[k][1] = c1;
+        S.s_dc[k][2] = c2;
         have = true;
       }
-      S.run_pos[tid] = br.pos;
-      S.run_zb[tid] = have ? ((uint32_t)z | ((uint32_t)b << 8)) : 0xFFFFFFFFu;
-      if (r0 >= r1) S.run_zb[tid] = 0xFFFFFFFFu;
+      S.run_pos[tid] = d.pos;
+      S.run_zb[tid] = (have && r0 < r1) ? ((uint32_t)d.z | ((uint32_t)d.b << 8)) : 0xFFFFFFFFu;
     }
-    // ---- sync rounds ----
+    __syncthreads();
+    {
+      const int64_t t = wall_clock64();
+      tph[0] += t - tstamp;
+      tstamp = t;
+      const int64_t clk1 = __builtin_amdgcn_s_memtime();
+      // per-wave max symbols (= wave iterations) and total symbols
+      int wmax = nsym0;
+      for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
+      atomicAdd(&S.red[0], 0);
+      if (tid == 0) {
+        dbg_acc[2] = clk1 - clk0;
+        dbg_acc[3] = t - rt0;
+      }
+      atomicAdd((int*)&dbg_sh[0], nsym0);
+      if ((tid & 63) == 0) atomicAdd((int*)&dbg_sh[1], wmax);
+    }
+    // ---- sync rounds: re-decode a run from its left neighbour's end state
+    // until the trajectory merges with the stored one at a slot boundary ----
     int rounds = 0;
     for (;;) {
       if (tid == 0) S.flag = 0;
@@ -727,31 +793,33 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       }
       __syncthreads();
       if (redo) {
-        BitReader br;
-        br.init(words, npos);
-        int z = (int)(nzb & 0xFF), b = (int)(nzb >> 8);
+        Dec d;
+        dec_init(d, words, npos, (int)(nzb & 0xFF), (int)(nzb >> 8));
         bool merged = false;
         for (int k = r0; k < r1; k++) {
           if (slot_empty(k) || slot_known(k)) {
             merged = true;
             break;
           }
-          const uint32_t zb = (uint32_t)z | ((uint32_t)b << 8);
-          if (k > r0 && S.s_pos[k] == br.pos && S.s_zb[k] == zb) {
+          const uint32_t zb = (uint32_t)d.z | ((uint32_t)d.b << 8);
+          if (k > r0 && S.s_pos[k] == d.pos && S.s_zb[k] == zb) {
             merged = true;
             break;
           }
-          S.s_pos[k] = br.pos;
+          S.s_pos[k] = d.pos;
           S.s_zb[k] = zb;
-          int nblk = 0, dcs[kMaxComp] = {0, 0, 0};
-          decode_range<false>(S, br, z, b, bpm, slot_end(k), nblk, dcs, nullptr);
+          int nblk = 0, c0 = 0, c1 = 0, c2 = 0;
+          decode_range<false>(S, d, bw[0], bw[1], bw[2], bpm, slot_end(k), nblk, c0, c1, c2,
+                              nullptr);
           S.s_nblk[k] = nblk;
-          for (int c = 0; c < kMaxComp; c++) S.s_dc[k][c] = dcs[c];
+          S.s_dc[k][0] = c0;
+          S.s_dc[k][1] = c1;
+          S.s_dc[k][2] = c2;
         }
         if (!merged) {
-          const uint32_t zb = (uint32_t)z | ((uint32_t)b << 8);
-          if (S.run_pos[tid] != br.pos || S.run_zb[tid] != zb) {
-            S.run_pos[tid] = br.pos;
+          const uint32_t zb = (uint32_t)d.z | ((uint32_t)d.b << 8);
+          if (S.run_pos[tid] != d.pos || S.run_zb[tid] != zb) {
+            S.run_pos[tid] = d.pos;
             S.run_zb[tid] = zb;
             S.flag = 1;
           }
@@ -764,6 +832,11 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       if (!again || rounds > kEnThreads + 2) break;
     }
     rounds_total += rounds;
+    {
+      const int64_t t = wall_clock64();
+      tph[1] += t - tstamp;
+      tstamp = t;
+    }
 
     // ---- segmented exclusive scan over runs: (absolute next block, DC preds) ----
     {
@@ -781,7 +854,6 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       S.scan_flag[tid] = flag;
       for (int i = 0; i < 4; i++) S.scan_v[tid][i] = v[i];
       __syncthreads();
-      // inclusive Hillis-Steele segmented scan
       for (int off = 1; off < kEnThreads; off <<= 1) {
         int pf = 0, pv[4] = {0, 0, 0, 0};
         const bool take = tid >= off;
@@ -797,6 +869,11 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
         __syncthreads();
       }
     }
+    {
+      const int64_t t = wall_clock64();
+      tph[2] += t - tstamp;
+      tstamp = t;
+    }
     // ---- write pass ----
     {
       WriteCtx wc;
@@ -807,43 +884,51 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
         wc.nb = S.scan_v[tid - 1][0];
         for (int c = 0; c < kMaxComp; c++) wc.dc[c] = S.scan_v[tid - 1][1 + c];
       }
-      BitReader br;
-      int z = 0, b = 0;
+      Dec d;
+      d.pos = 0;
+      d.z = d.b = 0;
       bool have = false;
       int rc = kOk;
       for (int k = r0; k < r1 && rc == kOk; k++) {
         if (slot_empty(k)) continue;
         const int s = slot_seg(k);
         if (slot_known(k)) {
-          z = 0;
-          b = 0;
-          br.init(words, slot_start(k));
+          dec_init(d, words, slot_start(k), 0, 0);
           wc.nb = ri > 0 ? s * ri * bpm : 0;
           wc.dc[0] = wc.dc[1] = wc.dc[2] = 0;
         } else if (!have) {
           const uint32_t zb = S.s_zb[k];
-          br.init(words, S.s_pos[k]);
-          z = (int)(zb & 0xFF);
-          b = (int)(zb >> 8);
+          dec_init(d, words, S.s_pos[k], (int)(zb & 0xFF), (int)(zb >> 8));
         }
         have = true;
         wc.seg_end_blk = ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks;
         wc.seg_end_bits = seg_end_bits(s);
-        int dummy = 0;
-        rc = decode_range<true>(S, br, z, b, bpm, slot_end(k), dummy, nullptr, &wc);
+        int dummy = 0, c0 = 0, c1 = 0, c2 = 0;
+        rc = decode_range<true>(S, d, bw[0], bw[1], bw[2], bpm, slot_end(k), dummy, c0, c1, c2,
+                                &wc);
         // last slot of its segment: every block of the segment must be done
-        const bool last = (k + 1 >= nslots) || slot_j(k + 1) == 0 || slot_empty(k + 1);
         // (nb beyond the segment only happens for garbage after its last block)
-        if (rc == kOk && last && (wc.nb < wc.seg_end_blk || (wc.nb == wc.seg_end_blk && z != 0)))
+        const bool last = (k + 1 >= nslots) || slot_j(k + 1) == 0 || slot_empty(k + 1);
+        if (rc == kOk && last && (wc.nb < wc.seg_end_blk || (wc.nb == wc.seg_end_blk && d.z != 0)))
           rc = kErrTruncated;
       }
       if (rc != kOk) atomicCAS(&S.err, kOk, rc);
     }
     __syncthreads();
+    {
+      const int64_t t = wall_clock64();
+      tph[3] += t - tstamp;
+      tstamp = t;
+    }
   }
   if (tid == 0) {
     if (S.err != kOk) infos[img].status = S.err;
     infos[img].sync_rounds = rounds_total;
+    for (int i = 0; i < 4; i++) infos[img].tphase[i] = tph[i];
+    infos[img].dbg[0] = dbg_sh[0];
+    infos[img].dbg[1] = dbg_sh[1];
+    infos[img].dbg[2] = dbg_acc[2];
+    infos[img].dbg[3] = dbg_acc[3];
   }
 }
 
