@@ -57,8 +57,19 @@ struct ImageDesc {      // host-filled per image
   // resize geometry (host computed from the probe; device recomputes nothing)
   int32_t sw, sh, dx, dy, ow, oh;
   int32_t taps_x[kMaxComp], taps_y[kMaxComp];
-  int32_t pad_;
+  int32_t rs_ty;        // resize: output rows per workgroup tile
+  int32_t rs_cw;        // resize: content columns per chunk
+  int32_t pad2_;
 };
+
+// resize tiling: LDS holds kRsRows horizontally filtered source rows of one
+// kRsCols-wide column chunk (int16, Q6)
+constexpr int kRsCols = 128;
+constexpr int kRsRows = 136;
+constexpr int kRsMaxTy = 16;
+constexpr int kRsSrcW = 384;        // staged source bytes per row
+constexpr int kRsSrcBytes = 24576;  // staged source window (rows x kRsSrcW)
+constexpr int kRsWts = 4096;        // staged horizontal weights (int16)
 
 struct ImageInfo {      // device-filled by the parse kernel
   int32_t status;
@@ -84,6 +95,7 @@ struct BatchParams {
   int32_t resize, filter;
   int32_t out_w, out_h;  // full-res mode: common size
   int32_t sub_bits;      // Huffman subsequence size (bits, multiple of 32)
+  int32_t debug_mask;    // diagnostics: skip kernel phases (timing ablations only)
   float mean[3], std[3];
 };
 

@@ -211,6 +211,7 @@ struct Layout {
   int64_t out_elems_per_image = 0;
   int max_blocks = 0, max_len = 0;
   int64_t max_px = 0;
+  int64_t max_tiles = 0;
   int ow = 0, oh = 0;
 };
 
@@ -322,6 +323,33 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
       }
       int ml = g.sw > g.sh ? g.sw : g.sh;
       if (ml > L.max_len) L.max_len = ml;
+      // tile sizes: the LDS-staged source window of one (rs_ty rows x rs_cw
+      // columns) tile must fit kRsRows / kRsSrcW / kRsSrcBytes / kRsWts
+      int ty = kRsMaxTy, tcw = kRsCols;
+      auto fits = [&](int ty_, int cw_) {
+        for (int c = 0; c < p.ncomp; c++) {
+          const float sy = fmaxf((float)chh[c] / (float)g.sh, 1.0f);
+          const float sx = fmaxf((float)cw[c] / (float)g.sw, 1.0f);
+          const int tpy = ((d.taps_y[c] + 1) / 2) * 2, tpx = ((d.taps_x[c] + 1) / 2) * 2;
+          const int rows = (int)ceilf((float)(ty_ - 1) * sy) + 2 + tpy;
+          const int wsrc = (int)ceilf((float)(cw_ - 1) * sx) + 2 + tpx + 8;  // + dword realignment
+          if (rows > kRsRows || wsrc > kRsSrcW || rows * wsrc > kRsSrcBytes ||
+              cw_ * tpx > kRsWts || ty_ * tpy > kRsMaxTy * kRsRows)
+            return false;
+        }
+        return true;
+      };
+      while (tcw > 1 && !fits(1, tcw)) tcw--;
+      while (ty > 1 && !fits(ty, tcw)) ty--;
+      if (!fits(ty, tcw)) {
+        if (status) status[i] = SPDL_HJ_ERR_BAD_GEOMETRY;
+        set_err(err, errlen, "Failed to decode an image. (image %d: resize tile does not fit)", i);
+        return SPDL_HJ_ERR_BAD_GEOMETRY;
+      }
+      d.rs_ty = ty;
+      d.rs_cw = tcw;
+      const int64_t tiles = (g.oh + ty - 1) / ty;
+      if (tiles > L.max_tiles) L.max_tiles = tiles;
     }
     int64_t px = (int64_t)g.ow * g.oh;
     if (px > L.max_px) L.max_px = px;
@@ -344,6 +372,7 @@ struct spdl_hj_ctx {
   float timings[kStages] = {};
   int ntimings = 0;
   int sub_bits = 512;
+  int debug_mask = 0;
 };
 
 namespace {
@@ -442,6 +471,7 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
   bp.out_w = L.ow;
   bp.out_h = L.oh;
   bp.sub_bits = ctx->sub_bits;
+  bp.debug_mask = ctx->debug_mask;
   for (int c = 0; c < 3; c++) {
     bp.mean[c] = out->mean[c];
     bp.std[c] = out->std[c];
@@ -452,7 +482,8 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
                             n, st));
       mark(ctx, 6, st);
       HJ_HIP(launch_resize(static_cast<const uint8_t*>(ctx->planes.p), desc, infos,
-                           static_cast<const int32_t*>(ctx->wts.p), out_dev, bp, L.max_px, n, st));
+                           static_cast<const int32_t*>(ctx->wts.p), out_dev, bp, L.max_tiles, n,
+                           st));
     } else {
       mark(ctx, 6, st);
       HJ_HIP(launch_csc(static_cast<const uint8_t*>(ctx->planes.p), desc, infos, out_dev, bp,
@@ -741,6 +772,10 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "sub_bits")) {
     if (value < 32 || value > (1 << 24) || value % 32) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->sub_bits = (int)value;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "debug_mask")) {  // timing ablations only: output is wrong
+    ctx->debug_mask = (int)value;
     return SPDL_HJ_OK;
   }
   return SPDL_HJ_ERR_INVALID_ARG;

@@ -321,38 +321,35 @@ __global__ void __launch_bounds__(256) parse_kernel(const uint8_t* __restrict__ 
 // ---------------------------------------------------------------------------
 
 constexpr int kDsThreads = 256;
-constexpr int kDsPer = 16;
+constexpr int kDsPer = 32;
 constexpr int kDsTile = kDsThreads * kDsPer;
 
-// block-wide exclusive scan of two counters (keep bytes, RST markers)
-__device__ static void block_scan2(int a, int b, int& ea, int& eb, int& ta, int& tb, int* sa,
-                                   int* sb) {
-  const int tid = threadIdx.x;
-  sa[tid] = a;
-  sb[tid] = b;
-  __syncthreads();
-  for (int off = 1; off < kDsThreads; off <<= 1) {
-    int va = tid >= off ? sa[tid - off] : 0, vb = tid >= off ? sb[tid - off] : 0;
-    __syncthreads();
-    sa[tid] += va;
-    sb[tid] += vb;
-    __syncthreads();
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int u = __shfl_up(v, d, 64);
+    if (lane >= d) v += u;
   }
-  ea = sa[tid] - a;
-  eb = sb[tid] - b;
-  ta = sa[kDsThreads - 1];
-  tb = sb[kDsThreads - 1];
-  __syncthreads();
+  return v;
 }
 
+// Destuff one image per workgroup, tile by tile (8 KB).  Tile bytes (plus the
+// previous 16 and next 16 bytes) are loaded with 16-byte loads into LDS and
+// classified there: a byte is kept unless it follows 0xFF (stuffed 0x00 or a
+// marker code), an 0xFF is kept when followed by 0x00, runs of 0xFF are fill,
+// an 0xFF starting RSTn splits a segment and any other marker ends the scan.
+// Kept bytes are compacted in LDS (wave shuffle scans, 4 barriers per tile)
+// and written with dword stores; the partial tail dword carries over.
 __global__ void __launch_bounds__(kDsThreads) destuff_kernel(const uint8_t* __restrict__ bytes,
                                                              const ImageDesc* __restrict__ desc,
                                                              ImageInfo* __restrict__ infos,
                                                              uint8_t* __restrict__ clean,
                                                              uint32_t* __restrict__ segs) {
-  __shared__ int sa[kDsThreads], sb[kDsThreads];
-  __shared__ int term;
-  const int img = blockIdx.x, tid = threadIdx.x;
+  __shared__ int wk[4], wr[4], wt[4];
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kDsTile + 32];
+  __shared__ __attribute__((aligned(16))) uint8_t ob[kDsTile + 16];
+  const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (infos[img].status != kOk) return;
   const ImageDesc dd = desc[img];
   const uint8_t* d = bytes + dd.in_off;
@@ -360,70 +357,116 @@ __global__ void __launch_bounds__(kDsThreads) destuff_kernel(const uint8_t* __re
   const int start = infos[img].scan_start;
   uint8_t* out = clean + dd.in_off;
   uint32_t* sg = segs + dd.seg_off;
-  int carry_keep = 0, carry_rst = 0;
+  int carry_keep = 0, carry_rst = 0, pend = 0;  // pend: bytes at ob[0..pend) not yet stored
+  uint32_t tailw = 0;                           // thread 0: those bytes, carried in a register
   bool overflow = false;
   if (tid == 0) sg[0] = 0;
-  for (int base = start;; base += kDsTile) {
-    if (tid == 0) term = 0x7FFFFFFF;
-    __syncthreads();
+  const int abase = start & ~15;  // tiles are 16-byte aligned in the file
+  auto at = [&](int j) -> int { return j < size ? (int)d[j] : 0xD9; };
+  for (int base = abase;; base += kDsTile) {
+    // stage [base - 16, base + kDsTile + 16)
+    for (int q = tid; q < kDsTile / 16 + 2; q += kDsThreads) {
+      const int o = base - 16 + q * 16;
+      if (o >= 0 && o + 16 <= size) {
+        *reinterpret_cast<uint4*>(tile + q * 16) = *reinterpret_cast<const uint4*>(d + o);
+      } else {
+        for (int i = 0; i < 16; i++) tile[q * 16 + i] = (o + i >= 0 && o + i < size) ? d[o + i] : 0;
+      }
+    }
+    __syncthreads();  // (1)
+    if (tid == 0) reinterpret_cast<uint32_t*>(ob)[0] = tailw;
+    auto tb = [&](int j) -> int { return j < size ? (int)tile[j - base + 16] : 0xD9; };
     const int j0 = base + tid * kDsPer;
-    // pass 1: find the first terminating marker in the tile
-    for (int j = j0; j < j0 + kDsPer && j < size; j++) {
-      if (d[j] != 0xFF) continue;
-      if (j > start && d[j - 1] == 0xFF) continue;  // fill byte of a marker run
-      if (j + 1 < size && d[j + 1] == 0x00) continue; // stuffed data 0xFF
-      int k = j + 1;
-      while (k < size && d[k] == 0xFF) k++;
-      if (!(k < size && d[k] >= 0xD0 && d[k] <= 0xD7)) {
-        atomicMin(&term, j);
+    const int jb = max(j0, start), je = min(j0 + kDsPer, size);
+    // pass 1: first terminating marker (wave min -> LDS)
+    int myterm = 0x7FFFFFFF;
+    for (int j = jb; j < je; j++) {
+      if (tb(j) != 0xFF) continue;
+      if (j > start && tb(j - 1) == 0xFF) continue;
+      if (tb(j + 1) == 0x00) continue;
+      int k2 = j + 1;
+      while (k2 < size && at(k2) == 0xFF) k2++;
+      if (!(k2 < size && at(k2) >= 0xD0 && at(k2) <= 0xD7)) {
+        myterm = j;
         break;
       }
     }
-    if (tid == 0 && base + kDsTile >= size) atomicMin(&term, size);
-    __syncthreads();
-    const int lim = term;
-    // pass 2: counts
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) myterm = min(myterm, __shfl_xor(myterm, o, 64));
+    // pass 2: counts up to this thread's terminator bound (refined below)
+    if (lane == 0) wt[wid] = myterm;
+    __syncthreads();  // (2)
+    int lim = min(min(wt[0], wt[1]), min(wt[2], wt[3]));
+    if (base + kDsTile >= size) lim = min(lim, size);
     int keep = 0, rst = 0;
-    for (int j = j0; j < j0 + kDsPer && j < lim; j++) {
-      const int c = d[j];
-      const bool prev_ff = j > start && d[j - 1] == 0xFF;
+    for (int j = jb; j < min(je, lim); j++) {
+      const int c = tb(j);
+      const bool prev_ff = j > start && tb(j - 1) == 0xFF;
       if (c != 0xFF) {
         keep += !prev_ff;
       } else if (!prev_ff) {
-        if (j + 1 < size && d[j + 1] == 0x00) keep++;
-        else rst++;  // before `lim`, a marker start is always RSTn
+        if (tb(j + 1) == 0x00) keep++;
+        else rst++;
       }
     }
-    int ek, er, tk, tr;
-    block_scan2(keep, rst, ek, er, tk, tr, sa, sb);
-    // pass 3: scatter
-    int o = carry_keep + ek, r = carry_rst + er;
-    for (int j = j0; j < j0 + kDsPer && j < lim; j++) {
-      const int c = d[j];
-      const bool prev_ff = j > start && d[j - 1] == 0xFF;
+    const int ik = wave_incl_scan(keep), ir = wave_incl_scan(rst);
+    if (lane == 63) {
+      wk[wid] = ik;
+      wr[wid] = ir;
+    }
+    __syncthreads();  // (3)
+    int ek = ik - keep, er = ir - rst, tk = 0, tr = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      if (w < wid) {
+        ek += wk[w];
+        er += wr[w];
+      }
+      tk += wk[w];
+      tr += wr[w];
+    }
+    // pass 3: compact into ob (after the pending tail bytes)
+    int o = pend + ek, r = carry_rst + er;
+    for (int j = jb; j < min(je, lim); j++) {
+      const int c = tb(j);
+      const bool prev_ff = j > start && tb(j - 1) == 0xFF;
       if (c != 0xFF) {
-        if (!prev_ff) out[o++] = (uint8_t)c;
+        if (!prev_ff) ob[o++] = (uint8_t)c;
       } else if (!prev_ff) {
-        if (j + 1 < size && d[j + 1] == 0x00) {
-          out[o++] = 0xFF;
+        if (tb(j + 1) == 0x00) {
+          ob[o++] = 0xFF;
         } else {
           r++;
-          if (r < dd.seg_cap) sg[r] = (uint32_t)o;
+          if (r < dd.seg_cap) sg[r] = (uint32_t)(carry_keep + (o - pend));
           else overflow = true;
         }
       }
     }
+    __syncthreads();  // (4)
+    // store whole dwords; the output dword grid is aligned to the image base
+    const int total = pend + tk;
+    const int nfull = total >> 2;
+    const int obase = carry_keep - pend;  // multiple of 4 by construction
+    for (int i = tid; i < nfull; i += kDsThreads)
+      reinterpret_cast<uint32_t*>(out + obase)[i] = reinterpret_cast<const uint32_t*>(ob)[i];
+    if (tid == 0) tailw = reinterpret_cast<const uint32_t*>(ob)[nfull];
+    pend = total & 3;
     carry_keep += tk;
     carry_rst += tr;
     if (lim < base + kDsTile) break;
+    __syncthreads();  // ob / tile reuse
   }
-  // zero padding so the bit reader never sees stale bytes past the data
-  if (tid < 16) out[carry_keep + tid] = 0;
-  if (overflow) infos[img].status = kErrBadRestart;
+  // flush the pending tail and zero padding (the bit reader reads a few words
+  // past the data)
   if (tid == 0) {
+    uint32_t w = pend ? (tailw & (0xFFFFFFFFu >> (8 * (4 - pend)))) : 0u;
+    uint32_t* o32 = reinterpret_cast<uint32_t*>(out + (carry_keep - pend));
+    o32[0] = w;
+    for (int i = 1; i <= 5; i++) o32[i] = 0;
     infos[img].clean_len = carry_keep;
     infos[img].nseg = min(carry_rst + 1, dd.seg_cap);
   }
+  if (overflow) infos[img].status = kErrBadRestart;
 }
 
 // ---------------------------------------------------------------------------
@@ -1141,48 +1184,44 @@ __global__ void __launch_bounds__(256) weights_kernel(const ImageDesc* __restric
 }
 #pragma clang fp contract(on)
 
-__device__ __forceinline__ int resize_plane_px(const uint8_t* __restrict__ src, int pw, int ph,
-                                               int stride, const int32_t* fx, const int16_t* wx,
-                                               int tx, const int32_t* fy, const int16_t* wy,
-                                               int ty, int cx, int cy) {
-  const int x0 = fx[cx], y0 = fy[cy];
-  const int16_t* wxr = wx + (int64_t)cx * tx;
-  const int16_t* wyr = wy + (int64_t)cy * ty;
-  int32_t acc = 0;
-  for (int a = 0; a < ty; a++) {
-    int r = y0 + a;
-    r = r < 0 ? 0 : (r >= ph ? ph - 1 : r);
-    const uint8_t* row = src + (int64_t)r * stride;
-    int32_t h = 0;
-    for (int t = 0; t < tx; t++) {
-      int k = x0 + t;
-      k = k < 0 ? 0 : (k >= pw ? pw - 1 : k);
-      h += (int32_t)wxr[t] * row[k];
-    }
-    acc += (int32_t)wyr[a] * ((h + 128) >> 8);
-  }
-  return clip_u8((acc + (1 << 19)) >> 20);
-}
-
+// Fused separable resize + colour conversion + pad/crop + normalise.
+// One workgroup = (image, band of rs_ty output rows).  For each chunk of
+// rs_cw content columns and each plane: the source window (rows x bytes) and
+// the chunk's horizontal weights are staged in LDS with coalesced loads, the
+// horizontal taps of every needed source row go to LDS (Q14 weights -> Q6
+// int16, (acc + 128) >> 8), the vertical taps read that ((acc + 2^19) >> 20,
+// clamp), then YCbCr -> RGB and the band is stored.  The host picks rs_ty and
+// rs_cw per image so every staged buffer fits.  Arithmetic: exactly
+// oracle/jpeg_oracle.c resize_plane + jo_resize_planes.
 __global__ void __launch_bounds__(256) resize_kernel(const uint8_t* __restrict__ planes,
                                                      const ImageDesc* __restrict__ desc,
                                                      const ImageInfo* __restrict__ infos,
                                                      const int32_t* __restrict__ pool,
                                                      void* __restrict__ out, const BatchParams p) {
-  const int img = blockIdx.y;
+  __shared__ int16_t tmp[kRsRows][kRsCols];
+  __shared__ uint8_t ob[kMaxComp][kRsMaxTy][kRsCols];
+  __shared__ __attribute__((aligned(16))) uint8_t srcb[kRsSrcBytes];
+  __shared__ int16_t wts[kRsWts];
+  __shared__ int16_t wtsy[kRsMaxTy * kRsRows];
+  __shared__ int32_t xfirst[kRsCols];
+  __shared__ int32_t yfirst[kRsMaxTy];
+  const int img = blockIdx.y, tid = threadIdx.x;
   const ImageInfo& in = infos[img];
   if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
-  const int ow = dd.ow, oh = dd.oh;
-  const int64_t npx = (int64_t)ow * oh;
-  // table pointers
+  const int ow = dd.ow, oh = dd.oh, TY = dd.rs_ty, CW = dd.rs_cw;
+  const int y0 = blockIdx.x * TY;
+  if (y0 >= oh) return;
+  const int y1 = min(y0 + TY, oh);
+  const int cy_lo = max(y0 - dd.dy, 0), cy_hi = min(y1 - dd.dy, dd.sh);
+  const int ncomp = dd.ncomp;
   const int32_t* fxp[kMaxComp];
   const int16_t* wxp[kMaxComp];
   const int32_t* fyp[kMaxComp];
   const int16_t* wyp[kMaxComp];
   int txs[kMaxComp], tys[kMaxComp];
   int64_t off = dd.wt_off;
-  for (int c = 0; c < dd.ncomp; c++) {
+  for (int c = 0; c < ncomp; c++) {
     txs[c] = ((dd.taps_x[c] + 1) / 2) * 2;
     tys[c] = ((dd.taps_y[c] + 1) / 2) * 2;
     fxp[c] = pool + off;
@@ -1192,23 +1231,134 @@ __global__ void __launch_bounds__(256) resize_kernel(const uint8_t* __restrict__
     wyp[c] = reinterpret_cast<const int16_t*>(pool + off + dd.sh);
     off += (int64_t)dd.sh * (1 + tys[c] / 2);
   }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int y = (int)(i / ow), x = (int)(i - (int64_t)y * ow);
-    const int cx = x - dd.dx, cy = y - dd.dy;
-    int rgb[3] = {0, 0, 0};
-    if (cx >= 0 && cx < dd.sw && cy >= 0 && cy < dd.sh) {
-      int v[kMaxComp];
-      for (int c = 0; c < dd.ncomp; c++)
-        v[c] = resize_plane_px(planes + dd.plane_off[c], in.comp_w[c], in.comp_hpx[c],
-                               dd.plane_stride[c], fxp[c], wxp[c], txs[c], fyp[c], wyp[c], tys[c],
-                               cx, cy);
-      if (dd.ncomp == 1)
-        rgb[0] = rgb[1] = rgb[2] = v[0];
-      else
-        ycc_rgb(v[0], v[1], v[2], rgb);
+  // content columns visible in the output
+  const int vis_lo = max(-dd.dx, 0), vis_hi = min(ow - dd.dx, dd.sw);
+  const int nry = cy_hi - cy_lo;
+  for (int cx_lo = vis_lo; cx_lo < max(vis_hi, vis_lo + 1); cx_lo += CW) {
+    const int cx_hi = min(cx_lo + CW, vis_hi);
+    const int ncols = cx_hi - cx_lo;
+    if (ncols > 0 && nry > 0) {
+      for (int c = 0; c < ncomp; c++) {
+        const uint8_t* src = planes + dd.plane_off[c];
+        const int stride = dd.plane_stride[c], pw = in.comp_w[c], ph = in.comp_hpx[c];
+        const int tx = txs[c], ty = tys[c];
+        const int lo = fyp[c][cy_lo];
+        const int nrows = fyp[c][cy_hi - 1] + ty - lo;
+        const int xs_lo = fxp[c][cx_lo];
+        const int wsrc = fxp[c][cx_hi - 1] + tx - xs_lo;
+        if (nrows > kRsRows || wsrc > kRsSrcW || nrows * wsrc > kRsSrcBytes ||
+            ncols * tx > kRsWts || nry * ty > kRsMaxTy * kRsRows)
+          continue;  // defensive: the host tiling guarantees these fit
+        // stage the source window with dword loads from a 4-aligned start;
+        // edge tiles (window past the plane) take the clamped byte path
+        const int xa = xs_lo & ~3;
+        const int wal = ((xs_lo + wsrc - xa) + 3) & ~3;
+        const int sh = xs_lo - xa;  // window offset inside the staged row
+        const int tr = tid >> 6, tc = tid & 63;
+        if (!(p.debug_mask & 1)) {
+        if (xs_lo >= 0 && xs_lo + wsrc <= pw && nrows * wal <= kRsSrcBytes) {
+          // all of a thread's loads are issued before any LDS store, so their
+          // latencies overlap (a load -> store -> load chain pays each one)
+          const int nw = wal >> 2, total = nrows * nw;
+          uint32_t* d32 = reinterpret_cast<uint32_t*>(srcb);
+          for (int q0 = 0; q0 < total; q0 += 256 * 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              const int q = q0 + u * 256 + tid;
+              if (q < total) {
+                const int rr = q / nw, j = q - rr * nw;
+                const int r = min(max(lo + rr, 0), ph - 1);
+                v[u] = reinterpret_cast<const uint32_t*>(src + (int64_t)r * stride + xa)[j];
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              const int q = q0 + u * 256 + tid;
+              if (q < total) d32[q] = v[u];
+            }
+          }
+        } else {
+          for (int rr = tr; rr < nrows; rr += 4) {
+            const int r = min(max(lo + rr, 0), ph - 1);
+            for (int j = tc; j < wal; j += 64) {
+              const int x = min(max(xa + j, 0), pw - 1);
+              srcb[rr * wal + j] = src[(int64_t)r * stride + x];
+            }
+          }
+        }
+        }
+        for (int i = tid; i < ncols * tx; i += 256) wts[i] = wxp[c][(int64_t)cx_lo * tx + i];
+        for (int i = tid; i < ncols; i += 256) xfirst[i] = fxp[c][cx_lo + i] - xs_lo + sh;
+        for (int i = tid; i < nry * ty; i += 256) wtsy[i] = wyp[c][(int64_t)cy_lo * ty + i];
+        for (int i = tid; i < nry; i += 256) yfirst[i] = fyp[c][cy_lo + i] - lo;
+        __syncthreads();
+        // horizontal taps.  Common case (<= 16 taps): a thread owns one column,
+        // keeps its weights in registers and walks rows with a fully unrolled
+        // tap loop (independent LDS reads in flight).  Otherwise the generic
+        // (tr, tc) mapping.
+        if (!(p.debug_mask & 2)) {
+          if (tx <= 16) {
+            const int half = tid >> 7, col = tid & 127;  // 2 threads per column
+            for (int xx = col; xx < ncols; xx += 128) {
+              int32_t wr[16];
+#pragma unroll
+              for (int t = 0; t < 16; t++) wr[t] = t < tx ? (int32_t)wts[xx * tx + t] : 0;
+              const int xf = xfirst[xx];
+              for (int rr = half; rr < nrows; rr += 2) {
+                const uint8_t* row = srcb + rr * wal + xf;
+                int32_t h = 0;
+#pragma unroll
+                for (int t = 0; t < 16; t++) h += wr[t] * (int32_t)row[t];
+                tmp[rr][xx] = (int16_t)((h + 128) >> 8);
+              }
+            }
+          } else {
+            for (int xx = tc; xx < ncols; xx += 64) {
+              const int16_t* w = wts + xx * tx;
+              const int xf = xfirst[xx];
+              for (int rr = tr; rr < nrows; rr += 4) {
+                const uint8_t* row = srcb + rr * wal + xf;
+                int32_t h = 0;
+                for (int t = 0; t < tx; t++) h += (int32_t)w[t] * row[t];
+                tmp[rr][xx] = (int16_t)((h + 128) >> 8);
+              }
+            }
+          }
+        }
+        __syncthreads();
+        if (!(p.debug_mask & 4))
+        for (int yy = tr; yy < nry; yy += 4) {
+          const int base = yfirst[yy];
+          const int16_t* w = wtsy + yy * ty;
+          for (int xx = tc; xx < ncols; xx += 64) {
+            int32_t acc = 0;
+            for (int t = 0; t < ty; t++) acc += (int32_t)w[t] * tmp[base + t][xx];
+            ob[c][yy][xx] = clip_u8((acc + (1 << 19)) >> 20);
+          }
+        }
+        __syncthreads();
+      }
     }
-    store_rgb(out, dd.out_off, p.pix_fmt, p.dtype, ow, oh, x, y, rgb, p);
+    // store the part of the band this chunk covers (pad columns go with the
+    // first / last chunk)
+    const int xa = (cx_lo == vis_lo) ? 0 : cx_lo + dd.dx;
+    const int xb = (cx_hi >= vis_hi) ? ow : cx_hi + dd.dx;
+    const int nx = xb - xa;
+    for (int i = tid; i < (y1 - y0) * nx; i += 256) {
+      const int yy = i / nx, x = xa + (i - yy * nx), y = y0 + yy;
+      const int cx = x - dd.dx, cy = y - dd.dy;
+      int rgb[3] = {0, 0, 0};
+      if (cx >= cx_lo && cx < cx_hi && cy >= cy_lo && cy < cy_hi) {
+        const int oy = cy - cy_lo, ox = cx - cx_lo;
+        if (ncomp == 1)
+          rgb[0] = rgb[1] = rgb[2] = ob[0][oy][ox];
+        else
+          ycc_rgb(ob[0][oy][ox], ob[1][oy][ox], ob[2][oy][ox], rgb);
+      }
+      if (!(p.debug_mask & 8)) store_rgb(out, dd.out_off, p.pix_fmt, p.dtype, ow, oh, x, y, rgb, p);
+    }
+    __syncthreads();
   }
 }
 
@@ -1276,12 +1426,10 @@ hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageI
   return hipGetLastError();
 }
 hipError_t launch_resize(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
-                         const int32_t* pool, void* out, const BatchParams& p, int64_t max_px,
+                         const int32_t* pool, void* out, const BatchParams& p, int64_t max_tiles,
                          int n, hipStream_t st) {
-  int64_t gx64 = (max_px + 255) / 256;
-  int gx = (int)(gx64 < 4096 ? gx64 : 4096);
-  hipLaunchKernelGGL(resize_kernel, dim3(gx, n), dim3(256), 0, st, planes, desc, infos, pool, out,
-                     p);
+  hipLaunchKernelGGL(resize_kernel, dim3((int)max_tiles, n), dim3(256), 0, st, planes, desc, infos,
+                     pool, out, p);
   return hipGetLastError();
 }
 hipError_t launch_planes_copy(const uint8_t* planes, const ImageDesc* desc,

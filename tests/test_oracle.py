@@ -1,0 +1,193 @@
+"""CPU tests of the oracle (no GPU): pinned against the committed golden
+fixtures (IJG libjpeg 9d outputs and the reference's own filter strings)."""
+
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "jpeg", "*.jpg")))
+
+
+def _jpeg(name):
+    with open(os.path.join(GOLD, "jpeg", name + ".jpg"), "rb") as f:
+        return f.read()
+
+
+def test_fixtures_present():
+    assert len(CASES) >= 10
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_entropy_decode_matches_libjpeg_coefficients(oracle, name):
+    """Huffman decode + DC prediction, bit-exact vs jpeg_read_coefficients."""
+    ref = np.load(os.path.join(GOLD, name + ".libjpeg.npz"))
+    _, levels = oracle.decode_coefs(_jpeg(name))
+    assert len(levels) == len([k for k in ref.files if k.startswith("coef")])
+    for c, lv in enumerate(levels):
+        np.testing.assert_array_equal(lv, ref[f"coef{c}"], strict=True)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_islow_pipeline_matches_libjpeg(oracle, name):
+    """IDCT islow + nearest chroma + JFIF integer CSC: bit-exact vs libjpeg 9d
+    (dct_method=JDCT_ISLOW, do_fancy_upsampling=FALSE)."""
+    ref = np.load(os.path.join(GOLD, name + ".libjpeg.npz"))["rgb_islow"]
+    hyp = oracle.decode_rgb(_jpeg(name), oracle.IDCT_ISLOW, "rgb24")
+    np.testing.assert_array_equal(hyp, ref, strict=True)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_regression(oracle, name):
+    """Simple-IDCT (FFmpeg) planes / rgb / resize / fp16: pinned regression."""
+    ref = np.load(os.path.join(GOLD, name + ".oracle.npz"))
+    data = _jpeg(name)
+    planes = oracle.decode_planes(data, oracle.IDCT_SIMPLE)
+    for c, p in enumerate(planes):
+        np.testing.assert_array_equal(p, ref[f"plane{c}"], strict=True)
+    np.testing.assert_array_equal(oracle.decode_rgb(data, 0, "rgb24"), ref["rgb24_simple"])
+    rs = oracle.Resize(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224)
+    np.testing.assert_array_equal(oracle.decode_resize(data, rs, "rgb24"), ref["pad224_rgb24"])
+    f16 = oracle.decode_resize(data, rs, "rgb", normalize=True).view(np.uint16)
+    np.testing.assert_array_equal(f16, ref["pad224_f16"])
+
+
+def _fdct_matrix():
+    return np.array([[(np.sqrt(1 / 8) if k == 0 else np.sqrt(2 / 8)) *
+                      np.cos((2 * n + 1) * k * np.pi / 16) for n in range(8)] for k in range(8)])
+
+
+@pytest.mark.parametrize("idct", [0, 1])
+def test_idct_accuracy_ieee1180_style(oracle, idct):
+    """Both integer IDCTs stay within 1 of the exact IDCT (IEEE 1180-style)."""
+    C = _fdct_matrix()
+    rng = np.random.default_rng(7)
+    worst = 0
+    for it in range(1500):
+        L = 5 if it % 2 == 0 else int(rng.integers(1, 256))
+        x = rng.integers(-L, L + 1, size=(8, 8)).astype(float)
+        F = np.clip(np.rint(C @ x @ C.T).astype(int), -2048, 2047)
+        ref = np.clip(np.rint(C.T @ F @ C) + 128, 0, 255)
+        blk = F.copy()
+        blk[0, 0] += 1024  # FFmpeg DC bias carried by the coefficients
+        out = oracle.idct_block(blk.astype(np.int16).reshape(64), idct).astype(int)
+        worst = max(worst, int(np.abs(out - ref).max()))
+    assert worst <= 1
+
+
+def _py_simple_idct(blk):
+    """Independent pure-Python restatement of FFmpeg simple_idct 8-bit
+    (simple_idct_template.c: idctRowCondDC + idctSparseColPut)."""
+    W1, W2, W3, W4, W5, W6, W7 = 22725, 21407, 19266, 16383, 12873, 8867, 4520
+    M = 0xFFFFFFFF
+
+    def s32(x):
+        x &= M
+        return x - (1 << 32) if x & 0x80000000 else x
+
+    def s16(x):
+        x &= 0xFFFF
+        return x - 0x10000 if x & 0x8000 else x
+
+    b = [int(v) for v in blk]
+    for i in range(8):
+        r = b[8 * i: 8 * i + 8]
+        if not any(r[1:]):
+            b[8 * i: 8 * i + 8] = [s16(r[0] << 3)] * 8
+            continue
+        a0 = W4 * r[0] + (1 << 10)
+        a1, a2, a3 = a0, a0, a0
+        a0 += W2 * r[2]; a1 += W6 * r[2]; a2 -= W6 * r[2]; a3 -= W2 * r[2]
+        b0 = W1 * r[1] + W3 * r[3]; b1 = W3 * r[1] - W7 * r[3]
+        b2 = W5 * r[1] - W1 * r[3]; b3 = W7 * r[1] - W5 * r[3]
+        a0 += W4 * r[4] + W6 * r[6]; a1 += -W4 * r[4] - W2 * r[6]
+        a2 += -W4 * r[4] + W2 * r[6]; a3 += W4 * r[4] - W6 * r[6]
+        b0 += W5 * r[5] + W7 * r[7]; b1 += -W1 * r[5] - W5 * r[7]
+        b2 += W7 * r[5] + W3 * r[7]; b3 += W3 * r[5] - W1 * r[7]
+        o = [a0 + b0, a1 + b1, a2 + b2, a3 + b3, a3 - b3, a2 - b2, a1 - b1, a0 - b0]
+        b[8 * i: 8 * i + 8] = [s16(s32(v) >> 11) for v in o]
+    out = np.zeros((8, 8), np.uint8)
+    for i in range(8):
+        c = [b[i + 8 * k] for k in range(8)]
+        a0 = W4 * (c[0] + (1 << 19) // W4)
+        a1, a2, a3 = a0, a0, a0
+        a0 += W2 * c[2]; a1 += W6 * c[2]; a2 -= W6 * c[2]; a3 -= W2 * c[2]
+        b0 = W1 * c[1] + W3 * c[3]; b1 = W3 * c[1] - W7 * c[3]
+        b2 = W5 * c[1] - W1 * c[3]; b3 = W7 * c[1] - W5 * c[3]
+        a0 += W4 * c[4]; a1 -= W4 * c[4]; a2 -= W4 * c[4]; a3 += W4 * c[4]
+        b0 += W5 * c[5]; b1 -= W1 * c[5]; b2 += W7 * c[5]; b3 += W3 * c[5]
+        a0 += W6 * c[6]; a1 -= W2 * c[6]; a2 += W2 * c[6]; a3 -= W6 * c[6]
+        b0 += W7 * c[7]; b1 -= W5 * c[7]; b2 += W3 * c[7]; b3 -= W1 * c[7]
+        o = [a0 + b0, a1 + b1, a2 + b2, a3 + b3, a3 - b3, a2 - b2, a1 - b1, a0 - b0]
+        for r, v in enumerate(o):
+            out[r, i] = min(max(s32(v) >> 20, 0), 255)
+    return out
+
+
+def test_simple_idct_matches_independent_restatement(oracle):
+    """Two independent restatements of FFmpeg simple_idct agree bit for bit,
+    including the DC-only row shortcut (row[0] << 3, which differs from the
+    full row transform for large DC values)."""
+    rng = np.random.default_rng(11)
+    for it in range(400):
+        blk = np.zeros(64, np.int16)
+        blk[0] = 1024 + int(rng.integers(-1024, 1024))
+        for _ in range(int(rng.integers(0, 20))):
+            blk[int(rng.integers(0, 64))] = int(rng.integers(-400, 400))
+        if it % 3 == 0:
+            blk[1:8] = 0
+            blk[0] = int(rng.integers(1500, 4000))
+        np.testing.assert_array_equal(oracle.idct_block(blk, 0), _py_simple_idct(blk))
+
+
+@pytest.mark.parametrize(
+    "w,h,kw,expect",
+    [
+        (640, 480, dict(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224),
+         dict(sw=224, sh=168, dx=0, dy=28, ow=224, oh=224)),
+        (480, 640, dict(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224),
+         dict(sw=168, sh=224, dx=28, dy=0, ow=224, oh=224)),
+        (640, 480, dict(fit_w=224, fit_h=224, aspect="increase", crop_w=224, crop_h=224),
+         dict(sw=299, sh=224, dx=-37, dy=0, ow=224, oh=224)),
+        (640, 480, dict(fit_w=256, fit_h=256, aspect="decrease", pad_w=256, pad_h=256,
+                        crop_w=224, crop_h=224),
+         dict(sw=256, sh=192, dx=-16, dy=16, ow=224, oh=224)),
+        (333, 227, dict(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224),
+         dict(sw=224, sh=153, dx=0, dy=35, ow=224, oh=224)),
+        (640, 480, dict(fit_w=160, fit_h=120), dict(sw=160, sh=120, dx=0, dy=0, ow=160, oh=120)),
+    ],
+)
+def test_geometry_ffmpeg_semantics(oracle, w, h, kw, expect):
+    """scale force_original_aspect_ratio (av_rescale rounding) + centred pad /
+    crop geometry, src/spdl/io/_preprocessing.py:214-234."""
+    assert oracle.geometry(w, h, oracle.Resize(**kw)) == expect
+
+
+def test_resize_weights_sum_and_identity(oracle):
+    first, w = oracle.axis_weights(640, 224)
+    assert (w.astype(np.int32).sum(axis=1) == 16384).all()
+    first, w = oracle.axis_weights(100, 100)
+    assert (w.max(axis=1) == 16384).all()  # identity at scale 1
+
+
+def test_filter_desc_strings_match_reference():
+    """Our filter-string builder reproduces the reference's
+    get_video_filter_desc (fixture generated by importing the reference)."""
+    from spdl_amd.io._preprocessing import get_video_filter_desc
+
+    for item in json.load(open(os.path.join(GOLD, "filter_desc.json"))):
+        assert get_video_filter_desc(**item["args"]) == item["desc"], item
+
+
+def test_oracle_errors(oracle):
+    from tests import cases
+
+    with pytest.raises(oracle.OracleError):
+        oracle.decode_rgb(cases.progressive())
+    with pytest.raises(oracle.OracleError):
+        oracle.decode_rgb(cases.truncated())
+    with pytest.raises(oracle.OracleError):
+        oracle.decode_rgb(b"\x00" * 100)
