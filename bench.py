@@ -50,6 +50,7 @@ def _args():
     p.add_argument("--cpu-images", type=int, default=1024)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sub-bits", type=int, default=0)
+    p.add_argument("--entropy-threads", type=int, default=0)
     p.add_argument("--with-copies", action="store_true",
                    help="also time the host-bytes path (pinned H2D + D2H of the output)")
     return p.parse_args()
@@ -113,6 +114,8 @@ def main():
     dec = _lib.Decoder(local)
     if a.sub_bits:
         dec.set_param("sub_bits", a.sub_bits)
+    if a.entropy_threads:
+        dec.set_param("entropy_threads", a.entropy_threads)
     out = torch.empty((a.batch, 224, 224, 3), dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream(device)
     nbytes_out = out.numel()

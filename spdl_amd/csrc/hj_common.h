@@ -14,6 +14,10 @@
 #pragma once
 #include <stdint.h>
 
+#ifndef HJ_HD
+#define HJ_HD __host__ __device__
+#endif
+
 namespace hj {
 
 constexpr int kMaxComp = 3;
@@ -22,6 +26,21 @@ constexpr int kLutBits = 10;
 constexpr int kLutSize = 1 << kLutBits;
 constexpr int kDcBias = 1024;  // FFmpeg mjpegdec last_dc start value (4 << bits)
 constexpr int kMaxTaps = 128;
+
+// Parallel Huffman decode: a restart segment is cut into slots of N bits, at
+// most kMaxSlots slots per pass; every slot keeps up to N + kRecPad symbol
+// records (a symbol consumes >= 1 bit; +1 truncation marker; uint4 padding).
+constexpr int kMaxSlots = 2048;
+constexpr int kRecPad = 4;
+constexpr int kMaxEntropyThreads = 1024;  // largest entropy workgroup
+// N for a scan whose longest segment has `maxbits` bits (host and device
+// agree; `maxbits` <= 8 * compressed size bounds it on the host)
+inline HJ_HD uint32_t slot_bits(uint32_t maxbits, int sub_bits) {
+  uint32_t need = (maxbits + kMaxSlots - 1) / kMaxSlots;
+  need = (need + 31) & ~31u;
+  const uint32_t n = (uint32_t)sub_bits;
+  return need > n ? need : n;
+}
 
 // LUT entry (u32): [0:5) nbits consumed, [5:7) kind, [8:16) symbol,
 // [16:32) value (int16, kind==Full) or sub-table index (kind==Sub)
@@ -60,6 +79,8 @@ struct ImageDesc {      // host-filled per image
   int32_t rs_ty;        // resize: output rows per workgroup tile
   int32_t rs_cw;        // resize: content columns per chunk
   int32_t pad2_;
+  int64_t rec_off;      // entropy symbol records: offset (u32 units) and capacity
+  int64_t rec_cap;
 };
 
 // resize tiling: LDS holds kRsRows horizontally filtered source rows of one

@@ -22,7 +22,7 @@ hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageInfo*, HuffTable*
 hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, uint8_t*, uint32_t*, int,
                           hipStream_t);
 hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
-                          const HuffTable*, int16_t*, int, int, hipStream_t);
+                          const HuffTable*, int16_t*, uint32_t*, int, int, int, hipStream_t);
 hipError_t launch_idct(const int16_t*, const ImageDesc*, const ImageInfo*, uint8_t*, int, int, int,
                        hipStream_t);
 hipError_t launch_weights(const ImageDesc*, const ImageInfo*, int32_t*, int, int, int,
@@ -207,7 +207,7 @@ int max_taps(int src_len, int dst_len, int filter) {
 
 struct Layout {
   std::vector<ImageDesc> desc;
-  int64_t total_blocks = 0, total_planes = 0, total_segs = 0, total_wts = 0;
+  int64_t total_blocks = 0, total_planes = 0, total_segs = 0, total_wts = 0, total_recs = 0;
   int64_t out_elems_per_image = 0;
   int max_blocks = 0, max_len = 0;
   int64_t max_px = 0;
@@ -216,8 +216,8 @@ struct Layout {
 };
 
 int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_image_info* infos,
-                 int n, const spdl_hj_output* out, Layout& L, int32_t* status, char* err,
-                 size_t errlen) {
+                 int n, const spdl_hj_output* out, int sub_bits, Layout& L, int32_t* status,
+                 char* err, size_t errlen) {
   L.desc.assign(n, ImageDesc{});
   for (int i = 0; i < n; i++) {
     ImageDesc& d = L.desc[i];
@@ -282,6 +282,15 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     d.seg_cap = (int32_t)(sizes[i] / 2 + 2);
     d.seg_off = L.total_segs;
     L.total_segs += d.seg_cap;
+    {
+      // entropy records: kMaxSlots slots of N + kRecPad records, N bounded by
+      // the compressed size (the device derives N from the destuffed length)
+      const uint64_t bits = (uint64_t)sizes[i] * 8u;
+      const uint32_t nb = slot_bits(bits > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bits, sub_bits);
+      d.rec_cap = (int64_t)(kMaxSlots + kMaxEntropyThreads) * (nb + kRecPad);
+      d.rec_off = L.total_recs;
+      L.total_recs += d.rec_cap;
+    }
     Geom g;
     int rc = geometry(p.width, p.height, out, &g);
     if (rc) {
@@ -363,7 +372,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
 
 struct spdl_hj_ctx {
   int device = 0;
-  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts;
+  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts, recs;
   PinBuf pin_in, pin_desc, pin_status;
   hipEvent_t staging_free = nullptr;  // host staging may be rewritten after this
   hipEvent_t batch_done = nullptr;    // device workspace free after this
@@ -373,6 +382,7 @@ struct spdl_hj_ctx {
   int ntimings = 0;
   int sub_bits = 512;
   int debug_mask = 0;
+  int entropy_threads = 512;
 };
 
 namespace {
@@ -437,6 +447,7 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
   HJ_HIP(ctx->luts.ensure(sizeof(HuffTable) * 8 * n));
   HJ_HIP(ctx->coefs.ensure((size_t)L.total_blocks * 128 + 256));
   HJ_HIP(ctx->planes.ensure((size_t)L.total_planes + 256));
+  HJ_HIP(ctx->recs.ensure((size_t)L.total_recs * 4 + 256));
   if (out->resize) HJ_HIP(ctx->wts.ensure((size_t)L.total_wts * 4 + 256));
   HJ_HIP(ctx->pin_desc.ensure(sizeof(ImageDesc) * n));
   HJ_HIP(ctx->pin_status.ensure(sizeof(int32_t) * n));
@@ -456,7 +467,8 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
   HJ_HIP(launch_entropy(static_cast<const uint8_t*>(ctx->clean.p),
                         static_cast<const uint32_t*>(ctx->segs.p), desc, infos,
                         static_cast<const HuffTable*>(ctx->luts.p),
-                        static_cast<int16_t*>(ctx->coefs.p), ctx->sub_bits, n, st));
+                        static_cast<int16_t*>(ctx->coefs.p), static_cast<uint32_t*>(ctx->recs.p),
+                        ctx->sub_bits, ctx->entropy_threads, n, st));
   mark(ctx, 4, st);
   HJ_HIP(launch_idct(static_cast<const int16_t*>(ctx->coefs.p), desc, infos,
                      static_cast<uint8_t*>(ctx->planes.p), out->idct, L.max_blocks, n, st));
@@ -581,7 +593,7 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
   DeviceGuard g(c->device);
   if (c->batch_done) (void)hipEventSynchronize(c->batch_done);
   DevBuf* bufs[] = {&c->bytes, &c->clean, &c->segs, &c->desc, &c->info,
-                    &c->luts,  &c->coefs, &c->planes, &c->wts};
+                    &c->luts,  &c->coefs, &c->planes, &c->wts, &c->recs};
   for (DevBuf* b : bufs) b->release();
   c->pin_in.release();
   c->pin_desc.release();
@@ -617,7 +629,8 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
     total += round_up((int64_t)sizes[i] + 64, 256);
   }
   Layout L;
-  int rc = build_layout(offs.data(), szs.data(), infos.data(), n, out, L, status, err, errlen);
+  int rc = build_layout(offs.data(), szs.data(), infos.data(), n, out, ctx->sub_bits, L, status, err,
+                        errlen);
   if (rc) return rc;
   HJ_HIP(ctx->pin_in.ensure((size_t)total));
   HJ_HIP(ctx->bytes.ensure((size_t)total));
@@ -648,7 +661,7 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
   DeviceGuard g(ctx->device);
   hipStream_t st = static_cast<hipStream_t>(stream);
   Layout L;
-  int rc = build_layout(offsets, sizes, infos, n, out, L, status, err, errlen);
+  int rc = build_layout(offsets, sizes, infos, n, out, ctx->sub_bits, L, status, err, errlen);
   if (rc) return rc;
   mark(ctx, 0, st);
   return run_pipeline(ctx, dev_data, dev_bytes, L, n, out, out_dev, out_bytes, st, sync, status,
@@ -673,7 +686,7 @@ int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   o.idct = idct;
   int64_t off = 0, sz = (int64_t)size, total = round_up(sz + 64, 256);
   Layout L;
-  rc = build_layout(&off, &sz, &info, 1, &o, L, nullptr, err, errlen);
+  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen);
   if (rc) return rc;
   HJ_HIP(ctx->pin_in.ensure((size_t)total));
   HJ_HIP(ctx->bytes.ensure((size_t)total));
@@ -721,7 +734,7 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   spdl_hj_output o{};
   int64_t off = 0, sz = (int64_t)size, total = round_up(sz + 64, 256);
   Layout L;
-  rc = build_layout(&off, &sz, &info, 1, &o, L, nullptr, err, errlen);
+  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen);
   if (rc) return rc;
   HJ_HIP(ctx->pin_in.ensure((size_t)total));
   HJ_HIP(ctx->bytes.ensure((size_t)total));
@@ -772,6 +785,11 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "sub_bits")) {
     if (value < 32 || value > (1 << 24) || value % 32) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->sub_bits = (int)value;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "entropy_threads")) {  // workgroup size of the Huffman kernel
+    if (value != 256 && value != 512 && value != 1024) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->entropy_threads = (int)value;
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "debug_mask")) {  // timing ablations only: output is wrong

@@ -473,12 +473,12 @@ __global__ void __launch_bounds__(kDsThreads) destuff_kernel(const uint8_t* __re
 // entropy_kernel
 // ---------------------------------------------------------------------------
 
-constexpr int kEnThreads = 256;
-constexpr int kMaxSlots = 2048;
 constexpr int kMaxLds = 6;  // distinct tables held in LDS
+constexpr int kWinWords = 16;  // bit-reader window per thread (words)
 
 constexpr int kSubPool = 2048;  // LDS entries for second-level tables of all tables
 
+template <int NT>
 struct EntShared {
   uint32_t lut[kMaxLds][kLutSize];
   uint32_t sub[kSubPool];
@@ -487,64 +487,83 @@ struct EntShared {
   uint8_t vals[kMaxLds][256];
   uint32_t s_pos[kMaxSlots];
   uint32_t s_zb[kMaxSlots];   // z | b << 8
-  int32_t s_nblk[kMaxSlots];
-  int32_t s_dc[kMaxSlots][kMaxComp];
-  uint32_t run_pos[kEnThreads];
-  uint32_t run_zb[kEnThreads];
-  int32_t scan_flag[kEnThreads];
-  int32_t scan_v[kEnThreads][4];  // blk, dc0, dc1, dc2
+  uint32_t s_nrec[kMaxSlots];  // records of the slot's current trajectory
+  uint8_t s_endz[kMaxSlots];   // z at the slot's end
+  uint32_t run_pos[NT];
+  uint32_t run_zb[NT];
+  int32_t scan_flag[NT];
+  int32_t scan_v[NT][4];  // blk, dc0, dc1, dc2
   uint16_t qt[kMaxComp][64];
   uint8_t nat[64];
   int32_t tdc[kMaxBpm], tac[kMaxBpm], bcomp[kMaxBpm];
-  int32_t red[kEnThreads];
+  int32_t red[NT];
+  uint32_t win[kWinWords][NT];  // bit-reader windows
   int32_t flag;
   int32_t err;
 };
 
 // Per-thread bit reader over the destuffed stream (big-endian bytes read as
-// 32-bit words).  `buf` holds the next 33..64 bits MSB-first; `nxt` is the
-// following word, loaded one refill ahead so its latency overlaps ~5 symbols.
+// 32-bit words).  `buf` holds the next 33..64 bits MSB-first and `nxt` the
+// word after them.  Words come from a 16-word LDS window per thread
+// ([word][thread], conflict-free), restaged from HBM once every ~12 words:
+// the decode loop itself issues no global load, so its record stores never
+// stall it (on gfx9 a vmcnt wait for a load also waits for older stores).
 struct Dec {
-  const uint32_t* w;
   uint64_t buf;
   uint32_t nxt;
-  uint32_t wi;
+  uint32_t wi;   // absolute word index of nxt
+  uint32_t wb;   // absolute word index of the window's first word
   int cnt;
   uint32_t pos;  // absolute bit position of buf's MSB
-  int z, b;      // next coefficient index (0 = DC), block-in-MCU
+  uint32_t z;    // next coefficient index (0 = DC)
+  uint32_t bs;   // 2 * block-in-MCU
 };
 
-__device__ __forceinline__ void dec_init(Dec& d, const uint32_t* words, uint32_t p, int z, int b) {
-  d.w = words;
-  const uint32_t wi = p >> 5;
-  const uint64_t hi = __builtin_bswap32(words[wi]), lo = __builtin_bswap32(words[wi + 1]);
-  d.buf = ((hi << 32) | lo) << (p & 31);
-  d.cnt = 64 - (int)(p & 31);
-  d.nxt = words[wi + 2];
-  d.wi = wi + 3;
-  d.pos = p;
-  d.z = z;
-  d.b = b;
+template <int NT>
+__device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, uint32_t wb) {
+  const uint4* src = reinterpret_cast<const uint4*>(words + wb);  // wb % 4 == 0
+  const uint4 q0 = src[0], q1 = src[1], q2 = src[2], q3 = src[3];
+  const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+#pragma unroll
+  for (int i = 0; i < 16; i++) win[i * NT] = w[i];
 }
 
-__device__ __forceinline__ void dec_refill(Dec& d) {
+template <int NT>
+__device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
+                                         uint32_t z, uint32_t bs) {
+  const uint32_t w0 = p >> 5;
+  d.wb = w0 & ~3u;
+  win_stage<NT>(win, words, d.wb);
+  const uint64_t hi = __builtin_bswap32(win[(w0 - d.wb) * NT]);
+  const uint64_t lo = __builtin_bswap32(win[(w0 + 1 - d.wb) * NT]);
+  d.buf = ((hi << 32) | lo) << (p & 31);
+  d.cnt = 64 - (int)(p & 31);
+  d.wi = w0 + 2;
+  d.nxt = win[(d.wi - d.wb) * NT];
+  d.pos = p;
+  d.z = z;
+  d.bs = bs;
+}
+
+template <int NT>
+__device__ __forceinline__ void dec_refill(Dec& d, uint32_t* win, const uint32_t* words) {
   if (d.cnt <= 32) {
     d.buf |= (uint64_t)__builtin_bswap32(d.nxt) << (32 - d.cnt);
     d.cnt += 32;
-    d.nxt = d.w[d.wi++];
+    d.wi++;
+    if (d.wi - d.wb >= (uint32_t)kWinWords) {
+      d.wb = d.wi & ~3u;
+      win_stage<NT>(win, words, d.wb);
+    }
+    d.nxt = win[(d.wi - d.wb) * NT];
   }
-}
-
-// block-in-MCU -> (dc table, ac table, component), packed 8 bits per block in
-// three wave-uniform words
-__device__ __forceinline__ uint32_t binfo(int b, uint32_t w0, uint32_t w1, uint32_t w2) {
-  const uint32_t w = b < 4 ? w0 : (b < 8 ? w1 : w2);
-  return (w >> ((b & 3) * 8)) & 0xFF;
 }
 
 // Canonical decode of a code that is not fully resolved by the LUT (longer
 // than kLutBits, or a DC size > 15): returns a kKindCode entry, 0 if invalid.
-__device__ __attribute__((noinline)) uint32_t slow_symbol(const EntShared& S, int t, uint64_t buf,
+template <class SH>
+__device__ __attribute__((noinline)) uint32_t slow_symbol(const SH& S, int t, uint64_t buf,
                                                           bool is_dc) {
   const uint32_t w16 = (uint32_t)(buf >> 48);
   for (int l = 1; l <= 16; l++) {
@@ -558,108 +577,92 @@ __device__ __attribute__((noinline)) uint32_t slow_symbol(const EntShared& S, in
   return 0;
 }
 
-struct WriteCtx {
-  int16_t* coef;      // image coefficient base
-  int32_t nb;         // next block index to start
-  int32_t dc[kMaxComp];
-  int32_t seg_end_blk;
-  uint32_t seg_end_bits;
-};
+// Symbol records.  Round 0 and the sync rounds store, per slot, one 32-bit
+// record for every symbol that yields a coefficient and for every symbol the
+// sequential decoder would reject; the write pass replays the records of the
+// final (synchronised) trajectory without decoding again.  Layout per image
+// and pass: [local slot][record / 4][thread][record % 4], so the lanes of a
+// wave store and load adjacent 16-byte groups.
+//   [0,16)  level (int16, before dequantisation; DC: the difference)
+//   [16,22) zigzag index (coefficient) or z before the symbol (marker)
+//   [22]    DC symbol
+//   [23,25) component
+//   [25,27) kind: coefficient / invalid Huffman data / symbol crosses the end
+constexpr uint32_t kRecCoef = 0;
+constexpr uint32_t kRecErrHuff = 1;
+constexpr uint32_t kRecErrTrunc = 2;
 
-// Decode every symbol that starts in [d.pos, end).  One path for DC and AC
-// symbols (selects instead of branches: lanes of a wave decode different
-// streams, so any branch is paid by the whole wave).  Sync mode
-// (WRITE=false) is total -- invalid codes consume one bit, runs past
-// coefficient 63 end the block -- so every bit position yields one
-// deterministic trajectory; it accumulates blocks started and DC diffs.
-// Write mode stores dequantised coefficients, stops after the segment's last
-// block and reports corruption.
-template <bool WRITE>
-__device__ int decode_range(const EntShared& S, Dec& d, const uint32_t bw0, const uint32_t bw1,
-                            const uint32_t bw2, const int bpm, const uint32_t end, int& nblk,
-                            int& dc0, int& dc1, int& dc2, WriteCtx* wc, int* nsym = nullptr) {
-  uint32_t info = binfo(d.b, bw0, bw1, bw2);
+// Decode every symbol that starts in [d.pos, end) and append its records to
+// `rec`; returns the record count (<= end - d.pos + 1).  Total over any bit
+// position: an invalid code consumes one bit, a run past coefficient 63 ends
+// the block, so every start state yields one deterministic trajectory.  One
+// path for DC and AC symbols (selects, not branches: the 64 lanes of a wave
+// decode 64 unrelated streams, so any branch is paid by all of them).
+template <int NT, class SH>
+__device__ uint32_t decode_slot(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
+                                const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
+                                const uint32_t end, const uint32_t seg_end,
+                                uint32_t* __restrict__ rec) {
+  auto at = [&](uint32_t n) -> uint32_t& { return rec[(n >> 2) * (NT * 4) + (n & 3)]; };
+  uint32_t n = 0;
   while (d.pos < end) {
-    if (nsym) (*nsym)++;
-    if (WRITE && d.z == 0 && wc->nb >= wc->seg_end_blk) return kOk;
-    dec_refill(d);
-    const bool is_dc = d.z == 0;
-    const int t = is_dc ? (int)(info & 7) : (int)((info >> 3) & 7);
-    const int c = (int)(info >> 6);
-    uint32_t e = S.lut[t][(uint32_t)(d.buf >> (64 - kLutBits))];
+    dec_refill<NT>(d, win, words);
+    const uint32_t z = d.z;
+    const bool is_dc = z == 0;
+    // component of this block, then its DC or AC table slot
+    const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
+    const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
+    const uint32_t hi = (uint32_t)(d.buf >> 32);
+    uint32_t e = S.lut[t][hi >> (32 - kLutBits)];
     if (((e >> 5) & 3) == kKindSub)
-      e = S.sub[((e >> 16) << kSubBits) + (uint32_t)((d.buf >> (48)) & ((1u << kSubBits) - 1))];
-    if (((e >> 5) & 3) == kKindSlow) {
-      e = slow_symbol(S, t, d.buf, is_dc);
-      if (e == 0) {
-        if (WRITE) return kErrBadHuffman;
-        d.buf <<= 1;
-        d.cnt -= 1;
-        d.pos += 1;
-        continue;
-      }
-    }
-    const uint32_t len = e & 31, sym = (e >> 8) & 0xFF;
-    const bool full = ((e >> 5) & 3) == kKindFull;
-    const uint32_t sz = full ? 0u : (is_dc ? sym : (sym & 15u));
-    const uint64_t rest = d.buf << len;
-    const uint32_t raw = (uint32_t)((rest >> 1) >> (63 - sz));  // top sz bits, 0 if sz==0
-    const uint32_t half = (1u << sz) >> 1;
-    const int vx = (int)raw - (raw < half ? (int)((1u << sz) - 1u) : 0);
-    const int v = full ? (int)(int16_t)(e >> 16) : vx;
-    const uint32_t nbits = len + sz;
+      e = S.sub[((e >> 16) << kSubBits) | ((hi >> (32 - kLutBits - kSubBits)) & ((1u << kSubBits) - 1))];
+    if (((e >> 5) & 3) == kKindSlow) e = slow_symbol(S, (int)t, d.buf, is_dc);
+    const bool valid = e != 0u;
+    const uint32_t sym = (e >> 8) & 0xFF;
+    const uint32_t sz = ((e >> 5) & 3) == kKindFull ? 0u : (is_dc ? sym : (sym & 15u));
+    const uint32_t nbits = (valid ? (e & 31u) : 1u) + sz;  // <= 31: hi holds >= 32 valid bits
+    const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
+    const uint32_t msk = (1u << sz) - 1u;
+    // Full entries carry the value in bits 16..31 (sz == 0 there); Code
+    // entries have zeros there and the value follows the code (JPEG EXTEND)
+    const int v = (int)(int16_t)(e >> 16) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
     d.buf <<= nbits;
     d.cnt -= (int)nbits;
     d.pos += nbits;
-    const int r = is_dc ? 0 : (int)(sym >> 4);
-    const bool coef = is_dc || (sym & 15u) != 0;
-    const int zpos = d.z + r;
-    const bool bad_run = coef && zpos > 63;
-    int zn = coef ? zpos + 1 : (r == 15 ? d.z + 16 : 64);
-    zn = bad_run ? 64 : zn;
-    if (WRITE) {
-      if (bad_run || (!coef && r != 0 && r != 15)) return kErrBadHuffman;
-      const int zp = zpos & 63;
-      const int qv = S.qt[c][zp];
-      const int cur = c == 0 ? wc->dc[0] : (c == 1 ? wc->dc[1] : wc->dc[2]);
-      const int ndc = cur + v;
-      const uint32_t dq = (uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc;
-      const int32_t dqi = (int32_t)dq;
-      const int16_t val = is_dc ? (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi))
-                                : (int16_t)(v * qv);
-      const int blk = is_dc ? wc->nb : wc->nb - 1;
-      if (coef) wc->coef[(size_t)blk * 64 + S.nat[zp]] = val;
-      if (is_dc) {
-        wc->nb++;
-        if (c == 0) wc->dc[0] = ndc;
-        else if (c == 1) wc->dc[1] = ndc;
-        else wc->dc[2] = ndc;
-      }
-    } else {
-      nblk += is_dc ? 1 : 0;
-      dc0 += (is_dc && c == 0) ? v : 0;
-      dc1 += (is_dc && c == 1) ? v : 0;
-      dc2 += (is_dc && c == 2) ? v : 0;
-    }
-    const bool bend = zn >= 64;
-    const int bn = (d.b + 1 == bpm) ? 0 : d.b + 1;
-    d.z = bend ? 0 : zn;
-    d.b = bend ? bn : d.b;
-    info = binfo(d.b, bw0, bw1, bw2);
-    if (WRITE && d.pos > wc->seg_end_bits) return kErrTruncated;
+    const uint32_t r = is_dc ? 0u : (sym >> 4);
+    const bool coef = is_dc || (sym & 15u) != 0u;
+    const uint32_t zpos = z + r;
+    const bool bad_run = coef && zpos > 63u;
+    const bool bad = !valid || bad_run || (!coef && r != 0u && r != 15u);
+    uint32_t zn = coef ? zpos + 1u : (r == 15u ? z + 16u : 64u);
+    zn = bad_run ? 64u : zn;
+    zn = valid ? zn : z;
+    const uint32_t rc = ((uint32_t)v & 0xFFFFu) | (zpos << 16) | ((uint32_t)is_dc << 22) | (c << 23);
+    const uint32_t rb = (kRecErrHuff << 25) | (z << 16);
+    // unconditional store: a symbol without a record is overwritten by the next
+    at(n) = bad ? rb : rc;
+    n += (bad || coef) ? 1u : 0u;
+    if (d.pos > seg_end) at(n++) = (kRecErrTrunc << 25) | (z << 16);
+    const bool bend = zn >= 64u;
+    const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
+    d.z = bend ? 0u : zn;
+    d.bs = bend ? bsn : d.bs;
   }
-  return kOk;
+  return n;
 }
 
-__global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __restrict__ clean,
-                                                             const uint32_t* __restrict__ segs,
-                                                             const ImageDesc* __restrict__ desc,
-                                                             ImageInfo* __restrict__ infos,
-                                                             const HuffTable* __restrict__ luts,
-                                                             int16_t* __restrict__ coefs,
-                                                             const int sub_bits_param) {
-  __shared__ EntShared S;
+template <int NT>
+__global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
+                                                     const uint32_t* __restrict__ segs,
+                                                     const ImageDesc* __restrict__ desc,
+                                                     ImageInfo* __restrict__ infos,
+                                                     const HuffTable* __restrict__ luts,
+                                                     int16_t* __restrict__ coefs,
+                                                     uint32_t* __restrict__ recs,
+                                                     const int sub_bits_param) {
+  __shared__ EntShared<NT> S;
   const int img = blockIdx.x, tid = threadIdx.x;
+  uint32_t* win = &S.win[0][tid];
   if (infos[img].status != kOk) return;
   const ImageDesc dd = desc[img];
   const ImageInfo& in = infos[img];
@@ -672,7 +675,7 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
   const int nseg = ri > 0 ? (nmcu + ri - 1) / ri : 1;
 
   // ---- tables into LDS (dedup table slots per component) ----
-  uint32_t bw[3] = {0, 0, 0};
+  uint32_t bcomp = 0, tmap = 0;  // 2-bit component per block-in-MCU; 3-bit table slots
   {
     int slots[kMaxLds], ns = 0, ldc[kMaxComp] = {0, 0, 0}, lac[kMaxComp] = {0, 0, 0};
     for (int c = 0; c < in.ncomp; c++) {
@@ -696,25 +699,23 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       const bool fits = (pool + nsub) << kSubBits <= kSubPool;
       const int base = pool;
       if (fits) pool += nsub;
-      for (int k = tid; k < kLutSize; k += kEnThreads) {
+      for (int k = tid; k < kLutSize; k += NT) {
         uint32_t e = T.lut[k];
         if ((e >> 5 & 3) == kKindSub) e = fits ? e + ((uint32_t)base << 16) : 0u;
         S.lut[i][k] = e;
       }
       if (fits)
-        for (int k = tid; k < nsub << kSubBits; k += kEnThreads)
+        for (int k = tid; k < nsub << kSubBits; k += NT)
           S.sub[(base << kSubBits) + k] = T.sub[k];
       if (tid < 18) S.maxcode[i][tid] = T.maxcode[tid];
       if (tid < 17) S.valoff[i][tid] = T.valoff[tid];
-      S.vals[i][tid] = T.vals[tid];
+      if (tid < 256) S.vals[i][tid] = T.vals[tid];
     }
-    for (int k = tid; k < kMaxComp * 64; k += kEnThreads) S.qt[k / 64][k % 64] = in.qt[k / 64][k % 64];
+    for (int k = tid; k < kMaxComp * 64; k += NT) S.qt[k / 64][k % 64] = in.qt[k / 64][k % 64];
     if (tid < 64) S.nat[tid] = kNat[tid];
-    for (int b = 0; b < bpm; b++) {
-      const int c = in.mcu_comp[b];
-      const uint32_t v = (uint32_t)ldc[c] | ((uint32_t)lac[c] << 3) | ((uint32_t)c << 6);
-      bw[b >> 2] |= v << ((b & 3) * 8);
-    }
+    for (int b = 0; b < bpm; b++) bcomp |= (uint32_t)in.mcu_comp[b] << (2 * b);
+    for (int c = 0; c < kMaxComp; c++)
+      tmap |= ((uint32_t)ldc[c] << (3 * c)) | ((uint32_t)lac[c] << (9 + 3 * c));
     if (tid == 0) S.err = kOk;
   }
   if (nseg_found < nseg) {
@@ -730,39 +731,36 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
 
   // ---- subsequence size: keep every segment within kMaxSlots slots ----
   uint32_t maxbits = 0;
-  for (int s = tid; s < nseg; s += kEnThreads) {
+  for (int s = tid; s < nseg; s += NT) {
     const uint32_t a = seg_start_bits(s), e = seg_end_bits(s);
     maxbits = max(maxbits, e > a ? e - a : 0u);
   }
   S.red[tid] = (int32_t)maxbits;
   __syncthreads();
-  for (int off = kEnThreads / 2; off > 0; off >>= 1) {
+  for (int off = NT / 2; off > 0; off >>= 1) {
     if (tid < off) S.red[tid] = max(S.red[tid], S.red[tid + off]);
     __syncthreads();
   }
   maxbits = (uint32_t)S.red[0];
   __syncthreads();
-  uint32_t N = (uint32_t)sub_bits_param;
-  {
-    uint32_t need = (maxbits + kMaxSlots - 1) / kMaxSlots;
-    need = (need + 31) & ~31u;
-    if (need > N) N = need;
+  const uint32_t N = slot_bits(maxbits, sub_bits_param);
+  const uint32_t cap = N + kRecPad;  // records per slot
+  if ((int64_t)(kMaxSlots + NT) * cap > dd.rec_cap) {  // host sized the record buffer
+    if (tid == 0) infos[img].status = kErrBadGeometry;
+    return;
   }
   const int cmax = max(1, (int)((maxbits + N - 1) / N));
   const int seg_per_chunk = max(1, kMaxSlots / cmax);
   int16_t* coef_img = coefs + (size_t)dd.coef_off * 64;
+  uint32_t* rec_img = recs + dd.rec_off;
   int rounds_total = 0;
-  __shared__ int dbg_sh[2];
-  int64_t dbg_acc[4] = {0, 0, 0, 0};
-  if (tid < 2) dbg_sh[tid] = 0;
-  __syncthreads();
   int64_t tph[4] = {0, 0, 0, 0};
   int64_t tstamp = wall_clock64();
 
   for (int seg_lo = 0; seg_lo < nseg; seg_lo += seg_per_chunk) {
     const int nsc = min(seg_per_chunk, nseg - seg_lo);
     const int nslots = nsc * cmax;
-    const int K = (nslots + kEnThreads - 1) / kEnThreads;
+    const int K = (nslots + NT - 1) / NT;
     const int r0 = min(tid * K, nslots), r1 = min(r0 + K, nslots);
     auto slot_seg = [&](int k) { return seg_lo + k / cmax; };
     auto slot_j = [&](int k) { return k % cmax; };
@@ -775,51 +773,42 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       return slot_j(k) > 0 && slot_start(k) >= seg_end_bits(slot_seg(k));
     };
     auto slot_known = [&](int k) { return slot_j(k) == 0; };
+    // this thread's records of its k-th slot (k in [r0, r1))
+    auto slot_recs = [&](int k) {
+      return rec_img + ((size_t)(k - r0) * (cap / 4) * NT + tid) * 4;
+    };
+    auto decode_k = [&](Dec& d, int k) {
+      S.s_pos[k] = d.pos;
+      S.s_zb[k] = d.z | (d.bs << 8);
+      const uint32_t n = decode_slot<NT>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm,
+                                         slot_end(k), seg_end_bits(slot_seg(k)), slot_recs(k));
+      S.s_nrec[k] = n;
+      S.s_endz[k] = (uint8_t)d.z;
+    };
 
     // ---- round 0: every run from a guess at its first slot ----
-    int nsym0 = 0;
-    const int64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = wall_clock64();
     {
       Dec d;
       d.pos = 0;
-      d.z = d.b = 0;
+      d.z = d.bs = 0;
       bool have = false;
       for (int k = r0; k < r1; k++) {
         if (slot_empty(k)) {
           have = false;
           continue;
         }
-        if (slot_known(k) || !have) dec_init(d, words, slot_start(k), 0, 0);
-        S.s_pos[k] = d.pos;
-        S.s_zb[k] = (uint32_t)d.z | ((uint32_t)d.b << 8);
-        int nblk = 0, c0 = 0, c1 = 0, c2 = 0;
-        decode_range<false>(S, d, bw[0], bw[1], bw[2], bpm, slot_end(k), nblk, c0, c1, c2, nullptr,
-                            &nsym0);
-        S.s_nblk[k] = nblk;
-        S.s_dc[k][0] = c0;
-        S.s_dc[k][1] = c1;
-        S.s_dc[k][2] = c2;
+        if (slot_known(k) || !have) dec_init<NT>(d, win, words, slot_start(k), 0, 0);
+        decode_k(d, k);
         have = true;
       }
       S.run_pos[tid] = d.pos;
-      S.run_zb[tid] = (have && r0 < r1) ? ((uint32_t)d.z | ((uint32_t)d.b << 8)) : 0xFFFFFFFFu;
+      S.run_zb[tid] = (have && r0 < r1) ? (d.z | (d.bs << 8)) : 0xFFFFFFFFu;
     }
     __syncthreads();
     {
       const int64_t t = wall_clock64();
       tph[0] += t - tstamp;
       tstamp = t;
-      const int64_t clk1 = __builtin_amdgcn_s_memtime();
-      // per-wave max symbols (= wave iterations) and total symbols
-      int wmax = nsym0;
-      for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, __shfl_xor(wmax, o));
-      atomicAdd(&S.red[0], 0);
-      if (tid == 0) {
-        dbg_acc[2] = clk1 - clk0;
-        dbg_acc[3] = t - rt0;
-      }
-      atomicAdd((int*)&dbg_sh[0], nsym0);
-      if ((tid & 63) == 0) atomicAdd((int*)&dbg_sh[1], wmax);
     }
     // ---- sync rounds: re-decode a run from its left neighbour's end state
     // until the trajectory merges with the stored one at a slot boundary ----
@@ -837,30 +826,22 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       __syncthreads();
       if (redo) {
         Dec d;
-        dec_init(d, words, npos, (int)(nzb & 0xFF), (int)(nzb >> 8));
+        dec_init<NT>(d, win, words, npos, nzb & 0xFF, nzb >> 8);
         bool merged = false;
         for (int k = r0; k < r1; k++) {
           if (slot_empty(k) || slot_known(k)) {
             merged = true;
             break;
           }
-          const uint32_t zb = (uint32_t)d.z | ((uint32_t)d.b << 8);
+          const uint32_t zb = d.z | (d.bs << 8);
           if (k > r0 && S.s_pos[k] == d.pos && S.s_zb[k] == zb) {
             merged = true;
             break;
           }
-          S.s_pos[k] = d.pos;
-          S.s_zb[k] = zb;
-          int nblk = 0, c0 = 0, c1 = 0, c2 = 0;
-          decode_range<false>(S, d, bw[0], bw[1], bw[2], bpm, slot_end(k), nblk, c0, c1, c2,
-                              nullptr);
-          S.s_nblk[k] = nblk;
-          S.s_dc[k][0] = c0;
-          S.s_dc[k][1] = c1;
-          S.s_dc[k][2] = c2;
+          decode_k(d, k);
         }
         if (!merged) {
-          const uint32_t zb = (uint32_t)d.z | ((uint32_t)d.b << 8);
+          const uint32_t zb = d.z | (d.bs << 8);
           if (S.run_pos[tid] != d.pos || S.run_zb[tid] != zb) {
             S.run_pos[tid] = d.pos;
             S.run_zb[tid] = zb;
@@ -872,7 +853,7 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       const int again = S.flag;
       rounds++;
       __syncthreads();
-      if (!again || rounds > kEnThreads + 2) break;
+      if (!again || rounds > NT + 2) break;
     }
     rounds_total += rounds;
     {
@@ -881,7 +862,8 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       tstamp = t;
     }
 
-    // ---- segmented exclusive scan over runs: (absolute next block, DC preds) ----
+    // ---- per-run totals from the records, then a segmented exclusive scan
+    // over runs: (absolute next block, DC predictors) ----
     {
       int flag = 0, v[4] = {0, 0, 0, 0};
       for (int k = r0; k < r1; k++) {
@@ -891,13 +873,28 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
           v[0] = ri > 0 ? slot_seg(k) * ri * bpm : 0;
           v[1] = v[2] = v[3] = 0;
         }
-        v[0] += S.s_nblk[k];
-        for (int c = 0; c < kMaxComp; c++) v[1 + c] += S.s_dc[k][c];
+        const uint32_t* R = slot_recs(k);
+        const int n = (int)S.s_nrec[k];
+        for (int i = 0; i < n; i += 4) {
+          const uint4 q = *reinterpret_cast<const uint4*>(R + (size_t)(i >> 2) * (NT * 4));
+          const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const uint32_t x = w4[j];
+            const bool dc = i + j < n && (x >> 22 & 1u) && (x >> 25) == kRecCoef;
+            const int c = (int)((x >> 23) & 3u);
+            const int lv = dc ? (int)(int16_t)(x & 0xFFFFu) : 0;
+            v[0] += dc ? 1 : 0;
+            v[1] += c == 0 ? lv : 0;
+            v[2] += c == 1 ? lv : 0;
+            v[3] += c == 2 ? lv : 0;
+          }
+        }
       }
       S.scan_flag[tid] = flag;
       for (int i = 0; i < 4; i++) S.scan_v[tid][i] = v[i];
       __syncthreads();
-      for (int off = 1; off < kEnThreads; off <<= 1) {
+      for (int off = 1; off < NT; off <<= 1) {
         int pf = 0, pv[4] = {0, 0, 0, 0};
         const bool take = tid >= off;
         if (take) {
@@ -917,42 +914,76 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
       tph[2] += t - tstamp;
       tstamp = t;
     }
-    // ---- write pass ----
+    // ---- write pass: replay the records, dequantise, scatter to natural
+    // order; the sequential decoder's stop and error rules per segment ----
     {
-      WriteCtx wc;
-      wc.coef = coef_img;
-      wc.nb = 0;
-      wc.dc[0] = wc.dc[1] = wc.dc[2] = 0;
+      int nb = 0, dc0 = 0, dc1 = 0, dc2 = 0;
       if (tid > 0) {
-        wc.nb = S.scan_v[tid - 1][0];
-        for (int c = 0; c < kMaxComp; c++) wc.dc[c] = S.scan_v[tid - 1][1 + c];
+        nb = S.scan_v[tid - 1][0];
+        dc0 = S.scan_v[tid - 1][1];
+        dc1 = S.scan_v[tid - 1][2];
+        dc2 = S.scan_v[tid - 1][3];
       }
-      Dec d;
-      d.pos = 0;
-      d.z = d.b = 0;
-      bool have = false;
       int rc = kOk;
+      bool done = false;  // the segment's last block is complete
       for (int k = r0; k < r1 && rc == kOk; k++) {
         if (slot_empty(k)) continue;
         const int s = slot_seg(k);
         if (slot_known(k)) {
-          dec_init(d, words, slot_start(k), 0, 0);
-          wc.nb = ri > 0 ? s * ri * bpm : 0;
-          wc.dc[0] = wc.dc[1] = wc.dc[2] = 0;
-        } else if (!have) {
-          const uint32_t zb = S.s_zb[k];
-          dec_init(d, words, S.s_pos[k], (int)(zb & 0xFF), (int)(zb >> 8));
+          nb = ri > 0 ? s * ri * bpm : 0;
+          dc0 = dc1 = dc2 = 0;
+          done = false;
         }
-        have = true;
-        wc.seg_end_blk = ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks;
-        wc.seg_end_bits = seg_end_bits(s);
-        int dummy = 0, c0 = 0, c1 = 0, c2 = 0;
-        rc = decode_range<true>(S, d, bw[0], bw[1], bw[2], bpm, slot_end(k), dummy, c0, c1, c2,
-                                &wc);
+        if (done) continue;
+        const int seg_end_blk = ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks;
+        const uint32_t* R = slot_recs(k);
+        const int n = (int)S.s_nrec[k];
+        for (int i = 0; i < n && !done && rc == kOk; i += 4) {
+          const uint4 q = *reinterpret_cast<const uint4*>(R + (size_t)(i >> 2) * (NT * 4));
+          const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            if (i + j >= n || done || rc != kOk) break;
+            const uint32_t x = w4[j];
+            const uint32_t kind = x >> 25;
+            const int zz = (int)((x >> 16) & 63u);
+            if (kind != kRecCoef) {
+              // the sequential decoder stops at the segment's last block and
+              // never reads what follows; anything else is an error
+              if (nb > seg_end_blk || (nb == seg_end_blk && zz == 0)) done = true;
+              else rc = kind == kRecErrTrunc ? kErrTruncated : kErrBadHuffman;
+              break;
+            }
+            const bool is_dc = (x >> 22) & 1u;
+            const int c = (int)((x >> 23) & 3u);
+            const int lv = (int)(int16_t)(x & 0xFFFFu);
+            if ((is_dc ? nb : nb - 1) >= seg_end_blk) {
+              done = true;
+              break;
+            }
+            const int qv = S.qt[c][zz];
+            int16_t val;
+            int blk;
+            if (is_dc) {
+              const int cur = c == 0 ? dc0 : (c == 1 ? dc1 : dc2);
+              const int ndc = cur + lv;
+              if (c == 0) dc0 = ndc;
+              else if (c == 1) dc1 = ndc;
+              else dc2 = ndc;
+              const int32_t dqi = (int32_t)((uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc);
+              val = (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi));
+              blk = nb++;
+            } else {
+              val = (int16_t)(lv * qv);
+              blk = nb - 1;
+            }
+            coef_img[(size_t)blk * 64 + S.nat[zz]] = val;
+          }
+        }
         // last slot of its segment: every block of the segment must be done
-        // (nb beyond the segment only happens for garbage after its last block)
         const bool last = (k + 1 >= nslots) || slot_j(k + 1) == 0 || slot_empty(k + 1);
-        if (rc == kOk && last && (wc.nb < wc.seg_end_blk || (wc.nb == wc.seg_end_blk && d.z != 0)))
+        if (rc == kOk && !done && last &&
+            (nb < seg_end_blk || (nb == seg_end_blk && S.s_endz[k] != 0)))
           rc = kErrTruncated;
       }
       if (rc != kOk) atomicCAS(&S.err, kOk, rc);
@@ -968,10 +999,7 @@ __global__ void __launch_bounds__(kEnThreads) entropy_kernel(const uint8_t* __re
     if (S.err != kOk) infos[img].status = S.err;
     infos[img].sync_rounds = rounds_total;
     for (int i = 0; i < 4; i++) infos[img].tphase[i] = tph[i];
-    infos[img].dbg[0] = dbg_sh[0];
-    infos[img].dbg[1] = dbg_sh[1];
-    infos[img].dbg[2] = dbg_acc[2];
-    infos[img].dbg[3] = dbg_acc[3];
+    for (int i = 0; i < 4; i++) infos[img].dbg[i] = 0;
   }
 }
 
@@ -1397,10 +1425,17 @@ hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo
   return hipGetLastError();
 }
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
-                          ImageInfo* infos, const HuffTable* luts, int16_t* coefs, int sub_bits,
-                          int n, hipStream_t st) {
-  hipLaunchKernelGGL(entropy_kernel, dim3(n), dim3(kEnThreads), 0, st, clean, segs, desc, infos,
-                     luts, coefs, sub_bits);
+                          ImageInfo* infos, const HuffTable* luts, int16_t* coefs, uint32_t* recs,
+                          int sub_bits, int threads, int n, hipStream_t st) {
+  if (threads == 1024)
+    hipLaunchKernelGGL(entropy_kernel<1024>, dim3(n), dim3(1024), 0, st, clean, segs, desc, infos,
+                       luts, coefs, recs, sub_bits);
+  else if (threads == 512)
+    hipLaunchKernelGGL(entropy_kernel<512>, dim3(n), dim3(512), 0, st, clean, segs, desc, infos,
+                       luts, coefs, recs, sub_bits);
+  else
+    hipLaunchKernelGGL(entropy_kernel<256>, dim3(n), dim3(256), 0, st, clean, segs, desc, infos,
+                       luts, coefs, recs, sub_bits);
   return hipGetLastError();
 }
 hipError_t launch_idct(const int16_t* coefs, const ImageDesc* desc, const ImageInfo* infos,

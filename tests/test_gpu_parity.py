@@ -174,16 +174,33 @@ def test_corrupt_streams_agree_with_oracle(decoder, oracle, seed):
         np.testing.assert_array_equal(t.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("threads", [256, 512, 1024])
 @pytest.mark.parametrize("sub_bits", [32, 64, 256, 1024, 8192])
-def test_subsequence_sizes(oracle, sub_bits):
-    """The sync result must not depend on the subsequence size."""
+def test_subsequence_sizes(oracle, sub_bits, threads):
+    """The sync result must not depend on the subsequence size or on the
+    number of Huffman decoder threads per image."""
     from spdl_amd._lib import Decoder
 
     dec = Decoder(0)
     dec.set_param("sub_bits", sub_bits)
+    dec.set_param("entropy_threads", threads)
     for name in ["q90_420", "restart_blocks", "noise_420", "gray_odd"]:
         d = cases.case(name)
         info = oracle.parse(d)
         hyp = _decode(dec, [d], Output(pix_fmt="rgb24"), (info.height, info.width, 3))[0].numpy()
         np.testing.assert_array_equal(hyp, oracle.decode_rgb(d, 0, "rgb24"))
+    for seed in range(6):
+        d = cases.corrupt_scan(seed)
+        try:
+            ref = oracle.decode_rgb(d, 0, "rgb24")
+        except oracle.OracleError:
+            ref = None
+        info = oracle.parse(d)
+        t = torch.empty((info.height, info.width, 3), dtype=torch.uint8, device="cuda:0")
+        if ref is None:
+            with pytest.raises(RuntimeError):
+                dec.decode_batch([d], Output(pix_fmt="rgb24"), t.data_ptr(), t.numel())
+        else:
+            dec.decode_batch([d], Output(pix_fmt="rgb24"), t.data_ptr(), t.numel())
+            np.testing.assert_array_equal(t.cpu().numpy(), ref)
     dec.close()
