@@ -76,21 +76,31 @@ struct ImageDesc {      // host-filled per image
   // resize geometry (host computed from the probe; device recomputes nothing)
   int32_t sw, sh, dx, dy, ow, oh;
   int32_t taps_x[kMaxComp], taps_y[kMaxComp];
-  int32_t rs_ty;        // resize: output rows per workgroup tile
-  int32_t rs_cw;        // resize: content columns per chunk
+  // resize: visible content columns [vx0, vx0 + nvis) of the scaled image,
+  // horizontal-pass intermediate (int16 [rows][tmp_stride] per plane at
+  // tmp_off + tmp_plane[c]), vertical-pass band rows / column chunk
+  int32_t vx0, nvis;
+  int32_t tmp_stride;
+  int32_t v_rb, v_cols;
   int32_t pad2_;
+  int64_t tmp_off;
+  int64_t tmp_plane[kMaxComp];
   int64_t rec_off;      // entropy symbol records: offset (u32 units) and capacity
   int64_t rec_cap;
 };
 
-// resize tiling: LDS holds kRsRows horizontally filtered source rows of one
-// kRsCols-wide column chunk (int16, Q6)
-constexpr int kRsCols = 128;
-constexpr int kRsRows = 136;
-constexpr int kRsMaxTy = 16;
-constexpr int kRsSrcW = 384;        // staged source bytes per row
-constexpr int kRsSrcBytes = 24576;  // staged source window (rows x kRsSrcW)
-constexpr int kRsWts = 4096;        // staged horizontal weights (int16)
+// resize: horizontal pass stages up to kHMaxRows source rows (kHSrcBytes of
+// LDS) per workgroup; the vertical pass stages kVBuf int16 intermediate values
+// for a band of up to kVMaxRb output rows x kVMaxCols columns
+constexpr int kHSrcBytes = 16384;
+constexpr int kHMaxRows = 16;
+constexpr int kVBuf = 16384;
+constexpr int kVMaxRb = 8;
+constexpr int kVMaxCols = 256;
+inline HJ_HD int h_rows_per_group(int stride) {
+  const int r = kHSrcBytes / (stride > 0 ? stride : 1);
+  return r < 1 ? 1 : (r > kHMaxRows ? kHMaxRows : r);
+}
 
 struct ImageInfo {      // device-filled by the parse kernel
   int32_t status;

@@ -29,8 +29,8 @@ hipError_t launch_weights(const ImageDesc*, const ImageInfo*, int32_t*, int, int
                           hipStream_t);
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                       const BatchParams&, int64_t, int, hipStream_t);
-hipError_t launch_resize(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*, void*,
-                         const BatchParams&, int64_t, int, hipStream_t);
+hipError_t launch_resize(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*,
+                         int16_t*, void*, const BatchParams&, int64_t, int64_t, int, hipStream_t);
 }  // namespace hj
 
 using namespace hj;
@@ -211,7 +211,7 @@ struct Layout {
   int64_t out_elems_per_image = 0;
   int max_blocks = 0, max_len = 0;
   int64_t max_px = 0;
-  int64_t max_tiles = 0;
+  int64_t max_hgroups = 0, max_vbands = 0, total_tmp = 0;
   int ow = 0, oh = 0;
 };
 
@@ -332,33 +332,52 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
       }
       int ml = g.sw > g.sh ? g.sw : g.sh;
       if (ml > L.max_len) L.max_len = ml;
-      // tile sizes: the LDS-staged source window of one (rs_ty rows x rs_cw
-      // columns) tile must fit kRsRows / kRsSrcW / kRsSrcBytes / kRsWts
-      int ty = kRsMaxTy, tcw = kRsCols;
-      auto fits = [&](int ty_, int cw_) {
-        for (int c = 0; c < p.ncomp; c++) {
-          const float sy = fmaxf((float)chh[c] / (float)g.sh, 1.0f);
-          const float sx = fmaxf((float)cw[c] / (float)g.sw, 1.0f);
-          const int tpy = ((d.taps_y[c] + 1) / 2) * 2, tpx = ((d.taps_x[c] + 1) / 2) * 2;
-          const int rows = (int)ceilf((float)(ty_ - 1) * sy) + 2 + tpy;
-          const int wsrc = (int)ceilf((float)(cw_ - 1) * sx) + 2 + tpx + 8;  // + dword realignment
-          if (rows > kRsRows || wsrc > kRsSrcW || rows * wsrc > kRsSrcBytes ||
-              cw_ * tpx > kRsWts || ty_ * tpy > kRsMaxTy * kRsRows)
-            return false;
+      // visible content of the scaled image, horizontal-pass intermediate
+      d.vx0 = g.dx < 0 ? -g.dx : 0;
+      const int vx1 = (g.ow - g.dx) < g.sw ? (g.ow - g.dx) : g.sw;
+      d.nvis = vx1 > d.vx0 ? vx1 - d.vx0 : 0;
+      d.tmp_stride = (int32_t)round_up(d.nvis > 0 ? d.nvis : 1, 8);
+      d.tmp_off = L.total_tmp;
+      int64_t tsz = 0;
+      for (int c = 0; c < p.ncomp; c++) {
+        d.tmp_plane[c] = tsz;
+        tsz += (int64_t)chh[c] * d.tmp_stride;
+      }
+      L.total_tmp += round_up(tsz, 64);
+      for (int c = 0; c < p.ncomp; c++) {
+        const int64_t groups = (chh[c] + h_rows_per_group(d.plane_stride[c]) - 1) /
+                               h_rows_per_group(d.plane_stride[c]);
+        if (groups > L.max_hgroups) L.max_hgroups = groups;
+      }
+      // vertical pass: widest column chunk, then the tallest band whose
+      // staged intermediate rows fit kVBuf for every plane
+      int rb = 0, vc = 0;
+      for (int cand = kVMaxCols; cand >= 64 && rb == 0; cand -= 64) {
+        const int ncc = cand < d.nvis ? cand : (d.nvis > 0 ? d.nvis : 1);
+        for (int r = kVMaxRb; r >= 1; r--) {
+          bool ok = true;
+          for (int c = 0; c < p.ncomp; c++) {
+            const float sy = (float)chh[c] / (float)g.sh;
+            const int tpy = ((d.taps_y[c] + 1) / 2) * 2;
+            const int rows = (int)ceilf((float)(r - 1) * sy) + 2 + tpy;
+            if ((int64_t)rows * ncc > kVBuf) ok = false;
+          }
+          if (ok) {
+            rb = r;
+            vc = cand;
+            break;
+          }
         }
-        return true;
-      };
-      while (tcw > 1 && !fits(1, tcw)) tcw--;
-      while (ty > 1 && !fits(ty, tcw)) ty--;
-      if (!fits(ty, tcw)) {
+      }
+      if (rb == 0) {
         if (status) status[i] = SPDL_HJ_ERR_BAD_GEOMETRY;
         set_err(err, errlen, "Failed to decode an image. (image %d: resize tile does not fit)", i);
         return SPDL_HJ_ERR_BAD_GEOMETRY;
       }
-      d.rs_ty = ty;
-      d.rs_cw = tcw;
-      const int64_t tiles = (g.oh + ty - 1) / ty;
-      if (tiles > L.max_tiles) L.max_tiles = tiles;
+      d.v_rb = rb;
+      d.v_cols = vc;
+      const int64_t bands = (g.oh + rb - 1) / rb;
+      if (bands > L.max_vbands) L.max_vbands = bands;
     }
     int64_t px = (int64_t)g.ow * g.oh;
     if (px > L.max_px) L.max_px = px;
@@ -372,7 +391,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
 
 struct spdl_hj_ctx {
   int device = 0;
-  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts, recs;
+  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts, recs, rtmp;
   PinBuf pin_in, pin_desc, pin_status;
   hipEvent_t staging_free = nullptr;  // host staging may be rewritten after this
   hipEvent_t batch_done = nullptr;    // device workspace free after this
@@ -448,7 +467,10 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
   HJ_HIP(ctx->coefs.ensure((size_t)L.total_blocks * 128 + 256));
   HJ_HIP(ctx->planes.ensure((size_t)L.total_planes + 256));
   HJ_HIP(ctx->recs.ensure((size_t)L.total_recs * 4 + 256));
-  if (out->resize) HJ_HIP(ctx->wts.ensure((size_t)L.total_wts * 4 + 256));
+  if (out->resize) {
+    HJ_HIP(ctx->wts.ensure((size_t)L.total_wts * 4 + 256));
+    HJ_HIP(ctx->rtmp.ensure((size_t)L.total_tmp * 2 + 256));
+  }
   HJ_HIP(ctx->pin_desc.ensure(sizeof(ImageDesc) * n));
   HJ_HIP(ctx->pin_status.ensure(sizeof(int32_t) * n));
   HJ_HIP(hipEventSynchronize(ctx->staging_free));
@@ -494,8 +516,9 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
                             n, st));
       mark(ctx, 6, st);
       HJ_HIP(launch_resize(static_cast<const uint8_t*>(ctx->planes.p), desc, infos,
-                           static_cast<const int32_t*>(ctx->wts.p), out_dev, bp, L.max_tiles, n,
-                           st));
+                           static_cast<const int32_t*>(ctx->wts.p),
+                           static_cast<int16_t*>(ctx->rtmp.p), out_dev, bp, L.max_hgroups,
+                           L.max_vbands, n, st));
     } else {
       mark(ctx, 6, st);
       HJ_HIP(launch_csc(static_cast<const uint8_t*>(ctx->planes.p), desc, infos, out_dev, bp,
@@ -593,7 +616,7 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
   DeviceGuard g(c->device);
   if (c->batch_done) (void)hipEventSynchronize(c->batch_done);
   DevBuf* bufs[] = {&c->bytes, &c->clean, &c->segs, &c->desc, &c->info,
-                    &c->luts,  &c->coefs, &c->planes, &c->wts, &c->recs};
+                    &c->luts,  &c->coefs, &c->planes, &c->wts, &c->recs, &c->rtmp};
   for (DevBuf* b : bufs) b->release();
   c->pin_in.release();
   c->pin_desc.release();

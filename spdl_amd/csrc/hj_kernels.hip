@@ -1212,179 +1212,285 @@ __global__ void __launch_bounds__(256) weights_kernel(const ImageDesc* __restric
 }
 #pragma clang fp contract(on)
 
-// Fused separable resize + colour conversion + pad/crop + normalise.
-// One workgroup = (image, band of rs_ty output rows).  For each chunk of
-// rs_cw content columns and each plane: the source window (rows x bytes) and
-// the chunk's horizontal weights are staged in LDS with coalesced loads, the
-// horizontal taps of every needed source row go to LDS (Q14 weights -> Q6
-// int16, (acc + 128) >> 8), the vertical taps read that ((acc + 2^19) >> 20,
-// clamp), then YCbCr -> RGB and the band is stored.  The host picks rs_ty and
-// rs_cw per image so every staged buffer fits.  Arithmetic: exactly
-// oracle/jpeg_oracle.c resize_plane + jo_resize_planes.
-__global__ void __launch_bounds__(256) resize_kernel(const uint8_t* __restrict__ planes,
-                                                     const ImageDesc* __restrict__ desc,
-                                                     const ImageInfo* __restrict__ infos,
-                                                     const int32_t* __restrict__ pool,
-                                                     void* __restrict__ out, const BatchParams p) {
-  __shared__ int16_t tmp[kRsRows][kRsCols];
-  __shared__ uint8_t ob[kMaxComp][kRsMaxTy][kRsCols];
-  __shared__ __attribute__((aligned(16))) uint8_t srcb[kRsSrcBytes];
-  __shared__ int16_t wts[kRsWts];
-  __shared__ int16_t wtsy[kRsMaxTy * kRsRows];
-  __shared__ int32_t xfirst[kRsCols];
-  __shared__ int32_t yfirst[kRsMaxTy];
+// Weight tables of plane c (layout of weights_kernel): first index and
+// Q14 taps (padded to an even count) per destination column / row.
+struct PlaneWeights {
+  const int32_t* fx;
+  const int16_t* wx;
+  const int32_t* fy;
+  const int16_t* wy;
+  int tx, ty;
+};
+
+__device__ __forceinline__ PlaneWeights plane_weights(const ImageDesc& dd, const int32_t* pool,
+                                                      int c) {
+  PlaneWeights w{};
+  int64_t off = dd.wt_off;
+  for (int k = 0; k <= c; k++) {
+    const int tx = ((dd.taps_x[k] + 1) / 2) * 2, ty = ((dd.taps_y[k] + 1) / 2) * 2;
+    if (k == c) {
+      w.tx = tx;
+      w.ty = ty;
+      w.fx = pool + off;
+      w.wx = reinterpret_cast<const int16_t*>(pool + off + dd.sw);
+    }
+    off += (int64_t)dd.sw * (1 + tx / 2);
+    if (k == c) {
+      w.fy = pool + off;
+      w.wy = reinterpret_cast<const int16_t*>(pool + off + dd.sh);
+    }
+    off += (int64_t)dd.sh * (1 + ty / 2);
+  }
+  return w;
+}
+
+// Visible content rows [vy0, vy1) and columns [vx0, vx0 + nvis) of the
+// scaled image inside the output (pad / crop geometry).
+__device__ __forceinline__ void visible_rows(const ImageDesc& dd, int& vy0, int& vy1) {
+  vy0 = max(-dd.dy, 0);
+  vy1 = min(dd.oh - dd.dy, dd.sh);
+}
+
+// Horizontal pass: one workgroup = (row group, plane, image).  The group's
+// source rows are staged in LDS with 8-byte loads; a thread owns one visible
+// output column, keeps its taps in registers and writes the Q6 intermediate
+// ((acc + 128) >> 8) of every staged row: int16 [rows][tmp_stride] per plane.
+// Only rows some visible output row reads are computed.
+__global__ void __launch_bounds__(256) resize_h_kernel(const uint8_t* __restrict__ planes,
+                                                       const ImageDesc* __restrict__ desc,
+                                                       const ImageInfo* __restrict__ infos,
+                                                       const int32_t* __restrict__ pool,
+                                                       int16_t* __restrict__ tmp) {
+  __shared__ __attribute__((aligned(16))) uint8_t srcb[kHSrcBytes + 32];
+  const int img = blockIdx.z, c = blockIdx.y, tid = threadIdx.x;
+  const ImageInfo& in = infos[img];
+  if (in.status != kOk) return;
+  const ImageDesc& dd = desc[img];
+  if (c >= dd.ncomp || dd.nvis <= 0) return;
+  int vy0, vy1;
+  visible_rows(dd, vy0, vy1);
+  if (vy0 >= vy1) return;
+  const PlaneWeights W = plane_weights(dd, pool, c);
+  const int pw = in.comp_w[c], ph = in.comp_hpx[c], stride = dd.plane_stride[c];
+  const int rpw = h_rows_per_group(stride);
+  const int r_lo = max(W.fy[vy0], 0), r_hi = min(W.fy[vy1 - 1] + W.ty - 1, ph - 1);
+  const int ra = r_lo + (int)blockIdx.x * rpw;
+  if (ra > r_hi) return;
+  const int nr = min(rpw, r_hi + 1 - ra);
+  // stage nr full rows (stride is a multiple of 8): loads first, then stores;
+  // rows wider than the LDS buffer are read in place
+  const bool staged = stride <= kHSrcBytes;
+  const uint8_t* rows = staged ? srcb : planes + dd.plane_off[c] + (int64_t)ra * stride;
+  if (staged) {
+    const uint2* s = reinterpret_cast<const uint2*>(planes + dd.plane_off[c] + (int64_t)ra * stride);
+    uint2* d = reinterpret_cast<uint2*>(srcb);
+    const int n8 = nr * stride / 8;
+    for (int i0 = 0; i0 < n8; i0 += 256 * 8) {
+      uint2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + u * 256 + tid;
+        if (i < n8) v[u] = s[i];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + u * 256 + tid;
+        if (i < n8) d[i] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  int16_t* out = tmp + dd.tmp_off + (int64_t)dd.tmp_plane[c] + (int64_t)ra * dd.tmp_stride;
+  for (int xx = tid; xx < dd.nvis; xx += 256) {
+    const int cx = dd.vx0 + xx;
+    const int f = W.fx[cx];
+    const int16_t* wcol = W.wx + (int64_t)cx * W.tx;
+    if (W.tx <= 16) {
+      int32_t wr[16];
+#pragma unroll
+      for (int t = 0; t < 16; t++) wr[t] = t < W.tx ? (int32_t)wcol[t] : 0;
+      if (f >= 0 && f + 16 <= pw) {
+        // interior: 16 straight taps (zero weights past tx)
+        for (int rr = 0; rr < nr; rr++) {
+          const uint8_t* row = rows + (int64_t)rr * stride + f;
+          int32_t h = 0;
+#pragma unroll
+          for (int t = 0; t < 16; t++) h += wr[t] * (int32_t)row[t];
+          out[(int64_t)rr * dd.tmp_stride + xx] = (int16_t)((h + 128) >> 8);
+        }
+      } else {
+        int kx[16];
+#pragma unroll
+        for (int t = 0; t < 16; t++) kx[t] = min(max(f + t, 0), pw - 1);
+        for (int rr = 0; rr < nr; rr++) {
+          const uint8_t* row = rows + (int64_t)rr * stride;
+          int32_t h = 0;
+#pragma unroll
+          for (int t = 0; t < 16; t++) h += wr[t] * (int32_t)row[kx[t]];
+          out[(int64_t)rr * dd.tmp_stride + xx] = (int16_t)((h + 128) >> 8);
+        }
+      }
+    } else {
+      for (int rr = 0; rr < nr; rr++) {
+        const uint8_t* row = rows + (int64_t)rr * stride;
+        int32_t h = 0;
+        for (int t = 0; t < W.tx; t++) h += (int32_t)wcol[t] * row[min(max(f + t, 0), pw - 1)];
+        out[(int64_t)rr * dd.tmp_stride + xx] = (int16_t)((h + 128) >> 8);
+      }
+    }
+  }
+}
+
+// Copy `n` bytes LDS -> global with 4-byte stores where the destination is
+// aligned (head / tail bytes singly); all threads of the workgroup take part.
+__device__ __forceinline__ void lds_to_global(uint8_t* __restrict__ dst, const uint8_t* src,
+                                              int n, int tid) {
+  const int head = min(n, (int)((4 - ((uintptr_t)dst & 3)) & 3));
+  if (tid < head) dst[tid] = src[tid];
+  const int nw = (n - head) >> 2;
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
+  for (int i = tid; i < nw; i += 256) {
+    const uint8_t* q = src + head + 4 * i;
+    d32[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  }
+  const int t0 = head + 4 * nw;
+  if (t0 + tid < n) dst[t0 + tid] = src[t0 + tid];
+}
+
+// Vertical pass + colour conversion + pad/crop + (normalise) + store.  One
+// workgroup = (band of v_rb output rows, image); output columns in chunks of
+// v_cols, a thread per column.  Per plane the band's intermediate rows are
+// staged in LDS, each thread runs the vertical taps ((acc + 2^19) >> 20,
+// clamp) for its column, then YCbCr -> RGB; the band is assembled in LDS and
+// written with coalesced stores.  Arithmetic: oracle/jpeg_oracle.c
+// resize_plane + jo_resize_planes.
+__global__ void __launch_bounds__(256) resize_v_kernel(const int16_t* __restrict__ tmp,
+                                                       const ImageDesc* __restrict__ desc,
+                                                       ImageInfo* __restrict__ infos,
+                                                       const int32_t* __restrict__ pool,
+                                                       void* __restrict__ out, const BatchParams p) {
+  __shared__ int16_t tb[kVBuf];
+  __shared__ __attribute__((aligned(16))) uint8_t ost[kVMaxRb * kVMaxCols * 3 * 2];
+  __shared__ int16_t wys[kVMaxRb * kMaxTaps];
+  __shared__ int32_t fys[kVMaxRb];
   const int img = blockIdx.y, tid = threadIdx.x;
   const ImageInfo& in = infos[img];
   if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
-  const int ow = dd.ow, oh = dd.oh, TY = dd.rs_ty, CW = dd.rs_cw;
-  const int y0 = blockIdx.x * TY;
+  const int ow = dd.ow, oh = dd.oh, RB = dd.v_rb, VC = dd.v_cols;
+  const int y0 = (int)blockIdx.x * RB;
   if (y0 >= oh) return;
-  const int y1 = min(y0 + TY, oh);
-  const int cy_lo = max(y0 - dd.dy, 0), cy_hi = min(y1 - dd.dy, dd.sh);
+  const int nyb = min(RB, oh - y0);
   const int ncomp = dd.ncomp;
-  const int32_t* fxp[kMaxComp];
-  const int16_t* wxp[kMaxComp];
-  const int32_t* fyp[kMaxComp];
-  const int16_t* wyp[kMaxComp];
-  int txs[kMaxComp], tys[kMaxComp];
-  int64_t off = dd.wt_off;
-  for (int c = 0; c < ncomp; c++) {
-    txs[c] = ((dd.taps_x[c] + 1) / 2) * 2;
-    tys[c] = ((dd.taps_y[c] + 1) / 2) * 2;
-    fxp[c] = pool + off;
-    wxp[c] = reinterpret_cast<const int16_t*>(pool + off + dd.sw);
-    off += (int64_t)dd.sw * (1 + txs[c] / 2);
-    fyp[c] = pool + off;
-    wyp[c] = reinterpret_cast<const int16_t*>(pool + off + dd.sh);
-    off += (int64_t)dd.sh * (1 + tys[c] / 2);
-  }
-  // content columns visible in the output
-  const int vis_lo = max(-dd.dx, 0), vis_hi = min(ow - dd.dx, dd.sw);
-  const int nry = cy_hi - cy_lo;
-  for (int cx_lo = vis_lo; cx_lo < max(vis_hi, vis_lo + 1); cx_lo += CW) {
-    const int cx_hi = min(cx_lo + CW, vis_hi);
-    const int ncols = cx_hi - cx_lo;
-    if (ncols > 0 && nry > 0) {
+  // content rows of the band
+  const int cy0 = max(y0 - dd.dy, 0), cy1 = min(y0 + nyb - dd.dy, dd.sh);
+  const int ncy = cy1 - cy0;
+  const bool planar = p.pix_fmt == 0 || p.pix_fmt == 1;
+  const bool swap = p.pix_fmt == 1 || p.pix_fmt == 3;
+  const int esz = p.dtype == 0 ? 1 : 2;
+  for (int xc0 = 0; xc0 < ow; xc0 += VC) {
+    const int nxc = min(VC, ow - xc0);
+    const int x = xc0 + tid;
+    const int cx = x - dd.dx;
+    // content columns of the chunk: [ccx0, ccx0 + ncc)
+    const int ccx0 = max(xc0 - dd.dx, dd.vx0);
+    const int ncc = min(xc0 + nxc - dd.dx, dd.vx0 + dd.nvis) - ccx0;
+    const bool mine = tid < nxc && cx >= ccx0 && cx < ccx0 + ncc;
+    int val[kMaxComp][kVMaxRb];
+#pragma unroll
+    for (int c = 0; c < kMaxComp; c++)
+#pragma unroll
+      for (int yy = 0; yy < kVMaxRb; yy++) val[c][yy] = 0;
+    if (ncy > 0 && ncc > 0) {
       for (int c = 0; c < ncomp; c++) {
-        const uint8_t* src = planes + dd.plane_off[c];
-        const int stride = dd.plane_stride[c], pw = in.comp_w[c], ph = in.comp_hpx[c];
-        const int tx = txs[c], ty = tys[c];
-        const int lo = fyp[c][cy_lo];
-        const int nrows = fyp[c][cy_hi - 1] + ty - lo;
-        const int xs_lo = fxp[c][cx_lo];
-        const int wsrc = fxp[c][cx_hi - 1] + tx - xs_lo;
-        if (nrows > kRsRows || wsrc > kRsSrcW || nrows * wsrc > kRsSrcBytes ||
-            ncols * tx > kRsWts || nry * ty > kRsMaxTy * kRsRows)
-          continue;  // defensive: the host tiling guarantees these fit
-        // stage the source window with dword loads from a 4-aligned start;
-        // edge tiles (window past the plane) take the clamped byte path
-        const int xa = xs_lo & ~3;
-        const int wal = ((xs_lo + wsrc - xa) + 3) & ~3;
-        const int sh = xs_lo - xa;  // window offset inside the staged row
-        const int tr = tid >> 6, tc = tid & 63;
-        if (!(p.debug_mask & 1)) {
-        if (xs_lo >= 0 && xs_lo + wsrc <= pw && nrows * wal <= kRsSrcBytes) {
-          // all of a thread's loads are issued before any LDS store, so their
-          // latencies overlap (a load -> store -> load chain pays each one)
-          const int nw = wal >> 2, total = nrows * nw;
-          uint32_t* d32 = reinterpret_cast<uint32_t*>(srcb);
-          for (int q0 = 0; q0 < total; q0 += 256 * 8) {
-            uint32_t v[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-              const int q = q0 + u * 256 + tid;
-              if (q < total) {
-                const int rr = q / nw, j = q - rr * nw;
-                const int r = min(max(lo + rr, 0), ph - 1);
-                v[u] = reinterpret_cast<const uint32_t*>(src + (int64_t)r * stride + xa)[j];
-              }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-              const int q = q0 + u * 256 + tid;
-              if (q < total) d32[q] = v[u];
-            }
-          }
-        } else {
-          for (int rr = tr; rr < nrows; rr += 4) {
-            const int r = min(max(lo + rr, 0), ph - 1);
-            for (int j = tc; j < wal; j += 64) {
-              const int x = min(max(xa + j, 0), pw - 1);
-              srcb[rr * wal + j] = src[(int64_t)r * stride + x];
-            }
-          }
+        const PlaneWeights W = plane_weights(dd, pool, c);
+        const int ph = in.comp_hpx[c];
+        const int r_lo = min(max(W.fy[cy0], 0), ph - 1);
+        const int r_hi = min(max(W.fy[cy1 - 1] + W.ty - 1, 0), ph - 1);
+        const int nrows = r_hi - r_lo + 1;
+        if (nrows * ncc > kVBuf || W.ty > kMaxTaps) {  // the host tiling guarantees this fits
+          if (tid == 0) infos[img].status = kErrBadGeometry;
+          return;
         }
+        const int16_t* src = tmp + dd.tmp_off + (int64_t)dd.tmp_plane[c] +
+                             (int64_t)r_lo * dd.tmp_stride + (ccx0 - dd.vx0);
+        for (int i = tid; i < nrows * ncc; i += 256) {
+          const int rr = i / ncc, j = i - rr * ncc;
+          tb[i] = src[(int64_t)rr * dd.tmp_stride + j];
         }
-        for (int i = tid; i < ncols * tx; i += 256) wts[i] = wxp[c][(int64_t)cx_lo * tx + i];
-        for (int i = tid; i < ncols; i += 256) xfirst[i] = fxp[c][cx_lo + i] - xs_lo + sh;
-        for (int i = tid; i < nry * ty; i += 256) wtsy[i] = wyp[c][(int64_t)cy_lo * ty + i];
-        for (int i = tid; i < nry; i += 256) yfirst[i] = fyp[c][cy_lo + i] - lo;
+        for (int i = tid; i < ncy * W.ty; i += 256) wys[i] = W.wy[(int64_t)cy0 * W.ty + i];
+        if (tid < ncy) fys[tid] = W.fy[cy0 + tid];
         __syncthreads();
-        // horizontal taps.  Common case (<= 16 taps): a thread owns one column,
-        // keeps its weights in registers and walks rows with a fully unrolled
-        // tap loop (independent LDS reads in flight).  Otherwise the generic
-        // (tr, tc) mapping.
-        if (!(p.debug_mask & 2)) {
-          if (tx <= 16) {
-            const int half = tid >> 7, col = tid & 127;  // 2 threads per column
-            for (int xx = col; xx < ncols; xx += 128) {
-              int32_t wr[16];
+        if (mine) {
+          const int col = cx - ccx0;
 #pragma unroll
-              for (int t = 0; t < 16; t++) wr[t] = t < tx ? (int32_t)wts[xx * tx + t] : 0;
-              const int xf = xfirst[xx];
-              for (int rr = half; rr < nrows; rr += 2) {
-                const uint8_t* row = srcb + rr * wal + xf;
-                int32_t h = 0;
-#pragma unroll
-                for (int t = 0; t < 16; t++) h += wr[t] * (int32_t)row[t];
-                tmp[rr][xx] = (int16_t)((h + 128) >> 8);
+          for (int yy = 0; yy < kVMaxRb; yy++) {
+            if (yy < ncy) {
+              const int16_t* w = wys + yy * W.ty;
+              const int f = fys[yy];
+              int32_t acc = 0;
+              for (int t = 0; t < W.ty; t++) {
+                const int k = min(max(f + t, 0), ph - 1) - r_lo;
+                acc += (int32_t)w[t] * tb[k * ncc + col];
               }
+              val[c][yy] = clip_u8((acc + (1 << 19)) >> 20);
             }
-          } else {
-            for (int xx = tc; xx < ncols; xx += 64) {
-              const int16_t* w = wts + xx * tx;
-              const int xf = xfirst[xx];
-              for (int rr = tr; rr < nrows; rr += 4) {
-                const uint8_t* row = srcb + rr * wal + xf;
-                int32_t h = 0;
-                for (int t = 0; t < tx; t++) h += (int32_t)w[t] * row[t];
-                tmp[rr][xx] = (int16_t)((h + 128) >> 8);
-              }
-            }
-          }
-        }
-        __syncthreads();
-        if (!(p.debug_mask & 4))
-        for (int yy = tr; yy < nry; yy += 4) {
-          const int base = yfirst[yy];
-          const int16_t* w = wtsy + yy * ty;
-          for (int xx = tc; xx < ncols; xx += 64) {
-            int32_t acc = 0;
-            for (int t = 0; t < ty; t++) acc += (int32_t)w[t] * tmp[base + t][xx];
-            ob[c][yy][xx] = clip_u8((acc + (1 << 19)) >> 20);
           }
         }
         __syncthreads();
       }
     }
-    // store the part of the band this chunk covers (pad columns go with the
-    // first / last chunk)
-    const int xa = (cx_lo == vis_lo) ? 0 : cx_lo + dd.dx;
-    const int xb = (cx_hi >= vis_hi) ? ow : cx_hi + dd.dx;
-    const int nx = xb - xa;
-    for (int i = tid; i < (y1 - y0) * nx; i += 256) {
-      const int yy = i / nx, x = xa + (i - yy * nx), y = y0 + yy;
-      const int cx = x - dd.dx, cy = y - dd.dy;
-      int rgb[3] = {0, 0, 0};
-      if (cx >= cx_lo && cx < cx_hi && cy >= cy_lo && cy < cy_hi) {
-        const int oy = cy - cy_lo, ox = cx - cx_lo;
-        if (ncomp == 1)
-          rgb[0] = rgb[1] = rgb[2] = ob[0][oy][ox];
-        else
-          ycc_rgb(ob[0][oy][ox], ob[1][oy][ox], ob[2][oy][ox], rgb);
+    // colour conversion into the band staging buffer (pad pixels are black)
+    if (tid < nxc) {
+#pragma unroll
+      for (int yy = 0; yy < kVMaxRb; yy++) {
+        if (yy < nyb) {
+          const int cy = y0 + yy - dd.dy;
+          int rgb[3] = {0, 0, 0};
+          if (mine && cy >= cy0 && cy < cy1) {
+            const int k = cy - cy0;
+            if (ncomp == 1) rgb[0] = rgb[1] = rgb[2] = val[0][k];
+            else ycc_rgb(val[0][k], val[1][k], val[2][k], rgb);
+          }
+#pragma unroll
+          for (int ch = 0; ch < 3; ch++) {
+            const int v = rgb[swap ? 2 - ch : ch];
+            const int e = planar ? (ch * nyb + yy) * nxc + tid : (yy * nxc + tid) * 3 + ch;
+            if (esz == 1) {
+              ost[e] = (uint8_t)v;
+            } else {
+              float f = __fdiv_rn((float)v, 255.0f);
+              f = __fsub_rn(f, p.mean[ch]);
+              f = __fdiv_rn(f, p.std[ch]);
+              reinterpret_cast<__half*>(ost)[e] = __float2half_rn(f);
+            }
+          }
+        }
       }
-      if (!(p.debug_mask & 8)) store_rgb(out, dd.out_off, p.pix_fmt, p.dtype, ow, oh, x, y, rgb, p);
+    }
+    __syncthreads();
+    // coalesced stores: every (channel,) row of the chunk is contiguous
+    uint8_t* ob = static_cast<uint8_t*>(out) + dd.out_off * esz;
+    const int64_t pl = (int64_t)ow * oh;
+    if (!planar) {
+      if (nxc == ow) {  // whole rows: the band is one contiguous run
+        lds_to_global(ob + (int64_t)y0 * ow * 3 * esz, ost, nyb * ow * 3 * esz, tid);
+      } else {
+        for (int yy = 0; yy < nyb; yy++)
+          lds_to_global(ob + ((int64_t)(y0 + yy) * ow + xc0) * 3 * esz, ost + yy * nxc * 3 * esz,
+                        nxc * 3 * esz, tid);
+      }
+    } else {
+      for (int ch = 0; ch < 3; ch++) {
+        if (nxc == ow) {
+          lds_to_global(ob + (ch * pl + (int64_t)y0 * ow) * esz, ost + ch * nyb * nxc * esz,
+                        nyb * ow * esz, tid);
+        } else {
+          for (int yy = 0; yy < nyb; yy++)
+            lds_to_global(ob + (ch * pl + (int64_t)(y0 + yy) * ow + xc0) * esz,
+                          ost + (ch * nyb + yy) * nxc * esz, nxc * esz, tid);
+        }
+      }
     }
     __syncthreads();
   }
@@ -1461,10 +1567,12 @@ hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageI
   return hipGetLastError();
 }
 hipError_t launch_resize(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
-                         const int32_t* pool, void* out, const BatchParams& p, int64_t max_tiles,
-                         int n, hipStream_t st) {
-  hipLaunchKernelGGL(resize_kernel, dim3((int)max_tiles, n), dim3(256), 0, st, planes, desc, infos,
-                     pool, out, p);
+                         const int32_t* pool, int16_t* tmp, void* out, const BatchParams& p,
+                         int64_t h_groups, int64_t v_bands, int n, hipStream_t st) {
+  hipLaunchKernelGGL(resize_h_kernel, dim3((int)h_groups, kMaxComp, n), dim3(256), 0, st, planes,
+                     desc, infos, pool, tmp);
+  hipLaunchKernelGGL(resize_v_kernel, dim3((int)v_bands, n), dim3(256), 0, st, tmp, desc,
+                     const_cast<ImageInfo*>(infos), pool, out, p);
   return hipGetLastError();
 }
 hipError_t launch_planes_copy(const uint8_t* planes, const ImageDesc* desc,
