@@ -85,6 +85,9 @@ struct ImageDesc {      // host-filled per image
   int32_t pad2_;
   int64_t tmp_off;
   int64_t tmp_plane[kMaxComp];
+  int64_t ds_off;       // destuff chunk records: offset and count
+  int32_t ds_cap;
+  int32_t pad3_;
   int64_t rec_off;      // entropy symbol records: offset (u32 units) and capacity
   int64_t rec_cap;
 };
@@ -115,9 +118,17 @@ struct ImageInfo {      // device-filled by the parse kernel
   int32_t nseg;         // restart segments found by destuff
   int32_t clean_len;    // destuffed bytes
   int32_t sync_rounds;  // diagnostics: rounds the Huffman sync took
-  int32_t pad_;
+  int32_t scan_end;     // destuff: first byte past the entropy-coded data
   int64_t tphase[4];    // diagnostics: wall_clock64 ticks of the entropy phases
   int64_t dbg[4];       // diagnostics: symbols (round 0), wave iterations, shader clocks, rt ticks
+};
+
+// destuff: chunk-parallel over kDsChunk-byte chunks; per-chunk counts and prefixes
+constexpr int kDsChunk = 4096;
+struct DsChunk {
+  int32_t keep, rst, term;
+  int32_t keep_pre, rst_pre;
+  int32_t pad_[3];
 };
 
 struct BatchParams {

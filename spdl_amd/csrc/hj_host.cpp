@@ -19,7 +19,8 @@
 
 namespace hj {
 hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageInfo*, HuffTable*, int, hipStream_t);
-hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, uint8_t*, uint32_t*, int,
+hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, DsChunk*, uint8_t*,
+                          uint32_t*, int, int,
                           hipStream_t);
 hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
                           const HuffTable*, int16_t*, uint32_t*, int, int, int, hipStream_t);
@@ -212,6 +213,8 @@ struct Layout {
   int max_blocks = 0, max_len = 0;
   int64_t max_px = 0;
   int64_t max_hgroups = 0, max_vbands = 0, total_tmp = 0;
+  int64_t total_ds = 0;
+  int max_chunks = 0;
   int ow = 0, oh = 0;
 };
 
@@ -282,6 +285,10 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     d.seg_cap = (int32_t)(sizes[i] / 2 + 2);
     d.seg_off = L.total_segs;
     L.total_segs += d.seg_cap;
+    d.ds_cap = (int32_t)(sizes[i] / kDsChunk + 2);
+    d.ds_off = L.total_ds;
+    L.total_ds += d.ds_cap;
+    if (d.ds_cap > L.max_chunks) L.max_chunks = d.ds_cap;
     {
       // entropy records: kMaxSlots slots of N + kRecPad records, N bounded by
       // the compressed size (the device derives N from the destuffed length)
@@ -391,7 +398,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
 
 struct spdl_hj_ctx {
   int device = 0;
-  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts, recs, rtmp;
+  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts, recs, rtmp, dschunks;
   PinBuf pin_in, pin_desc, pin_status;
   hipEvent_t staging_free = nullptr;  // host staging may be rewritten after this
   hipEvent_t batch_done = nullptr;    // device workspace free after this
@@ -461,6 +468,7 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
   HJ_HIP(hipStreamWaitEvent(st, ctx->batch_done, 0));
   HJ_HIP(ctx->clean.ensure((size_t)max_end + 512));
   HJ_HIP(ctx->segs.ensure((size_t)L.total_segs * 4 + 64));
+  HJ_HIP(ctx->dschunks.ensure((size_t)L.total_ds * sizeof(DsChunk) + 64));
   HJ_HIP(ctx->desc.ensure(sizeof(ImageDesc) * n));
   HJ_HIP(ctx->info.ensure(sizeof(ImageInfo) * n));
   HJ_HIP(ctx->luts.ensure(sizeof(HuffTable) * 8 * n));
@@ -483,8 +491,9 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
   auto* infos = static_cast<ImageInfo*>(ctx->info.p);
   HJ_HIP(launch_parse(d_bytes, desc, infos, static_cast<HuffTable*>(ctx->luts.p), n, st));
   mark(ctx, 2, st);
-  HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<uint8_t*>(ctx->clean.p),
-                        static_cast<uint32_t*>(ctx->segs.p), n, st));
+  HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<DsChunk*>(ctx->dschunks.p),
+                        static_cast<uint8_t*>(ctx->clean.p), static_cast<uint32_t*>(ctx->segs.p),
+                        L.max_chunks, n, st));
   mark(ctx, 3, st);
   HJ_HIP(launch_entropy(static_cast<const uint8_t*>(ctx->clean.p),
                         static_cast<const uint32_t*>(ctx->segs.p), desc, infos,
@@ -616,7 +625,7 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
   DeviceGuard g(c->device);
   if (c->batch_done) (void)hipEventSynchronize(c->batch_done);
   DevBuf* bufs[] = {&c->bytes, &c->clean, &c->segs, &c->desc, &c->info,
-                    &c->luts,  &c->coefs, &c->planes, &c->wts, &c->recs, &c->rtmp};
+                    &c->luts,  &c->coefs, &c->planes, &c->wts, &c->recs, &c->rtmp, &c->dschunks};
   for (DevBuf* b : bufs) b->release();
   c->pin_in.release();
   c->pin_desc.release();

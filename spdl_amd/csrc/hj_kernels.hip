@@ -320,9 +320,24 @@ __global__ void __launch_bounds__(256) parse_kernel(const uint8_t* __restrict__ 
 // destuff_kernel
 // ---------------------------------------------------------------------------
 
+// Copy `n` bytes LDS -> global with 4-byte stores where the destination is
+// aligned (head / tail bytes singly); all threads of the workgroup take part.
+__device__ __forceinline__ void lds_to_global(uint8_t* __restrict__ dst, const uint8_t* src,
+                                              int n, int tid) {
+  const int head = min(n, (int)((4 - ((uintptr_t)dst & 3)) & 3));
+  if (tid < head) dst[tid] = src[tid];
+  const int nw = (n - head) >> 2;
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
+  for (int i = tid; i < nw; i += 256) {
+    const uint8_t* q = src + head + 4 * i;
+    d32[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  }
+  const int t0 = head + 4 * nw;
+  if (t0 + tid < n) dst[t0 + tid] = src[t0 + tid];
+}
+
 constexpr int kDsThreads = 256;
-constexpr int kDsPer = 32;
-constexpr int kDsTile = kDsThreads * kDsPer;
+constexpr int kDsPer = kDsChunk / kDsThreads;
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
   const int lane = threadIdx.x & 63;
@@ -334,139 +349,196 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
-// Destuff one image per workgroup, tile by tile (8 KB).  Tile bytes (plus the
-// previous 16 and next 16 bytes) are loaded with 16-byte loads into LDS and
-// classified there: a byte is kept unless it follows 0xFF (stuffed 0x00 or a
-// marker code), an 0xFF is kept when followed by 0x00, runs of 0xFF are fill,
-// an 0xFF starting RSTn splits a segment and any other marker ends the scan.
-// Kept bytes are compacted in LDS (wave shuffle scans, 4 barriers per tile)
-// and written with dword stores; the partial tail dword carries over.
-__global__ void __launch_bounds__(kDsThreads) destuff_kernel(const uint8_t* __restrict__ bytes,
-                                                             const ImageDesc* __restrict__ desc,
-                                                             ImageInfo* __restrict__ infos,
-                                                             uint8_t* __restrict__ clean,
-                                                             uint32_t* __restrict__ segs) {
-  __shared__ int wk[4], wr[4], wt[4];
-  __shared__ __attribute__((aligned(16))) uint8_t tile[kDsTile + 32];
-  __shared__ __attribute__((aligned(16))) uint8_t ob[kDsTile + 16];
-  const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (infos[img].status != kOk) return;
-  const ImageDesc dd = desc[img];
-  const uint8_t* d = bytes + dd.in_off;
-  const int size = (int)dd.in_size;
-  const int start = infos[img].scan_start;
-  uint8_t* out = clean + dd.in_off;
-  uint32_t* sg = segs + dd.seg_off;
-  int carry_keep = 0, carry_rst = 0, pend = 0;  // pend: bytes at ob[0..pend) not yet stored
-  uint32_t tailw = 0;                           // thread 0: those bytes, carried in a register
-  bool overflow = false;
-  if (tid == 0) sg[0] = 0;
-  const int abase = start & ~15;  // tiles are 16-byte aligned in the file
-  auto at = [&](int j) -> int { return j < size ? (int)d[j] : 0xD9; };
-  for (int base = abase;; base += kDsTile) {
-    // stage [base - 16, base + kDsTile + 16)
-    for (int q = tid; q < kDsTile / 16 + 2; q += kDsThreads) {
-      const int o = base - 16 + q * 16;
-      if (o >= 0 && o + 16 <= size) {
-        *reinterpret_cast<uint4*>(tile + q * 16) = *reinterpret_cast<const uint4*>(d + o);
+// Workgroup exclusive scan of two counters (256 threads = 4 waves); also
+// returns the totals.
+__device__ __forceinline__ void wg_scan2(int a, int b, int& ea, int& eb, int& ta, int& tb,
+                                        int* sh /* 8 ints */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+  if (lane == 63) {
+    sh[wid] = ia;
+    sh[4 + wid] = ib;
+  }
+  __syncthreads();
+  ea = ia - a;
+  eb = ib - b;
+  ta = tb = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    if (w < wid) {
+      ea += sh[w];
+      eb += sh[4 + w];
+    }
+    ta += sh[w];
+    tb += sh[4 + w];
+  }
+}
+
+// Classify the 16 bytes [j0, j0 + 16) of an entropy-coded segment run
+// (T.81 B.1.1.5, F.1.2.3): keep = data byte (a 0xFF followed by the stuffed
+// 0x00, or any byte not preceded by 0xFF); rst = 0xFF starting an RSTn marker
+// (fill 0xFF allowed before it); *term = first 0xFF starting any other marker
+// (bytes past the file read as 0xD9, EOI).  Bytes before `start` are ignored.
+__device__ __forceinline__ void ds_classify(const uint8_t* __restrict__ d, int size, int start,
+                                            int j0, uint32_t& keep, uint32_t& rst, int& term) {
+  uint8_t b[18];
+  b[0] = j0 > 0 && j0 - 1 < size ? d[j0 - 1] : 0;
+  if (j0 + 16 <= size) {
+    const uint4 q = *reinterpret_cast<const uint4*>(d + j0);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 16; i++) b[1 + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; i++) b[1 + i] = j0 + i < size ? d[j0 + i] : 0xD9;
+  }
+  b[17] = j0 + 16 < size ? d[j0 + 16] : 0xD9;
+  keep = rst = 0;
+  term = 0x7FFFFFFF;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int j = j0 + i;
+    if (j < start || j >= size) continue;
+    const bool prev_ff = j > start && b[i] == 0xFF;
+    if (b[1 + i] != 0xFF) {
+      keep |= (uint32_t)!prev_ff << i;
+    } else if (!prev_ff) {
+      if (b[2 + i] == 0x00) {
+        keep |= 1u << i;
       } else {
-        for (int i = 0; i < 16; i++) tile[q * 16 + i] = (o + i >= 0 && o + i < size) ? d[o + i] : 0;
-      }
-    }
-    __syncthreads();  // (1)
-    if (tid == 0) reinterpret_cast<uint32_t*>(ob)[0] = tailw;
-    auto tb = [&](int j) -> int { return j < size ? (int)tile[j - base + 16] : 0xD9; };
-    const int j0 = base + tid * kDsPer;
-    const int jb = max(j0, start), je = min(j0 + kDsPer, size);
-    // pass 1: first terminating marker (wave min -> LDS)
-    int myterm = 0x7FFFFFFF;
-    for (int j = jb; j < je; j++) {
-      if (tb(j) != 0xFF) continue;
-      if (j > start && tb(j - 1) == 0xFF) continue;
-      if (tb(j + 1) == 0x00) continue;
-      int k2 = j + 1;
-      while (k2 < size && at(k2) == 0xFF) k2++;
-      if (!(k2 < size && at(k2) >= 0xD0 && at(k2) <= 0xD7)) {
-        myterm = j;
-        break;
-      }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) myterm = min(myterm, __shfl_xor(myterm, o, 64));
-    // pass 2: counts up to this thread's terminator bound (refined below)
-    if (lane == 0) wt[wid] = myterm;
-    __syncthreads();  // (2)
-    int lim = min(min(wt[0], wt[1]), min(wt[2], wt[3]));
-    if (base + kDsTile >= size) lim = min(lim, size);
-    int keep = 0, rst = 0;
-    for (int j = jb; j < min(je, lim); j++) {
-      const int c = tb(j);
-      const bool prev_ff = j > start && tb(j - 1) == 0xFF;
-      if (c != 0xFF) {
-        keep += !prev_ff;
-      } else if (!prev_ff) {
-        if (tb(j + 1) == 0x00) keep++;
-        else rst++;
-      }
-    }
-    const int ik = wave_incl_scan(keep), ir = wave_incl_scan(rst);
-    if (lane == 63) {
-      wk[wid] = ik;
-      wr[wid] = ir;
-    }
-    __syncthreads();  // (3)
-    int ek = ik - keep, er = ir - rst, tk = 0, tr = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      if (w < wid) {
-        ek += wk[w];
-        er += wr[w];
-      }
-      tk += wk[w];
-      tr += wr[w];
-    }
-    // pass 3: compact into ob (after the pending tail bytes)
-    int o = pend + ek, r = carry_rst + er;
-    for (int j = jb; j < min(je, lim); j++) {
-      const int c = tb(j);
-      const bool prev_ff = j > start && tb(j - 1) == 0xFF;
-      if (c != 0xFF) {
-        if (!prev_ff) ob[o++] = (uint8_t)c;
-      } else if (!prev_ff) {
-        if (tb(j + 1) == 0x00) {
-          ob[o++] = 0xFF;
+        int k = j + 1;
+        while (k < size && d[k] == 0xFF) k++;
+        if (k < size && d[k] >= 0xD0 && d[k] <= 0xD7) {
+          rst |= 1u << i;
         } else {
-          r++;
-          if (r < dd.seg_cap) sg[r] = (uint32_t)(carry_keep + (o - pend));
-          else overflow = true;
+          term = min(term, j);
         }
       }
     }
-    __syncthreads();  // (4)
-    // store whole dwords; the output dword grid is aligned to the image base
-    const int total = pend + tk;
-    const int nfull = total >> 2;
-    const int obase = carry_keep - pend;  // multiple of 4 by construction
-    for (int i = tid; i < nfull; i += kDsThreads)
-      reinterpret_cast<uint32_t*>(out + obase)[i] = reinterpret_cast<const uint32_t*>(ob)[i];
-    if (tid == 0) tailw = reinterpret_cast<const uint32_t*>(ob)[nfull];
-    pend = total & 3;
-    carry_keep += tk;
-    carry_rst += tr;
-    if (lim < base + kDsTile) break;
-    __syncthreads();  // ob / tile reuse
   }
-  // flush the pending tail and zero padding (the bit reader reads a few words
-  // past the data)
+}
+
+// Destuffing runs as count -> per-image prefix -> write over 4 KB chunks of
+// every image at once (chunk k of image i starts at (scan_start & ~15) + 4096 k).
+__global__ void __launch_bounds__(kDsThreads) destuff_count_kernel(
+    const uint8_t* __restrict__ bytes, const ImageDesc* __restrict__ desc,
+    const ImageInfo* __restrict__ infos, DsChunk* __restrict__ chunks) {
+  __shared__ int sh[8];
+  __shared__ int shterm;
+  const int img = blockIdx.y, k = blockIdx.x, tid = threadIdx.x;
+  if (infos[img].status != kOk) return;
+  const ImageDesc& dd = desc[img];
+  const int size = (int)dd.in_size, start = infos[img].scan_start;
+  const int cbase = (start & ~15) + k * kDsChunk;
+  if (cbase >= size || k >= dd.ds_cap) return;
+  if (tid == 0) shterm = 0x7FFFFFFF;
+  uint32_t keep, rst;
+  int term;
+  ds_classify(bytes + dd.in_off, size, start, cbase + tid * kDsPer, keep, rst, term);
+  int ek, er, tk, tr;
+  wg_scan2(__popc(keep), __popc(rst), ek, er, tk, tr, sh);
+  if (term != 0x7FFFFFFF) atomicMin(&shterm, term);
+  __syncthreads();
   if (tid == 0) {
-    uint32_t w = pend ? (tailw & (0xFFFFFFFFu >> (8 * (4 - pend)))) : 0u;
-    uint32_t* o32 = reinterpret_cast<uint32_t*>(out + (carry_keep - pend));
-    o32[0] = w;
-    for (int i = 1; i <= 5; i++) o32[i] = 0;
-    infos[img].clean_len = carry_keep;
-    infos[img].nseg = min(carry_rst + 1, dd.seg_cap);
+    DsChunk& c = chunks[dd.ds_off + k];
+    c.keep = tk;
+    c.rst = tr;
+    c.term = shterm;
   }
-  if (overflow) infos[img].status = kErrBadRestart;
+}
+
+// One workgroup per image: exclusive prefix of the chunk counts up to the
+// first terminating marker; records the scan end (terminator or file end).
+__global__ void __launch_bounds__(kDsThreads) destuff_prefix_kernel(
+    const ImageDesc* __restrict__ desc, ImageInfo* __restrict__ infos,
+    DsChunk* __restrict__ chunks) {
+  __shared__ int sh[8];
+  __shared__ int shterm;
+  const int img = blockIdx.x, tid = threadIdx.x;
+  if (infos[img].status != kOk) return;
+  const ImageDesc& dd = desc[img];
+  const int size = (int)dd.in_size, start = infos[img].scan_start;
+  const int base = start & ~15;
+  const int nch = min(dd.ds_cap, (size - base + kDsChunk - 1) / kDsChunk);
+  if (tid == 0) shterm = 0x7FFFFFFF;
+  __syncthreads();
+  for (int k = tid; k < nch; k += kDsThreads) atomicMin(&shterm, chunks[dd.ds_off + k].term);
+  __syncthreads();
+  const int end = min(shterm, size);
+  int ck = 0, cr = 0;
+  for (int k0 = 0; k0 < nch; k0 += kDsThreads) {
+    const int k = k0 + tid;
+    const bool v = k < nch && base + k * kDsChunk < end;
+    const int kk = v ? chunks[dd.ds_off + k].keep : 0, rr = v ? chunks[dd.ds_off + k].rst : 0;
+    int ek, er, tk, tr;
+    wg_scan2(kk, rr, ek, er, tk, tr, sh);
+    if (k < nch) {
+      chunks[dd.ds_off + k].keep_pre = ck + ek;
+      chunks[dd.ds_off + k].rst_pre = cr + er;
+    }
+    ck += tk;
+    cr += tr;
+    __syncthreads();
+  }
+  if (tid == 0) infos[img].scan_end = end;
+}
+
+__global__ void __launch_bounds__(kDsThreads) destuff_write_kernel(
+    const uint8_t* __restrict__ bytes, const ImageDesc* __restrict__ desc,
+    ImageInfo* __restrict__ infos, const DsChunk* __restrict__ chunks, uint8_t* __restrict__ clean,
+    uint32_t* __restrict__ segs) {
+  __shared__ int sh[8];
+  __shared__ __attribute__((aligned(16))) uint8_t ob[kDsChunk];
+  const int img = blockIdx.y, k = blockIdx.x, tid = threadIdx.x;
+  if (infos[img].status != kOk) return;
+  const ImageDesc& dd = desc[img];
+  const int size = (int)dd.in_size, start = infos[img].scan_start, end = infos[img].scan_end;
+  const int base = start & ~15;
+  const int cbase = base + k * kDsChunk;
+  // the chunk holding the last scan byte also finishes the image
+  const int last = (max(end - 1, start) - base) / kDsChunk;
+  if (k > last || k >= dd.ds_cap) return;
+  const int j0 = cbase + tid * kDsPer;
+  uint32_t keep, rst;
+  int term;
+  ds_classify(bytes + dd.in_off, size, start, j0, keep, rst, term);
+  const int lim = end - j0;  // bytes at or past the scan end are not part of it
+  const uint32_t m = lim >= 16 ? 0xFFFFu : (lim <= 0 ? 0u : ((1u << lim) - 1u));
+  keep &= m;
+  rst &= m;
+  int ek, er, tk, tr;
+  wg_scan2(__popc(keep), __popc(rst), ek, er, tk, tr, sh);
+  const DsChunk& c = chunks[dd.ds_off + k];
+  uint32_t* sg = segs + dd.seg_off;
+  const uint8_t* d = bytes + dd.in_off;
+  // compact this thread's kept bytes; RSTn markers record segment starts
+  {
+    int o = ek, r = c.rst_pre + er;
+    bool overflow = false;
+    for (int i = 0; i < 16; i++) {
+      if (keep >> i & 1u) {
+        const uint8_t v = d[j0 + i];
+        ob[o++] = v;
+      } else if (rst >> i & 1u) {
+        r++;
+        if (r < dd.seg_cap) sg[r] = (uint32_t)(c.keep_pre + o);
+        else overflow = true;
+      }
+    }
+    if (overflow) infos[img].status = kErrBadRestart;
+  }
+  __syncthreads();
+  uint8_t* out = clean + dd.in_off;
+  lds_to_global(out + c.keep_pre, ob, tk, tid);
+  if (k == last) {
+    const int clen = c.keep_pre + tk;
+    if (tid < 64) out[clen + tid] = 0;  // zero padding past the data
+    if (tid == 0) {
+      infos[img].clean_len = clen;
+      infos[img].nseg = min(c.rst_pre + tr + 1, dd.seg_cap);
+      sg[0] = 0;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1341,22 +1413,6 @@ __global__ void __launch_bounds__(256) resize_h_kernel(const uint8_t* __restrict
   }
 }
 
-// Copy `n` bytes LDS -> global with 4-byte stores where the destination is
-// aligned (head / tail bytes singly); all threads of the workgroup take part.
-__device__ __forceinline__ void lds_to_global(uint8_t* __restrict__ dst, const uint8_t* src,
-                                              int n, int tid) {
-  const int head = min(n, (int)((4 - ((uintptr_t)dst & 3)) & 3));
-  if (tid < head) dst[tid] = src[tid];
-  const int nw = (n - head) >> 2;
-  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
-  for (int i = tid; i < nw; i += 256) {
-    const uint8_t* q = src + head + 4 * i;
-    d32[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-  }
-  const int t0 = head + 4 * nw;
-  if (t0 + tid < n) dst[t0 + tid] = src[t0 + tid];
-}
-
 // Vertical pass + colour conversion + pad/crop + (normalise) + store.  One
 // workgroup = (band of v_rb output rows, image); output columns in chunks of
 // v_cols, a thread per column.  Per plane the band's intermediate rows are
@@ -1525,9 +1581,13 @@ hipError_t launch_parse(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* 
   return hipGetLastError();
 }
 hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
-                          uint8_t* clean, uint32_t* segs, int n, hipStream_t st) {
-  hipLaunchKernelGGL(destuff_kernel, dim3(n), dim3(kDsThreads), 0, st, bytes, desc, infos, clean,
-                     segs);
+                          DsChunk* chunks, uint8_t* clean, uint32_t* segs, int max_chunks, int n,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(destuff_count_kernel, dim3(max_chunks, n), dim3(kDsThreads), 0, st, bytes,
+                     desc, infos, chunks);
+  hipLaunchKernelGGL(destuff_prefix_kernel, dim3(n), dim3(kDsThreads), 0, st, desc, infos, chunks);
+  hipLaunchKernelGGL(destuff_write_kernel, dim3(max_chunks, n), dim3(kDsThreads), 0, st, bytes,
+                     desc, infos, chunks, clean, segs);
   return hipGetLastError();
 }
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
