@@ -76,15 +76,15 @@ struct ImageDesc {      // host-filled per image
   // resize geometry (host computed from the probe; device recomputes nothing)
   int32_t sw, sh, dx, dy, ow, oh;
   int32_t taps_x[kMaxComp], taps_y[kMaxComp];
-  // resize: visible content columns [vx0, vx0 + nvis) of the scaled image,
-  // horizontal-pass intermediate (int16 [rows][tmp_stride] per plane at
-  // tmp_off + tmp_plane[c]), vertical-pass band rows / column chunk
-  int32_t vx0, nvis;
-  int32_t tmp_stride;
-  int32_t v_rb, v_cols;
+  // resize: visible content [vx0, vx0 + nvis) x [vy0, vy0 + nvy) of the
+  // scaled image; resampled planes (u8 [nvy][rp_stride] per plane) at rp_off;
+  // per-plane band rows r_rb and column chunk r_cols of resize_plane_kernel
+  int32_t vx0, nvis, vy0, nvy;
+  int32_t rp_stride;
+  int32_t r_cols;
+  int32_t r_rb[kMaxComp];
   int32_t pad2_;
-  int64_t tmp_off;
-  int64_t tmp_plane[kMaxComp];
+  int64_t rp_off;
   int64_t ds_off;       // destuff chunk records: offset and count
   int32_t ds_cap;
   int32_t pad3_;
@@ -92,14 +92,14 @@ struct ImageDesc {      // host-filled per image
   int64_t rec_cap;
 };
 
-// resize: horizontal pass stages up to kHMaxRows source rows (kHSrcBytes of
-// LDS) per workgroup; the vertical pass stages kVBuf int16 intermediate values
-// for a band of up to kVMaxRb output rows x kVMaxCols columns
+// resize: source rows are staged kHMaxRows at a time (kHSrcBytes of LDS); the
+// horizontal-pass intermediate of one band holds kTBuf int16 values
 constexpr int kHSrcBytes = 16384;
 constexpr int kHMaxRows = 16;
-constexpr int kVBuf = 16384;
-constexpr int kVMaxRb = 8;
-constexpr int kVMaxCols = 256;
+constexpr int kTBuf = 16384;
+constexpr int kRMaxRb = 64;
+constexpr int kRMaxCols = 256;
+constexpr int kVTaps = 32;  // vertical taps staged in LDS (more: read from HBM)
 inline HJ_HD int h_rows_per_group(int stride) {
   const int r = kHSrcBytes / (stride > 0 ? stride : 1);
   return r < 1 ? 1 : (r > kHMaxRows ? kHMaxRows : r);

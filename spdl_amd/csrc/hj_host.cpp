@@ -31,7 +31,7 @@ hipError_t launch_weights(const ImageDesc*, const ImageInfo*, int32_t*, int, int
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                       const BatchParams&, int64_t, int, hipStream_t);
 hipError_t launch_resize(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*,
-                         int16_t*, void*, const BatchParams&, int64_t, int64_t, int, hipStream_t);
+                         uint8_t*, void*, const BatchParams&, int64_t, int64_t, int, hipStream_t);
 }  // namespace hj
 
 using namespace hj;
@@ -212,7 +212,7 @@ struct Layout {
   int64_t out_elems_per_image = 0;
   int max_blocks = 0, max_len = 0;
   int64_t max_px = 0;
-  int64_t max_hgroups = 0, max_vbands = 0, total_tmp = 0;
+  int64_t max_bands = 0, max_quads = 0, total_rp = 0;
   int64_t total_ds = 0;
   int max_chunks = 0;
   int ow = 0, oh = 0;
@@ -339,52 +339,49 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
       }
       int ml = g.sw > g.sh ? g.sw : g.sh;
       if (ml > L.max_len) L.max_len = ml;
-      // visible content of the scaled image, horizontal-pass intermediate
+      // visible content of the scaled image and its resampled planes
       d.vx0 = g.dx < 0 ? -g.dx : 0;
       const int vx1 = (g.ow - g.dx) < g.sw ? (g.ow - g.dx) : g.sw;
       d.nvis = vx1 > d.vx0 ? vx1 - d.vx0 : 0;
-      d.tmp_stride = (int32_t)round_up(d.nvis > 0 ? d.nvis : 1, 8);
-      d.tmp_off = L.total_tmp;
-      int64_t tsz = 0;
-      for (int c = 0; c < p.ncomp; c++) {
-        d.tmp_plane[c] = tsz;
-        tsz += (int64_t)chh[c] * d.tmp_stride;
-      }
-      L.total_tmp += round_up(tsz, 64);
-      for (int c = 0; c < p.ncomp; c++) {
-        const int64_t groups = (chh[c] + h_rows_per_group(d.plane_stride[c]) - 1) /
-                               h_rows_per_group(d.plane_stride[c]);
-        if (groups > L.max_hgroups) L.max_hgroups = groups;
-      }
-      // vertical pass: widest column chunk, then the tallest band whose
-      // staged intermediate rows fit kVBuf for every plane
-      int rb = 0, vc = 0;
-      for (int cand = kVMaxCols; cand >= 64 && rb == 0; cand -= 64) {
+      d.vy0 = g.dy < 0 ? -g.dy : 0;
+      const int vy1 = (g.oh - g.dy) < g.sh ? (g.oh - g.dy) : g.sh;
+      d.nvy = vy1 > d.vy0 ? vy1 - d.vy0 : 0;
+      d.rp_stride = (int32_t)round_up(d.nvis > 0 ? d.nvis : 1, 16);
+      d.rp_off = L.total_rp;
+      L.total_rp += round_up((int64_t)p.ncomp * d.nvy * d.rp_stride, 256);
+      // resize_plane_kernel tiling: widest column chunk, then per plane the
+      // tallest band whose intermediate rows fit kTBuf
+      d.r_cols = 0;
+      for (int cand = kRMaxCols; cand >= 64 && d.r_cols == 0; cand -= 64) {
         const int ncc = cand < d.nvis ? cand : (d.nvis > 0 ? d.nvis : 1);
-        for (int r = kVMaxRb; r >= 1; r--) {
-          bool ok = true;
-          for (int c = 0; c < p.ncomp; c++) {
-            const float sy = (float)chh[c] / (float)g.sh;
-            const int tpy = ((d.taps_y[c] + 1) / 2) * 2;
+        bool all = true;
+        for (int c = 0; c < p.ncomp; c++) {
+          const float sy = (float)chh[c] / (float)g.sh;
+          const int tpy = ((d.taps_y[c] + 1) / 2) * 2;
+          int rb = 0;
+          for (int r = kRMaxRb; r >= 1; r--) {
             const int rows = (int)ceilf((float)(r - 1) * sy) + 2 + tpy;
-            if ((int64_t)rows * ncc > kVBuf) ok = false;
+            if ((int64_t)rows * ncc <= kTBuf) {
+              rb = r;
+              break;
+            }
           }
-          if (ok) {
-            rb = r;
-            vc = cand;
-            break;
-          }
+          if (rb == 0) all = false;
+          d.r_rb[c] = rb;
         }
+        if (all) d.r_cols = cand;
       }
-      if (rb == 0) {
+      if (d.r_cols == 0) {
         if (status) status[i] = SPDL_HJ_ERR_BAD_GEOMETRY;
         set_err(err, errlen, "Failed to decode an image. (image %d: resize tile does not fit)", i);
         return SPDL_HJ_ERR_BAD_GEOMETRY;
       }
-      d.v_rb = rb;
-      d.v_cols = vc;
-      const int64_t bands = (g.oh + rb - 1) / rb;
-      if (bands > L.max_vbands) L.max_vbands = bands;
+      for (int c = 0; c < p.ncomp; c++) {
+        const int64_t bands = (d.nvy + d.r_rb[c] - 1) / d.r_rb[c];
+        if (bands > L.max_bands) L.max_bands = bands;
+      }
+      const int64_t quads = (int64_t)((g.ow + 3) / 4) * g.oh;
+      if (quads > L.max_quads) L.max_quads = quads;
     }
     int64_t px = (int64_t)g.ow * g.oh;
     if (px > L.max_px) L.max_px = px;
@@ -398,7 +395,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
 
 struct spdl_hj_ctx {
   int device = 0;
-  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts, recs, rtmp, dschunks;
+  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts, recs, rplanes, dschunks;
   PinBuf pin_in, pin_desc, pin_status;
   hipEvent_t staging_free = nullptr;  // host staging may be rewritten after this
   hipEvent_t batch_done = nullptr;    // device workspace free after this
@@ -477,7 +474,7 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
   HJ_HIP(ctx->recs.ensure((size_t)L.total_recs * 4 + 256));
   if (out->resize) {
     HJ_HIP(ctx->wts.ensure((size_t)L.total_wts * 4 + 256));
-    HJ_HIP(ctx->rtmp.ensure((size_t)L.total_tmp * 2 + 256));
+    HJ_HIP(ctx->rplanes.ensure((size_t)L.total_rp + 256));
   }
   HJ_HIP(ctx->pin_desc.ensure(sizeof(ImageDesc) * n));
   HJ_HIP(ctx->pin_status.ensure(sizeof(int32_t) * n));
@@ -526,8 +523,8 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
       mark(ctx, 6, st);
       HJ_HIP(launch_resize(static_cast<const uint8_t*>(ctx->planes.p), desc, infos,
                            static_cast<const int32_t*>(ctx->wts.p),
-                           static_cast<int16_t*>(ctx->rtmp.p), out_dev, bp, L.max_hgroups,
-                           L.max_vbands, n, st));
+                           static_cast<uint8_t*>(ctx->rplanes.p), out_dev, bp, L.max_bands,
+                           L.max_quads, n, st));
     } else {
       mark(ctx, 6, st);
       HJ_HIP(launch_csc(static_cast<const uint8_t*>(ctx->planes.p), desc, infos, out_dev, bp,
@@ -625,7 +622,7 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
   DeviceGuard g(c->device);
   if (c->batch_done) (void)hipEventSynchronize(c->batch_done);
   DevBuf* bufs[] = {&c->bytes, &c->clean, &c->segs, &c->desc, &c->info,
-                    &c->luts,  &c->coefs, &c->planes, &c->wts, &c->recs, &c->rtmp, &c->dschunks};
+                    &c->luts,  &c->coefs, &c->planes, &c->wts, &c->recs, &c->rplanes, &c->dschunks};
   for (DevBuf* b : bufs) b->release();
   c->pin_in.release();
   c->pin_desc.release();

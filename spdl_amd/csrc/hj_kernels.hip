@@ -53,9 +53,32 @@ struct ParseScratch {
   int32_t valoff[8][17];
 };
 
-__device__ static int be16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
+// Header bytes: the first kHdrBytes of the file are staged in LDS by the
+// whole workgroup (one coalesced pass); the serial marker walk reads them
+// from there and only reaches into HBM for headers past that window.
+constexpr int kHdrBytes = 4096;
 
-__device__ static int parse_headers(const uint8_t* d, int size, ParseScratch& s) {
+struct Bytes {
+  const uint8_t* g;  // file in HBM
+  const uint8_t* l;  // its first nl bytes in LDS
+  int nl;
+  __device__ uint8_t operator[](int i) const { return i < nl ? l[i] : g[i]; }
+};
+
+struct BPtr {
+  const Bytes* b;
+  int o;
+  __device__ uint8_t operator[](int k) const { return (*b)[o + k]; }
+  __device__ BPtr operator+(int k) const { return BPtr{b, o + k}; }
+  __device__ BPtr& operator+=(int k) {
+    o += k;
+    return *this;
+  }
+};
+
+__device__ static int be16(BPtr p) { return (p[0] << 8) | p[1]; }
+
+__device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
   ImageInfo& in = s.info;
   if (size < 4 || d[0] != 0xFF || d[1] != 0xD8) return kErrNotJpeg;
   int have_sof = 0;
@@ -70,9 +93,9 @@ __device__ static int parse_headers(const uint8_t* d, int size, ParseScratch& s)
     if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
     if (m == 0xD9) return kErrBadHeader;
     if (pos + 2 > size) return kErrBadHeader;
-    int len = be16(d + pos);
+    int len = be16(BPtr{&d, pos});
     if (len < 2 || pos + len > size) return kErrBadHeader;
-    const uint8_t* p = d + pos + 2;
+    BPtr p{&d, pos + 2};
     int n = len - 2;
     pos += len;
     if (m == 0xDB) {
@@ -206,15 +229,20 @@ __global__ void __launch_bounds__(256) parse_kernel(const uint8_t* __restrict__ 
                                                     HuffTable* __restrict__ luts) {
   __shared__ ParseScratch s;
   __shared__ int st;
+  __shared__ __attribute__((aligned(16))) uint8_t hdr[kHdrBytes];
   const int img = blockIdx.x, tid = threadIdx.x;
   const ImageDesc dd = desc[img];
   {
     int* z = reinterpret_cast<int*>(&s);
     for (int i = tid; i < (int)(sizeof(ParseScratch) / 4); i += blockDim.x) z[i] = 0;
   }
+  const int nh = (int)min(dd.in_size, (int64_t)kHdrBytes) & ~15;  // whole 16-byte groups
+  for (int i = tid; i < nh / 16; i += blockDim.x)
+    reinterpret_cast<uint4*>(hdr)[i] = reinterpret_cast<const uint4*>(bytes + dd.in_off)[i];
   __syncthreads();
   if (tid == 0) {
-    int rc = parse_headers(bytes + dd.in_off, (int)dd.in_size, s);
+    const Bytes file{bytes + dd.in_off, hdr, nh};
+    int rc = parse_headers(file, (int)dd.in_size, s);
     if (rc == kOk) {
       // the host probe sized every buffer; it must agree with the device parse
       if (s.info.width != dd.width || s.info.height != dd.height || s.info.ncomp != dd.ncomp ||
@@ -1316,239 +1344,273 @@ __device__ __forceinline__ PlaneWeights plane_weights(const ImageDesc& dd, const
   return w;
 }
 
-// Visible content rows [vy0, vy1) and columns [vx0, vx0 + nvis) of the
-// scaled image inside the output (pad / crop geometry).
-__device__ __forceinline__ void visible_rows(const ImageDesc& dd, int& vy0, int& vy1) {
-  vy0 = max(-dd.dy, 0);
-  vy1 = min(dd.oh - dd.dy, dd.sh);
+// Horizontal taps of one column over nr staged rows, interior case: the
+// 4*NQ bytes from `f` are fetched as NQ+1 aligned dwords, realigned with
+// v_alignbyte, widened to int16 pairs with v_perm and accumulated with
+// v_dot2 against the packed Q14 weights (zeros past the real taps).  Writes
+// the Q6 intermediate ((acc + 128) >> 8) to out[rr * ostride].
+typedef short hj_short2 __attribute__((ext_vector_type(2)));
+
+template <int NQ>
+__device__ __forceinline__ void h_rows_dot2(const uint8_t* srcb, int stride, int f, int nr,
+                                            const uint32_t* wp, int16_t* out, int ostride) {
+  const int a = f & ~3;
+  const uint32_t sh = (uint32_t)(f & 3);
+#pragma unroll 2
+  for (int rr = 0; rr < nr; rr++) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(srcb + rr * stride + a);
+    uint32_t w[NQ + 1];
+#pragma unroll
+    for (int i = 0; i <= NQ; i++) w[i] = q[i];
+    int32_t h = 0;
+#pragma unroll
+    for (int i = 0; i < NQ; i++) {
+      const uint32_t u = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+      const uint32_t lo = __builtin_amdgcn_perm(0u, u, 0x0C010C00u);  // bytes 0,1 -> int16 x2
+      const uint32_t hi = __builtin_amdgcn_perm(0u, u, 0x0C030C02u);  // bytes 2,3
+      h = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, lo),
+                                 __builtin_bit_cast(hj_short2, wp[2 * i]), h, false);
+      h = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, hi),
+                                 __builtin_bit_cast(hj_short2, wp[2 * i + 1]), h, false);
+    }
+    out[rr * ostride] = (int16_t)((h + 128) >> 8);
+  }
 }
 
-// Horizontal pass: one workgroup = (row group, plane, image).  The group's
-// source rows are staged in LDS with 8-byte loads; a thread owns one visible
-// output column, keeps its taps in registers and writes the Q6 intermediate
-// ((acc + 128) >> 8) of every staged row: int16 [rows][tmp_stride] per plane.
-// Only rows some visible output row reads are computed.
-__global__ void __launch_bounds__(256) resize_h_kernel(const uint8_t* __restrict__ planes,
-                                                       const ImageDesc* __restrict__ desc,
-                                                       const ImageInfo* __restrict__ infos,
-                                                       const int32_t* __restrict__ pool,
-                                                       int16_t* __restrict__ tmp) {
+// Horizontal taps with clamped source columns.  Up to 16 taps: unrolled
+// with constant tap indices (weights stay in registers).  More taps (strong
+// downscale) or rows read in place: a loop over wcol.
+template <bool PACKED>
+__device__ __forceinline__ void h_rows_clamped(const uint8_t* rows, int stride, int f, int pw,
+                                               int nr, int tx, const uint32_t* wp,
+                                               const int16_t* wcol, int16_t* out, int ostride) {
+#pragma unroll 1
+  for (int rr = 0; rr < nr; rr++) {
+    const uint8_t* row = rows + (int64_t)rr * stride;
+    int32_t h = 0;
+    if (PACKED) {
+#pragma unroll
+      for (int t = 0; t < 16; t++) {
+        const int32_t wt = (int32_t)(int16_t)(wp[t >> 1] >> ((t & 1) * 16));
+        h += wt * (int32_t)row[min(max(f + t, 0), pw - 1)];
+      }
+    } else {
+      for (int t = 0; t < tx; t++) h += (int32_t)wcol[t] * row[min(max(f + t, 0), pw - 1)];
+    }
+    out[rr * ostride] = (int16_t)((h + 128) >> 8);
+  }
+}
+
+// One plane of the scaled image, one band of output rows: workgroup =
+// (band, plane, image).  Source rows the band needs are staged in LDS a
+// group at a time (the next group's loads are issued before the current
+// group is filtered); the horizontal taps (one thread per visible column,
+// v_dot2 on int16 pairs) fill an LDS intermediate (Q6 int16), the vertical
+// taps read it ((acc + 2^19) >> 20, clamp) and the band goes out as u8 rows
+// of the resampled plane.  Arithmetic: oracle/jpeg_oracle.c resize_plane.
+__global__ void __launch_bounds__(256) resize_plane_kernel(const uint8_t* __restrict__ planes,
+                                                           const ImageDesc* __restrict__ desc,
+                                                           ImageInfo* __restrict__ infos,
+                                                           const int32_t* __restrict__ pool,
+                                                           uint8_t* __restrict__ rplanes) {
   __shared__ __attribute__((aligned(16))) uint8_t srcb[kHSrcBytes + 32];
+  __shared__ int16_t tb[kTBuf];
+  __shared__ __attribute__((aligned(16))) int16_t wys[kRMaxRb * kVTaps];
+  __shared__ int32_t fys[kRMaxRb];
   const int img = blockIdx.z, c = blockIdx.y, tid = threadIdx.x;
   const ImageInfo& in = infos[img];
   if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
-  if (c >= dd.ncomp || dd.nvis <= 0) return;
-  int vy0, vy1;
-  visible_rows(dd, vy0, vy1);
-  if (vy0 >= vy1) return;
+  if (c >= dd.ncomp || dd.nvis <= 0 || dd.nvy <= 0) return;
+  const int RB = dd.r_rb[c];
+  const int yb0 = dd.vy0 + (int)blockIdx.x * RB;  // first content row of the band
+  if (yb0 >= dd.vy0 + dd.nvy) return;
+  const int nyb = min(RB, dd.vy0 + dd.nvy - yb0);
   const PlaneWeights W = plane_weights(dd, pool, c);
   const int pw = in.comp_w[c], ph = in.comp_hpx[c], stride = dd.plane_stride[c];
-  const int rpw = h_rows_per_group(stride);
-  const int r_lo = max(W.fy[vy0], 0), r_hi = min(W.fy[vy1 - 1] + W.ty - 1, ph - 1);
-  const int ra = r_lo + (int)blockIdx.x * rpw;
-  if (ra > r_hi) return;
-  const int nr = min(rpw, r_hi + 1 - ra);
-  // stage nr full rows (stride is a multiple of 8): loads first, then stores;
-  // rows wider than the LDS buffer are read in place
+  const int r_lo = min(max(W.fy[yb0], 0), ph - 1);
+  const int r_hi = min(max(W.fy[yb0 + nyb - 1] + W.ty - 1, 0), ph - 1);
+  const int nrows = r_hi - r_lo + 1;
+  const uint8_t* src_plane = planes + dd.plane_off[c];
   const bool staged = stride <= kHSrcBytes;
-  const uint8_t* rows = staged ? srcb : planes + dd.plane_off[c] + (int64_t)ra * stride;
-  if (staged) {
-    const uint2* s = reinterpret_cast<const uint2*>(planes + dd.plane_off[c] + (int64_t)ra * stride);
-    uint2* d = reinterpret_cast<uint2*>(srcb);
-    const int n8 = nr * stride / 8;
-    for (int i0 = 0; i0 < n8; i0 += 256 * 8) {
-      uint2 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int i = i0 + u * 256 + tid;
-        if (i < n8) v[u] = s[i];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int i = i0 + u * 256 + tid;
-        if (i < n8) d[i] = v[u];
-      }
+  const int G = h_rows_per_group(stride);
+  uint8_t* rp = rplanes + dd.rp_off + (int64_t)c * dd.nvy * dd.rp_stride;
+  // the band's vertical taps and first rows, once (read by every column)
+  const bool wy_lds = W.ty <= kVTaps;
+  if (wy_lds)
+    for (int i = tid; i < nyb * W.ty; i += 256) wys[i] = W.wy[(int64_t)yb0 * W.ty + i];
+  for (int i = tid; i < nyb; i += 256) fys[i] = W.fy[yb0 + i];
+  for (int cc0 = 0; cc0 < dd.nvis; cc0 += dd.r_cols) {
+    const int ncc = min(dd.r_cols, dd.nvis - cc0);
+    if (nrows * ncc > kTBuf) {  // the host tiling guarantees this fits
+      if (tid == 0) infos[img].status = kErrBadGeometry;
+      return;
     }
-  }
-  __syncthreads();
-  int16_t* out = tmp + dd.tmp_off + (int64_t)dd.tmp_plane[c] + (int64_t)ra * dd.tmp_stride;
-  for (int xx = tid; xx < dd.nvis; xx += 256) {
-    const int cx = dd.vx0 + xx;
-    const int f = W.fx[cx];
-    const int16_t* wcol = W.wx + (int64_t)cx * W.tx;
-    if (W.tx <= 16) {
-      int32_t wr[16];
+    // per-thread column state (a thread owns column cc0 + tid)
+    const bool mine = tid < ncc;
+    const int cx = dd.vx0 + cc0 + tid;
+    int f = 0;
+    const int16_t* wcol = nullptr;
+    uint32_t wp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (mine) {
+      f = W.fx[cx];
+      wcol = W.wx + (int64_t)cx * W.tx;
+      if (W.tx <= 16) {
 #pragma unroll
-      for (int t = 0; t < 16; t++) wr[t] = t < W.tx ? (int32_t)wcol[t] : 0;
-      if (f >= 0 && f + 16 <= pw) {
-        // interior: 16 straight taps (zero weights past tx)
-        for (int rr = 0; rr < nr; rr++) {
-          const uint8_t* row = rows + (int64_t)rr * stride + f;
-          int32_t h = 0;
-#pragma unroll
-          for (int t = 0; t < 16; t++) h += wr[t] * (int32_t)row[t];
-          out[(int64_t)rr * dd.tmp_stride + xx] = (int16_t)((h + 128) >> 8);
-        }
-      } else {
-        int kx[16];
-#pragma unroll
-        for (int t = 0; t < 16; t++) kx[t] = min(max(f + t, 0), pw - 1);
-        for (int rr = 0; rr < nr; rr++) {
-          const uint8_t* row = rows + (int64_t)rr * stride;
-          int32_t h = 0;
-#pragma unroll
-          for (int t = 0; t < 16; t++) h += wr[t] * (int32_t)row[kx[t]];
-          out[(int64_t)rr * dd.tmp_stride + xx] = (int16_t)((h + 128) >> 8);
+        for (int k = 0; k < 8; k++) {
+          const uint32_t w0 = 2 * k < W.tx ? (uint16_t)wcol[2 * k] : 0u;
+          const uint32_t w1 = 2 * k + 1 < W.tx ? (uint16_t)wcol[2 * k + 1] : 0u;
+          wp[k] = w0 | (w1 << 16);
         }
       }
-    } else {
-      for (int rr = 0; rr < nr; rr++) {
-        const uint8_t* row = rows + (int64_t)rr * stride;
-        int32_t h = 0;
-        for (int t = 0; t < W.tx; t++) h += (int32_t)wcol[t] * row[min(max(f + t, 0), pw - 1)];
-        out[(int64_t)rr * dd.tmp_stride + xx] = (int16_t)((h + 128) >> 8);
+    }
+    const bool interior = staged && W.tx <= 16 && f >= 0 && f + 16 <= pw;
+    // ---- horizontal taps, a group of G source rows at a time ----
+    uint2 pre[4];
+    auto load_group = [&](int g0) {
+      const uint2* s2 = reinterpret_cast<const uint2*>(src_plane + (int64_t)(r_lo + g0) * stride);
+      const int m8 = min(G, nrows - g0) * stride / 8;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i = u * 256 + tid;
+        if (i < m8) pre[u] = s2[i];
+      }
+      return m8;
+    };
+    int m8 = staged ? load_group(0) : 0;
+    for (int g0 = 0; g0 < nrows; g0 += G) {
+      const int ng = min(G, nrows - g0);
+      if (staged) {
+        // finish staging this group (the first 4 x 256 uint2 are prefetched)
+        uint2* d2 = reinterpret_cast<uint2*>(srcb);
+        const uint2* s2 = reinterpret_cast<const uint2*>(src_plane + (int64_t)(r_lo + g0) * stride);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = u * 256 + tid;
+          if (i < m8) d2[i] = pre[u];
+        }
+        for (int i = 4 * 256 + tid; i < m8; i += 256) d2[i] = s2[i];
+      }
+      __syncthreads();
+      if (staged && g0 + G < nrows) m8 = load_group(g0 + G);  // overlaps the taps below
+      if (mine) {
+        int16_t* out = tb + g0 * ncc + tid;
+        if (interior) {
+          if (W.tx <= 8) h_rows_dot2<2>(srcb, stride, f, ng, wp, out, ncc);
+          else h_rows_dot2<4>(srcb, stride, f, ng, wp, out, ncc);
+        } else if (staged && W.tx <= 16) {
+          h_rows_clamped<true>(srcb, stride, f, pw, ng, W.tx, wp, wcol, out, ncc);
+        } else if (staged) {
+          h_rows_clamped<false>(srcb, stride, f, pw, ng, W.tx, wp, wcol, out, ncc);
+        } else {
+          h_rows_clamped<false>(src_plane + (int64_t)(r_lo + g0) * stride, stride, f, pw, ng,
+                                W.tx, wp, wcol, out, ncc);
+        }
+      }
+      __syncthreads();
+    }
+    // ---- vertical taps: nyb output rows of this column ----
+    if (mine) {
+      for (int yy = 0; yy < nyb; yy++) {
+        const int y = yb0 + yy;
+        const int fy = fys[yy];
+        const int16_t* w = wy_lds ? wys + yy * W.ty : W.wy + (int64_t)y * W.ty;
+        int32_t acc = 0;
+        if (wy_lds && fy >= 0 && fy + W.ty <= ph) {
+          const int16_t* tcol = tb + (fy - r_lo) * ncc + tid;
+          for (int t = 0; t < W.ty; t += 2) {
+            const uint32_t wpair = *reinterpret_cast<const uint32_t*>(w + t);
+            const uint32_t vpair = (uint32_t)(uint16_t)tcol[t * ncc] |
+                                   ((uint32_t)(uint16_t)tcol[(t + 1) * ncc] << 16);
+            acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, vpair),
+                                         __builtin_bit_cast(hj_short2, wpair), acc, false);
+          }
+        } else {
+          for (int t = 0; t < W.ty; t++) {
+            const int k = min(max(fy + t, 0), ph - 1) - r_lo;
+            acc += (int32_t)w[t] * tb[k * ncc + tid];
+          }
+        }
+        rp[(int64_t)(y - dd.vy0) * dd.rp_stride + cc0 + tid] = clip_u8((acc + (1 << 19)) >> 20);
       }
     }
+    __syncthreads();
   }
 }
 
-// Vertical pass + colour conversion + pad/crop + (normalise) + store.  One
-// workgroup = (band of v_rb output rows, image); output columns in chunks of
-// v_cols, a thread per column.  Per plane the band's intermediate rows are
-// staged in LDS, each thread runs the vertical taps ((acc + 2^19) >> 20,
-// clamp) for its column, then YCbCr -> RGB; the band is assembled in LDS and
-// written with coalesced stores.  Arithmetic: oracle/jpeg_oracle.c
-// resize_plane + jo_resize_planes.
-__global__ void __launch_bounds__(256) resize_v_kernel(const int16_t* __restrict__ tmp,
-                                                       const ImageDesc* __restrict__ desc,
-                                                       ImageInfo* __restrict__ infos,
-                                                       const int32_t* __restrict__ pool,
-                                                       void* __restrict__ out, const BatchParams p) {
-  __shared__ int16_t tb[kVBuf];
-  __shared__ __attribute__((aligned(16))) uint8_t ost[kVMaxRb * kVMaxCols * 3 * 2];
-  __shared__ int16_t wys[kVMaxRb * kMaxTaps];
-  __shared__ int32_t fys[kVMaxRb];
-  const int img = blockIdx.y, tid = threadIdx.x;
+// Colour conversion + pad/crop + (normalise) + store, 4 output pixels of a
+// row per thread: resampled planes (u8, visible content only) -> RGB in the
+// caller's layout; pad pixels are black.  Arithmetic: jo_resize_planes.
+__global__ void __launch_bounds__(256) csc_store_kernel(const uint8_t* __restrict__ rplanes,
+                                                        const ImageDesc* __restrict__ desc,
+                                                        const ImageInfo* __restrict__ infos,
+                                                        void* __restrict__ out,
+                                                        const BatchParams p) {
+  const int img = blockIdx.y;
   const ImageInfo& in = infos[img];
   if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
-  const int ow = dd.ow, oh = dd.oh, RB = dd.v_rb, VC = dd.v_cols;
-  const int y0 = (int)blockIdx.x * RB;
-  if (y0 >= oh) return;
-  const int nyb = min(RB, oh - y0);
-  const int ncomp = dd.ncomp;
-  // content rows of the band
-  const int cy0 = max(y0 - dd.dy, 0), cy1 = min(y0 + nyb - dd.dy, dd.sh);
-  const int ncy = cy1 - cy0;
+  const int ow = dd.ow, oh = dd.oh;
+  const int qpr = (ow + 3) >> 2;  // pixel quads per row
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= qpr * oh) return;
+  const int y = q / qpr, x0 = (q - y * qpr) * 4;
+  const int np = min(4, ow - x0);
   const bool planar = p.pix_fmt == 0 || p.pix_fmt == 1;
   const bool swap = p.pix_fmt == 1 || p.pix_fmt == 3;
-  const int esz = p.dtype == 0 ? 1 : 2;
-  for (int xc0 = 0; xc0 < ow; xc0 += VC) {
-    const int nxc = min(VC, ow - xc0);
-    const int x = xc0 + tid;
-    const int cx = x - dd.dx;
-    // content columns of the chunk: [ccx0, ccx0 + ncc)
-    const int ccx0 = max(xc0 - dd.dx, dd.vx0);
-    const int ncc = min(xc0 + nxc - dd.dx, dd.vx0 + dd.nvis) - ccx0;
-    const bool mine = tid < nxc && cx >= ccx0 && cx < ccx0 + ncc;
-    int val[kMaxComp][kVMaxRb];
+  const int cy = y - dd.dy;
+  const int64_t pl = (int64_t)ow * oh;
+  const uint8_t* r0 = rplanes + dd.rp_off + (int64_t)(cy - dd.vy0) * dd.rp_stride;
+  const int64_t ps = (int64_t)dd.nvy * dd.rp_stride;
+  int v[4][3];
 #pragma unroll
-    for (int c = 0; c < kMaxComp; c++)
-#pragma unroll
-      for (int yy = 0; yy < kVMaxRb; yy++) val[c][yy] = 0;
-    if (ncy > 0 && ncc > 0) {
-      for (int c = 0; c < ncomp; c++) {
-        const PlaneWeights W = plane_weights(dd, pool, c);
-        const int ph = in.comp_hpx[c];
-        const int r_lo = min(max(W.fy[cy0], 0), ph - 1);
-        const int r_hi = min(max(W.fy[cy1 - 1] + W.ty - 1, 0), ph - 1);
-        const int nrows = r_hi - r_lo + 1;
-        if (nrows * ncc > kVBuf || W.ty > kMaxTaps) {  // the host tiling guarantees this fits
-          if (tid == 0) infos[img].status = kErrBadGeometry;
-          return;
-        }
-        const int16_t* src = tmp + dd.tmp_off + (int64_t)dd.tmp_plane[c] +
-                             (int64_t)r_lo * dd.tmp_stride + (ccx0 - dd.vx0);
-        for (int i = tid; i < nrows * ncc; i += 256) {
-          const int rr = i / ncc, j = i - rr * ncc;
-          tb[i] = src[(int64_t)rr * dd.tmp_stride + j];
-        }
-        for (int i = tid; i < ncy * W.ty; i += 256) wys[i] = W.wy[(int64_t)cy0 * W.ty + i];
-        if (tid < ncy) fys[tid] = W.fy[cy0 + tid];
-        __syncthreads();
-        if (mine) {
-          const int col = cx - ccx0;
-#pragma unroll
-          for (int yy = 0; yy < kVMaxRb; yy++) {
-            if (yy < ncy) {
-              const int16_t* w = wys + yy * W.ty;
-              const int f = fys[yy];
-              int32_t acc = 0;
-              for (int t = 0; t < W.ty; t++) {
-                const int k = min(max(f + t, 0), ph - 1) - r_lo;
-                acc += (int32_t)w[t] * tb[k * ncc + col];
-              }
-              val[c][yy] = clip_u8((acc + (1 << 19)) >> 20);
-            }
-          }
-        }
-        __syncthreads();
-      }
+  for (int k = 0; k < 4; k++) {
+    int rgb[3] = {0, 0, 0};
+    const int cx = x0 + k - dd.dx;
+    if (k < np && cy >= dd.vy0 && cy < dd.vy0 + dd.nvy && cx >= dd.vx0 && cx < dd.vx0 + dd.nvis) {
+      const int o = cx - dd.vx0;
+      if (dd.ncomp == 1) rgb[0] = rgb[1] = rgb[2] = r0[o];
+      else ycc_rgb(r0[o], r0[ps + o], r0[2 * ps + o], rgb);
     }
-    // colour conversion into the band staging buffer (pad pixels are black)
-    if (tid < nxc) {
 #pragma unroll
-      for (int yy = 0; yy < kVMaxRb; yy++) {
-        if (yy < nyb) {
-          const int cy = y0 + yy - dd.dy;
-          int rgb[3] = {0, 0, 0};
-          if (mine && cy >= cy0 && cy < cy1) {
-            const int k = cy - cy0;
-            if (ncomp == 1) rgb[0] = rgb[1] = rgb[2] = val[0][k];
-            else ycc_rgb(val[0][k], val[1][k], val[2][k], rgb);
-          }
-#pragma unroll
-          for (int ch = 0; ch < 3; ch++) {
-            const int v = rgb[swap ? 2 - ch : ch];
-            const int e = planar ? (ch * nyb + yy) * nxc + tid : (yy * nxc + tid) * 3 + ch;
-            if (esz == 1) {
-              ost[e] = (uint8_t)v;
-            } else {
-              float f = __fdiv_rn((float)v, 255.0f);
-              f = __fsub_rn(f, p.mean[ch]);
-              f = __fdiv_rn(f, p.std[ch]);
-              reinterpret_cast<__half*>(ost)[e] = __float2half_rn(f);
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // coalesced stores: every (channel,) row of the chunk is contiguous
-    uint8_t* ob = static_cast<uint8_t*>(out) + dd.out_off * esz;
-    const int64_t pl = (int64_t)ow * oh;
+    for (int ch = 0; ch < 3; ch++) v[k][ch] = rgb[swap ? 2 - ch : ch];
+  }
+  if (p.dtype == 0) {
+    uint8_t* ob = static_cast<uint8_t*>(out) + dd.out_off;
     if (!planar) {
-      if (nxc == ow) {  // whole rows: the band is one contiguous run
-        lds_to_global(ob + (int64_t)y0 * ow * 3 * esz, ost, nyb * ow * 3 * esz, tid);
+      uint8_t* d = ob + ((int64_t)y * ow + x0) * 3;
+      if (np == 4 && (((uintptr_t)d) & 3) == 0) {
+        uint32_t w0 = v[0][0] | (v[0][1] << 8) | (v[0][2] << 16) | (v[1][0] << 24);
+        uint32_t w1 = v[1][1] | (v[1][2] << 8) | (v[2][0] << 16) | (v[2][1] << 24);
+        uint32_t w2 = v[2][2] | (v[3][0] << 8) | (v[3][1] << 16) | (v[3][2] << 24);
+        reinterpret_cast<uint32_t*>(d)[0] = w0;
+        reinterpret_cast<uint32_t*>(d)[1] = w1;
+        reinterpret_cast<uint32_t*>(d)[2] = w2;
       } else {
-        for (int yy = 0; yy < nyb; yy++)
-          lds_to_global(ob + ((int64_t)(y0 + yy) * ow + xc0) * 3 * esz, ost + yy * nxc * 3 * esz,
-                        nxc * 3 * esz, tid);
+        for (int k = 0; k < np; k++)
+          for (int ch = 0; ch < 3; ch++) d[3 * k + ch] = (uint8_t)v[k][ch];
       }
     } else {
+#pragma unroll
       for (int ch = 0; ch < 3; ch++) {
-        if (nxc == ow) {
-          lds_to_global(ob + (ch * pl + (int64_t)y0 * ow) * esz, ost + ch * nyb * nxc * esz,
-                        nyb * ow * esz, tid);
-        } else {
-          for (int yy = 0; yy < nyb; yy++)
-            lds_to_global(ob + (ch * pl + (int64_t)(y0 + yy) * ow + xc0) * esz,
-                          ost + (ch * nyb + yy) * nxc * esz, nxc * esz, tid);
-        }
+        uint8_t* d = ob + ch * pl + (int64_t)y * ow + x0;
+        if (np == 4 && (((uintptr_t)d) & 3) == 0)
+          *reinterpret_cast<uint32_t*>(d) = v[0][ch] | (v[1][ch] << 8) | (v[2][ch] << 16) | (v[3][ch] << 24);
+        else
+          for (int k = 0; k < np; k++) d[k] = (uint8_t)v[k][ch];
       }
     }
-    __syncthreads();
+  } else {
+    __half* ob = static_cast<__half*>(out) + dd.out_off;
+    for (int k = 0; k < np; k++)
+#pragma unroll
+      for (int ch = 0; ch < 3; ch++) {
+        float fv = __fdiv_rn((float)v[k][ch], 255.0f);
+        fv = __fsub_rn(fv, p.mean[ch]);
+        fv = __fdiv_rn(fv, p.std[ch]);
+        const int64_t oi = planar ? ch * pl + (int64_t)y * ow + x0 + k : ((int64_t)y * ow + x0 + k) * 3 + ch;
+        ob[oi] = __float2half_rn(fv);
+      }
   }
 }
 
@@ -1627,12 +1689,12 @@ hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageI
   return hipGetLastError();
 }
 hipError_t launch_resize(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
-                         const int32_t* pool, int16_t* tmp, void* out, const BatchParams& p,
-                         int64_t h_groups, int64_t v_bands, int n, hipStream_t st) {
-  hipLaunchKernelGGL(resize_h_kernel, dim3((int)h_groups, kMaxComp, n), dim3(256), 0, st, planes,
-                     desc, infos, pool, tmp);
-  hipLaunchKernelGGL(resize_v_kernel, dim3((int)v_bands, n), dim3(256), 0, st, tmp, desc,
-                     const_cast<ImageInfo*>(infos), pool, out, p);
+                         const int32_t* pool, uint8_t* rplanes, void* out, const BatchParams& p,
+                         int64_t max_bands, int64_t max_quads, int n, hipStream_t st) {
+  hipLaunchKernelGGL(resize_plane_kernel, dim3((int)max_bands, kMaxComp, n), dim3(256), 0, st,
+                     planes, desc, const_cast<ImageInfo*>(infos), pool, rplanes);
+  hipLaunchKernelGGL(csc_store_kernel, dim3((int)((max_quads + 255) / 256), n), dim3(256), 0, st,
+                     rplanes, desc, infos, out, p);
   return hipGetLastError();
 }
 hipError_t launch_planes_copy(const uint8_t* planes, const ImageDesc* desc,
