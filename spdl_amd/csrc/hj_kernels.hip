@@ -51,6 +51,10 @@ struct ParseScratch {
   int32_t qhave[4];
   int32_t maxcode[8][18];
   int32_t valoff[8][17];
+  // table payloads in effect at SOS (file offsets), copied by all threads
+  int32_t dqt_off[4], dqt_pq[4];
+  int32_t dht_off[8], dht_n[8];
+  int32_t qtsel[kMaxComp];
 };
 
 // Header bytes: the first kHdrBytes of the file are staged in LDS by the
@@ -104,7 +108,8 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
         if (tq > 3 || pq > 1) return kErrBadHeader;
         int need = 1 + 64 * (pq + 1);
         if (n < need) return kErrBadHeader;
-        for (int i = 0; i < 64; i++) s.qt[tq][i] = pq ? (uint16_t)be16(p + 1 + 2 * i) : p[1 + i];
+        s.dqt_off[tq] = p.o + 1;
+        s.dqt_pq[tq] = pq;
         s.qhave[tq] = 1;
         p += need;
         n -= need;
@@ -124,7 +129,8 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
           code <<= 1;
         }
         if (total > 256 || n < 17 + total) return kErrBadHeader;
-        for (int i = 0; i < 256; i++) s.vals[slot][i] = i < total ? p[17 + i] : 0;
+        s.dht_off[slot] = p.o + 17;
+        s.dht_n[slot] = total;
         s.have[slot] = 1;
         p += 17 + total;
         n -= 17 + total;
@@ -188,7 +194,7 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
           return kErrBadHeader;
         in.comp_w[c] = (in.width * in.comp_h[c] + hmax - 1) / hmax;
         in.comp_hpx[c] = (in.height * in.comp_v[c] + vmax - 1) / vmax;
-        for (int i = 0; i < 64; i++) in.qt[c][i] = s.qt[comp_tq[c]][i];
+        s.qtsel[c] = comp_tq[c];
       }
       if (in.ncomp == 1) {
         in.comp_bw[0] = (in.comp_w[0] + 7) / 8;
@@ -280,6 +286,27 @@ __global__ void __launch_bounds__(256) parse_kernel(const uint8_t* __restrict__ 
   if (st != kOk) {
     if (tid == 0) infos[img] = s.info;
     return;
+  }
+  {
+    // table payloads: every thread copies a share
+    const Bytes file{bytes + dd.in_off, hdr, nh};
+    for (int i = tid; i < 8 * 256; i += blockDim.x) {
+      const int t = i >> 8, k = i & 255;
+      if (s.have[t]) s.vals[t][k] = k < s.dht_n[t] ? file[s.dht_off[t] + k] : 0;
+    }
+    for (int i = tid; i < 4 * 64; i += blockDim.x) {
+      const int t = i >> 6, k = i & 63;
+      if (s.qhave[t])
+        s.qt[t][k] = s.dqt_pq[t] ? (uint16_t)((file[s.dqt_off[t] + 2 * k] << 8) |
+                                              file[s.dqt_off[t] + 2 * k + 1])
+                                 : file[s.dqt_off[t] + k];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // the image's quantisation tables by component (as the thread-0 pass did)
+    for (int c = 0; c < s.info.ncomp; c++)
+      for (int i = 0; i < 64; i++) s.info.qt[c][i] = s.qt[s.qtsel[c]][i];
   }
   HuffTable* tabs = luts + (size_t)img * 8;
   for (int t = 0; t < 8; t++) {
@@ -975,12 +1002,18 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
         }
         const uint32_t* R = slot_recs(k);
         const int n = (int)S.s_nrec[k];
-        for (int i = 0; i < n; i += 4) {
-          const uint4 q = *reinterpret_cast<const uint4*>(R + (size_t)(i >> 2) * (NT * 4));
-          const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+        for (int i0 = 0; i0 < n; i0 += 16) {
+          // four 16-byte record groups in flight
+          uint4 qq[4];
 #pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const uint32_t x = w4[j];
+          for (int g = 0; g < 4; g++)
+            if (i0 + 4 * g < n)
+              qq[g] = *reinterpret_cast<const uint4*>(R + (size_t)((i0 >> 2) + g) * (NT * 4));
+#pragma unroll
+          for (int jj = 0; jj < 16; jj++) {
+            const int i = i0 + (jj & ~3), j = jj & 3;
+            const uint4 q = qq[jj >> 2];
+            const uint32_t x = j == 0 ? q.x : (j == 1 ? q.y : (j == 2 ? q.z : q.w));
             const bool dc = i + j < n && (x >> 22 & 1u) && (x >> 25) == kRecCoef;
             const int c = (int)((x >> 23) & 3u);
             const int lv = dc ? (int)(int16_t)(x & 0xFFFFu) : 0;
@@ -1038,46 +1071,51 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
         const int seg_end_blk = ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks;
         const uint32_t* R = slot_recs(k);
         const int n = (int)S.s_nrec[k];
-        for (int i = 0; i < n && !done && rc == kOk; i += 4) {
-          const uint4 q = *reinterpret_cast<const uint4*>(R + (size_t)(i >> 2) * (NT * 4));
-          const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+        for (int i0 = 0; i0 < n && !done && rc == kOk; i0 += 16) {
+          // four 16-byte record groups in flight before their scatter stores
+          uint4 qq[4];
 #pragma unroll
-          for (int j = 0; j < 4; j++) {
-            if (i + j >= n || done || rc != kOk) break;
-            const uint32_t x = w4[j];
-            const uint32_t kind = x >> 25;
-            const int zz = (int)((x >> 16) & 63u);
-            if (kind != kRecCoef) {
-              // the sequential decoder stops at the segment's last block and
-              // never reads what follows; anything else is an error
-              if (nb > seg_end_blk || (nb == seg_end_blk && zz == 0)) done = true;
-              else rc = kind == kRecErrTrunc ? kErrTruncated : kErrBadHuffman;
-              break;
+          for (int g = 0; g < 4; g++)
+            if (i0 + 4 * g < n)
+              qq[g] = *reinterpret_cast<const uint4*>(R + (size_t)((i0 >> 2) + g) * (NT * 4));
+#pragma unroll
+          for (int jj = 0; jj < 16; jj++) {
+            const int i = i0 + (jj & ~3), j = jj & 3;
+            const uint4 q = qq[jj >> 2];
+            const uint32_t x = j == 0 ? q.x : (j == 1 ? q.y : (j == 2 ? q.z : q.w));
+            if (i + j < n && !done && rc == kOk) {
+              const uint32_t kind = x >> 25;
+              const int zz = (int)((x >> 16) & 63u);
+              const bool is_dc = (x >> 22) & 1u;
+              const int c = (int)((x >> 23) & 3u);
+              const int lv = (int)(int16_t)(x & 0xFFFFu);
+              if (kind != kRecCoef) {
+                // the sequential decoder stops at the segment's last block and
+                // never reads what follows; anything else is an error
+                if (nb > seg_end_blk || (nb == seg_end_blk && zz == 0)) done = true;
+                else rc = kind == kRecErrTrunc ? kErrTruncated : kErrBadHuffman;
+              } else if ((is_dc ? nb : nb - 1) >= seg_end_blk) {
+                done = true;
+              } else {
+                const int qv = S.qt[c][zz];
+                int16_t val;
+                int blk;
+                if (is_dc) {
+                  const int cur = c == 0 ? dc0 : (c == 1 ? dc1 : dc2);
+                  const int ndc = cur + lv;
+                  if (c == 0) dc0 = ndc;
+                  else if (c == 1) dc1 = ndc;
+                  else dc2 = ndc;
+                  const int32_t dqi = (int32_t)((uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc);
+                  val = (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi));
+                  blk = nb++;
+                } else {
+                  val = (int16_t)(lv * qv);
+                  blk = nb - 1;
+                }
+                coef_img[(size_t)blk * 64 + S.nat[zz]] = val;
+              }
             }
-            const bool is_dc = (x >> 22) & 1u;
-            const int c = (int)((x >> 23) & 3u);
-            const int lv = (int)(int16_t)(x & 0xFFFFu);
-            if ((is_dc ? nb : nb - 1) >= seg_end_blk) {
-              done = true;
-              break;
-            }
-            const int qv = S.qt[c][zz];
-            int16_t val;
-            int blk;
-            if (is_dc) {
-              const int cur = c == 0 ? dc0 : (c == 1 ? dc1 : dc2);
-              const int ndc = cur + lv;
-              if (c == 0) dc0 = ndc;
-              else if (c == 1) dc1 = ndc;
-              else dc2 = ndc;
-              const int32_t dqi = (int32_t)((uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc);
-              val = (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi));
-              blk = nb++;
-            } else {
-              val = (int16_t)(lv * qv);
-              blk = nb - 1;
-            }
-            coef_img[(size_t)blk * 64 + S.nat[zz]] = val;
           }
         }
         // last slot of its segment: every block of the segment must be done
