@@ -34,6 +34,39 @@ from spdl_amd.synthetic import synthetic_batch  # noqa: E402
 
 METRIC = "images/sec device-resident JPEG→RGB224, 1/2/4/8×MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# Per-launch HBM-side bytes per kernel from the committed rocprofv3 --pmc
+# passes of this same command (tools/pmc_passes.sh + tools/pmc_traffic.py):
+# FETCH_SIZE / WRITE_SIZE cannot be read from inside the timed process.
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc", "traffic.json")
+# bench stage -> kernels launched in it
+STAGE_KERNELS = {
+    "parse": ["hj::parse_kernel"],
+    "destuff": ["hj::destuff_count_kernel", "hj::destuff_prefix_kernel", "hj::destuff_write_kernel"],
+    "entropy": ["hj::entropy_kernel<"],
+    "idct": ["hj::idct_kernel<"],
+    "weights": ["hj::weights_kernel"],
+    "output": ["hj::resize_plane_kernel", "hj::csc_store_kernel", "hj::csc_kernel"],
+}
+
+
+def _pmc_traffic(stage: str, batch: int):
+    """HBM bytes per launch of `stage`'s kernels from the committed PMC
+    summary (None when absent or recorded for another batch size)."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            rec = json.load(f)
+    except OSError:
+        return None
+    if rec.get("batch") not in (None, batch):
+        return None
+    tot, hit = 0, False
+    for name, v in rec["kernels"].items():
+        if any(name.startswith(k) for k in STAGE_KERNELS.get(stage, [])):
+            tot += v["traffic_bytes"]
+            hit = True
+    return tot if hit else None
+
+
 BATCH = 256
 OUT_SPEC = Output(pix_fmt="rgb24", resize=True, fit_w=224, fit_h=224, aspect="decrease",
                   pad_w=224, pad_h=224)
@@ -204,7 +237,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": None,
+                "traffic": _pmc_traffic(dominant, a.batch),
+                "traffic_source": "profiles/r01_pmc/traffic.json (rocprofv3 --pmc FETCH_SIZE, "
+                                  "WRITE_SIZE; separate passes; x1024, FETCH x2 gfx950)",
                 "algorithmic_bytes_per_image": round(per_image_bytes, 1),
             },
             "stages_ms": {k: round(v, 4) for k, v in stages_ms.items()},
