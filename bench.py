@@ -70,6 +70,17 @@ def _pmc_traffic(stage: str, batch: int):
 BATCH = 256
 OUT_SPEC = Output(pix_fmt="rgb24", resize=True, fit_w=224, fit_h=224, aspect="decrease",
                   pad_w=224, pad_h=224)
+# configs[3]: examples/imagenet_classification.py's filter chain (scale 256
+# decrease + pad 256 + centre crop 224) with its Preprocessing fused:
+# (x/255 - mean)/std in fp32 -> fp16 (or bf16), NCHW.
+IMAGENET_SPEC = Output(pix_fmt="rgb", resize=True, fit_w=256, fit_h=256, aspect="decrease",
+                       pad_w=256, pad_h=256, crop_w=224, crop_h=224, normalize=True)
+WORKLOADS = {
+    "pad224": ("configs[1]: synthetic 480x640 q90 4:2:0 baseline JPEG resident in HBM -> RGB "
+               "224x224 u8 (scale bicubic decrease + centred pad, rgb24)"),
+    "imagenet": ("configs[3]: synthetic 480x640 q90 4:2:0 baseline JPEG resident in HBM -> "
+                 "scale 256 decrease + pad 256 + crop 224, (x/255-mean)/std fused, NCHW {dt}"),
+}
 
 
 def _args():
@@ -84,6 +95,8 @@ def _args():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sub-bits", type=int, default=0)
     p.add_argument("--entropy-threads", type=int, default=0)
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="pad224")
+    p.add_argument("--norm-dtype", choices=["float16", "bfloat16"], default="float16")
     p.add_argument("--with-copies", action="store_true",
                    help="also time the host-bytes path (pinned H2D + D2H of the output)")
     return p.parse_args()
@@ -149,12 +162,17 @@ def main():
         dec.set_param("sub_bits", a.sub_bits)
     if a.entropy_threads:
         dec.set_param("entropy_threads", a.entropy_threads)
-    out = torch.empty((a.batch, 224, 224, 3), dtype=torch.uint8, device=device)
+    if a.workload == "imagenet":
+        spec = Output(**{**IMAGENET_SPEC.__dict__, "norm_dtype": a.norm_dtype})
+        out = torch.empty((a.batch, 3, 224, 224), dtype=spec.torch_dtype, device=device)
+    else:
+        spec = OUT_SPEC
+        out = torch.empty((a.batch, 224, 224, 3), dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream(device)
-    nbytes_out = out.numel()
+    nbytes_out = out.numel() * out.element_size()
 
     def step():
-        dec.decode_batch_device(dev.data_ptr(), dev.numel(), offs, sizes, infos, OUT_SPEC,
+        dec.decode_batch_device(dev.data_ptr(), dev.numel(), offs, sizes, infos, spec,
                                 out.data_ptr(), nbytes_out, stream=stream, sync=True)
 
     for _ in range(a.warmup):
@@ -186,7 +204,8 @@ def main():
     kernels = {k: v for k, v in stages_ms.items() if k not in ("h2d", "d2h_status")}
     dominant = max(kernels, key=kernels.get)
     comp_bytes = float(np.mean(sizes))
-    per_image_bytes = comp_bytes + 224 * 224 * 3  # §8(d): compressed in + RGB224 out
+    # §8(d): compressed in + RGB224 out (u8: 150,528 B; fp16/bf16: 301,056 B)
+    per_image_bytes = comp_bytes + nbytes_out / a.batch
     launch_bytes = per_image_bytes * a.batch
     dom_s = kernels[dominant] / 1000.0
     achieved = launch_bytes / dom_s / 1e9
@@ -197,13 +216,13 @@ def main():
         t1 = time.perf_counter()
         nrep = max(5, a.steps // 4)
         for _ in range(nrep):
-            dec.decode_batch(datas, OUT_SPEC, out.data_ptr(), nbytes_out, stream=stream)
+            dec.decode_batch(datas, spec, out.data_ptr(), nbytes_out, stream=stream)
             host_out.copy_(out, non_blocking=True)
             torch.cuda.synchronize(device)
         copies = a.batch * nrep / (time.perf_counter() - t1)
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "pad224":
         cpu = _cpu_baseline(datas, a.cpu_threads, a.cpu_images)
 
     if rank == 0:
@@ -219,11 +238,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
+            "dtype": "u8" if a.workload == "pad224" else
+                     {"float16": "f16", "bfloat16": "bf16"}[a.norm_dtype] + " out (int decode, f32 normalise)",
             "data": "synthetic",
             "config": {
-                "workload": "configs[1]: synthetic 480x640 q90 4:2:0 baseline JPEG resident in "
-                            "HBM -> RGB 224x224 u8 (scale bicubic decrease + centred pad, rgb24)",
+                "workload": WORKLOADS[a.workload].format(dt=a.norm_dtype),
                 "global_batch": world * a.batch,
                 "per_gpu_batch": a.batch,
                 "mean_jpeg_bytes": round(comp_bytes, 1),
@@ -237,7 +256,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": _pmc_traffic(dominant, a.batch),
+                "traffic": _pmc_traffic(dominant, a.batch) if a.workload == "pad224" else None,
                 "traffic_source": "profiles/r01_pmc/traffic.json (rocprofv3 --pmc FETCH_SIZE, "
                                   "WRITE_SIZE; separate passes; x1024, FETCH x2 gfx950)",
                 "algorithmic_bytes_per_image": round(per_image_bytes, 1),

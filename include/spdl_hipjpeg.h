@@ -57,7 +57,10 @@ enum spdl_hj_pix_fmt {
 
 enum spdl_hj_aspect { SPDL_HJ_ASPECT_NONE = 0, SPDL_HJ_ASPECT_DECREASE = 1, SPDL_HJ_ASPECT_INCREASE = 2 };
 enum spdl_hj_filter { SPDL_HJ_FILTER_BICUBIC = 0, SPDL_HJ_FILTER_BILINEAR = 1 };
-enum spdl_hj_dtype { SPDL_HJ_DTYPE_U8 = 0, SPDL_HJ_DTYPE_F16 = 1 };
+/* F16 / BF16: (x/255 - mean)/std in IEEE fp32 (the reference's
+ * Preprocessing.forward, examples/imagenet_classification.py:95-106), rounded
+ * to nearest even into half / bfloat16. */
+enum spdl_hj_dtype { SPDL_HJ_DTYPE_U8 = 0, SPDL_HJ_DTYPE_F16 = 1, SPDL_HJ_DTYPE_BF16 = 2 };
 /* IDCT: FFmpeg simple_idct (the reference CPU path) or IJG islow (libjpeg). */
 enum spdl_hj_idct { SPDL_HJ_IDCT_SIMPLE = 0, SPDL_HJ_IDCT_ISLOW = 1 };
 
@@ -69,7 +72,7 @@ enum spdl_hj_idct { SPDL_HJ_IDCT_SIMPLE = 0, SPDL_HJ_IDCT_ISLOW = 1 };
  * fit_w/fit_h <= 0 mean "input size"; pad/crop <= 0 mean "absent". */
 typedef struct spdl_hj_output {
   int32_t pix_fmt;      /* spdl_hj_pix_fmt */
-  int32_t dtype;        /* spdl_hj_dtype; F16 applies (x/255 - mean)/std */
+  int32_t dtype;        /* spdl_hj_dtype; F16/BF16 apply (x/255 - mean)/std */
   int32_t idct;         /* spdl_hj_idct */
   int32_t resize;       /* 0 = none, 1 = apply the chain below */
   int32_t fit_w, fit_h, aspect;
@@ -126,6 +129,62 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
                                 const spdl_hj_output* out, void* out_dev, size_t out_bytes,
                                 void* stream, int32_t sync, int32_t* status, char* err,
                                 size_t errlen);
+
+/* ---- asynchronous submission and the pinned staging ring ----------------
+ * A context owns a ring of 3 slots (pinned staging + device copy of the
+ * JPEG bytes + descriptor/status staging).  Every decode call takes the next
+ * slot; a call with sync == 0 returns once the batch is enqueued: the H2D copy
+ * runs on the context's own copy stream and `stream` waits for it, so the host
+ * can pack batch k+1 and its copy can run while batch k's kernels execute
+ * (the reference copies synchronously: transfer_buffer_impl,
+ * src/libspdl/cuda/transfer.cpp:37-67; transfer_tensor's pinned cache,
+ * src/spdl/io/_transfer.py:82-177).  A slot is reused 3 submissions later, so
+ * wait for a ticket before submitting 3 more batches or its statuses are lost. */
+
+/* Ticket of the most recent submission on `ctx` (0 if none). */
+int64_t spdl_hj_last_ticket(spdl_hj_ctx* ctx);
+
+/* Block until the batch `ticket` has finished; per-image codes into
+ * status[0..n) (optional); returns the first failure like the sync call. */
+int spdl_hj_wait(spdl_hj_ctx* ctx, int64_t ticket, int32_t* status, int32_t n, char* err,
+                 size_t errlen);
+
+/* Zero-repack ingest: take the next slot and return its pinned staging
+ * (>= bytes long) so the caller can place a region of its source there
+ * directly -- e.g. a run of consecutive tar members, whose payloads are
+ * 512-byte aligned inside the archive (reference iter_tarfile,
+ * src/spdl/io/_tar.py:33-82, yields them as zero-copy views). */
+int spdl_hj_staging_acquire(spdl_hj_ctx* ctx, size_t bytes, uint8_t** host_ptr, int64_t* ticket,
+                            char* err, size_t errlen);
+
+/* Multi-threaded memcpy of host memory into an acquired slot. */
+int spdl_hj_staging_fill(spdl_hj_ctx* ctx, int64_t ticket, size_t dst_off, const uint8_t* src,
+                         size_t len, char* err, size_t errlen);
+
+/* Multi-threaded pread(2) of [file_off, file_off + len) of `fd` into an
+ * acquired slot (page cache -> pinned staging, no intermediate copy). */
+int spdl_hj_staging_read(spdl_hj_ctx* ctx, int64_t ticket, size_t dst_off, int fd,
+                         int64_t file_off, size_t len, char* err, size_t errlen);
+
+/* Decode the images at offsets[i] (256-byte aligned), sizes[i] inside the
+ * first `len` staged bytes of slot `ticket`: one hipMemcpyAsync of the whole
+ * region, then the device pipeline (same output contract as
+ * spdl_hj_decode_batch). */
+int spdl_hj_decode_staged(spdl_hj_ctx* ctx, int64_t ticket, size_t len, const int64_t* offsets,
+                          const int64_t* sizes, int32_t n, const spdl_hj_output* out,
+                          void* out_dev, size_t out_bytes, void* stream, int32_t sync,
+                          int32_t* status, char* err, size_t errlen);
+
+/* Index the regular-file members of an in-memory tar archive from byte
+ * `start`, at most max_entries: payload offsets/sizes, NUL-terminated names
+ * concatenated into `names` (name_offs[i] indexes them; names/name_offs may
+ * be NULL).  Same member walk as the reference's InMemoryTarParserImpl
+ * (src/spdl/io/lib/archive/tar_iterator.cpp:125-195: ustar magic + checksum,
+ * GNU 'L' long names, pax 'x' path records, empty name = end).  *next_pos is
+ * where to resume (== size at the end of the archive). */
+int spdl_hj_tar_index(const uint8_t* data, size_t size, size_t start, int32_t max_entries,
+                      int64_t* offsets, int64_t* sizes, int64_t* name_offs, char* names,
+                      size_t names_cap, int32_t* n_out, size_t* next_pos);
 
 /* Raw decoded planes (parity surface, the reference's load_image with
  * filter_desc=None -> yuvj4xxp planes, src/spdl/io/_composite.py:254-295):

@@ -989,6 +989,17 @@ uint16_t jo_f32_to_f16(float f) {
   return (uint16_t)(sign | h);
 }
 
+/* fp32 -> bfloat16, round to nearest even (torch's Tensor.to(torch.bfloat16),
+ * used after the reference's fp32 normalisation,
+ * examples/imagenet_classification.py:95-106,162-163); NaN stays quiet NaN. */
+uint16_t jo_f32_to_bf16(float f) {
+  uint32_t x;
+  memcpy(&x, &f, 4);
+  if ((x & 0x7FFFFFFFu) > 0x7F800000u) return (uint16_t)((x >> 16) | 0x40);
+  x += 0x7FFFu + ((x >> 16) & 1u);
+  return (uint16_t)(x >> 16);
+}
+
 /* resize one plane (true dims pw x ph, stride st) to sw x sh:
  * horizontal Q14 taps -> Q6 intermediate ((acc + 128) >> 8), then vertical Q14
  * -> (acc + 2^19) >> 20, clamp u8. */
@@ -1080,7 +1091,7 @@ int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize
           float v = (float)rgb[src_ch] / 255.0f;
           v = v - mean[ch];
           v = v / stdv[ch];
-          ((uint16_t*)out)[oi] = jo_f32_to_f16(v);
+          ((uint16_t*)out)[oi] = dtype == JO_DTYPE_BF16 ? jo_f32_to_bf16(v) : jo_f32_to_f16(v);
         }
       }
     }

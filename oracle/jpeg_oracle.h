@@ -59,7 +59,7 @@ enum { JO_FMT_RGB = 0, JO_FMT_BGR = 1, JO_FMT_RGB24 = 2, JO_FMT_BGR24 = 3 };
 
 enum { JO_ASPECT_NONE = 0, JO_ASPECT_DECREASE = 1, JO_ASPECT_INCREASE = 2 };
 enum { JO_FILTER_BICUBIC = 0, JO_FILTER_BILINEAR = 1 };
-enum { JO_DTYPE_U8 = 0, JO_DTYPE_F16 = 1 };
+enum { JO_DTYPE_U8 = 0, JO_DTYPE_F16 = 1, JO_DTYPE_BF16 = 2 };
 
 #define JO_MAX_COMP 3
 #define JO_MAX_BPM 10
@@ -145,6 +145,7 @@ int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize
                      void* out, jo_geom* geom_out);
 
 uint16_t jo_f32_to_f16(float f);
+uint16_t jo_f32_to_bf16(float f);
 
 /* Multi-threaded batch (CPU baseline).  Image i goes to out + i*out_stride
  * bytes.  status[i] receives the per-image code.  Returns #failed. */

@@ -22,7 +22,7 @@ IDCT_SIMPLE, IDCT_ISLOW = 0, 1
 FMT = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
 ASPECT = {None: 0, "none": 0, "decrease": 1, "increase": 2}
 FILTER = {"bicubic": 0, "bilinear": 1}
-DTYPE_U8, DTYPE_F16 = 0, 1
+DTYPE_U8, DTYPE_F16, DTYPE_BF16 = 0, 1, 2
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
@@ -268,6 +268,7 @@ def decode_resize(
     normalize: bool = False,
     mean=IMAGENET_MEAN,
     std=IMAGENET_STD,
+    norm_dtype: str = "float16",
 ) -> np.ndarray:
     info = parse(data)
     g = geometry(info.width, info.height, rs)
@@ -278,12 +279,13 @@ def decode_resize(
     _, p = _buf(data)
     rc = lib().jo_decode_resize(
         p, len(data), idct, ctypes.byref(rs._c()), FMT[pix_fmt],
-        DTYPE_F16 if normalize else DTYPE_U8, m.ctypes.data, s.ctypes.data,
+        (DTYPE_BF16 if norm_dtype == "bfloat16" else DTYPE_F16) if normalize else DTYPE_U8,
+        m.ctypes.data, s.ctypes.data,
         out.ctypes.data, None,
     )
     if rc:
         raise OracleError(rc)
-    if normalize:
+    if normalize and norm_dtype != "bfloat16":  # bfloat16: raw uint16 bit patterns
         out = out.view(np.float16)
     shape = (3, g["oh"], g["ow"]) if pix_fmt in ("rgb", "bgr") else (g["oh"], g["ow"], 3)
     return out.reshape(shape)

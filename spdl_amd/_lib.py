@@ -22,7 +22,8 @@ PIX_FMTS = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
 ASPECT = {None: 0, "none": 0, "decrease": 1, "increase": 2}
 FILTERS = {"bicubic": 0, "bilinear": 1}
 IDCT = {"simple": 0, "islow": 1}
-DTYPE_U8, DTYPE_F16 = 0, 1
+DTYPE_U8, DTYPE_F16, DTYPE_BF16 = 0, 1, 2
+NORM_DTYPES = {"float16": DTYPE_F16, "bfloat16": DTYPE_BF16}
 
 EXPORTED = (
     "spdl_hj_abi_version",
@@ -38,6 +39,13 @@ EXPORTED = (
     "spdl_hj_stage_name",
     "spdl_hj_set_param",
     "spdl_hj_debug_entropy",
+    "spdl_hj_last_ticket",
+    "spdl_hj_wait",
+    "spdl_hj_staging_acquire",
+    "spdl_hj_staging_fill",
+    "spdl_hj_staging_read",
+    "spdl_hj_decode_staged",
+    "spdl_hj_tar_index",
 )
 
 
@@ -82,7 +90,7 @@ class Output:
     """
 
     pix_fmt: str = "rgb"
-    normalize: bool = False  # -> fp16 (x/255 - mean)/std
+    normalize: bool = False  # -> (x/255 - mean)/std in fp32, stored as norm_dtype
     idct: str = "simple"
     resize: bool = False
     fit_w: int = 0
@@ -95,13 +103,14 @@ class Output:
     filter: str = "bicubic"
     mean: tuple = (0.485, 0.456, 0.406)
     std: tuple = (0.229, 0.224, 0.225)
+    norm_dtype: str = "float16"  # or "bfloat16"
 
     def to_c(self) -> OutputSpec:
         if self.pix_fmt not in PIX_FMTS:
             raise RuntimeError(f"Unexpected pix_fmt: {self.pix_fmt}")
         return OutputSpec(
             PIX_FMTS[self.pix_fmt],
-            DTYPE_F16 if self.normalize else DTYPE_U8,
+            NORM_DTYPES[self.norm_dtype] if self.normalize else DTYPE_U8,
             IDCT[self.idct],
             int(bool(self.resize)),
             int(self.fit_w),
@@ -119,6 +128,14 @@ class Output:
     @property
     def planar(self) -> bool:
         return self.pix_fmt in ("rgb", "bgr")
+
+    @property
+    def torch_dtype(self):
+        import torch
+
+        if not self.normalize:
+            return torch.uint8
+        return torch.bfloat16 if self.norm_dtype == "bfloat16" else torch.float16
 
 
 _LIB = None
@@ -164,6 +181,21 @@ def lib() -> ctypes.CDLL:
         L.spdl_hj_stage_name.restype = ctypes.c_char_p
         L.spdl_hj_set_param.argtypes = [vp, cp, ctypes.c_int64]
         L.spdl_hj_debug_entropy.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, cp, sz]
+        i64 = ctypes.c_int64
+        L.spdl_hj_last_ticket.argtypes = [vp]
+        L.spdl_hj_last_ticket.restype = i64
+        L.spdl_hj_wait.argtypes = [vp, i64, vp, i32, cp, sz]
+        L.spdl_hj_staging_acquire.argtypes = [
+            vp, sz, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(i64), cp, sz
+        ]
+        L.spdl_hj_staging_fill.argtypes = [vp, i64, sz, vp, sz, cp, sz]
+        L.spdl_hj_staging_read.argtypes = [vp, i64, sz, ctypes.c_int, i64, sz, cp, sz]
+        L.spdl_hj_decode_staged.argtypes = [
+            vp, i64, sz, vp, vp, i32, ctypes.POINTER(OutputSpec), vp, sz, vp, i32, vp, cp, sz
+        ]
+        L.spdl_hj_tar_index.argtypes = [
+            vp, sz, sz, i32, vp, vp, vp, vp, sz, ctypes.POINTER(i32), ctypes.POINTER(sz)
+        ]
         ver = L.spdl_hj_abi_version()
         if ver != ABI_VERSION:
             raise RuntimeError(f"libspdl_hipjpeg ABI {ver} != expected {ABI_VERSION}")
@@ -191,6 +223,58 @@ def output_size(width: int, height: int, out: Output) -> tuple[int, int]:
     if rc:
         raise RuntimeError(f"invalid output geometry for {width}x{height} ({rc})")
     return ow.value, oh.value
+
+
+def buffer_address(src) -> tuple[int, int, object]:
+    """(address, length, keepalive) of a bytes-like object without copying
+    when it is writable or a numpy array; read-only bytes are viewed through
+    numpy (no copy either)."""
+    import numpy as np
+
+    if isinstance(src, np.ndarray):
+        a = np.ascontiguousarray(src).view(np.uint8).reshape(-1)
+        return a.ctypes.data, a.size, a
+    a = np.frombuffer(src, np.uint8)
+    return a.ctypes.data, a.size, a
+
+
+def tar_index(src, start: int = 0, max_entries: int = 1 << 20, with_names: bool = True):
+    """Regular-file members of an in-memory tar archive: list of (name,
+    offset, size) with payload offsets into `src`, plus the resume position.
+    Native walk (spdl_hj_tar_index) with the reference's semantics
+    (src/spdl/io/lib/archive/tar_iterator.cpp:125-195)."""
+    import numpy as np
+
+    addr, size, keep = buffer_address(src)
+    out = []
+    pos = start
+    while len(out) < max_entries:
+        want = min(max_entries - len(out), 4096)
+        offs = np.zeros(want, np.int64)
+        szs = np.zeros(want, np.int64)
+        noffs = np.zeros(want, np.int64)
+        names = ctypes.create_string_buffer(want * 128 + 65536) if with_names else None
+        n = ctypes.c_int32()
+        nxt = ctypes.c_size_t()
+        rc = lib().spdl_hj_tar_index(
+            addr, size, pos, want, offs.ctypes.data, szs.ctypes.data,
+            noffs.ctypes.data if with_names else None, names, len(names) if names else 0,
+            ctypes.byref(n), ctypes.byref(nxt))
+        if rc:
+            raise RuntimeError(f"tar index failed ({rc})")
+        raw = names.raw if with_names else b""
+        for i in range(n.value):
+            if with_names:
+                o = int(noffs[i])
+                name = raw[o: raw.index(b"\0", o)].decode("utf-8", "surrogateescape")
+            else:
+                name = ""
+            out.append((name, int(offs[i]), int(szs[i])))
+        pos = nxt.value
+        if n.value == 0 or pos >= size:
+            break
+    del keep
+    return out, pos
 
 
 def _stream_handle(stream) -> int | None:
@@ -285,6 +369,59 @@ class Decoder:
         if rc:
             raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
         return list(status)
+
+    # ---- asynchronous submission / staging ring (include/spdl_hipjpeg.h) ----
+    def last_ticket(self) -> int:
+        return int(lib().spdl_hj_last_ticket(self._h))
+
+    def wait(self, ticket: int, n: int = 0) -> list[int]:
+        status = (ctypes.c_int32 * max(n, 1))()
+        err = ctypes.create_string_buffer(1024)
+        rc = lib().spdl_hj_wait(self._h, int(ticket), status if n else None, n, err, 1024)
+        if rc:
+            raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
+        return list(status)[:n]
+
+    def staging_acquire(self, nbytes: int) -> tuple[int, int]:
+        """(pinned host address, ticket) of the next ring slot (>= nbytes)."""
+        ptr = ctypes.c_void_p()
+        ticket = ctypes.c_int64()
+        err = ctypes.create_string_buffer(1024)
+        rc = lib().spdl_hj_staging_acquire(self._h, int(nbytes), ctypes.byref(ptr),
+                                           ctypes.byref(ticket), err, 1024)
+        if rc:
+            raise RuntimeError(err.value.decode())
+        return int(ptr.value), int(ticket.value)
+
+    def staging_fill(self, ticket: int, dst_off: int, src_addr: int, nbytes: int) -> None:
+        err = ctypes.create_string_buffer(512)
+        rc = lib().spdl_hj_staging_fill(self._h, int(ticket), int(dst_off), src_addr, int(nbytes),
+                                        err, 512)
+        if rc:
+            raise RuntimeError(err.value.decode())
+
+    def staging_read(self, ticket: int, dst_off: int, fd: int, file_off: int,
+                     nbytes: int) -> None:
+        err = ctypes.create_string_buffer(512)
+        rc = lib().spdl_hj_staging_read(self._h, int(ticket), int(dst_off), int(fd),
+                                        int(file_off), int(nbytes), err, 512)
+        if rc:
+            raise RuntimeError(err.value.decode())
+
+    def decode_staged(self, ticket: int, nbytes: int, offsets, sizes, out: Output, out_ptr: int,
+                      out_bytes: int, stream=None, sync: bool = True) -> list[int]:
+        n = len(offsets)
+        offs = (ctypes.c_int64 * n)(*offsets)
+        szs = (ctypes.c_int64 * n)(*sizes)
+        status = (ctypes.c_int32 * max(n, 1))()
+        err = ctypes.create_string_buffer(1024)
+        spec = out.to_c()
+        rc = lib().spdl_hj_decode_staged(
+            self._h, int(ticket), int(nbytes), offs, szs, n, ctypes.byref(spec), out_ptr,
+            out_bytes, _stream_handle(stream), int(bool(sync)), status, err, 1024)
+        if rc:
+            raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
+        return list(status)[:n]
 
     def debug_entropy(self, data, nblocks: int):
         """Coefficients / destuffed bytes / diagnostics of one image (tests)."""

@@ -8,10 +8,18 @@
 // hipMemcpyAsync from pinned staging.
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/spdl_hipjpeg.h"
@@ -108,6 +116,96 @@ struct PinBuf {
     cap = 0;
   }
 };
+
+// Persistent host workers for the pinned-staging copies.  A 256-image batch
+// is ~28 MB; one core copies that at ~6-10 GB/s, slower than the GPU decodes
+// it, so the copy into pinned memory is split over a few threads.
+class CopyPool {
+ public:
+  explicit CopyPool(int n) {
+    for (int i = 0; i < n; i++) th_.emplace_back([this, i] { loop(i + 1); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int workers() const { return (int)th_.size() + 1; }
+  // fn(part, nparts) runs for part = 0..nparts-1 (part 0 on the caller).
+  void run(const std::function<void(int, int)>& fn) {
+    const int np = workers();
+    {
+      std::lock_guard<std::mutex> g(m_);
+      fn_ = &fn;
+      pending_ = np - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    fn(0, np);
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop(int part) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int, int)>* fn;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        fn = fn_;
+      }
+      (*fn)(part, workers());
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int, int)>* fn_ = nullptr;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// Copy n items of (dst_off, src, len) into `base`, zero-filling each item's
+// tail [len, padded) -- split by bytes over the pool when the total is large.
+struct CopyItem {
+  int64_t dst_off;
+  const uint8_t* src;
+  int64_t len, padded;
+};
+
+void parallel_pack(CopyPool* pool, uint8_t* base, const std::vector<CopyItem>& items) {
+  int64_t total = 0;
+  for (const CopyItem& it : items) total += it.padded;
+  auto body = [&](int part, int np) {
+    // byte range [lo, hi) of the concatenated padded items
+    const int64_t lo = total * part / np, hi = total * (part + 1) / np;
+    int64_t acc = 0;
+    for (const CopyItem& it : items) {
+      const int64_t a = acc, b = acc + it.padded;
+      acc = b;
+      if (b <= lo) continue;
+      if (a >= hi) break;
+      const int64_t s = lo > a ? lo - a : 0, e = (hi < b ? hi : b) - a;
+      const int64_t cs = s, ce = e < it.len ? e : it.len;
+      if (ce > cs) memcpy(base + it.dst_off + cs, it.src + cs, (size_t)(ce - cs));
+      const int64_t zs = s > it.len ? s : it.len;
+      if (e > zs) memset(base + it.dst_off + zs, 0, (size_t)(e - zs));
+    }
+  };
+  if (!pool || total < (4 << 20)) body(0, 1);
+  else pool->run(body);
+}
 
 // ---- host SOF probe (replaces nvjpegGetImageInfo) --------------------------
 int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
@@ -393,13 +491,33 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
 
 }  // namespace
 
+// One in-flight batch: pinned staging + device copy of the JPEG bytes, the
+// descriptor/status staging, and the events that say when each may be reused.
+// kSlots of them form the ring that lets batch k+1 be packed on the host and
+// copied (on the context's copy stream) while batch k's kernels run.
+constexpr int kSlots = 3;
+
+struct Slot {
+  PinBuf pin_in, pin_desc, pin_status;
+  DevBuf bytes;
+  hipEvent_t h2d_done = nullptr;  // bytes are in HBM
+  hipEvent_t done = nullptr;      // the batch's last kernel / status copy finished
+  int64_t ticket = 0;             // ticket of the batch occupying the slot (0 = none)
+  bool pending = false;           // submitted, not yet waited
+  bool staged = false;            // acquired by spdl_hj_staging_acquire, not submitted
+  int n = 0;
+};
+
 struct spdl_hj_ctx {
   int device = 0;
-  DevBuf bytes, clean, segs, desc, info, luts, coefs, planes, wts, recs, rplanes, dschunks;
-  PinBuf pin_in, pin_desc, pin_status;
-  hipEvent_t staging_free = nullptr;  // host staging may be rewritten after this
+  DevBuf clean, segs, desc, info, luts, coefs, planes, wts, recs, rplanes, dschunks;
+  Slot slots[kSlots];
+  int64_t next_ticket = 1;
+  int64_t last_ticket = 0;
+  hipStream_t copy = nullptr;         // H2D stream of the staging ring
   hipEvent_t batch_done = nullptr;    // device workspace free after this
   hipEvent_t ev[kStages + 1] = {};
+  CopyPool* pool = nullptr;
   bool profiling = false;
   float timings[kStages] = {};
   int ntimings = 0;
@@ -436,12 +554,53 @@ inline void mark(spdl_hj_ctx* c, int i, hipStream_t st) {
   if (c->profiling) (void)hipEventRecord(c->ev[i], st);
 }
 
-// device pipeline over bytes already in HBM
-int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, const Layout& L,
-                 int n, const spdl_hj_output* out, void* out_dev, size_t out_bytes,
-                 hipStream_t st, int sync, int32_t* status, char* err, size_t errlen,
-                 bool planes_only) {
-  const size_t esz = out->dtype == SPDL_HJ_DTYPE_F16 ? 2 : 1;
+// Take the next ring slot: its previous batch (if any) must have finished
+// before its pinned staging may be rewritten.  An un-waited ticket's
+// statuses are dropped here (the ring holds kSlots batches in flight).
+int acquire_slot(spdl_hj_ctx* ctx, Slot** out, char* err, size_t errlen) {
+  Slot& s = ctx->slots[ctx->next_ticket % kSlots];
+  if (s.staged) {
+    set_err(err, errlen, "staging slot of ticket %lld was acquired but never submitted",
+            (long long)s.ticket);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  if (s.ticket) HJ_HIP(hipEventSynchronize(s.done));
+  s.pending = false;
+  s.ticket = ctx->next_ticket++;
+  *out = &s;
+  return SPDL_HJ_OK;
+}
+
+Slot* find_slot(spdl_hj_ctx* ctx, int64_t ticket) {
+  if (ticket <= 0) return nullptr;
+  Slot& s = ctx->slots[ticket % kSlots];
+  return s.ticket == ticket ? &s : nullptr;
+}
+
+// Per-image statuses of a finished slot -> status[], first error -> err.
+int collect_status(Slot& s, int32_t* status, char* err, size_t errlen) {
+  const int32_t* stv = static_cast<const int32_t*>(s.pin_status.p);
+  int first_bad = -1;
+  for (int i = 0; i < s.n; i++) {
+    if (status) status[i] = stv[i];
+    if (stv[i] != SPDL_HJ_OK && first_bad < 0) first_bad = i;
+  }
+  s.pending = false;
+  if (first_bad >= 0) {
+    set_err(err, errlen, "Failed to decode an image. (image %d: %s)", first_bad,
+            status_str(stv[first_bad]));
+    return stv[first_bad];
+  }
+  return SPDL_HJ_OK;
+}
+
+// device pipeline over bytes already in HBM; `slot` provides the descriptor
+// and status staging and is marked done on `st` at the end.
+int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t bytes_len,
+                 const Layout& L, int n, const spdl_hj_output* out, void* out_dev,
+                 size_t out_bytes, hipStream_t st, int sync, int32_t* status, char* err,
+                 size_t errlen, bool planes_only) {
+  const size_t esz = out->dtype == SPDL_HJ_DTYPE_U8 ? 1 : 2;
   if (!planes_only && (size_t)L.out_elems_per_image * n * esz > out_bytes) {
     set_err(err, errlen, "output buffer too small: need %lld bytes, have %zu",
             (long long)(L.out_elems_per_image * n * esz), out_bytes);
@@ -455,13 +614,14 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
       return SPDL_HJ_ERR_INVALID_ARG;
     }
     int64_t e = L.desc[i].in_off + L.desc[i].in_size;
-    if ((size_t)e > bytes_len) {
+    if (L.desc[i].in_off < 0 || L.desc[i].in_size < 0 || (size_t)e > bytes_len) {
       set_err(err, errlen, "image %d extends past the input buffer", i);
       return SPDL_HJ_ERR_INVALID_ARG;
     }
     if (e > max_end) max_end = e;
   }
-  // the previous batch may still be using the workspace (async call)
+  // the previous batch may still be using the workspace (async call, maybe on
+  // another stream)
   HJ_HIP(hipStreamWaitEvent(st, ctx->batch_done, 0));
   HJ_HIP(ctx->clean.ensure((size_t)max_end + 512));
   HJ_HIP(ctx->segs.ensure((size_t)L.total_segs * 4 + 64));
@@ -476,11 +636,11 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
     HJ_HIP(ctx->wts.ensure((size_t)L.total_wts * 4 + 256));
     HJ_HIP(ctx->rplanes.ensure((size_t)L.total_rp + 256));
   }
-  HJ_HIP(ctx->pin_desc.ensure(sizeof(ImageDesc) * n));
-  HJ_HIP(ctx->pin_status.ensure(sizeof(int32_t) * n));
-  HJ_HIP(hipEventSynchronize(ctx->staging_free));
-  memcpy(ctx->pin_desc.p, L.desc.data(), sizeof(ImageDesc) * n);
-  HJ_HIP(hipMemcpyAsync(ctx->desc.p, ctx->pin_desc.p, sizeof(ImageDesc) * n,
+  HJ_HIP(slot.pin_desc.ensure(sizeof(ImageDesc) * n));
+  HJ_HIP(slot.pin_status.ensure(sizeof(int32_t) * n));
+  slot.n = n;
+  memcpy(slot.pin_desc.p, L.desc.data(), sizeof(ImageDesc) * n);
+  HJ_HIP(hipMemcpyAsync(ctx->desc.p, slot.pin_desc.p, sizeof(ImageDesc) * n,
                         hipMemcpyHostToDevice, st));
   HJ_HIP(hipMemsetAsync(ctx->coefs.p, 0, (size_t)L.total_blocks * 128, st));
   mark(ctx, 1, st);
@@ -535,13 +695,15 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
   }
   mark(ctx, 7, st);
   // per-image status: strided D2H of ImageInfo::status
-  HJ_HIP(hipMemcpy2DAsync(ctx->pin_status.p, sizeof(int32_t), ctx->info.p, sizeof(ImageInfo),
+  HJ_HIP(hipMemcpy2DAsync(slot.pin_status.p, sizeof(int32_t), ctx->info.p, sizeof(ImageInfo),
                           sizeof(int32_t), n, hipMemcpyDeviceToHost, st));
   mark(ctx, 8, st);
   HJ_HIP(hipEventRecord(ctx->batch_done, st));
-  HJ_HIP(hipEventRecord(ctx->staging_free, st));
+  HJ_HIP(hipEventRecord(slot.done, st));
+  slot.pending = true;
+  ctx->last_ticket = slot.ticket;
   if (!sync) return SPDL_HJ_OK;
-  HJ_HIP(hipStreamSynchronize(st));
+  HJ_HIP(hipEventSynchronize(slot.done));
   if (ctx->profiling) {
     ctx->ntimings = kStages;
     for (int i = 0; i < kStages; i++) {
@@ -550,24 +712,62 @@ int run_pipeline(spdl_hj_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, con
       ctx->timings[i] = ms * 1000.f;
     }
   }
-  const int32_t* stv = static_cast<const int32_t*>(ctx->pin_status.p);
-  int first_bad = -1;
-  for (int i = 0; i < n; i++) {
-    if (status) status[i] = stv[i];
-    if (stv[i] != SPDL_HJ_OK && first_bad < 0) first_bad = i;
-  }
-  if (first_bad >= 0) {
-    set_err(err, errlen, "Failed to decode an image. (image %d: %s)", first_bad,
-            status_str(stv[first_bad]));
-    return stv[first_bad];
-  }
+  return collect_status(slot, status, err, errlen);
+}
+
+// H2D of the slot's staged bytes on the copy stream; `st` waits for it.
+int stage_h2d(spdl_hj_ctx* ctx, Slot& s, size_t total, hipStream_t st, char* err, size_t errlen) {
+  HJ_HIP(s.bytes.ensure(total + 512));
+  mark(ctx, 0, ctx->copy);
+  HJ_HIP(hipMemcpyAsync(s.bytes.p, s.pin_in.p, total, hipMemcpyHostToDevice, ctx->copy));
+  HJ_HIP(hipEventRecord(s.h2d_done, ctx->copy));
+  HJ_HIP(hipStreamWaitEvent(st, s.h2d_done, 0));
   return SPDL_HJ_OK;
 }
 
 bool valid_output(const spdl_hj_output* o) {
-  return o && o->pix_fmt >= 0 && o->pix_fmt <= 3 && (o->dtype == 0 || o->dtype == 1) &&
+  return o && o->pix_fmt >= 0 && o->pix_fmt <= 3 && (o->dtype >= 0 && o->dtype <= 2) &&
          (o->idct == 0 || o->idct == 1) && (o->filter == 0 || o->filter == 1) &&
          o->aspect >= 0 && o->aspect <= 2;
+}
+
+// ---- tar (ustar / GNU 'L' long names / pax 'x' path) ------------------------
+// Same member walk as the reference's InMemoryTarParserImpl::parse_next
+// (src/spdl/io/lib/archive/tar_iterator.cpp:125-195): a header that fails the
+// magic/checksum test is skipped 512 bytes at a time; an empty name ends the
+// archive; 'L' and 'x' records name the next regular file; other types are
+// skipped with their payload; a member running past the buffer ends the walk.
+uint64_t tar_octal(const uint8_t* s, size_t n) {
+  uint64_t r = 0;
+  for (size_t i = 0; i < n && s[i] != 0 && s[i] != ' '; i++)
+    if (s[i] >= '0' && s[i] <= '7') r = r * 8 + (s[i] - '0');
+  return r;
+}
+
+bool tar_header_ok(const uint8_t* h) {
+  if (memcmp(h + 257, "ustar", 5) != 0) return false;
+  uint32_t sum = 0;
+  for (int i = 0; i < 512; i++) sum += (i >= 148 && i < 156) ? (uint32_t)' ' : h[i];
+  return tar_octal(h + 148, 8) == sum;
+}
+
+std::string tar_pax_path(const uint8_t* d, size_t n) {
+  // records "<len> key=value\n"
+  size_t pos = 0;
+  while (pos < n) {
+    const void* sp = memchr(d + pos, ' ', n - pos);
+    if (!sp) break;
+    const size_t rs = (size_t)(static_cast<const uint8_t*>(sp) - d) + 1;
+    if (rs + 5 <= n && memcmp(d + rs, "path=", 5) == 0) {
+      const void* nl = memchr(d + rs + 5, '\n', n - rs - 5);
+      if (nl) return std::string((const char*)d + rs + 5,
+                                 (size_t)(static_cast<const uint8_t*>(nl) - (d + rs + 5)));
+    }
+    const void* nl = memchr(d + pos, '\n', n - pos);
+    if (!nl) break;
+    pos = (size_t)(static_cast<const uint8_t*>(nl) - d) + 1;
+  }
+  return std::string();
 }
 
 }  // namespace
@@ -606,31 +806,44 @@ spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen) {
   DeviceGuard g(device);
   auto* c = new spdl_hj_ctx();
   c->device = device;
-  bool ok = hipEventCreateWithFlags(&c->staging_free, hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&c->batch_done, hipEventDisableTiming) == hipSuccess;
+  bool ok = hipEventCreateWithFlags(&c->batch_done, hipEventDisableTiming) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; ok && i < kSlots; i++)
+    ok = hipEventCreateWithFlags(&c->slots[i].h2d_done, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->slots[i].done, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; ok && i <= kStages; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
   if (!ok) {
-    set_err(err, errlen, "hipEventCreate failed");
+    set_err(err, errlen, "hipEventCreate / hipStreamCreate failed");
     spdl_hj_destroy(c);
     return nullptr;
   }
+  c->pool = new CopyPool(3);
   return c;
 }
 
 void spdl_hj_destroy(spdl_hj_ctx* c) {
   if (!c) return;
   DeviceGuard g(c->device);
+  for (Slot& s : c->slots)
+    if (s.ticket && s.done) (void)hipEventSynchronize(s.done);
   if (c->batch_done) (void)hipEventSynchronize(c->batch_done);
-  DevBuf* bufs[] = {&c->bytes, &c->clean, &c->segs, &c->desc, &c->info,
-                    &c->luts,  &c->coefs, &c->planes, &c->wts, &c->recs, &c->rplanes, &c->dschunks};
+  if (c->copy) (void)hipStreamSynchronize(c->copy);
+  DevBuf* bufs[] = {&c->clean, &c->segs, &c->desc, &c->info, &c->luts, &c->coefs,
+                    &c->planes, &c->wts, &c->recs, &c->rplanes, &c->dschunks};
   for (DevBuf* b : bufs) b->release();
-  c->pin_in.release();
-  c->pin_desc.release();
-  c->pin_status.release();
-  if (c->staging_free) (void)hipEventDestroy(c->staging_free);
+  for (Slot& s : c->slots) {
+    s.bytes.release();
+    s.pin_in.release();
+    s.pin_desc.release();
+    s.pin_status.release();
+    if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
   if (c->batch_done) (void)hipEventDestroy(c->batch_done);
+  if (c->copy) (void)hipStreamDestroy(c->copy);
   for (int i = 0; i <= kStages; i++)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  delete c->pool;
   delete c;
 }
 
@@ -645,6 +858,7 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
   hipStream_t st = static_cast<hipStream_t>(stream);
   std::vector<spdl_hj_image_info> infos(n);
   std::vector<int64_t> offs(n), szs(n);
+  std::vector<CopyItem> items(n);
   int64_t total = 0;
   for (int i = 0; i < n; i++) {
     int rc = probe(data[i], sizes[i], &infos[i]);
@@ -655,24 +869,22 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
     }
     offs[i] = total;
     szs[i] = (int64_t)sizes[i];
-    total += round_up((int64_t)sizes[i] + 64, 256);
+    const int64_t padded = round_up((int64_t)sizes[i] + 64, 256);
+    items[i] = {total, data[i], (int64_t)sizes[i], padded};
+    total += padded;
   }
   Layout L;
   int rc = build_layout(offs.data(), szs.data(), infos.data(), n, out, ctx->sub_bits, L, status, err,
                         errlen);
   if (rc) return rc;
-  HJ_HIP(ctx->pin_in.ensure((size_t)total));
-  HJ_HIP(ctx->bytes.ensure((size_t)total));
-  HJ_HIP(hipStreamWaitEvent(st, ctx->batch_done, 0));
-  HJ_HIP(hipEventSynchronize(ctx->staging_free));
-  auto* pin = static_cast<uint8_t*>(ctx->pin_in.p);
-  for (int i = 0; i < n; i++) {
-    memcpy(pin + offs[i], data[i], sizes[i]);
-    memset(pin + offs[i] + sizes[i], 0, (size_t)(round_up((int64_t)sizes[i] + 64, 256) - (int64_t)sizes[i]));
-  }
-  mark(ctx, 0, st);
-  HJ_HIP(hipMemcpyAsync(ctx->bytes.p, pin, (size_t)total, hipMemcpyHostToDevice, st));
-  return run_pipeline(ctx, static_cast<const uint8_t*>(ctx->bytes.p), (size_t)total, L, n, out,
+  Slot* s = nullptr;
+  rc = acquire_slot(ctx, &s, err, errlen);
+  if (rc) return rc;
+  HJ_HIP(s->pin_in.ensure((size_t)total));
+  parallel_pack(ctx->pool, static_cast<uint8_t*>(s->pin_in.p), items);
+  rc = stage_h2d(ctx, *s, (size_t)total, st, err, errlen);
+  if (rc) return rc;
+  return run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), (size_t)total, L, n, out,
                       out_dev, out_bytes, st, sync, status, err, errlen, false);
 }
 
@@ -692,9 +904,223 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
   Layout L;
   int rc = build_layout(offsets, sizes, infos, n, out, ctx->sub_bits, L, status, err, errlen);
   if (rc) return rc;
+  Slot* s = nullptr;
+  rc = acquire_slot(ctx, &s, err, errlen);
+  if (rc) return rc;
   mark(ctx, 0, st);
-  return run_pipeline(ctx, dev_data, dev_bytes, L, n, out, out_dev, out_bytes, st, sync, status,
-                      err, errlen, false);
+  return run_pipeline(ctx, *s, dev_data, dev_bytes, L, n, out, out_dev, out_bytes, st, sync,
+                      status, err, errlen, false);
+}
+
+int64_t spdl_hj_last_ticket(spdl_hj_ctx* ctx) { return ctx ? ctx->last_ticket : 0; }
+
+int spdl_hj_wait(spdl_hj_ctx* ctx, int64_t ticket, int32_t* status, int32_t n, char* err,
+                 size_t errlen) {
+  if (!ctx) return SPDL_HJ_ERR_INVALID_ARG;
+  Slot* s = find_slot(ctx, ticket);
+  if (!s || !s->pending) {
+    set_err(err, errlen, "unknown, already waited or overwritten ticket %lld", (long long)ticket);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  if (status && n < s->n) {
+    set_err(err, errlen, "status array too small (%d < %d)", n, s->n);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(ctx->device);
+  HJ_HIP(hipEventSynchronize(s->done));
+  return collect_status(*s, status, err, errlen);
+}
+
+int spdl_hj_staging_acquire(spdl_hj_ctx* ctx, size_t bytes, uint8_t** host_ptr, int64_t* ticket,
+                            char* err, size_t errlen) {
+  if (!ctx || !host_ptr || !ticket) {
+    set_err(err, errlen, "invalid argument");
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(ctx->device);
+  Slot* s = nullptr;
+  int rc = acquire_slot(ctx, &s, err, errlen);
+  if (rc) return rc;
+  HJ_HIP(s->pin_in.ensure(bytes + 512));
+  s->staged = true;
+  *host_ptr = static_cast<uint8_t*>(s->pin_in.p);
+  *ticket = s->ticket;
+  return SPDL_HJ_OK;
+}
+
+int spdl_hj_staging_fill(spdl_hj_ctx* ctx, int64_t ticket, size_t dst_off, const uint8_t* src,
+                         size_t len, char* err, size_t errlen) {
+  Slot* s = ctx ? find_slot(ctx, ticket) : nullptr;
+  if (!s || !s->staged || !src || dst_off + len > s->pin_in.cap) {
+    set_err(err, errlen, "invalid staging fill (ticket %lld)", (long long)ticket);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  std::vector<CopyItem> items(1, CopyItem{(int64_t)dst_off, src, (int64_t)len, (int64_t)len});
+  parallel_pack(ctx->pool, static_cast<uint8_t*>(s->pin_in.p), items);
+  return SPDL_HJ_OK;
+}
+
+int spdl_hj_staging_read(spdl_hj_ctx* ctx, int64_t ticket, size_t dst_off, int fd,
+                         int64_t file_off, size_t len, char* err, size_t errlen) {
+  Slot* s = ctx ? find_slot(ctx, ticket) : nullptr;
+  if (!s || !s->staged || fd < 0 || file_off < 0 || dst_off + len > s->pin_in.cap) {
+    set_err(err, errlen, "invalid staging read (ticket %lld)", (long long)ticket);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  uint8_t* base = static_cast<uint8_t*>(s->pin_in.p) + dst_off;
+  std::atomic<int> bad{0};
+  auto body = [&](int part, int np) {
+    // 64 KiB-aligned split so the page-cache copies stay sequential per thread
+    const size_t unit = 1 << 16, nu = (len + unit - 1) / unit;
+    size_t lo = nu * part / np * unit, hi = nu * (part + 1) / np * unit;
+    if (hi > len) hi = len;
+    while (lo < hi) {
+      const ssize_t r = pread(fd, base + lo, hi - lo, (off_t)(file_off + (int64_t)lo));
+      if (r <= 0) {
+        bad = 1;
+        return;
+      }
+      lo += (size_t)r;
+    }
+  };
+  if (len < (4u << 20)) body(0, 1);
+  else ctx->pool->run(body);
+  if (bad) {
+    set_err(err, errlen, "pread failed or hit end of file (offset %lld, %zu bytes)",
+            (long long)file_off, len);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  return SPDL_HJ_OK;
+}
+
+int spdl_hj_decode_staged(spdl_hj_ctx* ctx, int64_t ticket, size_t len, const int64_t* offsets,
+                          const int64_t* sizes, int32_t n, const spdl_hj_output* out,
+                          void* out_dev, size_t out_bytes, void* stream, int32_t sync,
+                          int32_t* status, char* err, size_t errlen) {
+  Slot* s = ctx ? find_slot(ctx, ticket) : nullptr;
+  if (!s || !s->staged) {
+    set_err(err, errlen, "ticket %lld does not name an acquired staging slot", (long long)ticket);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  s->staged = false;  // the slot is consumed whatever happens below
+  if (!offsets || !sizes || n <= 0 || !valid_output(out) || !out_dev || len + 512 > s->pin_in.cap) {
+    set_err(err, errlen, n <= 0 ? "the batch is empty" : "invalid argument");
+    s->ticket = 0;
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(ctx->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint8_t* host = static_cast<const uint8_t*>(s->pin_in.p);
+  std::vector<spdl_hj_image_info> infos(n);
+  for (int i = 0; i < n; i++) {
+    int rc = SPDL_HJ_ERR_INVALID_ARG;
+    if (offsets[i] >= 0 && sizes[i] >= 0 && (size_t)(offsets[i] + sizes[i]) <= len)
+      rc = probe(host + offsets[i], (size_t)sizes[i], &infos[i]);
+    if (status) status[i] = rc;
+    if (rc) {
+      set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, status_str(rc));
+      s->ticket = 0;
+      return rc;
+    }
+  }
+  Layout L;
+  int rc = build_layout(offsets, sizes, infos.data(), n, out, ctx->sub_bits, L, status, err, errlen);
+  if (rc) {
+    s->ticket = 0;
+    return rc;
+  }
+  memset(static_cast<uint8_t*>(s->pin_in.p) + len, 0, 512);  // tail read slack
+  rc = stage_h2d(ctx, *s, len + 512, st, err, errlen);
+  if (rc) return rc;
+  return run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), len + 512, L, n, out,
+                      out_dev, out_bytes, st, sync, status, err, errlen, false);
+}
+
+int spdl_hj_tar_index(const uint8_t* data, size_t size, size_t start, int32_t max_entries,
+                      int64_t* offsets, int64_t* sizes, int64_t* name_offs, char* names,
+                      size_t names_cap, int32_t* n_out, size_t* next_pos) {
+  if (!data || !offsets || !sizes || !n_out || !next_pos || max_entries < 0)
+    return SPDL_HJ_ERR_INVALID_ARG;
+  size_t pos = start, used = 0;
+  int32_t n = 0;
+  std::string pending;
+  bool at_end = false;
+  while (n < max_entries) {
+    const size_t entry_pos = pos;  // resume point if this entry does not fit
+    std::string path;
+    bool found = false;
+    pending.clear();
+    while (pos + 512 <= size) {
+      const uint8_t* h = data + pos;
+      if (!tar_header_ok(h)) {
+        pos += 512;
+        continue;
+      }
+      std::string fp;
+      if (h[0]) {
+        if (h[345]) {
+          fp.assign((const char*)h + 345, strnlen((const char*)h + 345, 155));
+          if (fp.back() != '/') fp += '/';
+        }
+        fp.append((const char*)h, strnlen((const char*)h, 100));
+      }
+      if (fp.empty() && pending.empty()) {
+        at_end = true;
+        break;
+      }
+      const uint64_t fsz = tar_octal(h + 124, 12);
+      const uint64_t padded = (fsz + 511) & ~511ull;
+      const char type = (char)h[156];
+      if (type == 'L' || type == 'x') {
+        pos += 512;
+        if (pos + fsz > size) {
+          at_end = true;
+          break;
+        }
+        if (type == 'L') {
+          pending.assign((const char*)data + pos, (size_t)fsz);
+          if (!pending.empty() && pending.back() == '\0') pending.pop_back();
+        } else {
+          pending = tar_pax_path(data + pos, (size_t)fsz);
+        }
+        pos += padded;
+        continue;
+      }
+      if (type == '0' || type == '\0') {
+        pos += 512;
+        if (!pending.empty()) fp = pending;
+        if (pos + fsz > size) {
+          at_end = true;
+          break;
+        }
+        path = fp;
+        offsets[n] = (int64_t)pos;
+        sizes[n] = (int64_t)fsz;
+        pos += padded;
+        found = true;
+        break;
+      }
+      pending.clear();
+      pos += 512 + padded;
+    }
+    if (!found) {
+      if (!at_end) pos = size;
+      break;
+    }
+    if (names && name_offs) {
+      if (used + path.size() + 1 > names_cap) {
+        pos = entry_pos;  // retry this entry with a fresh names buffer
+        break;
+      }
+      memcpy(names + used, path.c_str(), path.size() + 1);
+      name_offs[n] = (int64_t)used;
+      used += path.size() + 1;
+    }
+    n++;
+  }
+  *n_out = n;
+  *next_pos = at_end ? size : pos;
+  return SPDL_HJ_OK;
 }
 
 int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, int32_t idct,
@@ -717,14 +1143,15 @@ int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   Layout L;
   rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen);
   if (rc) return rc;
-  HJ_HIP(ctx->pin_in.ensure((size_t)total));
-  HJ_HIP(ctx->bytes.ensure((size_t)total));
-  HJ_HIP(hipStreamWaitEvent(st, ctx->batch_done, 0));
-  HJ_HIP(hipEventSynchronize(ctx->staging_free));
-  memcpy(ctx->pin_in.p, data, size);
-  memset(static_cast<uint8_t*>(ctx->pin_in.p) + size, 0, (size_t)(total - sz));
-  HJ_HIP(hipMemcpyAsync(ctx->bytes.p, ctx->pin_in.p, (size_t)total, hipMemcpyHostToDevice, st));
-  rc = run_pipeline(ctx, static_cast<const uint8_t*>(ctx->bytes.p), (size_t)total, L, 1, &o,
+  Slot* s = nullptr;
+  rc = acquire_slot(ctx, &s, err, errlen);
+  if (rc) return rc;
+  HJ_HIP(s->pin_in.ensure((size_t)total));
+  memcpy(s->pin_in.p, data, size);
+  memset(static_cast<uint8_t*>(s->pin_in.p) + size, 0, (size_t)(total - sz));
+  rc = stage_h2d(ctx, *s, (size_t)total, st, err, errlen);
+  if (rc) return rc;
+  rc = run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), (size_t)total, L, 1, &o,
                     nullptr, 0, st, 1, nullptr, err, errlen, true);
   if (rc) return rc;
   const ImageDesc& d = L.desc[0];
@@ -765,13 +1192,15 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   Layout L;
   rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen);
   if (rc) return rc;
-  HJ_HIP(ctx->pin_in.ensure((size_t)total));
-  HJ_HIP(ctx->bytes.ensure((size_t)total));
-  HJ_HIP(hipEventSynchronize(ctx->batch_done));
-  memcpy(ctx->pin_in.p, data, size);
-  memset(static_cast<uint8_t*>(ctx->pin_in.p) + size, 0, (size_t)(total - sz));
-  HJ_HIP(hipMemcpyAsync(ctx->bytes.p, ctx->pin_in.p, (size_t)total, hipMemcpyHostToDevice, st));
-  (void)run_pipeline(ctx, static_cast<const uint8_t*>(ctx->bytes.p), (size_t)total, L, 1, &o,
+  Slot* s = nullptr;
+  rc = acquire_slot(ctx, &s, err, errlen);
+  if (rc) return rc;
+  HJ_HIP(s->pin_in.ensure((size_t)total));
+  memcpy(s->pin_in.p, data, size);
+  memset(static_cast<uint8_t*>(s->pin_in.p) + size, 0, (size_t)(total - sz));
+  rc = stage_h2d(ctx, *s, (size_t)total, st, err, errlen);
+  if (rc) return rc;
+  (void)run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), (size_t)total, L, 1, &o,
                      nullptr, 0, st, 1, nullptr, err, errlen, true);
   ImageInfo hi;
   HJ_HIP(hipMemcpy(&hi, ctx->info.p, sizeof(ImageInfo), hipMemcpyDeviceToHost));

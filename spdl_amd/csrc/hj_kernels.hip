@@ -1217,6 +1217,17 @@ __device__ __forceinline__ void ycc_rgb(int y, int cb, int cr, int* rgb) {
   rgb[2] = clip_u8(y + cb_b);
 }
 
+// fp32 -> 16-bit output: dtype 1 = IEEE half (RNE), 2 = bfloat16 (RNE, as
+// torch's Tensor.to(torch.bfloat16) after the reference's fp32 normalisation,
+// examples/imagenet_classification.py:95-106,162-163).
+__device__ __forceinline__ uint16_t to_f16_bits(float f, int dtype) {
+  if (dtype == 1) return __half_as_ushort(__float2half_rn(f));
+  uint32_t x = __float_as_uint(f);
+  if ((x & 0x7FFFFFFFu) > 0x7F800000u) return (uint16_t)((x >> 16) | 0x40u);
+  x += 0x7FFFu + ((x >> 16) & 1u);
+  return (uint16_t)(x >> 16);
+}
+
 __device__ __forceinline__ void store_rgb(void* out, int64_t base, int fmt, int dtype, int ow,
                                           int oh, int x, int y, const int* rgb,
                                           const BatchParams& p) {
@@ -1233,7 +1244,7 @@ __device__ __forceinline__ void store_rgb(void* out, int64_t base, int fmt, int 
       float f = __fdiv_rn((float)v, 255.0f);
       f = __fsub_rn(f, p.mean[ch]);
       f = __fdiv_rn(f, p.std[ch]);
-      static_cast<__half*>(out)[oi] = __float2half_rn(f);
+      static_cast<uint16_t*>(out)[oi] = to_f16_bits(f, dtype);
     }
   }
 }
@@ -1639,7 +1650,7 @@ __global__ void __launch_bounds__(256) csc_store_kernel(const uint8_t* __restric
       }
     }
   } else {
-    __half* ob = static_cast<__half*>(out) + dd.out_off;
+    uint16_t* ob = static_cast<uint16_t*>(out) + dd.out_off;
     for (int k = 0; k < np; k++)
 #pragma unroll
       for (int ch = 0; ch < 3; ch++) {
@@ -1647,7 +1658,7 @@ __global__ void __launch_bounds__(256) csc_store_kernel(const uint8_t* __restric
         fv = __fsub_rn(fv, p.mean[ch]);
         fv = __fdiv_rn(fv, p.std[ch]);
         const int64_t oi = planar ? ch * pl + (int64_t)y * ow + x0 + k : ((int64_t)y * ow + x0 + k) * 3 + ch;
-        ob[oi] = __float2half_rn(fv);
+        ob[oi] = to_f16_bits(fv, p.dtype);
       }
   }
 }

@@ -11,6 +11,7 @@ from ._image import (
     load_image_batch_nvjpeg,
 )
 from ._preprocessing import get_video_filter_desc, parse_image_filter
+from ._tar import TarImageStream, iter_tarfile
 
 # HIP-named aliases: same functions, named for the hardware they run on.
 decode_image_hip = decode_image_nvjpeg
@@ -24,6 +25,8 @@ __all__ = [
     "decode_image_hip",
     "decode_image_nvjpeg",
     "get_video_filter_desc",
+    "iter_tarfile",
+    "TarImageStream",
     "load_image",
     "load_image_batch",
     "load_image_batch_hip",

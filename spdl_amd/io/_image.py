@@ -45,7 +45,7 @@ def _stream(cfg: CUDAConfig) -> int:
 
 
 def _alloc_out(cfg: CUDAConfig, shape, dtype) -> CUDABuffer:
-    nbytes = int(np.prod(shape)) * (2 if dtype == torch.float16 else 1)
+    nbytes = int(np.prod(shape)) * (1 if dtype == torch.uint8 else 2)
     if cfg.allocator is None:
         t = torch.empty(shape, dtype=dtype, device=f"cuda:{cfg.device_index}")
         return CUDABuffer(t, stream=cfg.stream)
@@ -63,7 +63,7 @@ def _decode(datas: list, out: Output, cfg: CUDAConfig, shape_per_image, batched:
     shape = (n, *shape_per_image) if batched else tuple(shape_per_image)
     buf = _alloc_out(cfg, shape, dtype)
     dec = _lib.thread_decoder(cfg.device_index)
-    nbytes = int(np.prod(shape)) * (2 if dtype == torch.float16 else 1)
+    nbytes = int(np.prod(shape)) * (1 if dtype == torch.uint8 else 2)
     dec.decode_batch(datas, out, buf.data_ptr(), nbytes, stream=_stream(cfg), sync=True)
     return buf
 
@@ -146,6 +146,7 @@ def load_image_batch(
     normalize: bool = False,
     mean=(0.485, 0.456, 0.406),
     std=(0.229, 0.224, 0.225),
+    norm_dtype: str = "float16",
     **kwargs,
 ):
     """Batch load images into one ``[B,H,W,3]`` buffer with the FFmpeg filter
@@ -154,7 +155,8 @@ def load_image_batch(
     Decoding runs on ``device_config``'s GPU (device 0 when absent); without a
     ``device_config`` the result is copied back to a host ``CPUBuffer``, like
     the reference's return type.  ``normalize=True`` fuses the ImageNet
-    epilogue ((x/255 - mean)/std -> fp16), an extension for config 4."""
+    epilogue ((x/255 - mean)/std in fp32 -> ``norm_dtype`` float16 or
+    bfloat16), an extension for config 4."""
     if not srcs:
         raise ValueError("`srcs` must not be empty.")
     for k in ("demux_config", "decode_config", "storage"):
@@ -168,7 +170,7 @@ def load_image_batch(
     out = parse_image_filter(filter_desc, default_pix_fmt=pix_fmt or "rgb24")
     if normalize:
         out = Output(**{**out.__dict__, "normalize": True, "mean": tuple(mean),
-                        "std": tuple(std)})
+                        "std": tuple(std), "norm_dtype": norm_dtype})
     cfg = device_config or CUDAConfig(0)
     datas, keep = [], []
     for i, s in enumerate(srcs):
@@ -186,7 +188,7 @@ def load_image_batch(
         raise RuntimeError("Failed to load all the images.")
     info = _lib.get_image_info(datas[0])
     ow, oh = _lib.output_size(info.width, info.height, out)
-    dtype = torch.float16 if out.normalize else torch.uint8
+    dtype = out.torch_dtype
     shape = _shape(out, ow, oh)
     try:
         buf = _decode(datas, out, cfg, shape, True, dtype=dtype)

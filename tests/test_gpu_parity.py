@@ -92,6 +92,31 @@ def test_normalize_fp16_bit_exact(decoder, oracle, pix_fmt):
     np.testing.assert_array_equal(hyp.view(np.uint16), ref.view(np.uint16), strict=True)
 
 
+@pytest.mark.parametrize("norm_dtype", ["float16", "bfloat16"])
+def test_normalize_matches_torch_preprocessing(decoder, oracle, norm_dtype):
+    """Config 4 epilogue vs the reference's own torch ops on our u8 output:
+    x.float()/255, (x - mean)/std in fp32, then .to(dtype) (reference
+    examples/imagenet_classification.py:95-106,162-163, NCHW via permute at
+    :265).  Tolerance 0: the fused kernel does the same IEEE fp32 ops."""
+    datas = [cases.case(n) for n in ("q90_420", "odd_227x333", "gray")]
+    kw = dict(fit_w=256, fit_h=256, aspect="decrease", pad_w=256, pad_h=256, crop_w=224,
+              crop_h=224)
+    u8 = _decode(decoder, datas, Output(pix_fmt="rgb24", resize=True, **kw), (224, 224, 3))
+    tdt = torch.bfloat16 if norm_dtype == "bfloat16" else torch.float16
+    out = Output(pix_fmt="rgb", resize=True, normalize=True, norm_dtype=norm_dtype, **kw)
+    hyp = _decode(decoder, datas, out, (3, 224, 224), dtype=tdt)
+    mean = torch.tensor([0.4850, 0.4560, 0.4060]).view(1, 3, 1, 1)
+    std = torch.tensor([0.2290, 0.2240, 0.2250]).view(1, 3, 1, 1)
+    x = u8.permute(0, 3, 1, 2).float() / 255.0
+    ref = ((x - mean) / std).to(tdt)
+    assert torch.equal(hyp.view(torch.int16), ref.view(torch.int16))
+    if norm_dtype == "bfloat16":
+        for i, d in enumerate(datas):
+            o = oracle.decode_resize(d, oracle.Resize(**kw), pix_fmt="rgb", normalize=True,
+                                     norm_dtype="bfloat16")
+            np.testing.assert_array_equal(hyp[i].view(torch.int16).numpy().view(np.uint16), o)
+
+
 def test_batch_mixed_sizes_resize(decoder, oracle):
     names = ["q90_420", "odd_227x333", "gray", "restart_blocks", "q90_444", "noise_420",
              "large_1080p", "optimized"]

@@ -191,3 +191,25 @@ def test_oracle_errors(oracle):
         oracle.decode_rgb(cases.truncated())
     with pytest.raises(oracle.OracleError):
         oracle.decode_rgb(b"\x00" * 100)
+
+
+def test_bf16_rounding_matches_torch(oracle):
+    """jo_f32_to_bf16 == torch's fp32 -> bfloat16 cast (RNE) on the values the
+    normalisation produces and on rounding ties / specials."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    L = oracle.lib()
+    L.jo_f32_to_bf16.argtypes = [ctypes.c_float]
+    L.jo_f32_to_bf16.restype = ctypes.c_uint16
+    mean = np.array([0.485, 0.456, 0.406], np.float32)
+    std = np.array([0.229, 0.224, 0.225], np.float32)
+    v = (np.arange(256, dtype=np.float32)[:, None] / np.float32(255.0) - mean) / std
+    vals = np.concatenate([v.reshape(-1), np.array(
+        [0.0, -0.0, 1.0 + 2 ** -8, 1.0 + 3 * 2 ** -8, 3.0e38, -3.4e38, 1e-40, np.inf, -np.inf],
+        np.float32)])
+    hyp = np.array([L.jo_f32_to_bf16(float(x)) for x in vals], np.uint16)
+    ref = torch.from_numpy(vals).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+    np.testing.assert_array_equal(hyp, ref)
