@@ -97,6 +97,8 @@ def _args():
     p.add_argument("--entropy-threads", type=int, default=0)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="pad224")
     p.add_argument("--norm-dtype", choices=["float16", "bfloat16"], default="float16")
+    p.add_argument("--sync-steps", action="store_true",
+                   help="one synchronous call per step (no overlap of host work)")
     p.add_argument("--with-copies", action="store_true",
                    help="also time the host-bytes path (pinned H2D + D2H of the output)")
     return p.parse_args()
@@ -171,23 +173,44 @@ def main():
     stream = torch.cuda.current_stream(device)
     nbytes_out = out.numel() * out.element_size()
 
-    def step():
+    def submit(sync: bool) -> int:
         dec.decode_batch_device(dev.data_ptr(), dev.numel(), offs, sizes, infos, spec,
-                                out.data_ptr(), nbytes_out, stream=stream, sync=True)
+                                out.data_ptr(), nbytes_out, stream=stream, sync=sync)
+        return dec.last_ticket()
 
+    # Steps are submitted asynchronously through the decoder's ring (at most
+    # two batches in flight): batch k+1's host-side layout and launches
+    # overlap batch k's kernels, as in a data loader.  Each batch is waited
+    # for (statuses checked) and its per-stage HIP-event timings collected.
     for _ in range(a.warmup):
-        step()
+        submit(True)
     dec.set_profiling(True)
     stages = {}
+
+    def collect(ticket: int):
+        st = dec.wait(ticket, a.batch)
+        assert not any(st), st
+        for k, v in dec.last_timings().items():
+            stages[k] = stages.get(k, 0.0) + v
+
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
+    prev = None
     for _ in range(a.steps):
-        step()
-        for k, v in dec.last_timings().items():
-            stages[k] = stages.get(k, 0.0) + v
+        if a.sync_steps:
+            submit(True)
+            for k, v in dec.last_timings().items():
+                stages[k] = stages.get(k, 0.0) + v
+            continue
+        t = submit(False)
+        if prev is not None:
+            collect(prev)
+        prev = t
+    if prev is not None:
+        collect(prev)
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
@@ -216,7 +239,7 @@ def main():
         t1 = time.perf_counter()
         nrep = max(5, a.steps // 4)
         for _ in range(nrep):
-            dec.decode_batch(datas, spec, out.data_ptr(), nbytes_out, stream=stream)
+            dec.decode_batch(datas, spec, out.data_ptr(), nbytes_out, stream=stream, sync=True)
             host_out.copy_(out, non_blocking=True)
             torch.cuda.synchronize(device)
         copies = a.batch * nrep / (time.perf_counter() - t1)

@@ -5,7 +5,7 @@ Workload: a tar archive of synthetic 480x640 q90 4:2:0 JPEGs (the
 per rank, in the page cache.  Each pass streams the whole archive through
 ``spdl_amd.io.TarImageStream``:
 
-  pread (3+1 host threads) -> pinned ring slot -> ONE hipMemcpyAsync per batch
+  pread (7+1 host threads) -> pinned ring slot -> ONE hipMemcpyAsync per batch
   on the decoder's copy stream -> decode kernels (RGB 224x224 u8, pad mode)
 
 with batch k+1's read and copy overlapping batch k's kernels.  ``--d2h`` also
@@ -101,7 +101,8 @@ def main():
                     j = k & 1
                     if d2h_ev[j] is not None:
                         d2h_ev[j].synchronize()  # host buffer j is free again
-                    d2h.wait_stream(torch.cuda.current_stream(device))
+                    # t is complete (the stream waited for its ticket); only
+                    # the allocator must not recycle it before the copy ends
                     with torch.cuda.stream(d2h):
                         host[j][: t.shape[0]].copy_(t, non_blocking=True)
                         t.record_stream(d2h)

@@ -505,7 +505,9 @@ struct Slot {
   int64_t ticket = 0;             // ticket of the batch occupying the slot (0 = none)
   bool pending = false;           // submitted, not yet waited
   bool staged = false;            // acquired by spdl_hj_staging_acquire, not submitted
+  bool profiled = false;          // ev[] were recorded for this batch
   int n = 0;
+  hipEvent_t ev[kStages + 1] = {};  // stage boundaries (profiling only)
 };
 
 struct spdl_hj_ctx {
@@ -516,7 +518,6 @@ struct spdl_hj_ctx {
   int64_t last_ticket = 0;
   hipStream_t copy = nullptr;         // H2D stream of the staging ring
   hipEvent_t batch_done = nullptr;    // device workspace free after this
-  hipEvent_t ev[kStages + 1] = {};
   CopyPool* pool = nullptr;
   bool profiling = false;
   float timings[kStages] = {};
@@ -550,8 +551,8 @@ struct DeviceGuard {
     }                                                                                    \
   } while (0)
 
-inline void mark(spdl_hj_ctx* c, int i, hipStream_t st) {
-  if (c->profiling) (void)hipEventRecord(c->ev[i], st);
+inline void mark(spdl_hj_ctx* c, Slot& s, int i, hipStream_t st) {
+  if (c->profiling) (void)hipEventRecord(s.ev[i], st);
 }
 
 // Take the next ring slot: its previous batch (if any) must have finished
@@ -577,8 +578,18 @@ Slot* find_slot(spdl_hj_ctx* ctx, int64_t ticket) {
   return s.ticket == ticket ? &s : nullptr;
 }
 
-// Per-image statuses of a finished slot -> status[], first error -> err.
-int collect_status(Slot& s, int32_t* status, char* err, size_t errlen) {
+// Per-image statuses of a finished slot -> status[], first error -> err;
+// its stage timings -> ctx->timings when it was profiled.
+int collect_status(spdl_hj_ctx* ctx, Slot& s, int32_t* status, char* err, size_t errlen) {
+  if (s.profiled) {
+    ctx->ntimings = kStages;
+    for (int i = 0; i < kStages; i++) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, s.ev[i], s.ev[i + 1]) != hipSuccess) ms = -1.f;
+      ctx->timings[i] = ms * 1000.f;
+    }
+    s.profiled = false;
+  }
   const int32_t* stv = static_cast<const int32_t*>(s.pin_status.p);
   int first_bad = -1;
   for (int i = 0; i < s.n; i++) {
@@ -643,24 +654,24 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   HJ_HIP(hipMemcpyAsync(ctx->desc.p, slot.pin_desc.p, sizeof(ImageDesc) * n,
                         hipMemcpyHostToDevice, st));
   HJ_HIP(hipMemsetAsync(ctx->coefs.p, 0, (size_t)L.total_blocks * 128, st));
-  mark(ctx, 1, st);
+  mark(ctx, slot, 1, st);
   auto* desc = static_cast<const ImageDesc*>(ctx->desc.p);
   auto* infos = static_cast<ImageInfo*>(ctx->info.p);
   HJ_HIP(launch_parse(d_bytes, desc, infos, static_cast<HuffTable*>(ctx->luts.p), n, st));
-  mark(ctx, 2, st);
+  mark(ctx, slot, 2, st);
   HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<DsChunk*>(ctx->dschunks.p),
                         static_cast<uint8_t*>(ctx->clean.p), static_cast<uint32_t*>(ctx->segs.p),
                         L.max_chunks, n, st));
-  mark(ctx, 3, st);
+  mark(ctx, slot, 3, st);
   HJ_HIP(launch_entropy(static_cast<const uint8_t*>(ctx->clean.p),
                         static_cast<const uint32_t*>(ctx->segs.p), desc, infos,
                         static_cast<const HuffTable*>(ctx->luts.p),
                         static_cast<int16_t*>(ctx->coefs.p), static_cast<uint32_t*>(ctx->recs.p),
                         ctx->sub_bits, ctx->entropy_threads, n, st));
-  mark(ctx, 4, st);
+  mark(ctx, slot, 4, st);
   HJ_HIP(launch_idct(static_cast<const int16_t*>(ctx->coefs.p), desc, infos,
                      static_cast<uint8_t*>(ctx->planes.p), out->idct, L.max_blocks, n, st));
-  mark(ctx, 5, st);
+  mark(ctx, slot, 5, st);
   BatchParams bp{};
   bp.n = n;
   bp.pix_fmt = out->pix_fmt;
@@ -680,45 +691,38 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
     if (out->resize) {
       HJ_HIP(launch_weights(desc, infos, static_cast<int32_t*>(ctx->wts.p), out->filter, L.max_len,
                             n, st));
-      mark(ctx, 6, st);
+      mark(ctx, slot, 6, st);
       HJ_HIP(launch_resize(static_cast<const uint8_t*>(ctx->planes.p), desc, infos,
                            static_cast<const int32_t*>(ctx->wts.p),
                            static_cast<uint8_t*>(ctx->rplanes.p), out_dev, bp, L.max_bands,
                            L.max_quads, n, st));
     } else {
-      mark(ctx, 6, st);
+      mark(ctx, slot, 6, st);
       HJ_HIP(launch_csc(static_cast<const uint8_t*>(ctx->planes.p), desc, infos, out_dev, bp,
                         L.max_px, n, st));
     }
   } else {
-    mark(ctx, 6, st);
+    mark(ctx, slot, 6, st);
   }
-  mark(ctx, 7, st);
+  mark(ctx, slot, 7, st);
   // per-image status: strided D2H of ImageInfo::status
   HJ_HIP(hipMemcpy2DAsync(slot.pin_status.p, sizeof(int32_t), ctx->info.p, sizeof(ImageInfo),
                           sizeof(int32_t), n, hipMemcpyDeviceToHost, st));
-  mark(ctx, 8, st);
+  mark(ctx, slot, 8, st);
   HJ_HIP(hipEventRecord(ctx->batch_done, st));
   HJ_HIP(hipEventRecord(slot.done, st));
   slot.pending = true;
+  slot.profiled = ctx->profiling;
   ctx->last_ticket = slot.ticket;
   if (!sync) return SPDL_HJ_OK;
   HJ_HIP(hipEventSynchronize(slot.done));
-  if (ctx->profiling) {
-    ctx->ntimings = kStages;
-    for (int i = 0; i < kStages; i++) {
-      float ms = 0.f;
-      if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) != hipSuccess) ms = -1.f;
-      ctx->timings[i] = ms * 1000.f;
-    }
-  }
-  return collect_status(slot, status, err, errlen);
+  return collect_status(ctx, slot, status, err, errlen);
 }
 
 // H2D of the slot's staged bytes on the copy stream; `st` waits for it.
 int stage_h2d(spdl_hj_ctx* ctx, Slot& s, size_t total, hipStream_t st, char* err, size_t errlen) {
   HJ_HIP(s.bytes.ensure(total + 512));
-  mark(ctx, 0, ctx->copy);
+  mark(ctx, s, 0, ctx->copy);
   HJ_HIP(hipMemcpyAsync(s.bytes.p, s.pin_in.p, total, hipMemcpyHostToDevice, ctx->copy));
   HJ_HIP(hipEventRecord(s.h2d_done, ctx->copy));
   HJ_HIP(hipStreamWaitEvent(st, s.h2d_done, 0));
@@ -811,13 +815,14 @@ spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen) {
   for (int i = 0; ok && i < kSlots; i++)
     ok = hipEventCreateWithFlags(&c->slots[i].h2d_done, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->slots[i].done, hipEventDisableTiming) == hipSuccess;
-  for (int i = 0; ok && i <= kStages; i++) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+  for (int i = 0; ok && i < kSlots; i++)
+    for (int k = 0; ok && k <= kStages; k++) ok = hipEventCreate(&c->slots[i].ev[k]) == hipSuccess;
   if (!ok) {
     set_err(err, errlen, "hipEventCreate / hipStreamCreate failed");
     spdl_hj_destroy(c);
     return nullptr;
   }
-  c->pool = new CopyPool(3);
+  c->pool = new CopyPool(7);  // + the calling thread: 8 copiers
   return c;
 }
 
@@ -838,11 +843,11 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
     s.pin_status.release();
     if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
     if (s.done) (void)hipEventDestroy(s.done);
+    for (int k = 0; k <= kStages; k++)
+      if (s.ev[k]) (void)hipEventDestroy(s.ev[k]);
   }
   if (c->batch_done) (void)hipEventDestroy(c->batch_done);
   if (c->copy) (void)hipStreamDestroy(c->copy);
-  for (int i = 0; i <= kStages; i++)
-    if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
   delete c->pool;
   delete c;
 }
@@ -907,7 +912,7 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
   if (rc) return rc;
-  mark(ctx, 0, st);
+  mark(ctx, *s, 0, st);
   return run_pipeline(ctx, *s, dev_data, dev_bytes, L, n, out, out_dev, out_bytes, st, sync,
                       status, err, errlen, false);
 }
@@ -928,7 +933,7 @@ int spdl_hj_wait(spdl_hj_ctx* ctx, int64_t ticket, int32_t* status, int32_t n, c
   }
   DeviceGuard g(ctx->device);
   HJ_HIP(hipEventSynchronize(s->done));
-  return collect_status(*s, status, err, errlen);
+  return collect_status(ctx, *s, status, err, errlen);
 }
 
 int spdl_hj_staging_acquire(spdl_hj_ctx* ctx, size_t bytes, uint8_t** host_ptr, int64_t* ticket,
