@@ -97,6 +97,8 @@ def _args():
     p.add_argument("--entropy-threads", type=int, default=0)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="pad224")
     p.add_argument("--norm-dtype", choices=["float16", "bfloat16"], default="float16")
+    p.add_argument("--lanes", type=int, default=2,
+                   help="concurrent decode pipelines in the context (1 or 2)")
     p.add_argument("--sync-steps", action="store_true",
                    help="one synchronous call per step (no overlap of host work)")
     p.add_argument("--with-copies", action="store_true",
@@ -164,18 +166,26 @@ def main():
         dec.set_param("sub_bits", a.sub_bits)
     if a.entropy_threads:
         dec.set_param("entropy_threads", a.entropy_threads)
+    dec.set_param("lanes", a.lanes)
     if a.workload == "imagenet":
         spec = Output(**{**IMAGENET_SPEC.__dict__, "norm_dtype": a.norm_dtype})
-        out = torch.empty((a.batch, 3, 224, 224), dtype=spec.torch_dtype, device=device)
+        outs = [torch.empty((a.batch, 3, 224, 224), dtype=spec.torch_dtype, device=device)
+                for _ in range(2)]
     else:
         spec = OUT_SPEC
-        out = torch.empty((a.batch, 224, 224, 3), dtype=torch.uint8, device=device)
+        outs = [torch.empty((a.batch, 224, 224, 3), dtype=torch.uint8, device=device)
+                for _ in range(2)]
+    out = outs[0]
     stream = torch.cuda.current_stream(device)
     nbytes_out = out.numel() * out.element_size()
+    nsub = [0]
 
     def submit(sync: bool) -> int:
+        # two output buffers: with two lanes, batches k and k+1 run concurrently
+        o = outs[nsub[0] & 1]
+        nsub[0] += 1
         dec.decode_batch_device(dev.data_ptr(), dev.numel(), offs, sizes, infos, spec,
-                                out.data_ptr(), nbytes_out, stream=stream, sync=sync)
+                                o.data_ptr(), nbytes_out, stream=stream, sync=sync)
         return dec.last_ticket()
 
     # Steps are submitted asynchronously through the decoder's ring (at most
@@ -271,6 +281,7 @@ def main():
                 "mean_jpeg_bytes": round(comp_bytes, 1),
                 "distinct_images": a.distinct,
                 "parallelism": f"{world} independent per-GPU slices, no collective",
+                "lanes": a.lanes,
             },
             "roofline": {
                 "bound": "hbm",

@@ -149,6 +149,10 @@ int64_t spdl_hj_last_ticket(spdl_hj_ctx* ctx);
 int spdl_hj_wait(spdl_hj_ctx* ctx, int64_t ticket, int32_t* status, int32_t n, char* err,
                  size_t errlen);
 
+/* Make `stream` wait (on the device, no host block) for batch `ticket`. */
+int spdl_hj_stream_wait(spdl_hj_ctx* ctx, int64_t ticket, void* stream, char* err,
+                        size_t errlen);
+
 /* Zero-repack ingest: take the next slot and return its pinned staging
  * (>= bytes long) so the caller can place a region of its source there
  * directly -- e.g. a run of consecutive tar members, whose payloads are
@@ -212,7 +216,12 @@ int spdl_hj_last_timings(spdl_hj_ctx* ctx, float* us, int32_t cap, int32_t* n_ou
 /* Names of the timed stages in the order spdl_hj_last_timings reports them. */
 const char* spdl_hj_stage_name(int32_t i);
 
-/* Tuning knobs (subsequence size in bits for the parallel Huffman decode). */
+/* Tuning knobs: "sub_bits" (slot size of the parallel Huffman decode),
+ * "entropy_threads" (256/512/1024), "lanes" (1 or 2 concurrent pipelines:
+ * with 2, successive batches alternate between two device workspaces and run
+ * on the context's own two streams, each ordered after the caller's stream at
+ * submission; completion is then observed through the ticket --
+ * spdl_hj_wait / spdl_hj_stream_wait -- not by the caller's stream). */
 int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value);
 
 #ifdef __cplusplus

@@ -42,6 +42,7 @@ EXPORTED = (
     "spdl_hj_last_ticket",
     "spdl_hj_wait",
     "spdl_hj_staging_acquire",
+    "spdl_hj_stream_wait",
     "spdl_hj_staging_fill",
     "spdl_hj_staging_read",
     "spdl_hj_decode_staged",
@@ -188,6 +189,7 @@ def lib() -> ctypes.CDLL:
         L.spdl_hj_staging_acquire.argtypes = [
             vp, sz, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(i64), cp, sz
         ]
+        L.spdl_hj_stream_wait.argtypes = [vp, i64, vp, cp, sz]
         L.spdl_hj_staging_fill.argtypes = [vp, i64, sz, vp, sz, cp, sz]
         L.spdl_hj_staging_read.argtypes = [vp, i64, sz, ctypes.c_int, i64, sz, cp, sz]
         L.spdl_hj_decode_staged.argtypes = [
@@ -381,6 +383,13 @@ class Decoder:
         if rc:
             raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
         return list(status)[:n]
+
+    def stream_wait(self, ticket: int, stream) -> None:
+        """Make `stream` wait on the device for batch `ticket`."""
+        err = ctypes.create_string_buffer(512)
+        rc = lib().spdl_hj_stream_wait(self._h, int(ticket), _stream_handle(stream), err, 512)
+        if rc:
+            raise RuntimeError(err.value.decode())
 
     def staging_acquire(self, nbytes: int) -> tuple[int, int]:
         """(pinned host address, ticket) of the next ring slot (>= nbytes)."""

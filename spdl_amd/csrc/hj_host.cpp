@@ -392,7 +392,8 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
       // the compressed size (the device derives N from the destuffed length)
       const uint64_t bits = (uint64_t)sizes[i] * 8u;
       const uint32_t nb = slot_bits(bits > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bits, sub_bits);
-      d.rec_cap = (int64_t)(kMaxSlots + kMaxEntropyThreads) * (nb + kRecPad);
+      // + per-slot state (uint4 per slot) at the end
+      d.rec_cap = (int64_t)(kMaxSlots + kMaxEntropyThreads) * (nb + kRecPad) + kMaxSlots * 4;
       d.rec_off = L.total_recs;
       L.total_recs += d.rec_cap;
     }
@@ -506,18 +507,31 @@ struct Slot {
   bool pending = false;           // submitted, not yet waited
   bool staged = false;            // acquired by spdl_hj_staging_acquire, not submitted
   bool profiled = false;          // ev[] were recorded for this batch
+  hipEvent_t submitted = nullptr; // lanes > 1: the caller's stream reached the submit
   int n = 0;
   hipEvent_t ev[kStages + 1] = {};  // stage boundaries (profiling only)
 };
 
+// Device workspace of one pipeline "lane".  With lanes > 1 successive
+// batches alternate between workspaces and run on the lanes' own streams, so
+// batch k+1's kernels can occupy the CUs that batch k's latency-bound
+// entropy kernel leaves idle (its sync rounds park most waves at barriers).
+constexpr int kMaxLanes = 2;
+
+struct Workspace {
+  DevBuf clean, segs, desc, info, luts, coefs, planes, wts, recs, rplanes, dschunks;
+  hipEvent_t done = nullptr;      // the workspace is free after this
+  hipStream_t stream = nullptr;   // lanes > 1 only
+};
+
 struct spdl_hj_ctx {
   int device = 0;
-  DevBuf clean, segs, desc, info, luts, coefs, planes, wts, recs, rplanes, dschunks;
+  Workspace ws[kMaxLanes];
+  int lanes = 1;
   Slot slots[kSlots];
   int64_t next_ticket = 1;
   int64_t last_ticket = 0;
   hipStream_t copy = nullptr;         // H2D stream of the staging ring
-  hipEvent_t batch_done = nullptr;    // device workspace free after this
   CopyPool* pool = nullptr;
   bool profiling = false;
   float timings[kStages] = {};
@@ -606,7 +620,8 @@ int collect_status(spdl_hj_ctx* ctx, Slot& s, int32_t* status, char* err, size_t
 }
 
 // device pipeline over bytes already in HBM; `slot` provides the descriptor
-// and status staging and is marked done on `st` at the end.
+// and status staging and is marked done on `st` at the end.  `st` is the
+// execution stream (exec_stream()), the workspace is the slot's lane.
 int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t bytes_len,
                  const Layout& L, int n, const spdl_hj_output* out, void* out_dev,
                  size_t out_bytes, hipStream_t st, int sync, int32_t* status, char* err,
@@ -631,46 +646,47 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
     }
     if (e > max_end) max_end = e;
   }
+  Workspace& W = ctx->ws[slot.ticket % ctx->lanes];
   // the previous batch may still be using the workspace (async call, maybe on
   // another stream)
-  HJ_HIP(hipStreamWaitEvent(st, ctx->batch_done, 0));
-  HJ_HIP(ctx->clean.ensure((size_t)max_end + 512));
-  HJ_HIP(ctx->segs.ensure((size_t)L.total_segs * 4 + 64));
-  HJ_HIP(ctx->dschunks.ensure((size_t)L.total_ds * sizeof(DsChunk) + 64));
-  HJ_HIP(ctx->desc.ensure(sizeof(ImageDesc) * n));
-  HJ_HIP(ctx->info.ensure(sizeof(ImageInfo) * n));
-  HJ_HIP(ctx->luts.ensure(sizeof(HuffTable) * 8 * n));
-  HJ_HIP(ctx->coefs.ensure((size_t)L.total_blocks * 128 + 256));
-  HJ_HIP(ctx->planes.ensure((size_t)L.total_planes + 256));
-  HJ_HIP(ctx->recs.ensure((size_t)L.total_recs * 4 + 256));
+  HJ_HIP(hipStreamWaitEvent(st, W.done, 0));
+  HJ_HIP(W.clean.ensure((size_t)max_end + 512));
+  HJ_HIP(W.segs.ensure((size_t)L.total_segs * 4 + 64));
+  HJ_HIP(W.dschunks.ensure((size_t)L.total_ds * sizeof(DsChunk) + 64));
+  HJ_HIP(W.desc.ensure(sizeof(ImageDesc) * n));
+  HJ_HIP(W.info.ensure(sizeof(ImageInfo) * n));
+  HJ_HIP(W.luts.ensure(sizeof(HuffTable) * 8 * n));
+  HJ_HIP(W.coefs.ensure((size_t)L.total_blocks * 128 + 256));
+  HJ_HIP(W.planes.ensure((size_t)L.total_planes + 256));
+  HJ_HIP(W.recs.ensure((size_t)L.total_recs * 4 + 256));
   if (out->resize) {
-    HJ_HIP(ctx->wts.ensure((size_t)L.total_wts * 4 + 256));
-    HJ_HIP(ctx->rplanes.ensure((size_t)L.total_rp + 256));
+    HJ_HIP(W.wts.ensure((size_t)L.total_wts * 4 + 256));
+    HJ_HIP(W.rplanes.ensure((size_t)L.total_rp + 256));
   }
   HJ_HIP(slot.pin_desc.ensure(sizeof(ImageDesc) * n));
   HJ_HIP(slot.pin_status.ensure(sizeof(int32_t) * n));
   slot.n = n;
   memcpy(slot.pin_desc.p, L.desc.data(), sizeof(ImageDesc) * n);
-  HJ_HIP(hipMemcpyAsync(ctx->desc.p, slot.pin_desc.p, sizeof(ImageDesc) * n,
+  HJ_HIP(hipMemcpyAsync(W.desc.p, slot.pin_desc.p, sizeof(ImageDesc) * n,
                         hipMemcpyHostToDevice, st));
-  HJ_HIP(hipMemsetAsync(ctx->coefs.p, 0, (size_t)L.total_blocks * 128, st));
+  HJ_HIP(hipMemsetAsync(W.coefs.p, 0, (size_t)L.total_blocks * 128, st));
   mark(ctx, slot, 1, st);
-  auto* desc = static_cast<const ImageDesc*>(ctx->desc.p);
-  auto* infos = static_cast<ImageInfo*>(ctx->info.p);
-  HJ_HIP(launch_parse(d_bytes, desc, infos, static_cast<HuffTable*>(ctx->luts.p), n, st));
+  auto* desc = static_cast<const ImageDesc*>(W.desc.p);
+  auto* infos = static_cast<ImageInfo*>(W.info.p);
+  HJ_HIP(launch_parse(d_bytes, desc, infos, static_cast<HuffTable*>(W.luts.p), n, st));
   mark(ctx, slot, 2, st);
-  HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<DsChunk*>(ctx->dschunks.p),
-                        static_cast<uint8_t*>(ctx->clean.p), static_cast<uint32_t*>(ctx->segs.p),
+  HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<DsChunk*>(W.dschunks.p),
+                        static_cast<uint8_t*>(W.clean.p), static_cast<uint32_t*>(W.segs.p),
                         L.max_chunks, n, st));
   mark(ctx, slot, 3, st);
-  HJ_HIP(launch_entropy(static_cast<const uint8_t*>(ctx->clean.p),
-                        static_cast<const uint32_t*>(ctx->segs.p), desc, infos,
-                        static_cast<const HuffTable*>(ctx->luts.p),
-                        static_cast<int16_t*>(ctx->coefs.p), static_cast<uint32_t*>(ctx->recs.p),
+  HJ_HIP(launch_entropy(static_cast<const uint8_t*>(W.clean.p),
+                        static_cast<const uint32_t*>(W.segs.p), desc, infos,
+                        static_cast<const HuffTable*>(W.luts.p),
+                        static_cast<int16_t*>(W.coefs.p), static_cast<uint32_t*>(W.recs.p),
                         ctx->sub_bits, ctx->entropy_threads, n, st));
   mark(ctx, slot, 4, st);
-  HJ_HIP(launch_idct(static_cast<const int16_t*>(ctx->coefs.p), desc, infos,
-                     static_cast<uint8_t*>(ctx->planes.p), out->idct, L.max_blocks, n, st));
+  HJ_HIP(launch_idct(static_cast<const int16_t*>(W.coefs.p), desc, infos,
+                     static_cast<uint8_t*>(W.planes.p), out->idct, L.max_blocks, n, st));
   mark(ctx, slot, 5, st);
   BatchParams bp{};
   bp.n = n;
@@ -689,16 +705,16 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   }
   if (!planes_only) {
     if (out->resize) {
-      HJ_HIP(launch_weights(desc, infos, static_cast<int32_t*>(ctx->wts.p), out->filter, L.max_len,
+      HJ_HIP(launch_weights(desc, infos, static_cast<int32_t*>(W.wts.p), out->filter, L.max_len,
                             n, st));
       mark(ctx, slot, 6, st);
-      HJ_HIP(launch_resize(static_cast<const uint8_t*>(ctx->planes.p), desc, infos,
-                           static_cast<const int32_t*>(ctx->wts.p),
-                           static_cast<uint8_t*>(ctx->rplanes.p), out_dev, bp, L.max_bands,
+      HJ_HIP(launch_resize(static_cast<const uint8_t*>(W.planes.p), desc, infos,
+                           static_cast<const int32_t*>(W.wts.p),
+                           static_cast<uint8_t*>(W.rplanes.p), out_dev, bp, L.max_bands,
                            L.max_quads, n, st));
     } else {
       mark(ctx, slot, 6, st);
-      HJ_HIP(launch_csc(static_cast<const uint8_t*>(ctx->planes.p), desc, infos, out_dev, bp,
+      HJ_HIP(launch_csc(static_cast<const uint8_t*>(W.planes.p), desc, infos, out_dev, bp,
                         L.max_px, n, st));
     }
   } else {
@@ -706,10 +722,10 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   }
   mark(ctx, slot, 7, st);
   // per-image status: strided D2H of ImageInfo::status
-  HJ_HIP(hipMemcpy2DAsync(slot.pin_status.p, sizeof(int32_t), ctx->info.p, sizeof(ImageInfo),
+  HJ_HIP(hipMemcpy2DAsync(slot.pin_status.p, sizeof(int32_t), W.info.p, sizeof(ImageInfo),
                           sizeof(int32_t), n, hipMemcpyDeviceToHost, st));
   mark(ctx, slot, 8, st);
-  HJ_HIP(hipEventRecord(ctx->batch_done, st));
+  HJ_HIP(hipEventRecord(W.done, st));
   HJ_HIP(hipEventRecord(slot.done, st));
   slot.pending = true;
   slot.profiled = ctx->profiling;
@@ -717,6 +733,24 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   if (!sync) return SPDL_HJ_OK;
   HJ_HIP(hipEventSynchronize(slot.done));
   return collect_status(ctx, slot, status, err, errlen);
+}
+
+// Stream the batch of `slot` executes on: the caller's stream with one lane;
+// otherwise its lane's own stream, ordered after everything the caller's
+// stream has queued so far (its output allocation, say).  Completion is then
+// observed through the ticket (spdl_hj_wait / spdl_hj_stream_wait), not by
+// the caller's stream.
+int exec_stream(spdl_hj_ctx* ctx, Slot& slot, hipStream_t st, hipStream_t* xs, char* err,
+                size_t errlen) {
+  if (ctx->lanes <= 1) {
+    *xs = st;
+    return SPDL_HJ_OK;
+  }
+  Workspace& W = ctx->ws[slot.ticket % ctx->lanes];
+  HJ_HIP(hipEventRecord(slot.submitted, st));
+  HJ_HIP(hipStreamWaitEvent(W.stream, slot.submitted, 0));
+  *xs = W.stream;
+  return SPDL_HJ_OK;
 }
 
 // H2D of the slot's staged bytes on the copy stream; `st` waits for it.
@@ -810,11 +844,14 @@ spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen) {
   DeviceGuard g(device);
   auto* c = new spdl_hj_ctx();
   c->device = device;
-  bool ok = hipEventCreateWithFlags(&c->batch_done, hipEventDisableTiming) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess;
+  bool ok = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; ok && i < kMaxLanes; i++)
+    ok = hipEventCreateWithFlags(&c->ws[i].done, hipEventDisableTiming) == hipSuccess &&
+         hipStreamCreateWithFlags(&c->ws[i].stream, hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; ok && i < kSlots; i++)
     ok = hipEventCreateWithFlags(&c->slots[i].h2d_done, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&c->slots[i].done, hipEventDisableTiming) == hipSuccess;
+         hipEventCreateWithFlags(&c->slots[i].done, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->slots[i].submitted, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; ok && i < kSlots; i++)
     for (int k = 0; ok && k <= kStages; k++) ok = hipEventCreate(&c->slots[i].ev[k]) == hipSuccess;
   if (!ok) {
@@ -831,11 +868,18 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
   DeviceGuard g(c->device);
   for (Slot& s : c->slots)
     if (s.ticket && s.done) (void)hipEventSynchronize(s.done);
-  if (c->batch_done) (void)hipEventSynchronize(c->batch_done);
+  for (Workspace& w : c->ws) {
+    if (w.done) (void)hipEventSynchronize(w.done);
+    if (w.stream) (void)hipStreamSynchronize(w.stream);
+  }
   if (c->copy) (void)hipStreamSynchronize(c->copy);
-  DevBuf* bufs[] = {&c->clean, &c->segs, &c->desc, &c->info, &c->luts, &c->coefs,
-                    &c->planes, &c->wts, &c->recs, &c->rplanes, &c->dschunks};
-  for (DevBuf* b : bufs) b->release();
+  for (Workspace& w : c->ws) {
+    DevBuf* bufs[] = {&w.clean, &w.segs, &w.desc, &w.info, &w.luts, &w.coefs,
+                      &w.planes, &w.wts, &w.recs, &w.rplanes, &w.dschunks};
+    for (DevBuf* b : bufs) b->release();
+    if (w.done) (void)hipEventDestroy(w.done);
+    if (w.stream) (void)hipStreamDestroy(w.stream);
+  }
   for (Slot& s : c->slots) {
     s.bytes.release();
     s.pin_in.release();
@@ -843,10 +887,10 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
     s.pin_status.release();
     if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
     if (s.done) (void)hipEventDestroy(s.done);
+    if (s.submitted) (void)hipEventDestroy(s.submitted);
     for (int k = 0; k <= kStages; k++)
       if (s.ev[k]) (void)hipEventDestroy(s.ev[k]);
   }
-  if (c->batch_done) (void)hipEventDestroy(c->batch_done);
   if (c->copy) (void)hipStreamDestroy(c->copy);
   delete c->pool;
   delete c;
@@ -887,10 +931,12 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
   if (rc) return rc;
   HJ_HIP(s->pin_in.ensure((size_t)total));
   parallel_pack(ctx->pool, static_cast<uint8_t*>(s->pin_in.p), items);
-  rc = stage_h2d(ctx, *s, (size_t)total, st, err, errlen);
+  hipStream_t xs;
+  rc = exec_stream(ctx, *s, st, &xs, err, errlen);
+  if (!rc) rc = stage_h2d(ctx, *s, (size_t)total, xs, err, errlen);
   if (rc) return rc;
   return run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), (size_t)total, L, n, out,
-                      out_dev, out_bytes, st, sync, status, err, errlen, false);
+                      out_dev, out_bytes, xs, sync, status, err, errlen, false);
 }
 
 int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_t dev_bytes,
@@ -912,8 +958,11 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
   if (rc) return rc;
-  mark(ctx, *s, 0, st);
-  return run_pipeline(ctx, *s, dev_data, dev_bytes, L, n, out, out_dev, out_bytes, st, sync,
+  hipStream_t xs;
+  rc = exec_stream(ctx, *s, st, &xs, err, errlen);
+  if (rc) return rc;
+  mark(ctx, *s, 0, xs);
+  return run_pipeline(ctx, *s, dev_data, dev_bytes, L, n, out, out_dev, out_bytes, xs, sync,
                       status, err, errlen, false);
 }
 
@@ -934,6 +983,18 @@ int spdl_hj_wait(spdl_hj_ctx* ctx, int64_t ticket, int32_t* status, int32_t n, c
   DeviceGuard g(ctx->device);
   HJ_HIP(hipEventSynchronize(s->done));
   return collect_status(ctx, *s, status, err, errlen);
+}
+
+int spdl_hj_stream_wait(spdl_hj_ctx* ctx, int64_t ticket, void* stream, char* err,
+                        size_t errlen) {
+  Slot* s = ctx ? find_slot(ctx, ticket) : nullptr;
+  if (!s) {
+    set_err(err, errlen, "unknown or overwritten ticket %lld", (long long)ticket);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(ctx->device);
+  HJ_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(stream), s->done, 0));
+  return SPDL_HJ_OK;
 }
 
 int spdl_hj_staging_acquire(spdl_hj_ctx* ctx, size_t bytes, uint8_t** host_ptr, int64_t* ticket,
@@ -1035,10 +1096,12 @@ int spdl_hj_decode_staged(spdl_hj_ctx* ctx, int64_t ticket, size_t len, const in
     return rc;
   }
   memset(static_cast<uint8_t*>(s->pin_in.p) + len, 0, 512);  // tail read slack
-  rc = stage_h2d(ctx, *s, len + 512, st, err, errlen);
+  hipStream_t xs;
+  rc = exec_stream(ctx, *s, st, &xs, err, errlen);
+  if (!rc) rc = stage_h2d(ctx, *s, len + 512, xs, err, errlen);
   if (rc) return rc;
   return run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), len + 512, L, n, out,
-                      out_dev, out_bytes, st, sync, status, err, errlen, false);
+                      out_dev, out_bytes, xs, sync, status, err, errlen, false);
 }
 
 int spdl_hj_tar_index(const uint8_t* data, size_t size, size_t start, int32_t max_entries,
@@ -1154,11 +1217,15 @@ int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   HJ_HIP(s->pin_in.ensure((size_t)total));
   memcpy(s->pin_in.p, data, size);
   memset(static_cast<uint8_t*>(s->pin_in.p) + size, 0, (size_t)(total - sz));
-  rc = stage_h2d(ctx, *s, (size_t)total, st, err, errlen);
+  hipStream_t xs;
+  rc = exec_stream(ctx, *s, st, &xs, err, errlen);
+  if (!rc) rc = stage_h2d(ctx, *s, (size_t)total, xs, err, errlen);
   if (rc) return rc;
   rc = run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), (size_t)total, L, 1, &o,
-                    nullptr, 0, st, 1, nullptr, err, errlen, true);
+                    nullptr, 0, xs, 1, nullptr, err, errlen, true);
   if (rc) return rc;
+  Workspace& W = ctx->ws[s->ticket % ctx->lanes];
+  st = xs;
   const ImageDesc& d = L.desc[0];
   int hmax = 1, vmax = 1;
   for (int c = 0; c < info.ncomp; c++) {
@@ -1169,7 +1236,7 @@ int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
     int w = info.ncomp == 1 ? info.width : (info.width * info.h_samp[c] + hmax - 1) / hmax;
     int h = info.ncomp == 1 ? info.height : (info.height * info.v_samp[c] + vmax - 1) / vmax;
     HJ_HIP(hipMemcpy2DAsync(planes[c], (size_t)w,
-                            static_cast<const uint8_t*>(ctx->planes.p) + d.plane_off[c],
+                            static_cast<const uint8_t*>(W.planes.p) + d.plane_off[c],
                             (size_t)d.plane_stride[c], (size_t)w, (size_t)h,
                             hipMemcpyDeviceToHost, st));
   }
@@ -1203,12 +1270,15 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   HJ_HIP(s->pin_in.ensure((size_t)total));
   memcpy(s->pin_in.p, data, size);
   memset(static_cast<uint8_t*>(s->pin_in.p) + size, 0, (size_t)(total - sz));
-  rc = stage_h2d(ctx, *s, (size_t)total, st, err, errlen);
+  hipStream_t xs;
+  rc = exec_stream(ctx, *s, st, &xs, err, errlen);
+  if (!rc) rc = stage_h2d(ctx, *s, (size_t)total, xs, err, errlen);
   if (rc) return rc;
   (void)run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), (size_t)total, L, 1, &o,
-                     nullptr, 0, st, 1, nullptr, err, errlen, true);
+                     nullptr, 0, xs, 1, nullptr, err, errlen, true);
+  Workspace& W = ctx->ws[s->ticket % ctx->lanes];
   ImageInfo hi;
-  HJ_HIP(hipMemcpy(&hi, ctx->info.p, sizeof(ImageInfo), hipMemcpyDeviceToHost));
+  HJ_HIP(hipMemcpy(&hi, W.info.p, sizeof(ImageInfo), hipMemcpyDeviceToHost));
   diag[0] = hi.status;
   diag[1] = hi.clean_len;
   diag[2] = hi.nseg;
@@ -1216,11 +1286,11 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   for (int i = 0; i < 4; i++) diag[4 + i] = (int32_t)hi.tphase[i];
   for (int i = 0; i < 4; i++) diag[8 + i] = (int32_t)hi.dbg[i];
   size_t nc = (size_t)L.desc[0].nblocks * 64;
-  if (coefs) HJ_HIP(hipMemcpy(coefs, ctx->coefs.p, 2 * (nc < coef_cap ? nc : coef_cap),
+  if (coefs) HJ_HIP(hipMemcpy(coefs, W.coefs.p, 2 * (nc < coef_cap ? nc : coef_cap),
                               hipMemcpyDeviceToHost));
   if (clean && hi.clean_len > 0) {
     size_t n = (size_t)hi.clean_len < clean_cap ? (size_t)hi.clean_len : clean_cap;
-    HJ_HIP(hipMemcpy(clean, ctx->clean.p, n, hipMemcpyDeviceToHost));
+    HJ_HIP(hipMemcpy(clean, W.clean.p, n, hipMemcpyDeviceToHost));
   }
   return SPDL_HJ_OK;
 }
@@ -1253,6 +1323,11 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "entropy_threads")) {  // workgroup size of the Huffman kernel
     if (value != 256 && value != 512 && value != 1024) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->entropy_threads = (int)value;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "lanes")) {  // concurrent pipelines (workspaces + streams)
+    if (value < 1 || value > kMaxLanes) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->lanes = (int)value;
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "debug_mask")) {  // timing ablations only: output is wrong

@@ -612,22 +612,27 @@ struct EntShared {
   int32_t maxcode[kMaxLds][18];
   int32_t valoff[kMaxLds][17];
   uint8_t vals[kMaxLds][256];
-  uint32_t s_pos[kMaxSlots];
-  uint32_t s_zb[kMaxSlots];   // z | b << 8
-  uint32_t s_nrec[kMaxSlots];  // records of the slot's current trajectory
-  uint8_t s_endz[kMaxSlots];   // z at the slot's end
   uint32_t run_pos[NT];
   uint32_t run_zb[NT];
-  int32_t scan_flag[NT];
-  int32_t scan_v[NT][4];  // blk, dc0, dc1, dc2
   uint16_t qt[kMaxComp][64];
   uint8_t nat[64];
   int32_t tdc[kMaxBpm], tac[kMaxBpm], bcomp[kMaxBpm];
-  int32_t red[NT];
-  uint32_t win[kWinWords][NT];  // bit-reader windows
+  // The bit-reader windows are dead outside round 0 / the sync rounds, so the
+  // reduction and scan scratch share their storage (keeps the workgroup at
+  // <= 80 KiB of LDS: two entropy workgroups -- e.g. of two concurrent
+  // batches -- fit one CU and fill each other's barrier stalls).
+  union {
+    uint32_t win[kWinWords][NT];  // bit-reader windows
+    struct {
+      int32_t scan_flag[NT];
+      int32_t scan_v[NT][4];  // blk, dc0, dc1, dc2
+      int32_t red[NT];
+    } sc;
+  };
   int32_t flag;
   int32_t err;
 };
+static_assert(sizeof(EntShared<512>) <= 80 * 1024, "entropy LDS must allow 2 workgroups per CU");
 
 // Per-thread bit reader over the destuffed stream (big-endian bytes read as
 // 32-bit words).  `buf` holds the next 33..64 bits MSB-first and `nxt` the
@@ -674,15 +679,26 @@ __device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* 
 }
 
 template <int NT>
-__device__ __forceinline__ void dec_refill(Dec& d, uint32_t* win, const uint32_t* words) {
+__device__ __forceinline__ void dec_refill(Dec& d, const uint32_t* win) {
   if (d.cnt <= 32) {
     d.buf |= (uint64_t)__builtin_bswap32(d.nxt) << (32 - d.cnt);
     d.cnt += 32;
     d.wi++;
-    if (d.wi - d.wb >= (uint32_t)kWinWords) {
-      d.wb = d.wi & ~3u;
-      win_stage<NT>(win, words, d.wb);
-    }
+    d.nxt = win[(d.wi - d.wb) * NT];  // in the window: see dec_restage
+  }
+}
+
+// Wave-uniform window restage: when any active lane is about to read past its
+// window, every active lane restages from its own position.  The global load
+// and its vmcnt wait (which on gfx9 also waits for the lane's older record
+// stores) then happen once per ~40 symbol steps of the wave instead of in
+// most steps (a per-lane restage fires in ~3/4 of the iterations of a
+// 64-lane wave).  Keeps wi - wb <= kWinWords - 1 after the next refill.
+template <int NT>
+__device__ __forceinline__ void dec_restage(Dec& d, uint32_t* win, const uint32_t* words) {
+  if (__any((d.wi - d.wb) >= (uint32_t)(kWinWords - 1))) {
+    d.wb = d.wi & ~3u;
+    win_stage<NT>(win, words, d.wb);
     d.nxt = win[(d.wi - d.wb) * NT];
   }
 }
@@ -733,7 +749,8 @@ __device__ uint32_t decode_slot(const SH& S, Dec& d, uint32_t* win, const uint32
   auto at = [&](uint32_t n) -> uint32_t& { return rec[(n >> 2) * (NT * 4) + (n & 3)]; };
   uint32_t n = 0;
   while (d.pos < end) {
-    dec_refill<NT>(d, win, words);
+    dec_restage<NT>(d, win, words);
+    dec_refill<NT>(d, win);
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
     // component of this block, then its DC or AC table slot
@@ -862,17 +879,17 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
     const uint32_t a = seg_start_bits(s), e = seg_end_bits(s);
     maxbits = max(maxbits, e > a ? e - a : 0u);
   }
-  S.red[tid] = (int32_t)maxbits;
+  S.sc.red[tid] = (int32_t)maxbits;
   __syncthreads();
   for (int off = NT / 2; off > 0; off >>= 1) {
-    if (tid < off) S.red[tid] = max(S.red[tid], S.red[tid + off]);
+    if (tid < off) S.sc.red[tid] = max(S.sc.red[tid], S.sc.red[tid + off]);
     __syncthreads();
   }
-  maxbits = (uint32_t)S.red[0];
+  maxbits = (uint32_t)S.sc.red[0];
   __syncthreads();
   const uint32_t N = slot_bits(maxbits, sub_bits_param);
   const uint32_t cap = N + kRecPad;  // records per slot
-  if ((int64_t)(kMaxSlots + NT) * cap > dd.rec_cap) {  // host sized the record buffer
+  if ((int64_t)(kMaxSlots + NT) * cap + kMaxSlots * 4 > dd.rec_cap) {  // host-sized records
     if (tid == 0) infos[img].status = kErrBadGeometry;
     return;
   }
@@ -880,6 +897,9 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
   const int seg_per_chunk = max(1, kMaxSlots / cmax);
   int16_t* coef_img = coefs + (size_t)dd.coef_off * 64;
   uint32_t* rec_img = recs + dd.rec_off;
+  // per-slot state {start pos, start z | bs << 8, records, end z}, after the
+  // records; each slot is only ever touched by the thread that owns it
+  uint4* sst = reinterpret_cast<uint4*>(rec_img + dd.rec_cap - kMaxSlots * 4);
   int rounds_total = 0;
   int64_t tph[4] = {0, 0, 0, 0};
   int64_t tstamp = wall_clock64();
@@ -905,12 +925,10 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       return rec_img + ((size_t)(k - r0) * (cap / 4) * NT + tid) * 4;
     };
     auto decode_k = [&](Dec& d, int k) {
-      S.s_pos[k] = d.pos;
-      S.s_zb[k] = d.z | (d.bs << 8);
+      const uint32_t p0 = d.pos, zb0 = d.z | (d.bs << 8);
       const uint32_t n = decode_slot<NT>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm,
                                          slot_end(k), seg_end_bits(slot_seg(k)), slot_recs(k));
-      S.s_nrec[k] = n;
-      S.s_endz[k] = (uint8_t)d.z;
+      sst[k] = make_uint4(p0, zb0, n, d.z);
     };
 
     // ---- round 0: every run from a guess at its first slot ----
@@ -948,7 +966,10 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       if (tid > 0 && r0 < r1 && !slot_known(r0) && !slot_empty(r0)) {
         npos = S.run_pos[tid - 1];
         nzb = S.run_zb[tid - 1];
-        if (nzb != 0xFFFFFFFFu && (npos != S.s_pos[r0] || nzb != S.s_zb[r0])) redo = true;
+        if (nzb != 0xFFFFFFFFu) {
+          const uint4 q = sst[r0];
+          redo = npos != q.x || nzb != q.y;
+        }
       }
       __syncthreads();
       if (redo) {
@@ -961,9 +982,12 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
             break;
           }
           const uint32_t zb = d.z | (d.bs << 8);
-          if (k > r0 && S.s_pos[k] == d.pos && S.s_zb[k] == zb) {
-            merged = true;
-            break;
+          if (k > r0) {
+            const uint4 q = sst[k];
+            if (q.x == d.pos && q.y == zb) {
+              merged = true;
+              break;
+            }
           }
           decode_k(d, k);
         }
@@ -1001,7 +1025,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
           v[1] = v[2] = v[3] = 0;
         }
         const uint32_t* R = slot_recs(k);
-        const int n = (int)S.s_nrec[k];
+        const int n = (int)sst[k].z;
         for (int i0 = 0; i0 < n; i0 += 16) {
           // four 16-byte record groups in flight
           uint4 qq[4];
@@ -1024,20 +1048,20 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
           }
         }
       }
-      S.scan_flag[tid] = flag;
-      for (int i = 0; i < 4; i++) S.scan_v[tid][i] = v[i];
+      S.sc.scan_flag[tid] = flag;
+      for (int i = 0; i < 4; i++) S.sc.scan_v[tid][i] = v[i];
       __syncthreads();
       for (int off = 1; off < NT; off <<= 1) {
         int pf = 0, pv[4] = {0, 0, 0, 0};
         const bool take = tid >= off;
         if (take) {
-          pf = S.scan_flag[tid - off];
-          for (int i = 0; i < 4; i++) pv[i] = S.scan_v[tid - off][i];
+          pf = S.sc.scan_flag[tid - off];
+          for (int i = 0; i < 4; i++) pv[i] = S.sc.scan_v[tid - off][i];
         }
         __syncthreads();
-        if (take && !S.scan_flag[tid]) {
-          for (int i = 0; i < 4; i++) S.scan_v[tid][i] += pv[i];
-          S.scan_flag[tid] = pf;
+        if (take && !S.sc.scan_flag[tid]) {
+          for (int i = 0; i < 4; i++) S.sc.scan_v[tid][i] += pv[i];
+          S.sc.scan_flag[tid] = pf;
         }
         __syncthreads();
       }
@@ -1052,10 +1076,10 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
     {
       int nb = 0, dc0 = 0, dc1 = 0, dc2 = 0;
       if (tid > 0) {
-        nb = S.scan_v[tid - 1][0];
-        dc0 = S.scan_v[tid - 1][1];
-        dc1 = S.scan_v[tid - 1][2];
-        dc2 = S.scan_v[tid - 1][3];
+        nb = S.sc.scan_v[tid - 1][0];
+        dc0 = S.sc.scan_v[tid - 1][1];
+        dc1 = S.sc.scan_v[tid - 1][2];
+        dc2 = S.sc.scan_v[tid - 1][3];
       }
       int rc = kOk;
       bool done = false;  // the segment's last block is complete
@@ -1070,7 +1094,8 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
         if (done) continue;
         const int seg_end_blk = ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks;
         const uint32_t* R = slot_recs(k);
-        const int n = (int)S.s_nrec[k];
+        const uint4 q = sst[k];
+        const int n = (int)q.z;
         for (int i0 = 0; i0 < n && !done && rc == kOk; i0 += 16) {
           // four 16-byte record groups in flight before their scatter stores
           uint4 qq[4];
@@ -1121,7 +1146,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
         // last slot of its segment: every block of the segment must be done
         const bool last = (k + 1 >= nslots) || slot_j(k + 1) == 0 || slot_empty(k + 1);
         if (rc == kOk && !done && last &&
-            (nb < seg_end_blk || (nb == seg_end_blk && S.s_endz[k] != 0)))
+            (nb < seg_end_blk || (nb == seg_end_blk && q.w != 0)))
           rc = kErrTruncated;
       }
       if (rc != kOk) atomicCAS(&S.err, kOk, rc);

@@ -121,6 +121,9 @@ class TarImageStream:
         members, _ = _lib.tar_index(view)
         self.members = [m for m in members if sel(m[0])]
         self._dec = _lib.Decoder(device_config.device_index)
+        # two pipelines: batch k+1's kernels share the CUs with batch k's
+        # latency-bound entropy decode (completion is tracked per ticket)
+        self._dec.set_param("lanes", 2 if self.depth >= 2 else 1)
         h, w = self._out_hw(view)
         self._shape = (3, h, w) if self.output.planar else (h, w, 3)
         self._dtype = self.output.torch_dtype
