@@ -97,6 +97,8 @@ def _args():
     p.add_argument("--entropy-threads", type=int, default=0)
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="pad224")
     p.add_argument("--norm-dtype", choices=["float16", "bfloat16"], default="float16")
+    p.add_argument("--inflight", type=int, default=2, choices=[1, 2, 3],
+                   help="batches submitted ahead before waiting the oldest")
     p.add_argument("--lanes", type=int, default=2,
                    help="concurrent decode pipelines in the context (1 or 2)")
     p.add_argument("--sync-steps", action="store_true",
@@ -117,7 +119,9 @@ def _pack_device(datas: list[bytes], device: torch.device):
         host[o : o + len(d)] = np.frombuffer(d, np.uint8)
     dev = torch.from_numpy(host).to(device)
     infos = [_lib.get_image_info(d) for d in datas]
-    return dev, offs, sizes, infos
+    # marshalled once: the step loop passes the same arrays every time
+    return (dev, np.asarray(offs, np.int64), np.asarray(sizes, np.int64),
+            (_lib.ImageInfo * len(infos))(*infos))
 
 
 def _cpu_baseline(datas, threads: int, n_images: int) -> dict:
@@ -170,27 +174,27 @@ def main():
     if a.workload == "imagenet":
         spec = Output(**{**IMAGENET_SPEC.__dict__, "norm_dtype": a.norm_dtype})
         outs = [torch.empty((a.batch, 3, 224, 224), dtype=spec.torch_dtype, device=device)
-                for _ in range(2)]
+                for _ in range(3)]
     else:
         spec = OUT_SPEC
         outs = [torch.empty((a.batch, 224, 224, 3), dtype=torch.uint8, device=device)
-                for _ in range(2)]
+                for _ in range(3)]
     out = outs[0]
     stream = torch.cuda.current_stream(device)
     nbytes_out = out.numel() * out.element_size()
     nsub = [0]
 
     def submit(sync: bool) -> int:
-        # two output buffers: with two lanes, batches k and k+1 run concurrently
-        o = outs[nsub[0] & 1]
+        # output buffer per in-flight batch (up to three)
+        o = outs[nsub[0] % len(outs)]
         nsub[0] += 1
         dec.decode_batch_device(dev.data_ptr(), dev.numel(), offs, sizes, infos, spec,
                                 o.data_ptr(), nbytes_out, stream=stream, sync=sync)
         return dec.last_ticket()
 
-    # Steps are submitted asynchronously through the decoder's ring (at most
-    # two batches in flight): batch k+1's host-side layout and launches
-    # overlap batch k's kernels, as in a data loader.  Each batch is waited
+    # Steps are submitted asynchronously through the decoder's ring (up to
+    # --inflight batches, executing on the context's two lanes):
+    # host-side layout and launches overlap the kernels, as in a data loader.  Each batch is waited
     # for (statuses checked) and its per-stage HIP-event timings collected.
     for _ in range(a.warmup):
         submit(True)
@@ -208,19 +212,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    prev = None
+    pending = []
     for _ in range(a.steps):
         if a.sync_steps:
             submit(True)
             for k, v in dec.last_timings().items():
                 stages[k] = stages.get(k, 0.0) + v
             continue
-        t = submit(False)
-        if prev is not None:
-            collect(prev)
-        prev = t
-    if prev is not None:
-        collect(prev)
+        pending.append(submit(False))
+        if len(pending) > a.inflight - 1:  # wait the oldest (the ring holds 3)
+            collect(pending.pop(0))
+    for t in pending:
+        collect(t)
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()

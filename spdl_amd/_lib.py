@@ -357,32 +357,48 @@ class Decoder:
     def decode_batch_device(self, dev_ptr: int, dev_bytes: int, offsets, sizes, infos,
                             out: Output, out_ptr: int, out_bytes: int, stream=None,
                             sync: bool = True) -> list[int]:
+        """``offsets``/``sizes``: sequences or int64 numpy arrays; ``infos``: a
+        sequence of ImageInfo or a prebuilt ``(ImageInfo * n)`` array (pass the
+        same objects again to skip re-marshalling on every call)."""
+        import numpy as np
+
         n = len(offsets)
-        offs = (ctypes.c_int64 * n)(*offsets)
-        szs = (ctypes.c_int64 * n)(*sizes)
-        inf = (ImageInfo * n)(*infos)
-        status = (ctypes.c_int32 * n)()
+        offs = np.ascontiguousarray(offsets, dtype=np.int64)
+        szs = np.ascontiguousarray(sizes, dtype=np.int64)
+        inf = infos if isinstance(infos, ctypes.Array) else (ImageInfo * n)(*infos)
+        status = np.zeros(n, np.int32)
         err = ctypes.create_string_buffer(1024)
-        spec = out.to_c()
+        spec = self._spec(out)
         rc = lib().spdl_hj_decode_batch_device(
-            self._h, dev_ptr, dev_bytes, offs, szs, inf, n, ctypes.byref(spec), out_ptr,
-            out_bytes, _stream_handle(stream), int(bool(sync)), status, err, 1024,
+            self._h, dev_ptr, dev_bytes, offs.ctypes.data, szs.ctypes.data, inf, n,
+            ctypes.byref(spec), out_ptr, out_bytes, _stream_handle(stream), int(bool(sync)),
+            status.ctypes.data, err, 1024,
         )
         if rc:
             raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
-        return list(status)
+        return status.tolist()
+
+    def _spec(self, out: Output) -> OutputSpec:
+        cache = self.__dict__.setdefault("_spec_cache", {})
+        spec = cache.get(out)
+        if spec is None:
+            spec = cache[out] = out.to_c()
+        return spec
 
     # ---- asynchronous submission / staging ring (include/spdl_hipjpeg.h) ----
     def last_ticket(self) -> int:
         return int(lib().spdl_hj_last_ticket(self._h))
 
     def wait(self, ticket: int, n: int = 0) -> list[int]:
-        status = (ctypes.c_int32 * max(n, 1))()
+        import numpy as np
+
+        status = np.zeros(max(n, 1), np.int32)
         err = ctypes.create_string_buffer(1024)
-        rc = lib().spdl_hj_wait(self._h, int(ticket), status if n else None, n, err, 1024)
+        rc = lib().spdl_hj_wait(self._h, int(ticket), status.ctypes.data if n else None, n, err,
+                                1024)
         if rc:
             raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
-        return list(status)[:n]
+        return status[:n].tolist()
 
     def stream_wait(self, ticket: int, stream) -> None:
         """Make `stream` wait on the device for batch `ticket`."""

@@ -669,7 +669,6 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   memcpy(slot.pin_desc.p, L.desc.data(), sizeof(ImageDesc) * n);
   HJ_HIP(hipMemcpyAsync(W.desc.p, slot.pin_desc.p, sizeof(ImageDesc) * n,
                         hipMemcpyHostToDevice, st));
-  HJ_HIP(hipMemsetAsync(W.coefs.p, 0, (size_t)L.total_blocks * 128, st));
   mark(ctx, slot, 1, st);
   auto* desc = static_cast<const ImageDesc*>(W.desc.p);
   auto* infos = static_cast<ImageInfo*>(W.info.p);

@@ -1071,6 +1071,18 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       tph[2] += t - tstamp;
       tstamp = t;
     }
+    // ---- clear the blocks whose DC symbol lies in this thread's run (a
+    // contiguous range; replaces a memset of the whole coefficient buffer):
+    // the write pass below may scatter into a block another run started, so
+    // the clears finish (barrier) before any coefficient is written ----
+    if (r0 < r1) {
+      int b0 = tid > 0 ? S.sc.scan_v[tid - 1][0] : 0;
+      if (slot_known(r0)) b0 = ri > 0 ? slot_seg(r0) * ri * bpm : 0;
+      const int b1 = min(S.sc.scan_v[tid][0], nblocks);
+      uint4* z4 = reinterpret_cast<uint4*>(coef_img);
+      for (int i = max(b0, 0) * 8; i < b1 * 8; i++) z4[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
     // ---- write pass: replay the records, dequantise, scatter to natural
     // order; the sequential decoder's stop and error rules per segment ----
     {
