@@ -13,7 +13,7 @@ import threading
 from dataclasses import dataclass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libspdl_hipjpeg.so")
+LIB_PATH = os.environ.get("SPDL_AMD_LIB") or os.path.join(_HERE, "lib", "libspdl_hipjpeg.so")
 
 ABI_VERSION = 1
 

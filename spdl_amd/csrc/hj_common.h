@@ -90,6 +90,12 @@ struct ImageDesc {      // host-filled per image
   int32_t pad3_;
   int64_t rec_off;      // entropy symbol records: offset (u32 units) and capacity
   int64_t rec_cap;
+  // resize weight tables depend only on the geometry: images of the same
+  // (component sizes, scaled size) share one table set at wt_off, computed
+  // by its owner (the first such image of the batch)
+  int32_t src_w[kMaxComp], src_h[kMaxComp];  // component sizes (host probe)
+  int32_t wt_owner;
+  int32_t pad4_;
 };
 
 // resize: source rows are staged kHMaxRows at a time (kHSrcBytes of LDS); the

@@ -17,6 +17,8 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -316,10 +318,21 @@ struct Layout {
   int ow = 0, oh = 0;
 };
 
+struct WtKey {
+  int ncomp;
+  int cw[3], ch[3];
+  int sw, sh;
+  bool operator<(const WtKey& o) const {
+    return std::tie(ncomp, cw[0], cw[1], cw[2], ch[0], ch[1], ch[2], sw, sh) <
+           std::tie(o.ncomp, o.cw[0], o.cw[1], o.cw[2], o.ch[0], o.ch[1], o.ch[2], o.sw, o.sh);
+  }
+};
+
 int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_image_info* infos,
                  int n, const spdl_hj_output* out, int sub_bits, Layout& L, int32_t* status,
                  char* err, size_t errlen) {
   L.desc.assign(n, ImageDesc{});
+  std::map<WtKey, int64_t> wt_tables;
   for (int i = 0; i < n; i++) {
     ImageDesc& d = L.desc[i];
     const spdl_hj_image_info& p = infos[i];
@@ -420,7 +433,12 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
               L.ow, L.oh, i, g.ow, g.oh);
       return SPDL_HJ_ERR_INVALID_ARG;
     }
+    for (int c = 0; c < p.ncomp; c++) {
+      d.src_w[c] = cw[c];
+      d.src_h[c] = chh[c];
+    }
     d.wt_off = L.total_wts;
+    d.wt_owner = 0;
     if (out->resize) {
       for (int c = 0; c < p.ncomp; c++) {
         d.taps_x[c] = max_taps(cw[c], g.sw, out->filter);
@@ -433,8 +451,19 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
                   i, p.width, p.height, g.sw, g.sh);
           return SPDL_HJ_ERR_BAD_GEOMETRY;
         }
-        L.total_wts += (int64_t)g.sw * (1 + (d.taps_x[c] + 1) / 2) +
-                       (int64_t)g.sh * (1 + (d.taps_y[c] + 1) / 2);
+      }
+      // one table set per distinct geometry (all images of a uniform batch
+      // share the first one's)
+      WtKey key{p.ncomp, {cw[0], cw[1], cw[2]}, {chh[0], chh[1], chh[2]}, g.sw, g.sh};
+      auto it = wt_tables.find(key);
+      if (it != wt_tables.end()) {
+        d.wt_off = it->second;
+      } else {
+        wt_tables.emplace(key, L.total_wts);
+        d.wt_owner = 1;
+        for (int c = 0; c < p.ncomp; c++)
+          L.total_wts += (int64_t)g.sw * (1 + (d.taps_x[c] + 1) / 2) +
+                         (int64_t)g.sh * (1 + (d.taps_y[c] + 1) / 2);
       }
       int ml = g.sw > g.sh ? g.sw : g.sh;
       if (ml > L.max_len) L.max_len = ml;

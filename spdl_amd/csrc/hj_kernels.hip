@@ -229,7 +229,7 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
   }
 }
 
-__global__ void __launch_bounds__(256) parse_kernel(const uint8_t* __restrict__ bytes,
+__global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict__ bytes,
                                                     const ImageDesc* __restrict__ desc,
                                                     ImageInfo* __restrict__ infos,
                                                     HuffTable* __restrict__ luts) {
@@ -1346,12 +1346,13 @@ __global__ void __launch_bounds__(256) weights_kernel(const ImageDesc* __restric
                                                       int32_t* __restrict__ pool,
                                                       const int filter) {
   const int img = blockIdx.z, which = blockIdx.y;  // which = plane*2 + axis
-  const ImageInfo& in = infos[img];
-  if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
+  // shared tables: only the owner writes them, whatever its decode status
+  // (the table depends on host-known geometry only)
+  if (!dd.wt_owner) return;
   const int c = which >> 1, axis = which & 1;
   if (c >= dd.ncomp) return;
-  const int src_len = axis == 0 ? in.comp_w[c] : in.comp_hpx[c];
+  const int src_len = axis == 0 ? dd.src_w[c] : dd.src_h[c];
   const int dst_len = axis == 0 ? dd.sw : dd.sh;
   const int taps = axis == 0 ? dd.taps_x[c] : dd.taps_y[c];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
