@@ -37,7 +37,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # Per-launch HBM-side bytes per kernel from the committed rocprofv3 --pmc
 # passes of this same command (tools/pmc_passes.sh + tools/pmc_traffic.py):
 # FETCH_SIZE / WRITE_SIZE cannot be read from inside the timed process.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v6", "traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v7", "traffic.json")
 # bench stage -> kernels launched in it
 STAGE_KERNELS = {
     "parse": ["hj::parse_kernel"],
@@ -86,8 +86,8 @@ WORKLOADS = {
 def _args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch", type=int, default=BATCH)
     p.add_argument("--distinct", type=int, default=32)
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -294,7 +294,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": _pmc_traffic(dominant, a.batch) if a.workload == "pad224" else None,
-                "traffic_source": "profiles/r01_v6/traffic.json (rocprofv3 --pmc FETCH_SIZE, "
+                "traffic_source": "profiles/r01_v7/traffic.json (rocprofv3 --pmc FETCH_SIZE, "
                                   "WRITE_SIZE; separate passes; x1024, FETCH x2 gfx950)",
                 "algorithmic_bytes_per_image": round(per_image_bytes, 1),
             },
