@@ -209,6 +209,19 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
                           size_t coef_cap, uint8_t* clean, size_t clean_cap, int32_t* diag,
                           char* err, size_t errlen);
 
+/* Batched NV12 -> planar RGB (bgr == 0) or BGR: src_dev is
+ * [num_frames, h2 = 1.5 H, width] u8 in device memory (pitch = width), dst_dev
+ * [num_frames, 3, H, width] u8.  matrix_coeff selects the matrix (1 BT.709
+ * default, 4 FCC, 5 BT.470, 6 BT.601, 7 SMPTE240M, 8 YCgCo, 9 BT.2020,
+ * 10 BT.2020C; other values mean 1).  Replaces nv12_to_planar_rgb/bgr
+ * (reference src/libspdl/cuda/color_conversion.cpp:27-95,
+ * detail/color_conversion.cu:90-138); like it, quads with x + 1 >= width are
+ * not written.  Needs no context (stateless). */
+int spdl_hj_nv12_to_planar_rgb(const uint8_t* src_dev, int32_t num_frames, int32_t h2,
+                               int32_t width, int32_t bgr, int32_t matrix_coeff, uint8_t* dst_dev,
+                               size_t dst_bytes, int device, void* stream, int32_t sync, char* err,
+                               size_t errlen);
+
 /* Per-kernel timing of the last batch, in microseconds, measured with HIP
  * events on the decode stream (filled only when enabled). */
 int spdl_hj_set_profiling(spdl_hj_ctx* ctx, int32_t enable);

@@ -1201,3 +1201,54 @@ int jo_decode_rgb_batch(const uint8_t* const* data, const size_t* sizes, int n, 
   j.status = status;
   return run_batch(&j, nthreads);
 }
+
+/* ---- NV12 -> planar RGB/BGR (the video path's colour conversion) ---------
+ * Restates the reference kernel nv12_to_planar_rgb24
+ * (src/libspdl/cuda/detail/color_conversion.cu:90-138, matrices :19-68,
+ * wrapper src/libspdl/cuda/color_conversion.cpp:27-78): per 2x2 luma quad
+ * one (U, V) pair; r = M[0][0]*(Y-16) + M[0][1]*(U-128) + M[0][2]*(V-128) in
+ * fp32 with the multiply-adds contracted the way LLVM's DAG combiner fuses
+ * (a*b + c*d) + e*f  ->  fma(e, f, fma(a, b, c*d)); clamp to [0, 255] and
+ * truncate.  Quads with x + 1 >= width are not written (the reference
+ * returns before writing them).  coeff outside 1..10 means 1 (BT.709).
+ * Parity unpinned vs the CUDA build (no CUDA toolchain here): the
+ * contraction order is the stated assumption. */
+static const float jo_yuv2rgb[10][3][3] = {
+    {{1.1644f, 0.0000f, 1.8337f}, {1.1644f, -0.2181f, -0.5451f}, {1.1644f, 2.1606f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.8337f}, {1.1644f, -0.2181f, -0.5451f}, {1.1644f, 2.1606f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.8337f}, {1.1644f, -0.2181f, -0.5451f}, {1.1644f, 2.1606f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.6301f}, {1.1644f, -0.3864f, -0.8289f}, {1.1644f, 2.0726f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.6325f}, {1.1644f, -0.4007f, -0.8315f}, {1.1644f, 2.0633f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.6325f}, {1.1644f, -0.4007f, -0.8315f}, {1.1644f, 2.0633f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.8351f}, {1.1644f, -0.2639f, -0.5550f}, {1.1644f, 2.1262f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.8337f}, {1.1644f, -0.2181f, -0.5451f}, {1.1644f, 2.1606f, 0.0000f}},
+    {{1.1689f, 0.0000f, 1.7237f}, {1.1689f, -0.1924f, -0.6679f}, {1.1689f, 2.1992f, 0.0000f}},
+    {{1.1689f, 0.0000f, 1.7237f}, {1.1689f, -0.1924f, -0.6679f}, {1.1689f, 2.1992f, 0.0000f}},
+};
+
+static uint8_t jo_clamp8f(float x) { return x < 0.0f ? 0 : (x > 255.0f ? 255 : (uint8_t)x); }
+
+void jo_nv12_to_rgb(const uint8_t* src, int frames, int height, int width, int bgr, int coeff,
+                    uint8_t* dst) {
+  if (coeff <= 0 || coeff > 10) coeff = 1;
+  const float(*m)[3] = jo_yuv2rgb[coeff - 1];
+  const size_t fsz = (size_t)(height + height / 2) * width, osz = (size_t)3 * height * width;
+  for (int f = 0; f < frames; f++) {
+    const uint8_t* yuv = src + f * fsz;
+    uint8_t* rgb = dst + f * osz;
+    for (int y = 0; y + 1 < height; y += 2)
+      for (int x = 0; x + 1 < width; x += 2) {
+        const uint8_t* uv = yuv + (size_t)(height + y / 2) * width + x;
+        const float fu = (float)((int)uv[0] - 128), fv = (float)((int)uv[1] - 128);
+        for (int dy = 0; dy < 2; dy++)
+          for (int dx = 0; dx < 2; dx++) {
+            const float fy = (float)((int)yuv[(size_t)(y + dy) * width + x + dx] - 16);
+            for (int ch = 0; ch < 3; ch++) {
+              const float v = fmaf(m[ch][2], fv, fmaf(m[ch][0], fy, m[ch][1] * fu));
+              const int oc = bgr ? 2 - ch : ch;
+              rgb[(size_t)oc * height * width + (size_t)(y + dy) * width + x + dx] = jo_clamp8f(v);
+            }
+          }
+      }
+  }
+}

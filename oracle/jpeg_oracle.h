@@ -149,6 +149,8 @@ uint16_t jo_f32_to_bf16(float f);
 
 /* Multi-threaded batch (CPU baseline).  Image i goes to out + i*out_stride
  * bytes.  status[i] receives the per-image code.  Returns #failed. */
+void jo_nv12_to_rgb(const uint8_t* src, int frames, int height, int width, int bgr, int coeff,
+                    uint8_t* dst);
 int jo_decode_resize_batch(const uint8_t* const* data, const size_t* sizes, int n,
                            int idct, const jo_resize* rs, int fmt, int dtype,
                            const float* mean, const float* stdv,

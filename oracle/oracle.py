@@ -316,6 +316,21 @@ def decode_resize_batch(
     return out, status, failed
 
 
+def nv12_to_rgb(nv12: np.ndarray, coeff: int = 1, bgr: bool = False) -> np.ndarray:
+    """[F, 1.5H, W] u8 NV12 -> [F, 3, H, W] u8 (jo_nv12_to_rgb; quads with
+    x + 1 >= W are left 0 here, unwritten by the reference)."""
+    a = np.ascontiguousarray(nv12, np.uint8)
+    F, h2, W = a.shape
+    H = h2 // 3 * 2
+    out = np.zeros((F, 3, H, W), np.uint8)
+    L = lib()
+    L.jo_nv12_to_rgb.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    L.jo_nv12_to_rgb.restype = None
+    L.jo_nv12_to_rgb(a.ctypes.data, F, H, W, int(bool(bgr)), int(coeff), out.ctypes.data)
+    return out
+
+
 def idct_block(coefs: np.ndarray, idct: int = IDCT_SIMPLE) -> np.ndarray:
     c = np.ascontiguousarray(coefs, np.int16).reshape(64)
     out = np.zeros(64, np.uint8)

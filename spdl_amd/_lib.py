@@ -47,6 +47,7 @@ EXPORTED = (
     "spdl_hj_staging_read",
     "spdl_hj_decode_staged",
     "spdl_hj_tar_index",
+    "spdl_hj_nv12_to_planar_rgb",
 )
 
 
@@ -197,6 +198,9 @@ def lib() -> ctypes.CDLL:
         ]
         L.spdl_hj_tar_index.argtypes = [
             vp, sz, sz, i32, vp, vp, vp, vp, sz, ctypes.POINTER(i32), ctypes.POINTER(sz)
+        ]
+        L.spdl_hj_nv12_to_planar_rgb.argtypes = [
+            vp, i32, i32, i32, i32, i32, vp, sz, ctypes.c_int, vp, i32, cp, sz
         ]
         ver = L.spdl_hj_abi_version()
         if ver != ABI_VERSION:

@@ -40,6 +40,7 @@ hipError_t launch_weights(const ImageDesc*, const ImageInfo*, int32_t*, int, int
                           hipStream_t);
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                       const BatchParams&, int64_t, int, hipStream_t);
+hipError_t launch_nv12(const uint8_t*, uint8_t*, int, int, int, int, int, hipStream_t);
 hipError_t launch_resize(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*,
                          uint8_t*, void*, const BatchParams&, int64_t, int64_t, int, hipStream_t);
 }  // namespace hj
@@ -1320,6 +1321,32 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
     size_t n = (size_t)hi.clean_len < clean_cap ? (size_t)hi.clean_len : clean_cap;
     HJ_HIP(hipMemcpy(clean, W.clean.p, n, hipMemcpyDeviceToHost));
   }
+  return SPDL_HJ_OK;
+}
+
+int spdl_hj_nv12_to_planar_rgb(const uint8_t* src_dev, int32_t num_frames, int32_t h2,
+                               int32_t width, int32_t bgr, int32_t matrix_coeff, uint8_t* dst_dev,
+                               size_t dst_bytes, int device, void* stream, int32_t sync, char* err,
+                               size_t errlen) {
+  if (!src_dev || !dst_dev || num_frames < 0 || width <= 0 || h2 <= 0) {
+    set_err(err, errlen, "invalid argument");
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  if (h2 % 3 != 0) {  // reference: src/libspdl/cuda/color_conversion.cpp:45-50
+    set_err(err, errlen,
+            "The height of NV12 image (h*1.5) must be divisible by 3. Found: %d", (int)h2);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  const int32_t height = h2 / 3 * 2;
+  if ((size_t)num_frames * 3 * height * width > dst_bytes) {
+    set_err(err, errlen, "output buffer too small");
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  if (matrix_coeff <= 0 || matrix_coeff > 10) matrix_coeff = 1;  // silently BT.709
+  DeviceGuard g(device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HJ_HIP(launch_nv12(src_dev, dst_dev, num_frames, height, width, bgr != 0, matrix_coeff, st));
+  if (sync) HJ_HIP(hipStreamSynchronize(st));
   return SPDL_HJ_OK;
 }
 

@@ -1775,6 +1775,66 @@ hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageI
   hipLaunchKernelGGL(csc_kernel, dim3(gx, n), dim3(256), 0, st, planes, desc, infos, out, p);
   return hipGetLastError();
 }
+// ---------------------------------------------------------------------------
+// NV12 -> planar RGB/BGR (the video path's colour conversion; reference
+// src/libspdl/cuda/detail/color_conversion.cu:90-138).  One thread per 2x2
+// luma quad, x fastest so the 2-byte loads and stores of a wave are
+// contiguous.  Arithmetic: oracle jo_nv12_to_rgb (explicit fma order).
+// ---------------------------------------------------------------------------
+__constant__ float kYuv2Rgb[10][3][3] = {
+    {{1.1644f, 0.0000f, 1.8337f}, {1.1644f, -0.2181f, -0.5451f}, {1.1644f, 2.1606f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.8337f}, {1.1644f, -0.2181f, -0.5451f}, {1.1644f, 2.1606f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.8337f}, {1.1644f, -0.2181f, -0.5451f}, {1.1644f, 2.1606f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.6301f}, {1.1644f, -0.3864f, -0.8289f}, {1.1644f, 2.0726f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.6325f}, {1.1644f, -0.4007f, -0.8315f}, {1.1644f, 2.0633f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.6325f}, {1.1644f, -0.4007f, -0.8315f}, {1.1644f, 2.0633f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.8351f}, {1.1644f, -0.2639f, -0.5550f}, {1.1644f, 2.1262f, 0.0000f}},
+    {{1.1644f, 0.0000f, 1.8337f}, {1.1644f, -0.2181f, -0.5451f}, {1.1644f, 2.1606f, 0.0000f}},
+    {{1.1689f, 0.0000f, 1.7237f}, {1.1689f, -0.1924f, -0.6679f}, {1.1689f, 2.1992f, 0.0000f}},
+    {{1.1689f, 0.0000f, 1.7237f}, {1.1689f, -0.1924f, -0.6679f}, {1.1689f, 2.1992f, 0.0000f}},
+};
+
+__device__ __forceinline__ uint8_t clamp8f(float x) {
+  return x < 0.0f ? 0 : (x > 255.0f ? 255 : (uint8_t)x);
+}
+
+__global__ void __launch_bounds__(256) nv12_kernel(const uint8_t* __restrict__ src,
+                                                   uint8_t* __restrict__ dst, int height,
+                                                   int width, int bgr, int coeff) {
+  const int qx = blockIdx.x * 256 + threadIdx.x, qy = blockIdx.y, f = blockIdx.z;
+  const int x = 2 * qx, y = 2 * qy;
+  if (x + 1 >= width || y + 1 >= height) return;
+  const float(*m)[3] = kYuv2Rgb[coeff - 1];
+  const uint8_t* yuv = src + (size_t)f * (height + height / 2) * width;
+  uint8_t* rgb = dst + (size_t)f * 3 * height * width;
+  const uint8_t* uv = yuv + (size_t)(height + qy) * width + x;
+  const float fu = (float)((int)uv[0] - 128), fv = (float)((int)uv[1] - 128);
+  const size_t plane = (size_t)height * width;
+#pragma unroll
+  for (int dy = 0; dy < 2; dy++) {
+    const uint8_t* yr = yuv + (size_t)(y + dy) * width + x;
+    const float y0 = (float)((int)yr[0] - 16), y1 = (float)((int)yr[1] - 16);
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+      const float t = m[ch][1] * fu;
+      const uint8_t a = clamp8f(__fmaf_rn(m[ch][2], fv, __fmaf_rn(m[ch][0], y0, t)));
+      const uint8_t b = clamp8f(__fmaf_rn(m[ch][2], fv, __fmaf_rn(m[ch][0], y1, t)));
+      uint8_t* o = rgb + (size_t)(bgr ? 2 - ch : ch) * plane + (size_t)(y + dy) * width + x;
+      o[0] = a;
+      o[1] = b;
+    }
+  }
+}
+
+hipError_t launch_nv12(const uint8_t* src, uint8_t* dst, int frames, int height, int width,
+                       int bgr, int coeff, hipStream_t st) {
+  const int qx = width / 2, qy = height / 2;
+  if (frames <= 0 || qx <= 0 || qy <= 0) return hipSuccess;
+  hipLaunchKernelGGL(nv12_kernel, dim3((qx + 255) / 256, qy, frames), dim3(256), 0, st, src, dst,
+                     height, width, bgr, coeff);
+  return hipGetLastError();
+}
+
 hipError_t launch_resize(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
                          const int32_t* pool, uint8_t* rplanes, void* out, const BatchParams& p,
                          int64_t max_bands, int64_t max_quads, int n, hipStream_t st) {

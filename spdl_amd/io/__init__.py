@@ -2,6 +2,7 @@
 reference src/spdl/io/__init__.py:20-86), backed by gfx950 HIP kernels."""
 
 from ._buffer import CPUBuffer, CUDABuffer
+from ._color import nv12_to_bgr, nv12_to_rgb
 from ._config import CUDAConfig, cuda_config
 from ._convert import to_numpy, to_torch
 from ._image import (
@@ -31,6 +32,8 @@ __all__ = [
     "load_image_batch",
     "load_image_batch_hip",
     "load_image_batch_nvjpeg",
+    "nv12_to_bgr",
+    "nv12_to_rgb",
     "parse_image_filter",
     "to_numpy",
     "to_torch",

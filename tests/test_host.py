@@ -17,7 +17,7 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 
 def _declared_symbols():
     hdr = open(os.path.join(ROOT, "include", "spdl_hipjpeg.h")).read()
-    return sorted(set(re.findall(r"\b(spdl_hj_[a-z_]+)\s*\(", hdr)))
+    return sorted(set(re.findall(r"\b(spdl_hj_[a-z0-9_]+)\s*\(", hdr)))
 
 
 def test_library_exports_every_declared_symbol():
