@@ -42,14 +42,41 @@ inline HJ_HD uint32_t slot_bits(uint32_t maxbits, int sub_bits) {
   return need > n ? need : n;
 }
 
-// LUT entry (u32): [0:5) nbits consumed, [5:7) kind, [8:16) symbol,
-// [16:32) value (int16, kind==Full) or sub-table index (kind==Sub)
+// LUT entry (u32), everything a decode step needs precomputed:
+//   [0,5)   bits taken by the code (Full: code + value bits)
+//   [5,7)   kind
+//   [7,12)  value bits that follow the code (0 for Full)
+//   [12,19) z advance: DC 1, AC coefficient run+1, ZRL 16, EOB or any other
+//           size-0 AC symbol 64 (ends the block)
+//   [19]    the symbol yields a coefficient
+//   [20]    AC size-0 symbol other than EOB / ZRL (the sequential decoder
+//           rejects it)
+//   [21,32) Full: the value (int11); Sub: the sub-table index
 constexpr uint32_t kKindSlow = 0;  // invalid, or a sub-table that did not fit
 constexpr uint32_t kKindCode = 1;  // code resolved, value bits follow
 constexpr uint32_t kKindFull = 2;  // code + value resolved
 constexpr uint32_t kKindSub = 3;   // code longer than kLutBits: look up sub[idx][next 6 bits]
 constexpr int kSubBits = 16 - kLutBits;
 constexpr int kMaxSub = 16;        // 64-entry sub-tables per Huffman table
+constexpr int kEntHiShift = 21;    // value / sub-table index field
+
+inline HJ_HD uint32_t hj_entry(uint32_t kind, int len, int sym, bool is_dc, int v) {
+  const int size = is_dc ? sym : (sym & 15);
+  const int run = is_dc ? 0 : (sym >> 4);
+  uint32_t zinc, coef = 0, bad = 0;
+  if (is_dc || size) {
+    zinc = (uint32_t)run + 1u;
+    coef = 1;
+  } else if (run == 15) {
+    zinc = 16;
+  } else {
+    zinc = 64;
+    bad = run != 0;
+  }
+  const uint32_t sz = kind == kKindFull ? 0u : (uint32_t)size;
+  return (uint32_t)len | (kind << 5) | (sz << 7) | (zinc << 12) | (coef << 19) | (bad << 20) |
+         (((uint32_t)v & 0x7FFu) << kEntHiShift);
+}
 
 struct HuffTable {
   uint32_t lut[kLutSize];

@@ -402,12 +402,9 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     L.total_ds += d.ds_cap;
     if (d.ds_cap > L.max_chunks) L.max_chunks = d.ds_cap;
     {
-      // entropy records: kMaxSlots slots of N + kRecPad records, N bounded by
-      // the compressed size (the device derives N from the destuffed length)
-      const uint64_t bits = (uint64_t)sizes[i] * 8u;
-      const uint32_t nb = slot_bits(bits > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bits, sub_bits);
-      // + per-slot state (uint4 per slot) at the end
-      d.rec_cap = (int64_t)(kMaxSlots + kMaxEntropyThreads) * (nb + kRecPad) + kMaxSlots * 4;
+      // entropy slot state (u32 units): two uint4 per slot -- start state,
+      // blocks started, end z, DC sums
+      d.rec_cap = (int64_t)kMaxSlots * 8;
       d.rec_off = L.total_recs;
       L.total_recs += d.rec_cap;
     }

@@ -323,46 +323,42 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     }
     const int nsub = p_hi >= p_lo ? p_hi - p_lo + 1 : 0;
     const bool sub_ok = nsub <= kMaxSub;
-    // one 16-bit window -> entry (levels share this)
-    auto entry16 = [&](uint32_t w16, int max_len) -> uint32_t {
+    // one 16-bit window -> entry (levels share this): codes up to max_len
+    // bits; the value is folded in (Full) when code + value fit full_max bits
+    // (level 1: |v| < 2^9; sub-tables: codes >= 11 bits, |v| < 2^5 -- both
+    // fit the entry's int11 field)
+    auto entry16 = [&](uint32_t w16, int max_len, int full_max) -> uint32_t {
       for (int l = 1; l <= max_len; l++) {
         const int code = (int)(w16 >> (16 - l));
         if (code <= s.maxcode[t][l]) {
           const int sym = s.vals[t][s.valoff[t][l] + code];
           const int sz = is_dc ? sym : (sym & 15);
           if (is_dc && sym > 15) return 0u;  // invalid size -> slow path reports it
-          if (l + sz <= 16) {
+          if (l + sz <= full_max) {
             int v = 0;
             if (sz) {
               const int raw = (int)((w16 >> (16 - l - sz)) & ((1u << sz) - 1));
               v = raw < (1 << (sz - 1)) ? raw - ((1 << sz) - 1) : raw;
             }
-            return (uint32_t)(l + sz) | (kKindFull << 5) | ((uint32_t)sym << 8) |
-                   ((uint32_t)(uint16_t)(int16_t)v << 16);
+            return hj_entry(kKindFull, l + sz, sym, is_dc, v);
           }
-          return (uint32_t)l | (kKindCode << 5) | ((uint32_t)sym << 8);
+          return hj_entry(kKindCode, l, sym, is_dc, 0);
         }
       }
       return 0u;
     };
     for (int idx = tid; idx < kLutSize; idx += blockDim.x) {
       // level 1 resolves codes (and code+value) that fit in kLutBits
-      uint32_t e = entry16((uint32_t)idx << kSubBits, kLutBits);
-      if ((e >> 5 & 3) == kKindFull && (e & 31) > kLutBits) {
-        // value bits beyond the level-1 window: keep the code, read the value later
-        const uint32_t sym = (e >> 8) & 0xFF;
-        const int sz = is_dc ? (int)sym : (int)(sym & 15);
-        e = (uint32_t)((e & 31) - sz) | (kKindCode << 5) | (sym << 8);
-      }
+      uint32_t e = entry16((uint32_t)idx << kSubBits, kLutBits, kLutBits);
       if (e == 0u && idx >= p_lo && idx <= p_hi)
-        e = sub_ok ? ((kKindSub << 5) | ((uint32_t)(idx - p_lo) << 16)) : 0u;
+        e = sub_ok ? ((kKindSub << 5) | ((uint32_t)(idx - p_lo) << kEntHiShift)) : 0u;
       tabs[t].lut[idx] = e;
     }
     if (sub_ok)
       for (int i = tid; i < nsub << kSubBits; i += blockDim.x)
         tabs[t].sub[i] = entry16(((uint32_t)(p_lo + (i >> kSubBits)) << kSubBits) |
                                      (uint32_t)(i & ((1 << kSubBits) - 1)),
-                                 16);
+                                 16, 16);
     if (tid == 0) tabs[t].nsub = sub_ok ? nsub : 0;
     for (int i = tid; i < 18; i += blockDim.x) tabs[t].maxcode[i] = s.maxcode[t][i];
     for (int i = tid; i < 17; i += blockDim.x) tabs[t].valoff[i] = s.valoff[t][i];
@@ -714,86 +710,151 @@ __device__ __attribute__((noinline)) uint32_t slow_symbol(const SH& S, int t, ui
     if (code <= S.maxcode[t][l]) {
       const int sym = S.vals[t][S.valoff[t][l] + code];
       if (is_dc && sym > 15) return 0;
-      return (uint32_t)l | (kKindCode << 5) | ((uint32_t)sym << 8);
+      return hj_entry(kKindCode, l, sym, is_dc, 0);
     }
   }
   return 0;
 }
 
-// Symbol records.  Round 0 and the sync rounds store, per slot, one 32-bit
-// record for every symbol that yields a coefficient and for every symbol the
-// sequential decoder would reject; the write pass replays the records of the
-// final (synchronised) trajectory without decoding again.  Layout per image
-// and pass: [local slot][record / 4][thread][record % 4], so the lanes of a
-// wave store and load adjacent 16-byte groups.
-//   [0,16)  level (int16, before dequantisation; DC: the difference)
-//   [16,22) zigzag index (coefficient) or z before the symbol (marker)
-//   [22]    DC symbol
-//   [23,25) component
-//   [25,27) kind: coefficient / invalid Huffman data / symbol crosses the end
-constexpr uint32_t kRecCoef = 0;
-constexpr uint32_t kRecErrHuff = 1;
-constexpr uint32_t kRecErrTrunc = 2;
+// The entry of the symbol at the head of `hi` in table slot t (two-level LUT,
+// canonical fallback); 0 = invalid code.
+template <class SH>
+__device__ __forceinline__ uint32_t lookup(const SH& S, uint32_t t, uint32_t hi, uint64_t buf,
+                                           bool is_dc) {
+  uint32_t e = S.lut[t][hi >> (32 - kLutBits)];
+  if (((e >> 5) & 3) == kKindSub)
+    e = S.sub[((e >> kEntHiShift) << kSubBits) |
+              ((hi >> (32 - kLutBits - kSubBits)) & ((1u << kSubBits) - 1))];
+  if (((e >> 5) & 3) == kKindSlow) e = slow_symbol(S, (int)t, buf, is_dc);
+  return e;
+}
 
-// Decode every symbol that starts in [d.pos, end) and append its records to
-// `rec`; returns the record count (<= end - d.pos + 1).  Total over any bit
-// position: an invalid code consumes one bit, a run past coefficient 63 ends
-// the block, so every start state yields one deterministic trajectory.  One
-// path for DC and AC symbols (selects, not branches: the 64 lanes of a wave
-// decode 64 unrelated streams, so any branch is paid by all of them).
+// Per-slot sums of the state-only decode: blocks started and DC differences
+// per component (the inputs of the block-index / DC-predictor scan).
+struct SlotSums {
+  int nblk, dc0, dc1, dc2;
+};
+
+// State-only decode of every symbol that starts in [d.pos, end): bit
+// position, z and block-in-MCU advance, block count and DC sums -- no
+// stores, so the loop carries no memory traffic besides the bit window.
+// Total over any bit position: an invalid code consumes one bit, a run past
+// coefficient 63 ends the block, so every start state has one trajectory.
+// One path for DC and AC (selects, not branches: the 64 lanes of a wave
+// decode 64 unrelated streams).
 template <int NT, class SH>
-__device__ uint32_t decode_slot(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
-                                const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
-                                const uint32_t end, const uint32_t seg_end,
-                                uint32_t* __restrict__ rec) {
-  auto at = [&](uint32_t n) -> uint32_t& { return rec[(n >> 2) * (NT * 4) + (n & 3)]; };
-  uint32_t n = 0;
+__device__ void decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
+                             const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
+                             const uint32_t end, SlotSums& ss) {
   while (d.pos < end) {
     dec_restage<NT>(d, win, words);
     dec_refill<NT>(d, win);
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
-    // component of this block, then its DC or AC table slot
     const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
     const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
     const uint32_t hi = (uint32_t)(d.buf >> 32);
-    uint32_t e = S.lut[t][hi >> (32 - kLutBits)];
-    if (((e >> 5) & 3) == kKindSub)
-      e = S.sub[((e >> 16) << kSubBits) | ((hi >> (32 - kLutBits - kSubBits)) & ((1u << kSubBits) - 1))];
-    if (((e >> 5) & 3) == kKindSlow) e = slow_symbol(S, (int)t, d.buf, is_dc);
+    const uint32_t e = lookup(S, t, hi, d.buf, is_dc);
     const bool valid = e != 0u;
-    const uint32_t sym = (e >> 8) & 0xFF;
-    const uint32_t sz = ((e >> 5) & 3) == kKindFull ? 0u : (is_dc ? sym : (sym & 15u));
-    const uint32_t nbits = (valid ? (e & 31u) : 1u) + sz;  // <= 31: hi holds >= 32 valid bits
+    const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
+    const uint32_t nbits = valid ? (e & 31u) + sz : 1u;  // <= 31
+    // DC difference (JPEG EXTEND; Full entries carry it, sz == 0 there)
     const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
     const uint32_t msk = (1u << sz) - 1u;
-    // Full entries carry the value in bits 16..31 (sz == 0 there); Code
-    // entries have zeros there and the value follows the code (JPEG EXTEND)
-    const int v = (int)(int16_t)(e >> 16) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
+    const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
+    const bool dcok = is_dc && valid;
+    const int dv = dcok ? v : 0;
+    ss.nblk += dcok ? 1 : 0;
+    ss.dc0 += c == 0u ? dv : 0;
+    ss.dc1 += c == 1u ? dv : 0;
+    ss.dc2 += c == 2u ? dv : 0;
     d.buf <<= nbits;
     d.cnt -= (int)nbits;
     d.pos += nbits;
-    const uint32_t r = is_dc ? 0u : (sym >> 4);
-    const bool coef = is_dc || (sym & 15u) != 0u;
-    const uint32_t zpos = z + r;
-    const bool bad_run = coef && zpos > 63u;
-    const bool bad = !valid || bad_run || (!coef && r != 0u && r != 15u);
-    uint32_t zn = coef ? zpos + 1u : (r == 15u ? z + 16u : 64u);
-    zn = bad_run ? 64u : zn;
-    zn = valid ? zn : z;
-    const uint32_t rc = ((uint32_t)v & 0xFFFFu) | (zpos << 16) | ((uint32_t)is_dc << 22) | (c << 23);
-    const uint32_t rb = (kRecErrHuff << 25) | (z << 16);
-    // unconditional store: a symbol without a record is overwritten by the next
-    at(n) = bad ? rb : rc;
-    n += (bad || coef) ? 1u : 0u;
-    if (d.pos > seg_end) at(n++) = (kRecErrTrunc << 25) | (z << 16);
+    const uint32_t zn = valid ? z + __builtin_amdgcn_ubfe(e, 12, 7) : z;
     const bool bend = zn >= 64u;
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
-  return n;
 }
+
+// Full decode of the symbols that start in [d.pos, end) from a synchronised
+// state: dequantise, scatter in natural order, and apply the sequential
+// decoder's stop / error rules of the segment (blocks [.., seg_end_blk),
+// scan bits [.., seg_end)) -- oracle jo_decode_coefs.  nb = blocks started so
+// far (absolute), dc* = DC predictors (sums of differences).  Returns the
+// status; sets `done` once the segment's last block is complete.
+template <int NT, class SH>
+__device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
+                            const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
+                            const uint32_t end, const uint32_t seg_end, const int seg_end_blk,
+                            int16_t* __restrict__ coef_img, int& nb, int& dc0, int& dc1, int& dc2,
+                            bool& done) {
+  int rc = kOk;
+  while (d.pos < end && !done && rc == kOk) {
+    dec_restage<NT>(d, win, words);
+    dec_refill<NT>(d, win);
+    const uint32_t z = d.z;
+    const bool is_dc = z == 0;
+    const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
+    const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
+    const uint32_t hi = (uint32_t)(d.buf >> 32);
+    const uint32_t e = lookup(S, t, hi, d.buf, is_dc);
+    const bool valid = e != 0u;
+    const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
+    const uint32_t nbits = valid ? (e & 31u) + sz : 1u;
+    const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
+    const uint32_t msk = (1u << sz) - 1u;
+    const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
+    d.buf <<= nbits;
+    d.cnt -= (int)nbits;
+    d.pos += nbits;
+    const uint32_t zinc = __builtin_amdgcn_ubfe(e, 12, 7);
+    const bool coef = valid && ((e >> 19) & 1u);
+    const uint32_t zz = z + zinc - 1u;  // coefficient index (DC: 0)
+    const bool bad = !valid || (coef && zz > 63u) || ((e >> 20) & 1u);
+    if (bad) {
+      // the sequential decoder stops at the segment's last block and never
+      // reads what follows; anything else is an error
+      if (nb > seg_end_blk || (nb == seg_end_blk && z == 0u)) done = true;
+      else rc = kErrBadHuffman;
+    } else if (coef) {
+      if ((is_dc ? nb : nb - 1) >= seg_end_blk) {
+        done = true;
+      } else {
+        const int qv = S.qt[c][zz];
+        int16_t val;
+        int blk;
+        if (is_dc) {
+          const int cur = c == 0u ? dc0 : (c == 1u ? dc1 : dc2);
+          const int ndc = cur + (int)(int16_t)v;
+          if (c == 0u) dc0 = ndc;
+          else if (c == 1u) dc1 = ndc;
+          else dc2 = ndc;
+          const int32_t dqi = (int32_t)((uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc);
+          val = (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi));
+          blk = nb++;
+        } else {
+          val = (int16_t)((int)(int16_t)v * qv);
+          blk = nb - 1;
+        }
+        coef_img[(size_t)blk * 64 + S.nat[zz]] = val;
+      }
+    }
+    if (!done && rc == kOk && d.pos > seg_end) {  // the symbol runs past the segment
+      if (nb > seg_end_blk || (nb == seg_end_blk && z == 0u)) done = true;
+      else rc = kErrTruncated;
+    }
+    const uint32_t zn = valid ? z + zinc : z;
+    const bool bend = zn >= 64u;
+    const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
+    d.z = bend ? 0u : zn;
+    d.bs = bend ? bsn : d.bs;
+  }
+  return rc;
+}
+
 
 template <int NT>
 __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
@@ -845,7 +906,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       if (fits) pool += nsub;
       for (int k = tid; k < kLutSize; k += NT) {
         uint32_t e = T.lut[k];
-        if ((e >> 5 & 3) == kKindSub) e = fits ? e + ((uint32_t)base << 16) : 0u;
+        if ((e >> 5 & 3) == kKindSub) e = fits ? e + ((uint32_t)base << kEntHiShift) : 0u;
         S.lut[i][k] = e;
       }
       if (fits)
@@ -888,18 +949,17 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
   maxbits = (uint32_t)S.sc.red[0];
   __syncthreads();
   const uint32_t N = slot_bits(maxbits, sub_bits_param);
-  const uint32_t cap = N + kRecPad;  // records per slot
-  if ((int64_t)(kMaxSlots + NT) * cap + kMaxSlots * 4 > dd.rec_cap) {  // host-sized records
+  if ((int64_t)kMaxSlots * 8 > dd.rec_cap) {  // host-sized slot state
     if (tid == 0) infos[img].status = kErrBadGeometry;
     return;
   }
   const int cmax = max(1, (int)((maxbits + N - 1) / N));
   const int seg_per_chunk = max(1, kMaxSlots / cmax);
   int16_t* coef_img = coefs + (size_t)dd.coef_off * 64;
-  uint32_t* rec_img = recs + dd.rec_off;
-  // per-slot state {start pos, start z | bs << 8, records, end z}, after the
-  // records; each slot is only ever touched by the thread that owns it
-  uint4* sst = reinterpret_cast<uint4*>(rec_img + dd.rec_cap - kMaxSlots * 4);
+  // per-slot state, two uint4 per slot: {start pos, start z | bs << 8,
+  // blocks started, end z}, {DC sums of components 0..2, 0}; each slot is only
+  // ever touched by the thread that owns it
+  uint4* sst = reinterpret_cast<uint4*>(recs + dd.rec_off);
   int rounds_total = 0;
   int64_t tph[4] = {0, 0, 0, 0};
   int64_t tstamp = wall_clock64();
@@ -920,15 +980,12 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       return slot_j(k) > 0 && slot_start(k) >= seg_end_bits(slot_seg(k));
     };
     auto slot_known = [&](int k) { return slot_j(k) == 0; };
-    // this thread's records of its k-th slot (k in [r0, r1))
-    auto slot_recs = [&](int k) {
-      return rec_img + ((size_t)(k - r0) * (cap / 4) * NT + tid) * 4;
-    };
     auto decode_k = [&](Dec& d, int k) {
       const uint32_t p0 = d.pos, zb0 = d.z | (d.bs << 8);
-      const uint32_t n = decode_slot<NT>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm,
-                                         slot_end(k), seg_end_bits(slot_seg(k)), slot_recs(k));
-      sst[k] = make_uint4(p0, zb0, n, d.z);
+      SlotSums ss{0, 0, 0, 0};
+      decode_state<NT>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, slot_end(k), ss);
+      sst[2 * k] = make_uint4(p0, zb0, (uint32_t)ss.nblk, d.z);
+      sst[2 * k + 1] = make_uint4((uint32_t)ss.dc0, (uint32_t)ss.dc1, (uint32_t)ss.dc2, 0u);
     };
 
     // ---- round 0: every run from a guess at its first slot ----
@@ -967,7 +1024,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
         npos = S.run_pos[tid - 1];
         nzb = S.run_zb[tid - 1];
         if (nzb != 0xFFFFFFFFu) {
-          const uint4 q = sst[r0];
+          const uint4 q = sst[2 * r0];
           redo = npos != q.x || nzb != q.y;
         }
       }
@@ -983,7 +1040,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
           }
           const uint32_t zb = d.z | (d.bs << 8);
           if (k > r0) {
-            const uint4 q = sst[k];
+            const uint4 q = sst[2 * k];
             if (q.x == d.pos && q.y == zb) {
               merged = true;
               break;
@@ -1024,29 +1081,11 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
           v[0] = ri > 0 ? slot_seg(k) * ri * bpm : 0;
           v[1] = v[2] = v[3] = 0;
         }
-        const uint32_t* R = slot_recs(k);
-        const int n = (int)sst[k].z;
-        for (int i0 = 0; i0 < n; i0 += 16) {
-          // four 16-byte record groups in flight
-          uint4 qq[4];
-#pragma unroll
-          for (int g = 0; g < 4; g++)
-            if (i0 + 4 * g < n)
-              qq[g] = *reinterpret_cast<const uint4*>(R + (size_t)((i0 >> 2) + g) * (NT * 4));
-#pragma unroll
-          for (int jj = 0; jj < 16; jj++) {
-            const int i = i0 + (jj & ~3), j = jj & 3;
-            const uint4 q = qq[jj >> 2];
-            const uint32_t x = j == 0 ? q.x : (j == 1 ? q.y : (j == 2 ? q.z : q.w));
-            const bool dc = i + j < n && (x >> 22 & 1u) && (x >> 25) == kRecCoef;
-            const int c = (int)((x >> 23) & 3u);
-            const int lv = dc ? (int)(int16_t)(x & 0xFFFFu) : 0;
-            v[0] += dc ? 1 : 0;
-            v[1] += c == 0 ? lv : 0;
-            v[2] += c == 1 ? lv : 0;
-            v[3] += c == 2 ? lv : 0;
-          }
-        }
+        const uint4 qa = sst[2 * k], qb = sst[2 * k + 1];
+        v[0] += (int)qa.z;
+        v[1] += (int)qb.x;
+        v[2] += (int)qb.y;
+        v[3] += (int)qb.z;
       }
       S.sc.scan_flag[tid] = flag;
       for (int i = 0; i < 4; i++) S.sc.scan_v[tid][i] = v[i];
@@ -1071,94 +1110,61 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       tph[2] += t - tstamp;
       tstamp = t;
     }
+    // the scan scratch shares LDS with the bit windows: take this thread's
+    // values before the write pass restages windows
+    int nb = 0, dc0 = 0, dc1 = 0, dc2 = 0;
+    if (tid > 0) {
+      nb = S.sc.scan_v[tid - 1][0];
+      dc0 = S.sc.scan_v[tid - 1][1];
+      dc1 = S.sc.scan_v[tid - 1][2];
+      dc2 = S.sc.scan_v[tid - 1][3];
+    }
+    const int run_end_blk = S.sc.scan_v[tid][0];
+    __syncthreads();
     // ---- clear the blocks whose DC symbol lies in this thread's run (a
     // contiguous range; replaces a memset of the whole coefficient buffer):
     // the write pass below may scatter into a block another run started, so
     // the clears finish (barrier) before any coefficient is written ----
     if (r0 < r1) {
-      int b0 = tid > 0 ? S.sc.scan_v[tid - 1][0] : 0;
-      if (slot_known(r0)) b0 = ri > 0 ? slot_seg(r0) * ri * bpm : 0;
-      const int b1 = min(S.sc.scan_v[tid][0], nblocks);
+      const int b0 = slot_known(r0) ? (ri > 0 ? slot_seg(r0) * ri * bpm : 0) : nb;
+      const int b1 = min(run_end_blk, nblocks);
       uint4* z4 = reinterpret_cast<uint4*>(coef_img);
       for (int i = max(b0, 0) * 8; i < b1 * 8; i++) z4[i] = make_uint4(0u, 0u, 0u, 0u);
     }
     __syncthreads();
-    // ---- write pass: replay the records, dequantise, scatter to natural
-    // order; the sequential decoder's stop and error rules per segment ----
+    // ---- write pass: decode each run once more from its synchronised
+    // start, dequantise, scatter to natural order; the sequential decoder's
+    // stop and error rules per segment ----
     {
-      int nb = 0, dc0 = 0, dc1 = 0, dc2 = 0;
-      if (tid > 0) {
-        nb = S.sc.scan_v[tid - 1][0];
-        dc0 = S.sc.scan_v[tid - 1][1];
-        dc1 = S.sc.scan_v[tid - 1][2];
-        dc2 = S.sc.scan_v[tid - 1][3];
-      }
       int rc = kOk;
       bool done = false;  // the segment's last block is complete
+      bool have = false;  // the decoder holds this run's state
+      Dec d;
       for (int k = r0; k < r1 && rc == kOk; k++) {
-        if (slot_empty(k)) continue;
+        if (slot_empty(k)) {
+          have = false;
+          continue;
+        }
         const int s = slot_seg(k);
         if (slot_known(k)) {
           nb = ri > 0 ? s * ri * bpm : 0;
           dc0 = dc1 = dc2 = 0;
           done = false;
+          dec_init<NT>(d, win, words, slot_start(k), 0, 0);
+          have = true;
+        } else if (!have) {
+          const uint4 q = sst[2 * k];
+          dec_init<NT>(d, win, words, q.x, q.y & 0xFF, q.y >> 8);
+          have = true;
         }
         if (done) continue;
         const int seg_end_blk = ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks;
-        const uint32_t* R = slot_recs(k);
-        const uint4 q = sst[k];
-        const int n = (int)q.z;
-        for (int i0 = 0; i0 < n && !done && rc == kOk; i0 += 16) {
-          // four 16-byte record groups in flight before their scatter stores
-          uint4 qq[4];
-#pragma unroll
-          for (int g = 0; g < 4; g++)
-            if (i0 + 4 * g < n)
-              qq[g] = *reinterpret_cast<const uint4*>(R + (size_t)((i0 >> 2) + g) * (NT * 4));
-#pragma unroll
-          for (int jj = 0; jj < 16; jj++) {
-            const int i = i0 + (jj & ~3), j = jj & 3;
-            const uint4 q = qq[jj >> 2];
-            const uint32_t x = j == 0 ? q.x : (j == 1 ? q.y : (j == 2 ? q.z : q.w));
-            if (i + j < n && !done && rc == kOk) {
-              const uint32_t kind = x >> 25;
-              const int zz = (int)((x >> 16) & 63u);
-              const bool is_dc = (x >> 22) & 1u;
-              const int c = (int)((x >> 23) & 3u);
-              const int lv = (int)(int16_t)(x & 0xFFFFu);
-              if (kind != kRecCoef) {
-                // the sequential decoder stops at the segment's last block and
-                // never reads what follows; anything else is an error
-                if (nb > seg_end_blk || (nb == seg_end_blk && zz == 0)) done = true;
-                else rc = kind == kRecErrTrunc ? kErrTruncated : kErrBadHuffman;
-              } else if ((is_dc ? nb : nb - 1) >= seg_end_blk) {
-                done = true;
-              } else {
-                const int qv = S.qt[c][zz];
-                int16_t val;
-                int blk;
-                if (is_dc) {
-                  const int cur = c == 0 ? dc0 : (c == 1 ? dc1 : dc2);
-                  const int ndc = cur + lv;
-                  if (c == 0) dc0 = ndc;
-                  else if (c == 1) dc1 = ndc;
-                  else dc2 = ndc;
-                  const int32_t dqi = (int32_t)((uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc);
-                  val = (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi));
-                  blk = nb++;
-                } else {
-                  val = (int16_t)(lv * qv);
-                  blk = nb - 1;
-                }
-                coef_img[(size_t)blk * 64 + S.nat[zz]] = val;
-              }
-            }
-          }
-        }
+        rc = decode_write<NT>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, slot_end(k),
+                              seg_end_bits(s), seg_end_blk, coef_img, nb, dc0, dc1, dc2, done);
         // last slot of its segment: every block of the segment must be done
         const bool last = (k + 1 >= nslots) || slot_j(k + 1) == 0 || slot_empty(k + 1);
         if (rc == kOk && !done && last &&
-            (nb < seg_end_blk || (nb == seg_end_blk && q.w != 0)))
+            (nb < seg_end_blk || (nb == seg_end_blk && d.z != 0)))
           rc = kErrTruncated;
       }
       if (rc != kOk) atomicCAS(&S.err, kOk, rc);
