@@ -610,8 +610,7 @@ struct EntShared {
   uint8_t vals[kMaxLds][256];
   uint32_t run_pos[NT];
   uint32_t run_zb[NT];
-  uint16_t qt[kMaxComp][64];
-  uint8_t nat[64];
+  uint32_t qn[kMaxComp][64];  // zigzag k -> natural index | quantiser << 8
   int32_t tdc[kMaxBpm], tac[kMaxBpm], bcomp[kMaxBpm];
   // The bit-reader windows are dead outside round 0 / the sync rounds, so the
   // reduction and scan scratch share their storage (keeps the workgroup at
@@ -812,40 +811,35 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     d.pos += nbits;
     const uint32_t zinc = __builtin_amdgcn_ubfe(e, 12, 7);
     const bool coef = valid && ((e >> 19) & 1u);
-    const uint32_t zz = z + zinc - 1u;  // coefficient index (DC: 0)
-    const bool bad = !valid || (coef && zz > 63u) || ((e >> 20) & 1u);
-    if (bad) {
-      // the sequential decoder stops at the segment's last block and never
-      // reads what follows; anything else is an error
-      if (nb > seg_end_blk || (nb == seg_end_blk && z == 0u)) done = true;
-      else rc = kErrBadHuffman;
-    } else if (coef) {
-      if ((is_dc ? nb : nb - 1) >= seg_end_blk) {
-        done = true;
-      } else {
-        const int qv = S.qt[c][zz];
-        int16_t val;
-        int blk;
-        if (is_dc) {
-          const int cur = c == 0u ? dc0 : (c == 1u ? dc1 : dc2);
-          const int ndc = cur + (int)(int16_t)v;
-          if (c == 0u) dc0 = ndc;
-          else if (c == 1u) dc1 = ndc;
-          else dc2 = ndc;
-          const int32_t dqi = (int32_t)((uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc);
-          val = (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi));
-          blk = nb++;
-        } else {
-          val = (int16_t)((int)(int16_t)v * qv);
-          blk = nb - 1;
-        }
-        coef_img[(size_t)blk * 64 + S.nat[zz]] = val;
-      }
-    }
-    if (!done && rc == kOk && d.pos > seg_end) {  // the symbol runs past the segment
-      if (nb > seg_end_blk || (nb == seg_end_blk && z == 0u)) done = true;
-      else rc = kErrTruncated;
-    }
+    const uint32_t zz = (z + zinc - 1u) & 63u;  // coefficient index (DC: 0)
+    const bool bad = !valid || (coef && z + zinc > 64u) || ((e >> 20) & 1u);
+    // The sequential decoder's rules, branch-free (the lanes of a wave sit
+    // at unrelated symbols): it stops at the segment's last block and never
+    // reads what follows; anything else that is invalid is an error.
+    const bool past_a = nb > seg_end_blk || (nb == seg_end_blk && z == 0u);
+    const bool good = coef && !bad;
+    const bool stop = good && (is_dc ? nb : nb - 1) >= seg_end_blk;
+    const bool wr = good && !stop;
+    const uint32_t qn = S.qn[c][zz];
+    const int qv = (int)(qn >> 8);
+    const int v16 = (int)(int16_t)v;
+    const int cur = c == 0u ? dc0 : (c == 1u ? dc1 : dc2);
+    const int ndc = cur + v16;
+    const bool wdc = wr && is_dc;
+    dc0 = (wdc && c == 0u) ? ndc : dc0;
+    dc1 = (wdc && c == 1u) ? ndc : dc1;
+    dc2 = (wdc && c == 2u) ? ndc : dc2;
+    const int32_t dqi = (int32_t)((uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc);
+    const int16_t val = is_dc ? (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi))
+                              : (int16_t)(v16 * qv);
+    const int blk = is_dc ? nb : nb - 1;
+    if (wr) coef_img[(size_t)blk * 64 + (qn & 63u)] = val;
+    nb += wdc ? 1 : 0;
+    // a symbol running past the segment end (after the rule above)
+    const bool trunc = !bad && !stop && d.pos > seg_end;
+    const bool past_b = nb > seg_end_blk || (nb == seg_end_blk && z == 0u);
+    done = (bad && past_a) || stop || (trunc && past_b);
+    rc = (bad && !past_a) ? kErrBadHuffman : ((trunc && !past_b) ? kErrTruncated : kOk);
     const uint32_t zn = valid ? z + zinc : z;
     const bool bend = zn >= 64u;
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
@@ -916,8 +910,8 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       if (tid < 17) S.valoff[i][tid] = T.valoff[tid];
       if (tid < 256) S.vals[i][tid] = T.vals[tid];
     }
-    for (int k = tid; k < kMaxComp * 64; k += NT) S.qt[k / 64][k % 64] = in.qt[k / 64][k % 64];
-    if (tid < 64) S.nat[tid] = kNat[tid];
+    for (int k = tid; k < kMaxComp * 64; k += NT)
+      S.qn[k / 64][k % 64] = kNat[k % 64] | ((uint32_t)in.qt[k / 64][k % 64] << 8);
     for (int b = 0; b < bpm; b++) bcomp |= (uint32_t)in.mcu_comp[b] << (2 * b);
     for (int c = 0; c < kMaxComp; c++)
       tmap |= ((uint32_t)ldc[c] << (3 * c)) | ((uint32_t)lac[c] << (9 + 3 * c));
