@@ -37,7 +37,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # Per-launch HBM-side bytes per kernel from the committed rocprofv3 --pmc
 # passes of this same command (tools/pmc_passes.sh + tools/pmc_traffic.py):
 # FETCH_SIZE / WRITE_SIZE cannot be read from inside the timed process.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v7", "traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v8", "traffic.json")
 # bench stage -> kernels launched in it
 STAGE_KERNELS = {
     "parse": ["hj::parse_kernel"],
@@ -62,9 +62,9 @@ def _pmc_traffic(stage: str, batch: int):
     tot, hit = 0, False
     for name, v in rec["kernels"].items():
         if any(name.startswith(k) for k in STAGE_KERNELS.get(stage, [])):
-            tot += v["traffic_bytes"]
+            tot += v["traffic_bytes"] / max(1, v.get("dispatches", 1))
             hit = True
-    return tot if hit else None
+    return int(tot) if hit else None
 
 
 BATCH = 256
@@ -235,7 +235,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # correctness spot check of the last step (vs a fresh decode of image 0..3)
+    # correctness spot check outside the timed region: the last timed batch
+    # equals a fresh synchronous decode of the same inputs, and repeated
+    # inputs (the batch cycles through `distinct` files) decode identically
+    last = outs[(nsub[0] - 1) % len(outs)]
+    fresh = outs[nsub[0] % len(outs)]
+    dec.decode_batch_device(dev.data_ptr(), dev.numel(), offs, sizes, infos, spec,
+                            fresh.data_ptr(), nbytes_out, stream=stream, sync=True)
+    torch.cuda.synchronize(device)
+    assert torch.equal(last, fresh), "timed batch differs from a fresh decode"
+    if a.batch > a.distinct:
+        assert torch.equal(last[: a.distinct], last[a.distinct : 2 * a.distinct])
+
     stages_ms = {k: v / a.steps / 1000.0 for k, v in stages.items()}
     kernels = {k: v for k, v in stages_ms.items() if k not in ("h2d", "d2h_status")}
     dominant = max(kernels, key=kernels.get)
@@ -294,7 +305,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": _pmc_traffic(dominant, a.batch) if a.workload == "pad224" else None,
-                "traffic_source": "profiles/r01_v7/traffic.json (rocprofv3 --pmc FETCH_SIZE, "
+                "traffic_source": "profiles/r01_v8/traffic.json (rocprofv3 --pmc FETCH_SIZE, "
                                   "WRITE_SIZE; separate passes; x1024, FETCH x2 gfx950)",
                 "algorithmic_bytes_per_image": round(per_image_bytes, 1),
             },

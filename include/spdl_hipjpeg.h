@@ -222,6 +222,14 @@ int spdl_hj_nv12_to_planar_rgb(const uint8_t* src_dev, int32_t num_frames, int32
                                size_t dst_bytes, int device, void* stream, int32_t sync, char* err,
                                size_t errlen);
 
+/* Host <-> device copy of `bytes` (kind 0: host -> device, 1: device ->
+ * host).  pinned != 0: hipMemcpyAsync on `stream`, then the stream is
+ * synchronised; otherwise a synchronous hipMemcpy.  Replaces
+ * transfer_buffer_impl / transfer_buffer (reference
+ * src/libspdl/cuda/transfer.cpp:37-105). */
+int spdl_hj_copy(void* dst, const void* src, size_t bytes, int32_t kind, int device, void* stream,
+                 int32_t pinned, char* err, size_t errlen);
+
 /* Per-kernel timing of the last batch, in microseconds, measured with HIP
  * events on the decode stream (filled only when enabled). */
 int spdl_hj_set_profiling(spdl_hj_ctx* ctx, int32_t enable);

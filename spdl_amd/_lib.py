@@ -48,6 +48,7 @@ EXPORTED = (
     "spdl_hj_decode_staged",
     "spdl_hj_tar_index",
     "spdl_hj_nv12_to_planar_rgb",
+    "spdl_hj_copy",
 )
 
 
@@ -202,6 +203,7 @@ def lib() -> ctypes.CDLL:
         L.spdl_hj_nv12_to_planar_rgb.argtypes = [
             vp, i32, i32, i32, i32, i32, vp, sz, ctypes.c_int, vp, i32, cp, sz
         ]
+        L.spdl_hj_copy.argtypes = [vp, vp, sz, i32, ctypes.c_int, vp, i32, cp, sz]
         ver = L.spdl_hj_abi_version()
         if ver != ABI_VERSION:
             raise RuntimeError(f"libspdl_hipjpeg ABI {ver} != expected {ABI_VERSION}")

@@ -1347,6 +1347,29 @@ int spdl_hj_nv12_to_planar_rgb(const uint8_t* src_dev, int32_t num_frames, int32
   return SPDL_HJ_OK;
 }
 
+int spdl_hj_copy(void* dst, const void* src, size_t bytes, int32_t kind, int device, void* stream,
+                 int32_t pinned, char* err, size_t errlen) {
+  if ((!dst || !src) && bytes) {
+    set_err(err, errlen, "invalid argument");
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  if (kind != 0 && kind != 1) {
+    set_err(err, errlen, "invalid copy kind %d", (int)kind);
+    return SPDL_HJ_ERR_INVALID_ARG;
+  }
+  if (!bytes) return SPDL_HJ_OK;
+  DeviceGuard g(device);
+  const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+  if (pinned) {  // reference transfer_buffer_impl: async on the stream + sync
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    HJ_HIP(hipMemcpyAsync(dst, src, bytes, k, st));
+    HJ_HIP(hipStreamSynchronize(st));
+  } else {
+    HJ_HIP(hipMemcpy(dst, src, bytes, k));
+  }
+  return SPDL_HJ_OK;
+}
+
 int spdl_hj_set_profiling(spdl_hj_ctx* ctx, int32_t enable) {
   if (!ctx) return SPDL_HJ_ERR_INVALID_ARG;
   ctx->profiling = enable != 0;

@@ -13,6 +13,14 @@ from ._image import (
 )
 from ._preprocessing import get_video_filter_desc, parse_image_filter
 from ._tar import TarImageStream, iter_tarfile
+from ._transfer import (
+    CPUStorage,
+    convert_array,
+    cpu_storage,
+    transfer_buffer,
+    transfer_buffer_cpu,
+    transfer_tensor,
+)
 
 # HIP-named aliases: same functions, named for the hardware they run on.
 decode_image_hip = decode_image_nvjpeg
@@ -20,8 +28,11 @@ load_image_batch_hip = load_image_batch_nvjpeg
 
 __all__ = [
     "CPUBuffer",
+    "CPUStorage",
     "CUDABuffer",
     "CUDAConfig",
+    "convert_array",
+    "cpu_storage",
     "cuda_config",
     "decode_image_hip",
     "decode_image_nvjpeg",
@@ -37,4 +48,7 @@ __all__ = [
     "parse_image_filter",
     "to_numpy",
     "to_torch",
+    "transfer_buffer",
+    "transfer_buffer_cpu",
+    "transfer_tensor",
 ]

@@ -131,7 +131,10 @@ def load_image_batch_nvjpeg(
 def _to_host(buf: CUDABuffer) -> CPUBuffer:
     from ._convert import to_torch
 
-    return CPUBuffer(to_torch(buf).cpu().numpy())
+    t = to_torch(buf).cpu()
+    if t.dtype == torch.bfloat16:  # numpy has no bfloat16: keep the bit patterns
+        return CPUBuffer(t.view(torch.int16).numpy().view(np.uint16), dtype=torch.bfloat16)
+    return CPUBuffer(t.numpy())
 
 
 def load_image_batch(
