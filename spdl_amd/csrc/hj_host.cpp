@@ -543,7 +543,7 @@ struct Slot {
 // batches alternate between workspaces and run on the lanes' own streams, so
 // batch k+1's kernels can occupy the CUs that batch k's latency-bound
 // entropy kernel leaves idle (its sync rounds park most waves at barriers).
-constexpr int kMaxLanes = 2;
+constexpr int kMaxLanes = 3;
 
 struct Workspace {
   DevBuf clean, segs, desc, info, luts, coefs, planes, wts, recs, rplanes, dschunks;

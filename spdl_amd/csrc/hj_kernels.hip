@@ -359,7 +359,10 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
         tabs[t].sub[i] = entry16(((uint32_t)(p_lo + (i >> kSubBits)) << kSubBits) |
                                      (uint32_t)(i & ((1 << kSubBits) - 1)),
                                  16, 16);
-    if (tid == 0) tabs[t].nsub = sub_ok ? nsub : 0;
+    if (tid == 0) {
+      tabs[t].nsub = sub_ok ? nsub : 0;
+      tabs[t].long_slow = sub_ok ? 0 : 1;  // long codes left to the canonical path
+    }
     for (int i = tid; i < 18; i += blockDim.x) tabs[t].maxcode[i] = s.maxcode[t][i];
     for (int i = tid; i < 17; i += blockDim.x) tabs[t].valoff[i] = s.valoff[t][i];
     for (int i = tid; i < 256; i += blockDim.x) tabs[t].vals[i] = s.vals[t][i];
@@ -596,21 +599,28 @@ __global__ void __launch_bounds__(kDsThreads) destuff_write_kernel(
 // entropy_kernel
 // ---------------------------------------------------------------------------
 
-constexpr int kMaxLds = 6;  // distinct tables held in LDS
-constexpr int kWinWords = 16;  // bit-reader window per thread (words)
+constexpr int kMaxTabs = 2 * kMaxComp;  // distinct (DC, AC) tables of a scan
+#ifndef HJ_WIN_WORDS
+#define HJ_WIN_WORDS 8
+#endif
+constexpr int kWinWords = HJ_WIN_WORDS;  // bit-reader window per thread (words)
 
 constexpr int kSubPool = 2048;  // LDS entries for second-level tables of all tables
 
-template <int NT>
+// NTAB = distinct Huffman tables the workgroup holds in LDS.  The common case
+// (luma + chroma DC/AC: 4 tables, gray: 2) runs the NTAB = 4 instance, small
+// enough for three entropy workgroups per CU; an image whose scan uses 5-6
+// distinct tables is left to the NTAB = 6 instance launched after it.
+template <int NT, int NTAB>
 struct EntShared {
-  uint32_t lut[kMaxLds][kLutSize];
+  uint32_t lut[NTAB][kLutSize];
   uint32_t sub[kSubPool];
-  int32_t maxcode[kMaxLds][18];
-  int32_t valoff[kMaxLds][17];
-  uint8_t vals[kMaxLds][256];
+  int32_t maxcode[NTAB][18];
+  int32_t valoff[NTAB][17];
+  uint8_t vals[NTAB][256];
   uint32_t run_pos[NT];
   uint32_t run_zb[NT];
-  uint32_t qn[kMaxComp][64];  // zigzag k -> natural index | quantiser << 8
+  uint32_t qdc[kMaxComp];  // DC quantiser per component
   int32_t tdc[kMaxBpm], tac[kMaxBpm], bcomp[kMaxBpm];
   // The bit-reader windows are dead outside round 0 / the sync rounds, so the
   // reduction and scan scratch share their storage (keeps the workgroup at
@@ -627,35 +637,91 @@ struct EntShared {
   int32_t flag;
   int32_t err;
 };
-static_assert(sizeof(EntShared<512>) <= 80 * 1024, "entropy LDS must allow 2 workgroups per CU");
+static_assert(sizeof(EntShared<512, 4>) <= 160 * 1024 / 3,
+              "entropy LDS must allow 3 workgroups per CU");
 
 // Per-thread bit reader over the destuffed stream (big-endian bytes read as
-// 32-bit words).  `buf` holds the next 33..64 bits MSB-first and `nxt` the
-// word after them.  Words come from a 16-word LDS window per thread
-// ([word][thread], conflict-free), restaged from HBM once every ~12 words:
-// the decode loop itself issues no global load, so its record stores never
-// stall it (on gfx9 a vmcnt wait for a load also waits for older stores).
+// 32-bit words).  Words come from an 8-word LDS window per thread
+// ([word][thread], conflict-free), restaged from HBM once every 4-7 words:
+// the decode loop itself issues no global load, so its coefficient stores
+// never stall it (on gfx9 a vmcnt wait for a load also waits for older
+// stores).
+//
+// HJ_POS_READER (default): the state is the bit position alone; each step
+// reads the two window words holding bits [pos, pos + 32) (one
+// ds_read2st64) and funnel-shifts them -- no bit buffer to refill, no
+// branch.  Otherwise a 64-bit buffer with a refill step (kept for A/B).
+#ifndef HJ_POS_READER
+#define HJ_POS_READER 1
+#endif
 struct Dec {
-  uint64_t buf;
-  uint32_t nxt;
+#if !HJ_POS_READER
+  uint64_t buf;  // the next 33..64 bits MSB-first
+  uint32_t nxt;  // the word after them
   uint32_t wi;   // absolute word index of nxt
-  uint32_t wb;   // absolute word index of the window's first word
   int cnt;
-  uint32_t pos;  // absolute bit position of buf's MSB
+#endif
+  uint32_t wb;   // absolute word index of the window's first word
+  uint32_t pos;  // absolute bit position of the next symbol
   uint32_t z;    // next coefficient index (0 = DC)
   uint32_t bs;   // 2 * block-in-MCU
 };
 
 template <int NT>
 __device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, uint32_t wb) {
+  static_assert(kWinWords % 4 == 0, "window is staged in uint4 units");
   const uint4* src = reinterpret_cast<const uint4*>(words + wb);  // wb % 4 == 0
-  const uint4 q0 = src[0], q1 = src[1], q2 = src[2], q3 = src[3];
-  const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+  uint4 q[kWinWords / 4];
 #pragma unroll
-  for (int i = 0; i < 16; i++) win[i * NT] = w[i];
+  for (int i = 0; i < kWinWords / 4; i++) q[i] = src[i];
+#if HJ_POS_READER
+  // stored MSB-first (byte-swapped once here instead of at every read)
+#pragma unroll
+  for (int i = 0; i < kWinWords / 4; i++) {
+    q[i].x = __builtin_bswap32(q[i].x);
+    q[i].y = __builtin_bswap32(q[i].y);
+    q[i].z = __builtin_bswap32(q[i].z);
+    q[i].w = __builtin_bswap32(q[i].w);
+  }
+#endif
+#pragma unroll
+  for (int i = 0; i < kWinWords / 4; i++) {
+    win[(4 * i + 0) * NT] = q[i].x;
+    win[(4 * i + 1) * NT] = q[i].y;
+    win[(4 * i + 2) * NT] = q[i].z;
+    win[(4 * i + 3) * NT] = q[i].w;
+  }
 }
 
+#if HJ_POS_READER
+template <int NT>
+__device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
+                                         uint32_t z, uint32_t bs) {
+  d.wb = (p >> 5) & ~3u;
+  win_stage<NT>(win, words, d.wb);
+  d.pos = p;
+  d.z = z;
+  d.bs = bs;
+}
+
+// The 32 bits at d.pos, MSB-first.  Wave-uniform window restage: when any
+// active lane is about to read past its window, every active lane restages
+// from its own position, so the global load and its vmcnt wait happen once
+// per ~25 symbol steps of the wave.
+template <int NT>
+__device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
+  uint32_t w = (d.pos >> 5) - d.wb;
+  if (__any(w >= (uint32_t)(kWinWords - 1))) {
+    d.wb = (d.pos >> 5) & ~3u;
+    win_stage<NT>(win, words, d.wb);
+    w = (d.pos >> 5) - d.wb;
+  }
+  const uint32_t lo = win[(w + 1) * NT], hi = win[w * NT];
+  return (uint32_t)(((((uint64_t)hi << 32) | lo) << (d.pos & 31u)) >> 32);
+}
+
+__device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) { d.pos += nbits; }
+#else
 template <int NT>
 __device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
                                          uint32_t z, uint32_t bs) {
@@ -698,12 +764,26 @@ __device__ __forceinline__ void dec_restage(Dec& d, uint32_t* win, const uint32_
   }
 }
 
+template <int NT>
+__device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
+  dec_restage<NT>(d, win, words);
+  dec_refill<NT>(d, win);
+  return (uint32_t)(d.buf >> 32);
+}
+
+__device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) {
+  d.buf <<= nbits;
+  d.cnt -= (int)nbits;
+  d.pos += nbits;
+}
+#endif
+
 // Canonical decode of a code that is not fully resolved by the LUT (longer
 // than kLutBits, or a DC size > 15): returns a kKindCode entry, 0 if invalid.
 template <class SH>
-__device__ __attribute__((noinline)) uint32_t slow_symbol(const SH& S, int t, uint64_t buf,
+__device__ __attribute__((noinline)) uint32_t slow_symbol(const SH& S, int t, uint32_t hi,
                                                           bool is_dc) {
-  const uint32_t w16 = (uint32_t)(buf >> 48);
+  const uint32_t w16 = hi >> 16;
   for (int l = 1; l <= 16; l++) {
     const int code = (int)(w16 >> (16 - l));
     if (code <= S.maxcode[t][l]) {
@@ -717,98 +797,113 @@ __device__ __attribute__((noinline)) uint32_t slow_symbol(const SH& S, int t, ui
 
 // The entry of the symbol at the head of `hi` in table slot t (two-level LUT,
 // canonical fallback); 0 = invalid code.
-template <class SH>
-__device__ __forceinline__ uint32_t lookup(const SH& S, uint32_t t, uint32_t hi, uint64_t buf,
-                                           bool is_dc) {
+// SLOW = false: every table's long codes are in LDS sub-tables, so a Slow
+// entry is 0 (invalid code) and the canonical fallback is not needed.
+template <bool SLOW, class SH>
+__device__ __forceinline__ uint32_t lookup(const SH& S, uint32_t t, uint32_t hi, bool is_dc) {
   uint32_t e = S.lut[t][hi >> (32 - kLutBits)];
   if (((e >> 5) & 3) == kKindSub)
     e = S.sub[((e >> kEntHiShift) << kSubBits) |
               ((hi >> (32 - kLutBits - kSubBits)) & ((1u << kSubBits) - 1))];
-  if (((e >> 5) & 3) == kKindSlow) e = slow_symbol(S, (int)t, buf, is_dc);
+  if constexpr (SLOW) {
+    if (((e >> 5) & 3) == kKindSlow) e = slow_symbol(S, (int)t, hi, is_dc);
+  }
   return e;
 }
 
-// Per-slot sums of the state-only decode: blocks started and DC differences
-// per component (the inputs of the block-index / DC-predictor scan).
-struct SlotSums {
-  int nblk, dc0, dc1, dc2;
-};
-
 // State-only decode of every symbol that starts in [d.pos, end): bit
-// position, z and block-in-MCU advance, block count and DC sums -- no
-// stores, so the loop carries no memory traffic besides the bit window.
-// Total over any bit position: an invalid code consumes one bit, a run past
-// coefficient 63 ends the block, so every start state has one trajectory.
-// One path for DC and AC (selects, not branches: the 64 lanes of a wave
-// decode 64 unrelated streams).
-template <int NT, class SH>
-__device__ void decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
-                             const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
-                             const uint32_t end, SlotSums& ss) {
+// position, z and block-in-MCU advance and the number of blocks started --
+// no stores and no coefficient values (DC predictors are resolved after the
+// write pass), so the loop carries no memory traffic besides the bit window.
+// Total over any bit position: an invalid code (entry 0) consumes one bit, a
+// run past coefficient 63 ends the block, so every start state has one
+// trajectory.  One path for DC and AC (selects, not branches: the 64 lanes of
+// a wave decode 64 unrelated streams).  Returns the blocks started.
+template <int NT, bool SLOW, class SH>
+__device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
+                            const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
+                            const uint32_t end) {
+  int nblk = 0;
   while (d.pos < end) {
-    dec_restage<NT>(d, win, words);
-    dec_refill<NT>(d, win);
+    const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
     const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
     const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
-    const uint32_t hi = (uint32_t)(d.buf >> 32);
-    const uint32_t e = lookup(S, t, hi, d.buf, is_dc);
-    const bool valid = e != 0u;
-    const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
-    const uint32_t nbits = valid ? (e & 31u) + sz : 1u;  // <= 31
-    // DC difference (JPEG EXTEND; Full entries carry it, sz == 0 there)
-    const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
-    const uint32_t msk = (1u << sz) - 1u;
-    const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
-    const bool dcok = is_dc && valid;
-    const int dv = dcok ? v : 0;
-    ss.nblk += dcok ? 1 : 0;
-    ss.dc0 += c == 0u ? dv : 0;
-    ss.dc1 += c == 1u ? dv : 0;
-    ss.dc2 += c == 2u ? dv : 0;
-    d.buf <<= nbits;
-    d.cnt -= (int)nbits;
-    d.pos += nbits;
-    const uint32_t zn = valid ? z + __builtin_amdgcn_ubfe(e, 12, 7) : z;
+    const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
+    // entry 0 (invalid) takes one bit, advances nothing and starts no block
+    const uint32_t nbits = max((e & 31u) + __builtin_amdgcn_ubfe(e, 7, 5), 1u);  // <= 31
+    nblk += is_dc ? (int)__builtin_amdgcn_ubfe(e, 19, 1) : 0;  // DC: coef bit = valid
+    dec_skip(d, nbits);
+    const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool bend = zn >= 64u;
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
+  return nblk;
 }
 
 // Full decode of the symbols that start in [d.pos, end) from a synchronised
 // state: dequantise, scatter in natural order, and apply the sequential
 // decoder's stop / error rules of the segment (blocks [.., seg_end_blk),
 // scan bits [.., seg_end)) -- oracle jo_decode_coefs.  nb = blocks started so
-// far (absolute), dc* = DC predictors (sums of differences).  Returns the
-// status; sets `done` once the segment's last block is complete.
-template <int NT, class SH>
+// far (absolute).  DC coefficients are stored as raw differences; the
+// predictors are applied after the pass.  Returns the status; sets `done`
+// once the segment's last block is complete.
+template <int NT, bool SLOW, class SH>
 __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
                             const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
                             const uint32_t end, const uint32_t seg_end, const int seg_end_blk,
-                            int16_t* __restrict__ coef_img, int& nb, int& dc0, int& dc1, int& dc2,
-                            bool& done) {
+                            int16_t* __restrict__ coef_img, int& nb, bool& done) {
   int rc = kOk;
-  while (d.pos < end && !done && rc == kOk) {
-    dec_restage<NT>(d, win, words);
-    dec_refill<NT>(d, win);
+  // Fast path: a symbol that can trigger none of the rules below -- a valid
+  // code, no run past coefficient 63, not running past the segment end, and
+  // not after the segment's last block started (nb < seg_end_blk) -- is
+  // decoded without them.  A lane leaves at the first symbol that could,
+  // before consuming it, and the careful loop continues from that state.
+  while (d.pos < end && nb < seg_end_blk) {
+    const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
     const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
     const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
-    const uint32_t hi = (uint32_t)(d.buf >> 32);
-    const uint32_t e = lookup(S, t, hi, d.buf, is_dc);
+    const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
+    const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
+    const uint32_t nbits = (e & 31u) + sz;
+    const uint32_t zinc = __builtin_amdgcn_ubfe(e, 12, 7);
+    const bool coef = (e >> 19) & 1u;
+    // (bitwise, not short-circuit: one exit test instead of nested branches)
+    if ((e == 0u) | (((e >> 20) & 1u) != 0u) | (coef & (z + zinc > 64u)) |
+        (d.pos + nbits > seg_end))
+      break;
+    const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
+    const uint32_t msk = (1u << sz) - 1u;
+    const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
+    dec_skip(d, nbits);
+    const int blk = is_dc ? nb : nb - 1;
+    if (coef) coef_img[(size_t)blk * 64 + ((z + zinc - 1u) & 63u)] = (int16_t)v;
+    nb += is_dc ? 1 : 0;
+    const uint32_t zn = z + zinc;
+    const bool bend = zn >= 64u;
+    const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
+    d.z = bend ? 0u : zn;
+    d.bs = bend ? bsn : d.bs;
+  }
+  while (d.pos < end && !done && rc == kOk) {
+    const uint32_t hi = dec_peek<NT>(d, win, words);
+    const uint32_t z = d.z;
+    const bool is_dc = z == 0;
+    const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
+    const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
+    const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
     const bool valid = e != 0u;
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
     const uint32_t nbits = valid ? (e & 31u) + sz : 1u;
     const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
     const uint32_t msk = (1u << sz) - 1u;
     const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
-    d.buf <<= nbits;
-    d.cnt -= (int)nbits;
-    d.pos += nbits;
+    dec_skip(d, nbits);
     const uint32_t zinc = __builtin_amdgcn_ubfe(e, 12, 7);
     const bool coef = valid && ((e >> 19) & 1u);
     const uint32_t zz = (z + zinc - 1u) & 63u;  // coefficient index (DC: 0)
@@ -820,21 +915,9 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const bool good = coef && !bad;
     const bool stop = good && (is_dc ? nb : nb - 1) >= seg_end_blk;
     const bool wr = good && !stop;
-    const uint32_t qn = S.qn[c][zz];
-    const int qv = (int)(qn >> 8);
-    const int v16 = (int)(int16_t)v;
-    const int cur = c == 0u ? dc0 : (c == 1u ? dc1 : dc2);
-    const int ndc = cur + v16;
-    const bool wdc = wr && is_dc;
-    dc0 = (wdc && c == 0u) ? ndc : dc0;
-    dc1 = (wdc && c == 1u) ? ndc : dc1;
-    dc2 = (wdc && c == 2u) ? ndc : dc2;
-    const int32_t dqi = (int32_t)((uint32_t)kDcBias + (uint32_t)qv * (uint32_t)ndc);
-    const int16_t val = is_dc ? (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi))
-                              : (int16_t)(v16 * qv);
     const int blk = is_dc ? nb : nb - 1;
-    if (wr) coef_img[(size_t)blk * 64 + (qn & 63u)] = val;
-    nb += wdc ? 1 : 0;
+    if (wr) coef_img[(size_t)blk * 64 + zz] = (int16_t)v;
+    nb += (wr && is_dc) ? 1 : 0;
     // a symbol running past the segment end (after the rule above)
     const bool trunc = !bad && !stop && d.pos > seg_end;
     const bool past_b = nb > seg_end_blk || (nb == seg_end_blk && z == 0u);
@@ -850,7 +933,31 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
 }
 
 
-template <int NT>
+// Segmented inclusive scan over the workgroup's runs (Hillis-Steele): a run
+// with `flag` set restarts the sums.  Results in S.sc.scan_v[tid][0, NV).
+template <int NT, int NV, class SH>
+__device__ void seg_scan(SH& S, int tid, int flag, const int (&v)[3]) {
+  S.sc.scan_flag[tid] = flag;
+#pragma unroll
+  for (int i = 0; i < NV; i++) S.sc.scan_v[tid][i] = v[i];
+  __syncthreads();
+  for (int off = 1; off < NT; off <<= 1) {
+    int pf = 0, pv[NV];
+    const bool take = tid >= off;
+#pragma unroll
+    for (int i = 0; i < NV; i++) pv[i] = take ? S.sc.scan_v[tid - off][i] : 0;
+    if (take) pf = S.sc.scan_flag[tid - off];
+    __syncthreads();
+    if (take && !S.sc.scan_flag[tid]) {
+#pragma unroll
+      for (int i = 0; i < NV; i++) S.sc.scan_v[tid][i] += pv[i];
+      S.sc.scan_flag[tid] = pf;
+    }
+    __syncthreads();
+  }
+}
+
+template <int NT, int NTAB>
 __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
                                                      const uint32_t* __restrict__ segs,
                                                      const ImageDesc* __restrict__ desc,
@@ -859,12 +966,33 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
                                                      int16_t* __restrict__ coefs,
                                                      uint32_t* __restrict__ recs,
                                                      const int sub_bits_param) {
-  __shared__ EntShared<NT> S;
+  __shared__ EntShared<NT, NTAB> S;
   const int img = blockIdx.x, tid = threadIdx.x;
   uint32_t* win = &S.win[0][tid];
   if (infos[img].status != kOk) return;
   const ImageDesc dd = desc[img];
   const ImageInfo& in = infos[img];
+  // The NTAB = 4 instance takes the images whose scan uses <= 4 distinct
+  // tables with every long code in sub-tables that fit the LDS pool (no
+  // canonical fallback in its loops); the NTAB = 6 instance takes the rest.
+  constexpr bool kSlow = NTAB > 4;
+  {
+    const HuffTable* tabs = luts + (size_t)img * 8;
+    int ns = 0, seen = 0, subs = 0;
+    bool slow = false;
+    for (int c = 0; c < in.ncomp; c++)
+      for (int k = 0; k < 2; k++) {
+        const int slot = k == 0 ? in.dc_tab[c] : 4 + in.ac_tab[c];
+        if (!(seen & (1 << slot))) {
+          ns++;
+          subs += tabs[slot].nsub;
+          slow |= tabs[slot].long_slow != 0;
+        }
+        seen |= 1 << slot;
+      }
+    const bool fast = ns <= 4 && (subs << kSubBits) <= kSubPool && !slow;
+    if (kSlow == fast) return;
+  }
   const int bpm = in.bpm, ri = in.ri, nmcu = in.mcux * in.mcuy;
   const int nblocks = in.nblocks;
   const uint32_t* words = reinterpret_cast<const uint32_t*>(clean + dd.in_off);
@@ -876,7 +1004,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
   // ---- tables into LDS (dedup table slots per component) ----
   uint32_t bcomp = 0, tmap = 0;  // 2-bit component per block-in-MCU; 3-bit table slots
   {
-    int slots[kMaxLds], ns = 0, ldc[kMaxComp] = {0, 0, 0}, lac[kMaxComp] = {0, 0, 0};
+    int slots[kMaxTabs], ns = 0, ldc[kMaxComp] = {0, 0, 0}, lac[kMaxComp] = {0, 0, 0};
     for (int c = 0; c < in.ncomp; c++) {
       const int want[2] = {in.dc_tab[c], 4 + in.ac_tab[c]};
       for (int k = 0; k < 2; k++) {
@@ -911,7 +1039,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       if (tid < 256) S.vals[i][tid] = T.vals[tid];
     }
     for (int k = tid; k < kMaxComp * 64; k += NT)
-      S.qn[k / 64][k % 64] = kNat[k % 64] | ((uint32_t)in.qt[k / 64][k % 64] << 8);
+      if (k % 64 == 0) S.qdc[k / 64] = in.qt[k / 64][0];
     for (int b = 0; b < bpm; b++) bcomp |= (uint32_t)in.mcu_comp[b] << (2 * b);
     for (int c = 0; c < kMaxComp; c++)
       tmap |= ((uint32_t)ldc[c] << (3 * c)) | ((uint32_t)lac[c] << (9 + 3 * c));
@@ -950,12 +1078,13 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
   const int cmax = max(1, (int)((maxbits + N - 1) / N));
   const int seg_per_chunk = max(1, kMaxSlots / cmax);
   int16_t* coef_img = coefs + (size_t)dd.coef_off * 64;
-  // per-slot state, two uint4 per slot: {start pos, start z | bs << 8,
-  // blocks started, end z}, {DC sums of components 0..2, 0}; each slot is only
-  // ever touched by the thread that owns it
+  // per-slot state, one uint4 per slot: {start pos, start z | bs << 8, blocks
+  // started, end z}; each slot is only ever touched by the thread that owns it
   uint4* sst = reinterpret_cast<uint4*>(recs + dd.rec_off);
+  auto seg_first_blk = [&](int s) { return ri > 0 ? s * ri * bpm : 0; };
+  auto seg_end_blk = [&](int s) { return ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks; };
   int rounds_total = 0;
-  int64_t tph[4] = {0, 0, 0, 0};
+  int64_t tph[4] = {0, 0, 0, 0}, dcfix = 0;
   int64_t tstamp = wall_clock64();
 
   for (int seg_lo = 0; seg_lo < nseg; seg_lo += seg_per_chunk) {
@@ -976,10 +1105,9 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
     auto slot_known = [&](int k) { return slot_j(k) == 0; };
     auto decode_k = [&](Dec& d, int k) {
       const uint32_t p0 = d.pos, zb0 = d.z | (d.bs << 8);
-      SlotSums ss{0, 0, 0, 0};
-      decode_state<NT>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, slot_end(k), ss);
-      sst[2 * k] = make_uint4(p0, zb0, (uint32_t)ss.nblk, d.z);
-      sst[2 * k + 1] = make_uint4((uint32_t)ss.dc0, (uint32_t)ss.dc1, (uint32_t)ss.dc2, 0u);
+      const int nblk = decode_state<NT, kSlow>(S, d, win, words, bcomp, tmap,
+                                               2u * (uint32_t)bpm, slot_end(k));
+      sst[k] = make_uint4(p0, zb0, (uint32_t)nblk, d.z);
     };
 
     // ---- round 0: every run from a guess at its first slot ----
@@ -1018,7 +1146,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
         npos = S.run_pos[tid - 1];
         nzb = S.run_zb[tid - 1];
         if (nzb != 0xFFFFFFFFu) {
-          const uint4 q = sst[2 * r0];
+          const uint4 q = sst[r0];
           redo = npos != q.x || nzb != q.y;
         }
       }
@@ -1034,7 +1162,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
           }
           const uint32_t zb = d.z | (d.bs << 8);
           if (k > r0) {
-            const uint4 q = sst[2 * k];
+            const uint4 q = sst[k];
             if (q.x == d.pos && q.y == zb) {
               merged = true;
               break;
@@ -1064,40 +1192,19 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       tstamp = t;
     }
 
-    // ---- per-run totals from the records, then a segmented exclusive scan
-    // over runs: (absolute next block, DC predictors) ----
+    // ---- per-run block totals, then a segmented inclusive scan over runs:
+    // the absolute block index after each run ----
     {
-      int flag = 0, v[4] = {0, 0, 0, 0};
+      int flag = 0, v[3] = {0, 0, 0};
       for (int k = r0; k < r1; k++) {
         if (slot_empty(k)) continue;
         if (slot_known(k)) {
           flag = 1;
-          v[0] = ri > 0 ? slot_seg(k) * ri * bpm : 0;
-          v[1] = v[2] = v[3] = 0;
+          v[0] = seg_first_blk(slot_seg(k));
         }
-        const uint4 qa = sst[2 * k], qb = sst[2 * k + 1];
-        v[0] += (int)qa.z;
-        v[1] += (int)qb.x;
-        v[2] += (int)qb.y;
-        v[3] += (int)qb.z;
+        v[0] += (int)sst[k].z;
       }
-      S.sc.scan_flag[tid] = flag;
-      for (int i = 0; i < 4; i++) S.sc.scan_v[tid][i] = v[i];
-      __syncthreads();
-      for (int off = 1; off < NT; off <<= 1) {
-        int pf = 0, pv[4] = {0, 0, 0, 0};
-        const bool take = tid >= off;
-        if (take) {
-          pf = S.sc.scan_flag[tid - off];
-          for (int i = 0; i < 4; i++) pv[i] = S.sc.scan_v[tid - off][i];
-        }
-        __syncthreads();
-        if (take && !S.sc.scan_flag[tid]) {
-          for (int i = 0; i < 4; i++) S.sc.scan_v[tid][i] += pv[i];
-          S.sc.scan_flag[tid] = pf;
-        }
-        __syncthreads();
-      }
+      seg_scan<NT, 1>(S, tid, flag, v);
     }
     {
       const int64_t t = wall_clock64();
@@ -1106,24 +1213,29 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
     }
     // the scan scratch shares LDS with the bit windows: take this thread's
     // values before the write pass restages windows
-    int nb = 0, dc0 = 0, dc1 = 0, dc2 = 0;
-    if (tid > 0) {
-      nb = S.sc.scan_v[tid - 1][0];
-      dc0 = S.sc.scan_v[tid - 1][1];
-      dc1 = S.sc.scan_v[tid - 1][2];
-      dc2 = S.sc.scan_v[tid - 1][3];
-    }
+    int nb = tid > 0 ? S.sc.scan_v[tid - 1][0] : 0;
     const int run_end_blk = S.sc.scan_v[tid][0];
     __syncthreads();
-    // ---- clear the blocks whose DC symbol lies in this thread's run (a
-    // contiguous range; replaces a memset of the whole coefficient buffer):
-    // the write pass below may scatter into a block another run started, so
-    // the clears finish (barrier) before any coefficient is written ----
-    if (r0 < r1) {
-      const int b0 = slot_known(r0) ? (ri > 0 ? slot_seg(r0) * ri * bpm : 0) : nb;
-      const int b1 = min(run_end_blk, nblocks);
+    // This run's blocks [b0, b1): those whose DC symbol lies in the run --
+    // from its first slot's segment start (or the predecessor's end) to its
+    // count end, clamped to its last segment's end (symbols decoded from the
+    // fill bits after a segment's last block are not blocks).  The ranges of
+    // the runs are disjoint and cover every block of a well-formed scan.
+    int b0 = 0, b1 = 0;
+    {
+      int k0 = r0;
+      while (k0 < r1 && slot_empty(k0)) k0++;
+      if (k0 < r1) {
+        b0 = max(0, slot_known(k0) ? seg_first_blk(slot_seg(k0)) : nb);
+        b1 = min(min(run_end_blk, seg_end_blk(slot_seg(r1 - 1))), nblocks);
+      }
+    }
+    // ---- clear this run's blocks (replaces a memset of the coefficient
+    // buffer): the write pass may scatter into a block another run started,
+    // so the clears finish (barrier) before any coefficient is written ----
+    {
       uint4* z4 = reinterpret_cast<uint4*>(coef_img);
-      for (int i = max(b0, 0) * 8; i < b1 * 8; i++) z4[i] = make_uint4(0u, 0u, 0u, 0u);
+      for (int i = b0 * 8; i < b1 * 8; i++) z4[i] = make_uint4(0u, 0u, 0u, 0u);
     }
     __syncthreads();
     // ---- write pass: decode each run once more from its synchronised
@@ -1141,24 +1253,22 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
         }
         const int s = slot_seg(k);
         if (slot_known(k)) {
-          nb = ri > 0 ? s * ri * bpm : 0;
-          dc0 = dc1 = dc2 = 0;
+          nb = seg_first_blk(s);
           done = false;
           dec_init<NT>(d, win, words, slot_start(k), 0, 0);
           have = true;
         } else if (!have) {
-          const uint4 q = sst[2 * k];
+          const uint4 q = sst[k];
           dec_init<NT>(d, win, words, q.x, q.y & 0xFF, q.y >> 8);
           have = true;
         }
         if (done) continue;
-        const int seg_end_blk = ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks;
-        rc = decode_write<NT>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, slot_end(k),
-                              seg_end_bits(s), seg_end_blk, coef_img, nb, dc0, dc1, dc2, done);
+        const int seb = seg_end_blk(s);
+        rc = decode_write<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm,
+                                     slot_end(k), seg_end_bits(s), seb, coef_img, nb, done);
         // last slot of its segment: every block of the segment must be done
         const bool last = (k + 1 >= nslots) || slot_j(k + 1) == 0 || slot_empty(k + 1);
-        if (rc == kOk && !done && last &&
-            (nb < seg_end_blk || (nb == seg_end_blk && d.z != 0)))
+        if (rc == kOk && !done && last && (nb < seb || (nb == seb && d.z != 0)))
           rc = kErrTruncated;
       }
       if (rc != kOk) atomicCAS(&S.err, kOk, rc);
@@ -1169,12 +1279,69 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
       tph[3] += t - tstamp;
       tstamp = t;
     }
+    // ---- DC predictors: the write pass stored raw DC differences.  Sum them
+    // per component over this run's blocks, segmented-scan the sums over the
+    // runs (predictors restart at each restart segment), then replace each
+    // difference by clip(bias + q * predictor) -- oracle jo_decode_coefs ----
+    {
+      const int rblk = ri > 0 ? ri * bpm : 0x7FFFFFFF;
+      const int first_reset = ri > 0 ? (b0 + rblk - 1) / rblk * rblk : 0x7FFFFFFF;
+      const int bs0 = b0 % bpm;
+      int v[3] = {0, 0, 0}, flag = 0;
+      {
+        int bs = bs0, reset = first_reset;
+        for (int b = b0; b < b1; b++) {
+          if (b == reset) {
+            flag = 1;
+            v[0] = v[1] = v[2] = 0;
+            reset += rblk;
+          }
+          const uint32_t c = __builtin_amdgcn_ubfe(bcomp, 2u * (uint32_t)bs, 2);
+          const int dv = coef_img[(size_t)b * 64];
+          v[0] += c == 0u ? dv : 0;
+          v[1] += c == 1u ? dv : 0;
+          v[2] += c == 2u ? dv : 0;
+          bs = bs + 1 == bpm ? 0 : bs + 1;
+        }
+      }
+      seg_scan<NT, 3>(S, tid, flag, v);
+      int p0 = 0, p1 = 0, p2 = 0;
+      if (tid > 0) {
+        p0 = S.sc.scan_v[tid - 1][0];
+        p1 = S.sc.scan_v[tid - 1][1];
+        p2 = S.sc.scan_v[tid - 1][2];
+      }
+      __syncthreads();
+      int bs = bs0, reset = first_reset;
+      for (int b = b0; b < b1; b++) {
+        if (b == reset) {
+          p0 = p1 = p2 = 0;
+          reset += rblk;
+        }
+        const uint32_t c = __builtin_amdgcn_ubfe(bcomp, 2u * (uint32_t)bs, 2);
+        const int dv = coef_img[(size_t)b * 64];
+        const int cur = (c == 0u ? p0 : (c == 1u ? p1 : p2)) + dv;
+        p0 = c == 0u ? cur : p0;
+        p1 = c == 1u ? cur : p1;
+        p2 = c == 2u ? cur : p2;
+        const uint32_t q = S.qdc[c];
+        const int32_t dqi = (int32_t)((uint32_t)kDcBias + q * (uint32_t)cur);
+        coef_img[(size_t)b * 64] = (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi));
+        bs = bs + 1 == bpm ? 0 : bs + 1;
+      }
+    }
+    {
+      const int64_t t = wall_clock64();
+      dcfix += t - tstamp;
+      tstamp = t;
+    }
   }
   if (tid == 0) {
     if (S.err != kOk) infos[img].status = S.err;
     infos[img].sync_rounds = rounds_total;
     for (int i = 0; i < 4; i++) infos[img].tphase[i] = tph[i];
     for (int i = 0; i < 4; i++) infos[img].dbg[i] = 0;
+    infos[img].dbg[0] = dcfix;  // DC predictor pass (ticks)
   }
 }
 
@@ -1182,15 +1349,30 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
 // idct_kernel
 // ---------------------------------------------------------------------------
 
+typedef unsigned short hj_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_mul_lo16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t,
+                            __builtin_bit_cast(hj_u16x2, a) * __builtin_bit_cast(hj_u16x2, b));
+}
+
 template <int IDCT>
 __global__ void __launch_bounds__(256) idct_kernel(const int16_t* __restrict__ coefs,
                                                    const ImageDesc* __restrict__ desc,
                                                    const ImageInfo* __restrict__ infos,
                                                    uint8_t* __restrict__ planes) {
+  // quantisers in zig-zag order as u16 pairs, DC 1 (its coefficient is final)
+  __shared__ __attribute__((aligned(16))) uint32_t sq[kMaxComp][32];
   const int img = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const ImageInfo& in = infos[img];
-  if (in.status != kOk || j >= in.nblocks) return;
+  if (in.status != kOk) return;
+  for (int k = threadIdx.x; k < kMaxComp * 32; k += blockDim.x) {
+    const int cc = k / 32, i = k % 32;
+    const uint32_t q0 = i == 0 ? 1u : in.qt[cc][2 * i];
+    sq[cc][i] = q0 | ((uint32_t)in.qt[cc][2 * i + 1] << 16);
+  }
+  __syncthreads();
+  if (j >= in.nblocks) return;
   const ImageDesc& dd = desc[img];
   const int bpm = in.bpm;
   const int mcu = j / bpm, b = j - mcu * bpm;
@@ -1204,17 +1386,30 @@ __global__ void __launch_bounds__(256) idct_kernel(const int16_t* __restrict__ c
     bx = mx * in.comp_h[c] + in.mcu_dx[b];
     by = my * in.comp_v[c] + in.mcu_dy[b];
   }
-  int32_t blk[64];
+  // The entropy kernel stores raw levels in zig-zag order (DC final).  Dequantise
+  // two at a time (v_pk_mul_lo_u16: the int16 product the sequential decoder
+  // stores), then place them in natural order -- a compile-time permutation.
+  constexpr uint8_t kZigOf[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16,
+                                  26, 29, 42, 3,  8,  12, 17, 25, 30, 41, 43, 9,  11,
+                                  18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52,
+                                  54, 20, 22, 33, 38, 46, 51, 55, 60, 21, 34, 37, 47,
+                                  50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+  uint32_t zw[32];
   const uint4* src = reinterpret_cast<const uint4*>(coefs + ((size_t)dd.coef_off + j) * 64);
+  const uint4* qv = reinterpret_cast<const uint4*>(sq[c]);
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const uint4 q = src[i];
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    const uint4 lv = src[i], qq = qv[i];
+    zw[4 * i + 0] = pk_mul_lo16(lv.x, qq.x);
+    zw[4 * i + 1] = pk_mul_lo16(lv.y, qq.y);
+    zw[4 * i + 2] = pk_mul_lo16(lv.z, qq.z);
+    zw[4 * i + 3] = pk_mul_lo16(lv.w, qq.w);
+  }
+  int32_t blk[64];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      blk[8 * i + 2 * k] = sext16(w[k]);
-      blk[8 * i + 2 * k + 1] = sext16(w[k] >> 16);
-    }
+  for (int k = 0; k < 64; k++) {
+    const int zi = kZigOf[k];
+    blk[k] = sext16(zw[zi >> 1] >> ((zi & 1) * 16));
   }
   int32_t px[64];
   if (IDCT == 0) {
@@ -1742,15 +1937,23 @@ hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
                           ImageInfo* infos, const HuffTable* luts, int16_t* coefs, uint32_t* recs,
                           int sub_bits, int threads, int n, hipStream_t st) {
-  if (threads == 1024)
-    hipLaunchKernelGGL(entropy_kernel<1024>, dim3(n), dim3(1024), 0, st, clean, segs, desc, infos,
-                       luts, coefs, recs, sub_bits);
-  else if (threads == 512)
-    hipLaunchKernelGGL(entropy_kernel<512>, dim3(n), dim3(512), 0, st, clean, segs, desc, infos,
-                       luts, coefs, recs, sub_bits);
-  else
-    hipLaunchKernelGGL(entropy_kernel<256>, dim3(n), dim3(256), 0, st, clean, segs, desc, infos,
-                       luts, coefs, recs, sub_bits);
+  // two instances per batch: <=4 distinct tables (nearly every JPEG), then
+  // the images that need 5-6 (their workgroups in the first launch, and all
+  // others in the second, exit at once)
+#define HJ_ENT(T, NTAB)                                                                       \
+  hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(n), dim3(T), 0, st, clean, segs, desc, \
+                     infos, luts, coefs, recs, sub_bits)
+  if (threads == 1024) {
+    HJ_ENT(1024, 4);
+    HJ_ENT(1024, 6);
+  } else if (threads == 512) {
+    HJ_ENT(512, 4);
+    HJ_ENT(512, 6);
+  } else {
+    HJ_ENT(256, 4);
+    HJ_ENT(256, 6);
+  }
+#undef HJ_ENT
   return hipGetLastError();
 }
 hipError_t launch_idct(const int16_t* coefs, const ImageDesc* desc, const ImageInfo* infos,
