@@ -95,6 +95,8 @@ def _args():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sub-bits", type=int, default=0)
     p.add_argument("--entropy-threads", type=int, default=0)
+    p.add_argument("--warm-slots", type=int, default=-1,
+                   help="entropy round-0 warm-up slots before each run (-1: library default)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="pad224")
     p.add_argument("--norm-dtype", choices=["float16", "bfloat16"], default="float16")
     p.add_argument("--inflight", type=int, default=2, choices=[1, 2, 3],
@@ -170,6 +172,8 @@ def main():
         dec.set_param("sub_bits", a.sub_bits)
     if a.entropy_threads:
         dec.set_param("entropy_threads", a.entropy_threads)
+    if a.warm_slots >= 0:
+        dec.set_param("warmup_slots", a.warm_slots)
     dec.set_param("lanes", a.lanes)
     if a.workload == "imagenet":
         spec = Output(**{**IMAGENET_SPEC.__dict__, "norm_dtype": a.norm_dtype})

@@ -238,7 +238,9 @@ int spdl_hj_last_timings(spdl_hj_ctx* ctx, float* us, int32_t cap, int32_t* n_ou
 const char* spdl_hj_stage_name(int32_t i);
 
 /* Tuning knobs: "sub_bits" (slot size of the parallel Huffman decode),
- * "entropy_threads" (256/512/1024), "lanes" (1 or 2 concurrent pipelines:
+ * "entropy_threads" (256/512/1024), "warmup_slots" (0-64: slots a Huffman
+ * run decodes from a guessed state before its own first slot; default 8),
+ * "lanes" (1-3 concurrent pipelines:
  * with 2, successive batches alternate between two device workspaces and run
  * on the context's own two streams, each ordered after the caller's stream at
  * submission; completion is then observed through the ticket --

@@ -957,17 +957,15 @@ __device__ void seg_scan(SH& S, int tid, int flag, const int (&v)[3]) {
   }
 }
 
+// One image's scan, decoded by the whole workgroup.
 template <int NT, int NTAB>
-__global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
-                                                     const uint32_t* __restrict__ segs,
-                                                     const ImageDesc* __restrict__ desc,
-                                                     ImageInfo* __restrict__ infos,
-                                                     const HuffTable* __restrict__ luts,
-                                                     int16_t* __restrict__ coefs,
-                                                     uint32_t* __restrict__ recs,
-                                                     const int sub_bits_param) {
-  __shared__ EntShared<NT, NTAB> S;
-  const int img = blockIdx.x, tid = threadIdx.x;
+__device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
+                              const uint8_t* __restrict__ clean, const uint32_t* __restrict__ segs,
+                              const ImageDesc* __restrict__ desc, ImageInfo* __restrict__ infos,
+                              const HuffTable* __restrict__ luts, int16_t* __restrict__ coefs,
+                              uint32_t* __restrict__ recs, const int sub_bits_param,
+                              const int warm_slots) {
+  const int tid = threadIdx.x;
   uint32_t* win = &S.win[0][tid];
   if (infos[img].status != kOk) return;
   const ImageDesc dd = desc[img];
@@ -1121,7 +1119,18 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
           have = false;
           continue;
         }
-        if (slot_known(k) || !have) dec_init<NT>(d, win, words, slot_start(k), 0, 0);
+        if (slot_known(k)) {
+          dec_init<NT>(d, win, words, slot_start(k), 0, 0);
+        } else if (!have) {
+          // warm-up: guess a state warm_slots slots earlier (or take the
+          // segment start, which is exact) and decode up to the slot, so the
+          // run's first state is usually already synchronised and the sync
+          // rounds below have short chains to settle
+          const uint32_t ss = slot_start(k), s0 = seg_start_bits(slot_seg(k));
+          const uint32_t wb = (uint32_t)warm_slots * N;
+          dec_init<NT>(d, win, words, ss - s0 > wb ? ss - wb : s0, 0, 0);
+          decode_state<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, ss);
+        }
         decode_k(d, k);
         have = true;
       }
@@ -1342,6 +1351,29 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
     for (int i = 0; i < 4; i++) infos[img].tphase[i] = tph[i];
     for (int i = 0; i < 4; i++) infos[img].dbg[i] = 0;
     infos[img].dbg[0] = dcfix;  // DC predictor pass (ticks)
+  }
+}
+
+// The NTAB = 4 instance runs one workgroup per image.  The NTAB = 6 instance
+// (images with 5-6 distinct tables or long codes outside the LDS pool, rare)
+// runs a few workgroups that stride over the batch: every other image exits
+// at once, and the small grid does not wait for LDS behind the other lane's
+// entropy workgroups.
+template <int NT, int NTAB>
+__global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
+                                                     const uint32_t* __restrict__ segs,
+                                                     const ImageDesc* __restrict__ desc,
+                                                     ImageInfo* __restrict__ infos,
+                                                     const HuffTable* __restrict__ luts,
+                                                     int16_t* __restrict__ coefs,
+                                                     uint32_t* __restrict__ recs,
+                                                     const int sub_bits_param, const int warm_slots,
+                                                     const int n) {
+  __shared__ EntShared<NT, NTAB> S;
+  for (int img = blockIdx.x; img < n; img += gridDim.x) {
+    entropy_image<NT, NTAB>(S, img, clean, segs, desc, infos, luts, coefs, recs, sub_bits_param,
+                            warm_slots);
+    __syncthreads();  // LDS is reused by the next image
   }
 }
 
@@ -1936,13 +1968,13 @@ hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo
 }
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
                           ImageInfo* infos, const HuffTable* luts, int16_t* coefs, uint32_t* recs,
-                          int sub_bits, int threads, int n, hipStream_t st) {
-  // two instances per batch: <=4 distinct tables (nearly every JPEG), then
-  // the images that need 5-6 (their workgroups in the first launch, and all
-  // others in the second, exit at once)
-#define HJ_ENT(T, NTAB)                                                                       \
-  hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(n), dim3(T), 0, st, clean, segs, desc, \
-                     infos, luts, coefs, recs, sub_bits)
+                          int sub_bits, int warm_slots, int threads, int n, hipStream_t st) {
+  // two instances per batch: <=4 distinct tables (nearly every JPEG, one
+  // workgroup per image), then the images that need 5-6 (at most 16
+  // workgroups striding over the batch)
+#define HJ_ENT(T, NTAB)                                                                   \
+  hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(NTAB > 4 ? (n < 16 ? n : 16) : n), dim3(T), \
+                     0, st, clean, segs, desc, infos, luts, coefs, recs, sub_bits, warm_slots, n)
   if (threads == 1024) {
     HJ_ENT(1024, 4);
     HJ_ENT(1024, 6);
