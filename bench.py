@@ -37,7 +37,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # Per-launch HBM-side bytes per kernel from the committed rocprofv3 --pmc
 # passes of this same command (tools/pmc_passes.sh + tools/pmc_traffic.py):
 # FETCH_SIZE / WRITE_SIZE cannot be read from inside the timed process.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v8", "traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v9", "traffic.json")
 # bench stage -> kernels launched in it
 STAGE_KERNELS = {
     "parse": ["hj::parse_kernel"],
@@ -309,7 +309,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": _pmc_traffic(dominant, a.batch) if a.workload == "pad224" else None,
-                "traffic_source": "profiles/r01_v8/traffic.json (rocprofv3 --pmc FETCH_SIZE, "
+                "traffic_source": "profiles/r01_v9/traffic.json (rocprofv3 --pmc FETCH_SIZE, "
                                   "WRITE_SIZE; separate passes; x1024, FETCH x2 gfx950)",
                 "algorithmic_bytes_per_image": round(per_image_bytes, 1),
             },

@@ -56,7 +56,15 @@ enum spdl_hj_pix_fmt {
 };
 
 enum spdl_hj_aspect { SPDL_HJ_ASPECT_NONE = 0, SPDL_HJ_ASPECT_DECREASE = 1, SPDL_HJ_ASPECT_INCREASE = 2 };
-enum spdl_hj_filter { SPDL_HJ_FILTER_BICUBIC = 0, SPDL_HJ_FILTER_BILINEAR = 1 };
+/* BICUBIC / BILINEAR: swscale flags of the CPU path's scale filter
+ * (src/spdl/io/_preprocessing.py:214-234).  LANCZOS: Lanczos-3, the NPP
+ * NPPI_INTER_LANCZOS kernel of load_image_batch_nvjpeg's resize
+ * (src/libspdl/cuda/npp/detail/resize.cpp:36-116), also swscale flags=lanczos. */
+enum spdl_hj_filter {
+  SPDL_HJ_FILTER_BICUBIC = 0,
+  SPDL_HJ_FILTER_BILINEAR = 1,
+  SPDL_HJ_FILTER_LANCZOS = 2
+};
 /* F16 / BF16: (x/255 - mean)/std in IEEE fp32 (the reference's
  * Preprocessing.forward, examples/imagenet_classification.py:95-106), rounded
  * to nearest even into half / bfloat16. */

@@ -900,9 +900,44 @@ int jo_geometry(int w, int h, const jo_resize* rs, jo_geom* g) {
 /* Resampling kernel: Keys cubic with a = -0.6 (the B=0, C=0.6 member of the
  * family swscale's SWS_BICUBIC uses), support widened by the downscale factor
  * (anti-aliased); or a triangle (bilinear).  Every float step is one IEEE op. */
+/* sin(pi x) for 0 <= x <= 3 from float adds and multiplies only (odd Taylor
+ * polynomial of sin(pi r) to r^13 on the reduced argument |r| <= 1/2), so the
+ * GPU kernel (hj_kernels.hip lanczos_eval) evaluates the same IEEE ops and
+ * gets the same bits -- a libm sinf would not be reproducible there. */
+static float sinpi_poly(float x) {
+  float k = rintf(x);
+  float r = x - k;
+  float p = r * r;
+  float s = -7.37043094e-3f + p * 4.66302806e-4f;
+  s = 8.21458866e-2f + p * s;
+  s = -5.99264529e-1f + p * s;
+  s = 2.55016404f + p * s;
+  s = -5.16771278f + p * s;
+  s = 3.14159265f + p * s;
+  s = r * s;
+  return ((int)k & 1) ? -s : s;
+}
+
+/* Lanczos-3 windowed sinc, sinc(t) sinc(t/3) = 3 sin(pi t) sin(pi t/3) /
+ * (pi^2 t^2): the kernel of NPP's NPPI_INTER_LANCZOS resize that
+ * load_image_batch_nvjpeg uses (src/libspdl/cuda/npp/detail/resize.cpp:36-116),
+ * and of swscale's flags=lanczos (default parameter 3). */
+static float lanczos_eval(float t) {
+  if (t == 0.0f) return 1.0f;
+  if (t >= 3.0f) return 0.0f;
+  float a = sinpi_poly(t);
+  float b = sinpi_poly(t / 3.0f);
+  float num = 3.0f * a;
+  num = num * b;
+  float den = 9.8696044f * t;
+  den = den * t;
+  return num / den;
+}
+
 static float kernel_eval(int filter, float x) {
   float t = fabsf(x);
   if (filter == JO_FILTER_BILINEAR) return t < 1.0f ? 1.0f - t : 0.0f;
+  if (filter == JO_FILTER_LANCZOS) return lanczos_eval(t);
   float t2 = t * t;
   float t3 = t2 * t;
   if (t <= 1.0f) {
@@ -919,7 +954,9 @@ static float kernel_eval(int filter, float x) {
   return 0.0f;
 }
 
-static float filter_radius(int filter) { return filter == JO_FILTER_BILINEAR ? 1.0f : 2.0f; }
+static float filter_radius(int filter) {
+  return filter == JO_FILTER_BILINEAR ? 1.0f : filter == JO_FILTER_LANCZOS ? 3.0f : 2.0f;
+}
 
 int jo_max_taps(int src_len, int dst_len, int filter) {
   float scale = (float)src_len / (float)dst_len;

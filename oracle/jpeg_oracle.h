@@ -58,7 +58,7 @@ enum { JO_IDCT_SIMPLE = 0, JO_IDCT_ISLOW = 1 };
 enum { JO_FMT_RGB = 0, JO_FMT_BGR = 1, JO_FMT_RGB24 = 2, JO_FMT_BGR24 = 3 };
 
 enum { JO_ASPECT_NONE = 0, JO_ASPECT_DECREASE = 1, JO_ASPECT_INCREASE = 2 };
-enum { JO_FILTER_BICUBIC = 0, JO_FILTER_BILINEAR = 1 };
+enum { JO_FILTER_BICUBIC = 0, JO_FILTER_BILINEAR = 1, JO_FILTER_LANCZOS = 2 };
 enum { JO_DTYPE_U8 = 0, JO_DTYPE_F16 = 1, JO_DTYPE_BF16 = 2 };
 
 #define JO_MAX_COMP 3

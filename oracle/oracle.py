@@ -21,7 +21,7 @@ _BUILD = os.path.join(_HERE, "_build")
 IDCT_SIMPLE, IDCT_ISLOW = 0, 1
 FMT = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
 ASPECT = {None: 0, "none": 0, "decrease": 1, "increase": 2}
-FILTER = {"bicubic": 0, "bilinear": 1}
+FILTER = {"bicubic": 0, "bilinear": 1, "lanczos": 2}
 DTYPE_U8, DTYPE_F16, DTYPE_BF16 = 0, 1, 2
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)

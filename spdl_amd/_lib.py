@@ -20,7 +20,7 @@ ABI_VERSION = 1
 # enums (mirror include/spdl_hipjpeg.h)
 PIX_FMTS = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
 ASPECT = {None: 0, "none": 0, "decrease": 1, "increase": 2}
-FILTERS = {"bicubic": 0, "bilinear": 1}
+FILTERS = {"bicubic": 0, "bilinear": 1, "lanczos": 2}
 IDCT = {"simple": 0, "islow": 1}
 DTYPE_U8, DTYPE_F16, DTYPE_BF16 = 0, 1, 2
 NORM_DTYPES = {"float16": DTYPE_F16, "bfloat16": DTYPE_BF16}

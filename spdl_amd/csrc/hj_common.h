@@ -57,6 +57,7 @@ constexpr uint32_t kKindCode = 1;  // code resolved, value bits follow
 constexpr uint32_t kKindFull = 2;  // code + value resolved
 constexpr uint32_t kKindSub = 3;   // code longer than kLutBits: look up sub[idx][next 6 bits]
 constexpr int kSubBits = 16 - kLutBits;
+constexpr int kSubPool = 2048;  // entropy LDS entries for the second-level tables of a scan
 constexpr int kMaxSub = 16;        // 64-entry sub-tables per Huffman table
 constexpr int kEntHiShift = 21;    // value / sub-table index field
 
@@ -153,6 +154,9 @@ struct ImageInfo {      // device-filled by the parse kernel
   int32_t clean_len;    // destuffed bytes
   int32_t sync_rounds;  // diagnostics: rounds the Huffman sync took
   int32_t scan_end;     // destuff: first byte past the entropy-coded data
+  int32_t ent_wide;     // parse: scan needs the NTAB = 6 entropy instance (5-6 distinct
+                        // tables, long codes outside the LDS sub-table pool or slow codes)
+  int32_t pad_;
   int64_t tphase[4];    // diagnostics: wall_clock64 ticks of the entropy phases
   int64_t dbg[4];       // diagnostics: symbols (round 0), wave iterations, shader clocks, rt ticks
 };

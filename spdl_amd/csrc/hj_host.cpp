@@ -303,7 +303,10 @@ int geometry(int w, int h, const spdl_hj_output* o, Geom* g) {
 int max_taps(int src_len, int dst_len, int filter) {
   float scale = (float)src_len / (float)dst_len;
   float fscale = scale > 1.0f ? scale : 1.0f;
-  float support = (filter == SPDL_HJ_FILTER_BILINEAR ? 1.0f : 2.0f) * fscale;
+  float support = (filter == SPDL_HJ_FILTER_BILINEAR  ? 1.0f
+                   : filter == SPDL_HJ_FILTER_LANCZOS ? 3.0f
+                                                      : 2.0f) *
+                  fscale;
   return (int)ceilf(2.0f * support) + 1;
 }
 
@@ -792,7 +795,7 @@ int stage_h2d(spdl_hj_ctx* ctx, Slot& s, size_t total, hipStream_t st, char* err
 
 bool valid_output(const spdl_hj_output* o) {
   return o && o->pix_fmt >= 0 && o->pix_fmt <= 3 && (o->dtype >= 0 && o->dtype <= 2) &&
-         (o->idct == 0 || o->idct == 1) && (o->filter == 0 || o->filter == 1) &&
+         (o->idct == 0 || o->idct == 1) && (o->filter >= 0 && o->filter <= 2) &&
          o->aspect >= 0 && o->aspect <= 2;
 }
 

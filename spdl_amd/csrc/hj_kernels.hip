@@ -309,6 +309,7 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
       for (int i = 0; i < 64; i++) s.info.qt[c][i] = s.qt[s.qtsel[c]][i];
   }
   HuffTable* tabs = luts + (size_t)img * 8;
+  int tab_nsub[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tab_slow = 0;  // per table slot (thread 0 uses)
   for (int t = 0; t < 8; t++) {
     if (!s.have[t]) continue;
     const bool is_dc = t < 4;
@@ -359,6 +360,8 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
         tabs[t].sub[i] = entry16(((uint32_t)(p_lo + (i >> kSubBits)) << kSubBits) |
                                      (uint32_t)(i & ((1 << kSubBits) - 1)),
                                  16, 16);
+    tab_nsub[t] = sub_ok ? nsub : 0;
+    tab_slow |= sub_ok ? 0 : 1 << t;
     if (tid == 0) {
       tabs[t].nsub = sub_ok ? nsub : 0;
       tabs[t].long_slow = sub_ok ? 0 : 1;  // long codes left to the canonical path
@@ -367,7 +370,25 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     for (int i = tid; i < 17; i += blockDim.x) tabs[t].valoff[i] = s.valoff[t][i];
     for (int i = tid; i < 256; i += blockDim.x) tabs[t].vals[i] = s.vals[t][i];
   }
-  if (tid == 0) infos[img] = s.info;
+  if (tid == 0) {
+    // Which entropy instance decodes this scan: NTAB = 4 takes <= 4 distinct
+    // tables whose long codes all fit the LDS sub-table pool (no canonical
+    // fallback); NTAB = 6 the rest.  Decided once here, so the entropy
+    // kernels test one flag instead of walking the tables in HBM.
+    int ns = 0, seen = 0, subs = 0, slow = 0;
+    for (int c = 0; c < s.info.ncomp; c++)
+      for (int k = 0; k < 2; k++) {
+        const int slot = k == 0 ? s.info.dc_tab[c] : 4 + s.info.ac_tab[c];
+        if (!(seen & (1 << slot))) {
+          ns++;
+          subs += tab_nsub[slot];
+          slow |= (tab_slow >> slot) & 1;
+        }
+        seen |= 1 << slot;
+      }
+    s.info.ent_wide = !(ns <= 4 && (subs << kSubBits) <= kSubPool && !slow);
+    infos[img] = s.info;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -605,7 +626,6 @@ constexpr int kMaxTabs = 2 * kMaxComp;  // distinct (DC, AC) tables of a scan
 #endif
 constexpr int kWinWords = HJ_WIN_WORDS;  // bit-reader window per thread (words)
 
-constexpr int kSubPool = 2048;  // LDS entries for second-level tables of all tables
 
 // NTAB = distinct Huffman tables the workgroup holds in LDS.  The common case
 // (luma + chroma DC/AC: 4 tables, gray: 2) runs the NTAB = 4 instance, small
@@ -974,23 +994,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   // tables with every long code in sub-tables that fit the LDS pool (no
   // canonical fallback in its loops); the NTAB = 6 instance takes the rest.
   constexpr bool kSlow = NTAB > 4;
-  {
-    const HuffTable* tabs = luts + (size_t)img * 8;
-    int ns = 0, seen = 0, subs = 0;
-    bool slow = false;
-    for (int c = 0; c < in.ncomp; c++)
-      for (int k = 0; k < 2; k++) {
-        const int slot = k == 0 ? in.dc_tab[c] : 4 + in.ac_tab[c];
-        if (!(seen & (1 << slot))) {
-          ns++;
-          subs += tabs[slot].nsub;
-          slow |= tabs[slot].long_slow != 0;
-        }
-        seen |= 1 << slot;
-      }
-    const bool fast = ns <= 4 && (subs << kSubBits) <= kSubPool && !slow;
-    if (kSlow == fast) return;
-  }
+  if (kSlow != (in.ent_wide != 0)) return;  // (parse_kernel decides the instance)
   const int bpm = in.bpm, ri = in.ri, nmcu = in.mcux * in.mcuy;
   const int nblocks = in.nblocks;
   const uint32_t* words = reinterpret_cast<const uint32_t*>(clean + dd.in_off);
@@ -1370,10 +1374,30 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
                                                      const int sub_bits_param, const int warm_slots,
                                                      const int n) {
   __shared__ EntShared<NT, NTAB> S;
-  for (int img = blockIdx.x; img < n; img += gridDim.x) {
-    entropy_image<NT, NTAB>(S, img, clean, segs, desc, infos, luts, coefs, recs, sub_bits_param,
-                            warm_slots);
-    __syncthreads();  // LDS is reused by the next image
+  if constexpr (NTAB > 4) {
+    // Strided instance: the workgroup first tests the flags of its next NT
+    // images at once (one load per thread) and skips the chunk when none of
+    // them needs this instance -- the common case, where the launch is then
+    // one flag read per image instead of NT serial per-image checks.
+    const int tid = threadIdx.x;
+    for (int base = blockIdx.x; base < n; base += gridDim.x * NT) {
+      const int mine = base + tid * gridDim.x;
+      const bool need = mine < n && infos[mine].status == kOk && infos[mine].ent_wide != 0;
+      if (!__syncthreads_or(need)) continue;
+      for (int j = 0; j < NT; j++) {
+        const int img = base + j * gridDim.x;
+        if (img >= n) break;
+        entropy_image<NT, NTAB>(S, img, clean, segs, desc, infos, luts, coefs, recs,
+                                sub_bits_param, warm_slots);
+        __syncthreads();  // LDS is reused by the next image
+      }
+    }
+  } else {
+    for (int img = blockIdx.x; img < n; img += gridDim.x) {
+      entropy_image<NT, NTAB>(S, img, clean, segs, desc, infos, luts, coefs, recs, sub_bits_param,
+                              warm_slots);
+      __syncthreads();  // LDS is reused by the next image
+    }
   }
 }
 
@@ -1546,9 +1570,39 @@ __global__ void __launch_bounds__(256) csc_kernel(const uint8_t* __restrict__ pl
 // ---------------------------------------------------------------------------
 
 #pragma clang fp contract(off)
+// sin(pi x), 0 <= x <= 3: odd polynomial to r^13 on r = x - rint(x), the
+// oracle's op sequence (jpeg_oracle.c sinpi_poly), contraction off.
+__device__ float sinpi_poly(float x) {
+  const float k = rintf(x);
+  const float r = x - k;
+  const float p = r * r;
+  float s = -7.37043094e-3f + p * 4.66302806e-4f;
+  s = 8.21458866e-2f + p * s;
+  s = -5.99264529e-1f + p * s;
+  s = 2.55016404f + p * s;
+  s = -5.16771278f + p * s;
+  s = 3.14159265f + p * s;
+  s = r * s;
+  return ((int)k & 1) ? -s : s;
+}
+
+// Lanczos-3 (NPP NPPI_INTER_LANCZOS of resize_npp, swscale flags=lanczos)
+__device__ float lanczos_eval(float t) {
+  if (t == 0.0f) return 1.0f;
+  if (t >= 3.0f) return 0.0f;
+  const float a = sinpi_poly(t);
+  const float b = sinpi_poly(__fdiv_rn(t, 3.0f));
+  float num = 3.0f * a;
+  num = num * b;
+  float den = 9.8696044f * t;
+  den = den * t;
+  return __fdiv_rn(num, den);
+}
+
 __device__ float kernel_eval(int filter, float x) {
   const float t = fabsf(x);
   if (filter == 1) return t < 1.0f ? 1.0f - t : 0.0f;
+  if (filter == 2) return lanczos_eval(t);
   const float t2 = t * t;
   const float t3 = t2 * t;
   if (t <= 1.0f) {
@@ -1596,7 +1650,7 @@ __global__ void __launch_bounds__(256) weights_kernel(const ImageDesc* __restric
   int16_t* w = reinterpret_cast<int16_t*>(pool + off + dst_len) + (int64_t)i * ((taps + 1) / 2) * 2;
   const float scale = __fdiv_rn((float)src_len, (float)dst_len);
   const float fscale = scale > 1.0f ? scale : 1.0f;
-  const float support = (filter == 1 ? 1.0f : 2.0f) * fscale;
+  const float support = (filter == 1 ? 1.0f : filter == 2 ? 3.0f : 2.0f) * fscale;
   float center = ((float)i + 0.5f) * scale;
   center = center - 0.5f;
   const int lo = (int)ceilf(center - support);

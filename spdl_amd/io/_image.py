@@ -80,13 +80,22 @@ def decode_image_nvjpeg(
     scale_height: int = -1,
     pix_fmt: str = "rgb",
     sync: bool = True,
+    scale_algo: str = "lanczos",
 ) -> CUDABuffer:
     """Decode JPEG(s) on the GPU.  Same contract as the reference: a single
     source gives ``[3,H,W]`` (``"rgb"``/``"bgr"``) or ``[H,W,3]``
     (``"rgb24"``/``"bgr24"``), resized (stretch) when both scale sizes are
-    positive; a sequence gives ``[B,...]`` and requires the scale sizes."""
+    positive; a sequence gives ``[B,...]`` and requires the scale sizes.
+
+    ``scale_algo`` (an addition; the reference has no such argument) picks
+    the resampling kernel.  The default ``"lanczos"`` is Lanczos-3, the
+    kernel of the reference's ``resize_npp`` (NPPI_INTER_LANCZOS,
+    src/libspdl/cuda/npp/detail/resize.cpp:36-116); ``"bicubic"`` /
+    ``"bilinear"`` are the CPU path's swscale flags."""
     if device_config is None:
         raise ValueError("device_config must be provided.")
+    if scale_algo not in _lib.FILTERS:
+        raise ValueError(f"Unexpected scale_algo: {scale_algo}. Supported: {list(_lib.FILTERS)}")
     if pix_fmt not in _lib.PIX_FMTS:
         raise RuntimeError(
             f'Unexpected pix_fmt: {pix_fmt}. Supported values are "bgr", "bgr24", "rgb", "rgb24"'
@@ -97,11 +106,13 @@ def decode_image_nvjpeg(
             raise RuntimeError("No input is provided.")
         if scale_width <= 0 or scale_height <= 0:
             raise RuntimeError("Both `scale_width` and `scale_height` must be specified.")
-        out = Output(pix_fmt=pix_fmt, resize=True, fit_w=scale_width, fit_h=scale_height)
+        out = Output(pix_fmt=pix_fmt, resize=True, fit_w=scale_width, fit_h=scale_height,
+                     filter=scale_algo)
         return _decode(datas, out, device_config, _shape(out, scale_width, scale_height), True)
     data = _read(src)
     if scale_width > 0 and scale_height > 0:
-        out = Output(pix_fmt=pix_fmt, resize=True, fit_w=scale_width, fit_h=scale_height)
+        out = Output(pix_fmt=pix_fmt, resize=True, fit_w=scale_width, fit_h=scale_height,
+                     filter=scale_algo)
         w, h = scale_width, scale_height
     else:
         out = Output(pix_fmt=pix_fmt)
@@ -117,14 +128,18 @@ def load_image_batch_nvjpeg(
     width: int,
     height: int,
     pix_fmt: str = "rgb",
+    scale_algo: str = "lanczos",
 ) -> CUDABuffer:
-    """Batch load + resize (reference _composite.py:486-524)."""
+    """Batch load + resize (reference _composite.py:486-524): stretch to
+    ``width`` x ``height`` with the ``resize_npp`` kernel (Lanczos-3) unless
+    ``scale_algo`` says otherwise."""
     return decode_image_nvjpeg(
         [_read(s) for s in srcs],
         scale_width=width,
         scale_height=height,
         device_config=device_config,
         pix_fmt=pix_fmt,
+        scale_algo=scale_algo,
     )
 
 

@@ -13,7 +13,8 @@ from __future__ import annotations
 
 from .._lib import Output
 
-_FILTERS = {"bicubic": "bicubic", "bilinear": "bilinear", "fast_bilinear": "bilinear"}
+_FILTERS = {"bicubic": "bicubic", "bilinear": "bilinear", "fast_bilinear": "bilinear",
+            "lanczos": "lanczos"}
 
 
 def get_video_filter_desc(

@@ -65,6 +65,8 @@ def case(name: str) -> bytes:
         return _enc(synthetic_pixels(16, 1, 1), quality=90)
     if name == "optimized":
         return _enc(synthetic_pixels(17, 240, 320), quality=90, optimize=True)
+    if name == "six_tables":
+        return six_tables(case("q90_444"))
     if name == "large_1080p":
         return _enc(synthetic_pixels(18, 1080, 1920), quality=90, subsampling=2)
     raise KeyError(name)
@@ -73,8 +75,39 @@ def case(name: str) -> bytes:
 VALID = [
     "q90_420", "q75_420", "q95_420", "q90_444", "q90_422", "odd_227x333", "odd_444_101x67",
     "gray", "gray_odd", "noise_420", "noise_q100", "restart_rows", "restart_blocks",
-    "restart_every_mcu", "tiny_8x8", "tiny_1x1", "optimized", "large_1080p",
+    "restart_every_mcu", "tiny_8x8", "tiny_1x1", "optimized", "six_tables", "large_1080p",
 ]
+
+
+def six_tables(data: bytes) -> bytes:
+    """A 3-component JPEG re-labelled to use six distinct Huffman tables.
+
+    The chroma DC/AC tables (ids 1) are copied to ids 2 by an extra DHT
+    segment and the third component's SOS selectors point at them, so the
+    pixels are those of ``data`` while the scan holds DC0-2 + AC0-2: the
+    decoder's wide-table path (more tables than the common LDS layout).
+    """
+    d = bytearray(data)
+    tabs, pos, sos = {}, 2, None
+    while pos < len(d):
+        assert d[pos] == 0xFF
+        m, ln = d[pos + 1], (d[pos + 2] << 8) | d[pos + 3]
+        if m == 0xC4:  # DHT: one or more (class/id, 16 counts, values)
+            q = pos + 4
+            while q < pos + 2 + ln:
+                n = sum(d[q + 1:q + 17])
+                tabs[d[q]] = bytes(d[q:q + 17 + n])
+                q += 17 + n
+        if m == 0xDA:
+            sos = pos
+            break
+        pos += 2 + ln
+    assert sos is not None and d[sos + 4] == 3, "needs a 3-component scan"
+    seg = bytes([0x02]) + tabs[0x01][1:] + bytes([0x12]) + tabs[0x11][1:]
+    dht = b"\xff\xc4" + (len(seg) + 2).to_bytes(2, "big") + seg
+    assert d[sos + 10] == 0x11  # third component: DC1 / AC1
+    d[sos + 10] = 0x22
+    return bytes(d[:sos]) + dht + bytes(d[sos:])
 
 
 def progressive() -> bytes:

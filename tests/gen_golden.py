@@ -37,7 +37,7 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 CASES = [
     "q90_444", "q90_422", "odd_227x333", "odd_444_101x67", "gray", "gray_odd",
     "noise_q100", "restart_rows", "restart_blocks", "restart_every_mcu", "tiny_8x8",
-    "tiny_1x1", "optimized",
+    "tiny_1x1", "optimized", "six_tables",
 ]
 
 PAD224 = O.Resize(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224)
@@ -56,7 +56,10 @@ FILTER_ARGS = [
 
 def main() -> None:
     os.makedirs(os.path.join(GOLD, "jpeg"), exist_ok=True)
+    only = sys.argv[1:]  # optional: regenerate just these cases
     for name in CASES:
+        if only and name not in only:
+            continue
         data = cases.case(name)
         with open(os.path.join(GOLD, "jpeg", f"{name}.jpg"), "wb") as f:
             f.write(data)
@@ -77,6 +80,8 @@ def main() -> None:
             out[f"plane{c}"] = p
         np.savez_compressed(os.path.join(GOLD, f"{name}.oracle.npz"), **out)
         print(name, len(data), "bytes")
+    if only:
+        return
     sys.path.insert(0, "/root/reference/src")
     from spdl.io._preprocessing import get_video_filter_desc
 

@@ -71,7 +71,7 @@ RESIZES = {
 @pytest.mark.parametrize("name", ["q90_420", "odd_227x333", "gray", "q90_444", "restart_rows",
                                   "large_1080p", "tiny_8x8"])
 @pytest.mark.parametrize("rk", list(RESIZES))
-@pytest.mark.parametrize("filt", ["bicubic", "bilinear"])
+@pytest.mark.parametrize("filt", ["bicubic", "bilinear", "lanczos"])
 def test_resize_bit_exact(decoder, oracle, name, rk, filt):
     d = cases.case(name)
     kw = RESIZES[rk]

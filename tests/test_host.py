@@ -136,7 +136,8 @@ def test_filter_desc_parsing():
     with pytest.raises(ValueError):
         parse_image_filter("hflip")
     with pytest.raises(ValueError):
-        parse_image_filter("scale=w=224:h=224:flags=lanczos")
+        parse_image_filter("scale=w=224:h=224:flags=spline")
+    assert parse_image_filter("scale=w=224:h=224:flags=lanczos").filter == "lanczos"
 
 
 def test_output_spec_rejects_bad_pix_fmt():

@@ -213,3 +213,47 @@ def test_bf16_rounding_matches_torch(oracle):
     hyp = np.array([L.jo_f32_to_bf16(float(x)) for x in vals], np.uint16)
     ref = torch.from_numpy(vals).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
     np.testing.assert_array_equal(hyp, ref)
+
+
+def _lanczos3(x):
+    x = np.abs(np.asarray(x, dtype=np.float64))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        v = 3.0 * np.sin(np.pi * x) * np.sin(np.pi * x / 3.0) / (np.pi ** 2 * x * x)
+    return np.where(x == 0, 1.0, np.where(x < 3.0, v, 0.0))
+
+
+@pytest.mark.parametrize("src,dst", [(640, 224), (480, 168), (320, 224), (333, 256), (100, 700),
+                                     (1920, 224), (8, 8)])
+def test_lanczos_weights_follow_the_formula(oracle, src, dst):
+    """Lanczos-3 taps (NPP NPPI_INTER_LANCZOS / swscale flags=lanczos kernel):
+    the float-polynomial evaluation the GPU shares, quantised to Q14, stays
+    within one LSB of the float64 taps from sin() (bar the tap that absorbs
+    the rounding residual)."""
+    first, w = oracle.axis_weights(src, dst, "lanczos")
+    scale = src / dst
+    fs = max(scale, 1.0)
+    for i in range(dst):
+        c = (i + 0.5) * scale - 0.5
+        n = int(np.floor(c + 3 * fs)) - int(np.ceil(c - 3 * fs)) + 1
+        lo = int(first[i])
+        wf = _lanczos3((np.arange(lo, lo + n) - c) / fs)
+        ref = wf / wf.sum() * 16384.0
+        got = w[i, :n].astype(np.float64)
+        assert got.sum() == 16384
+        # every tap rounds to nearest; the largest one also takes the
+        # rounding residual that makes the taps sum to 16384
+        err = np.abs(got - ref)
+        # (float vs float64 evaluation may flip a tap that sits at x.5)
+        assert (err > 1.01).sum() <= 1 and err.max() <= 0.5 * n + 1.01, (i, err)
+        assert not w[i, n:].any()
+
+
+def test_lanczos_resize_close_to_bicubic(oracle):
+    """Sanity: Lanczos-3 and bicubic resamplings of the same picture agree to
+    a few levels (both are interpolating, antialiased kernels)."""
+    d = _jpeg("q90_444")
+    kw = dict(fit_w=160, fit_h=120)
+    a = oracle.decode_resize(d, oracle.Resize(filter="lanczos", **kw), "rgb24").astype(int)
+    b = oracle.decode_resize(d, oracle.Resize(filter="bicubic", **kw), "rgb24").astype(int)
+    assert a.shape == b.shape == (120, 160, 3)
+    assert np.abs(a - b).mean() < 2.0 and (a != b).any()
