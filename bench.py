@@ -95,6 +95,8 @@ def _args():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sub-bits", type=int, default=0)
     p.add_argument("--entropy-threads", type=int, default=0)
+    p.add_argument("--entropy-lds-pad", type=int, default=-1,
+                   help="extra dynamic LDS bytes per entropy workgroup (-1: library default)")
     p.add_argument("--warm-slots", type=int, default=-1,
                    help="entropy round-0 warm-up slots before each run (-1: library default)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="pad224")
@@ -172,6 +174,8 @@ def main():
         dec.set_param("sub_bits", a.sub_bits)
     if a.entropy_threads:
         dec.set_param("entropy_threads", a.entropy_threads)
+    if a.entropy_lds_pad >= 0:
+        dec.set_param("entropy_lds_pad", a.entropy_lds_pad)
     if a.warm_slots >= 0:
         dec.set_param("warmup_slots", a.warm_slots)
     dec.set_param("lanes", a.lanes)

@@ -33,7 +33,8 @@ hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, DsChunk*
                           uint32_t*, int, int,
                           hipStream_t);
 hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
-                          const HuffTable*, int16_t*, uint32_t*, int, int, int, int, hipStream_t);
+                          const HuffTable*, int16_t*, uint32_t*, int, int, int, int, int,
+                          hipStream_t);
 hipError_t launch_idct(const int16_t*, const ImageDesc*, const ImageInfo*, uint8_t*, int, int, int,
                        hipStream_t);
 hipError_t launch_weights(const ImageDesc*, const ImageInfo*, int32_t*, int, int, int,
@@ -570,6 +571,7 @@ struct spdl_hj_ctx {
   int debug_mask = 0;
   int entropy_threads = 512;
   int warm_slots = 8;  // entropy round 0: slots decoded before a run's first slot
+  int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
 };
 
 namespace {
@@ -713,7 +715,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<const uint32_t*>(W.segs.p), desc, infos,
                         static_cast<const HuffTable*>(W.luts.p),
                         static_cast<int16_t*>(W.coefs.p), static_cast<uint32_t*>(W.recs.p),
-                        ctx->sub_bits, ctx->warm_slots, ctx->entropy_threads, n, st));
+                        ctx->sub_bits, ctx->warm_slots, ctx->entropy_threads, ctx->entropy_lds_pad, n, st));
   mark(ctx, slot, 4, st);
   HJ_HIP(launch_idct(static_cast<const int16_t*>(W.coefs.p), desc, infos,
                      static_cast<uint8_t*>(W.planes.p), out->idct, L.max_blocks, n, st));
@@ -1407,6 +1409,11 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "warmup_slots")) {  // entropy round-0 warm-up before each run
     if (value < 0 || value > 64) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->warm_slots = (int)value;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "entropy_lds_pad")) {  // bytes; > ~26 KB leaves one entropy WG per CU
+    if (value < 0 || value > 64 * 1024) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->entropy_lds_pad = (int)value;
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "lanes")) {  // concurrent pipelines (workspaces + streams)

@@ -871,6 +871,9 @@ __device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
 // far (absolute).  DC coefficients are stored as raw differences; the
 // predictors are applied after the pass.  Returns the status; sets `done`
 // once the segment's last block is complete.
+#ifndef HJ_U32_STORE
+#define HJ_U32_STORE 1
+#endif
 template <int NT, bool SLOW, class SH>
 __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
                             const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
@@ -902,7 +905,12 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
     dec_skip(d, nbits);
     const int blk = is_dc ? nb : nb - 1;
+#if HJ_U32_STORE
+    // 32-bit element index (blk >= 0 here): an SGPR base + VGPR offset store
+    if (coef) coef_img[(uint32_t)blk * 64u + ((z + zinc - 1u) & 63u)] = (int16_t)v;
+#else
     if (coef) coef_img[(size_t)blk * 64 + ((z + zinc - 1u) & 63u)] = (int16_t)v;
+#endif
     nb += is_dc ? 1 : 0;
     const uint32_t zn = z + zinc;
     const bool bend = zn >= 64u;
@@ -2022,13 +2030,15 @@ hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo
 }
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
                           ImageInfo* infos, const HuffTable* luts, int16_t* coefs, uint32_t* recs,
-                          int sub_bits, int warm_slots, int threads, int n, hipStream_t st) {
+                          int sub_bits, int warm_slots, int threads, int lds_pad, int n,
+                          hipStream_t st) {
   // two instances per batch: <=4 distinct tables (nearly every JPEG, one
   // workgroup per image), then the images that need 5-6 (at most 16
   // workgroups striding over the batch)
 #define HJ_ENT(T, NTAB)                                                                   \
   hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(NTAB > 4 ? (n < 16 ? n : 16) : n), dim3(T), \
-                     0, st, clean, segs, desc, infos, luts, coefs, recs, sub_bits, warm_slots, n)
+                     NTAB > 4 ? 0 : lds_pad, st, clean, segs, desc, infos, luts, coefs, recs,    \
+                     sub_bits, warm_slots, n)
   if (threads == 1024) {
     HJ_ENT(1024, 4);
     HJ_ENT(1024, 6);
