@@ -91,7 +91,7 @@ def _args():
     p.add_argument("--batch", type=int, default=BATCH)
     p.add_argument("--distinct", type=int, default=32)
     p.add_argument("--cpu-threads", type=int, default=16)
-    p.add_argument("--cpu-images", type=int, default=1024)
+    p.add_argument("--cpu-images", type=int, default=8192)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sub-bits", type=int, default=0)
     p.add_argument("--entropy-threads", type=int, default=0)
