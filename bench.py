@@ -11,7 +11,10 @@ rank decodes its own 256-image slice with no collective on the data path
 cross-rank traffic.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-  N > 1 is launched by torch.distributed.run (one rank per GPU).
+  N > 1: either launched by torch.distributed.run (one rank per GPU), or
+  started plainly, in which case bench.py spawns the N rank processes itself
+  before any GPU call.  The barrier and the MAX-over-ranks reduction of the
+  elapsed time go over gloo (host); nothing crosses xGMI.
 """
 
 from __future__ import annotations
@@ -30,7 +33,15 @@ sys.path.insert(0, ROOT)
 
 from spdl_amd import _lib  # noqa: E402
 from spdl_amd._lib import Output  # noqa: E402
-from spdl_amd.synthetic import synthetic_batch  # noqa: E402
+from spdl_amd.distributed import (  # noqa: E402
+    barrier,
+    contiguous_shard,
+    init_host_group,
+    launched_world,
+    reduce_max,
+    spawn_ranks,
+)
+from spdl_amd.synthetic import synthetic_slice  # noqa: E402
 
 METRIC = "images/sec device-resident JPEG→RGB224, 1/2/4/8×MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -44,8 +55,7 @@ STAGE_KERNELS = {
     "destuff": ["hj::destuff_count_kernel", "hj::destuff_prefix_kernel", "hj::destuff_write_kernel"],
     "entropy": ["hj::entropy_kernel<"],
     "idct": ["hj::idct_kernel<"],
-    "weights": ["hj::weights_kernel"],
-    "output": ["hj::resize_plane_kernel", "hj::csc_store_kernel", "hj::csc_kernel"],
+    "output": ["hj::sws_kernel", "hj::csc_kernel"],
 }
 
 
@@ -90,8 +100,15 @@ def _args():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch", type=int, default=BATCH)
     p.add_argument("--distinct", type=int, default=32)
-    p.add_argument("--cpu-threads", type=int, default=16)
-    p.add_argument("--cpu-images", type=int, default=8192)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU baseline threads (0: every core this process may use)")
+    p.add_argument("--cpu-images", type=int, default=2048,
+                   help="CPU baseline sample per run (RGB224; half that for full-res)")
+    p.add_argument("--cpu-runs", type=int, default=5)
+    p.add_argument("--oracle-check", type=int, default=32,
+                   help="images of the last timed batch compared with the oracle")
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU-only rehearsal of the multi-rank launch and timing reduction")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sub-bits", type=int, default=0)
     p.add_argument("--entropy-threads", type=int, default=0)
@@ -128,46 +145,149 @@ def _pack_device(datas: list[bytes], device: torch.device):
             (_lib.ImageInfo * len(infos))(*infos))
 
 
-def _cpu_baseline(datas, threads: int, n_images: int) -> dict:
-    """The oracle (CPU restatement of the reference FFmpeg path) on the host
-    cores, same workload, bounded sample."""
+def _cpu_cores() -> dict:
+    """Host cores this process may use: the CPU affinity mask, capped by a
+    cgroup v2 CPU quota when one is set (a GPU box's share of a large host),
+    plus os.cpu_count() and the CPU model for the record."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            usable = max(1, min(usable, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"usable": usable, "nproc": os.cpu_count(), "model": model}
+
+
+def _mean_ci95(xs):
+    """Mean and 95 % confidence half-width (Student t) of repeated runs, as
+    the reference's examples/benchmark_utils.py:204-345 reports them."""
+    from scipy import stats
+
+    x = np.asarray(xs, np.float64)
+    if len(x) < 2:
+        return float(x.mean()), 0.0
+    half = stats.t.ppf(0.975, len(x) - 1) * x.std(ddof=1) / np.sqrt(len(x))
+    return float(x.mean()), float(half)
+
+
+def _cpu_baseline(datas, threads: int, n224: int, nfull: int, runs: int) -> dict:
+    """The oracle (CPU restatement of the reference FFmpeg path: mjpeg
+    simple_idct + swscale) on the host cores, one decoder per thread, over
+    bounded samples of the same workload: warmup, then `runs` timed runs,
+    mean +- 95 % CI.  RGB224 pad (the metric's output) and full-resolution
+    rgb24 are both timed."""
     from oracle import oracle as O
 
     rs = O.Resize(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224)
-    sample = [datas[i % len(datas)] for i in range(n_images)]
-    O.decode_resize_batch(sample[: min(64, n_images)], rs, "rgb24", nthreads=threads)  # warm
-    t0 = time.perf_counter()
-    _, status, failed = O.decode_resize_batch(sample, rs, "rgb24", nthreads=threads)
-    dt = time.perf_counter() - t0
-    assert failed == 0
+
+    def timed(fn, n):
+        sample = [datas[i % len(datas)] for i in range(n)]
+        fn(sample[: min(64, n)])  # warmup
+        rates = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            failed = fn(sample)
+            rates.append(n / (time.perf_counter() - t0))
+            assert failed == 0
+        return _mean_ci95(rates)
+
+    m224, c224 = timed(lambda s: O.decode_resize_batch(s, rs, "rgb24", nthreads=threads)[2], n224)
+    mfull, cfull = timed(lambda s: O.decode_rgb_batch(s, "rgb24", nthreads=threads)[2], nfull)
+    cores = _cpu_cores()
     return {
-        "value": round(n_images / dt, 1),
+        "value": round(m224, 1),
+        "ci95": round(c224, 1),
         "unit": "images/sec",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n_images} images (480x640 q90 4:2:0 -> RGB224 pad, bicubic), "
-                  f"{threads} threads, one decoder per thread; oracle/jpeg_oracle.c "
-                  f"(CPU restatement of src/libspdl FFmpeg path); wall {dt:.2f}s",
+        "fullres_value": round(mfull, 1),
+        "fullres_ci95": round(cfull, 1),
+        "host": {"nproc": cores["nproc"], "usable_cores": cores["usable"], "cpu": cores["model"]},
+        "sample": f"{runs} runs (after warmup) of {n224} images 480x640 q90 4:2:0 -> RGB224 pad "
+                  f"(bicubic swscale) and {runs} of {nfull} -> full-res rgb24; {threads} threads, "
+                  f"one decoder per thread; oracle/jpeg_oracle.c (CPU restatement of the "
+                  f"src/libspdl FFmpeg path); mean +- 95% CI",
     }
+
+
+def _oracle_check(datas, out: torch.Tensor, spec: Output, n_check: int) -> str:
+    """Bit-exact check of the first `n_check` images of a timed batch
+    against the oracle, outside the timed region."""
+    from oracle import oracle as O
+
+    host = out[:n_check].cpu()
+    kw = dict(fit_w=spec.fit_w, fit_h=spec.fit_h, aspect=spec.aspect, pad_w=spec.pad_w,
+              pad_h=spec.pad_h, crop_w=spec.crop_w, crop_h=spec.crop_h, filter=spec.filter)
+    for i in range(n_check):
+        ref = O.decode_resize(datas[i], O.Resize(**kw), pix_fmt=spec.pix_fmt,
+                              normalize=spec.normalize, norm_dtype=spec.norm_dtype)
+        hyp = host[i]
+        if spec.normalize:
+            hyp = hyp.view(torch.int16).numpy().view(np.uint16)
+            ref = ref.view(np.uint16)
+        else:
+            hyp = hyp.numpy()
+        if not np.array_equal(hyp, ref):
+            raise AssertionError(f"timed batch image {i} differs from the oracle")
+    return f"{n_check} images of the last timed batch bit-exact vs oracle"
+
+
+def _dry_run(a, rank: int, world: int) -> None:
+    """CPU-only rehearsal of the launch/partition/timing plumbing (tests):
+    the same rank slicing and MAX-over-ranks reduction, no GPU."""
+    import torch.distributed as dist
+
+    from spdl_amd.distributed import barrier, contiguous_shard, reduce_max
+
+    sl = contiguous_shard(world * a.batch, rank, world)
+    barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.05 * (rank + 1))
+    barrier()
+    elapsed = reduce_max(time.perf_counter() - t0)
+    slices = [None] * world
+    if world > 1:
+        dist.all_gather_object(slices, [sl.start, sl.stop])
+    else:
+        slices = [[sl.start, sl.stop]]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "global_batch": world * a.batch,
+                          "slices": slices, "elapsed": elapsed}), flush=True)
 
 
 def main():
     a = _args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
+    rank, world, local = launched_world()
+    if a.gpus > 1 and world == 1:
+        # one process per GPU, started before anything touches a device
+        # (reference examples/image_dataloading.py:291-317)
+        raise SystemExit(spawn_ranks(a.gpus, [os.path.abspath(__file__), *sys.argv[1:]]))
+    if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    init_host_group()
+    if a.dry_run:
+        _dry_run(a, rank, world)
+        return
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    datas = synthetic_batch(a.batch, distinct=a.distinct)
+    # this rank's contiguous slice of the global batch (configs[2]: 2048 -> 8 x 256)
+    sl = contiguous_shard(world * a.batch, rank, world)
+    datas = synthetic_slice(sl, distinct=a.distinct)
     dev, offs, sizes, infos = _pack_device(datas, device)
     dec = _lib.Decoder(local)
     if a.sub_bits:
@@ -201,9 +321,10 @@ def main():
         return dec.last_ticket()
 
     # Steps are submitted asynchronously through the decoder's ring (up to
-    # --inflight batches, executing on the context's two lanes):
-    # host-side layout and launches overlap the kernels, as in a data loader.  Each batch is waited
-    # for (statuses checked) and its per-stage HIP-event timings collected.
+    # --inflight batches, executing on the context's two lanes): host-side
+    # layout and launches overlap the kernels, as in a data loader.  Each
+    # batch is waited for (statuses checked) and its per-stage HIP-event
+    # timings collected.
     for _ in range(a.warmup):
         submit(True)
     dec.set_profiling(True)
@@ -216,8 +337,7 @@ def main():
             stages[k] = stages.get(k, 0.0) + v
 
     torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     pending = []
@@ -233,27 +353,15 @@ def main():
     for t in pending:
         collect(t)
     torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize(device)
-    elapsed = time.perf_counter() - t0
+    elapsed = reduce_max(time.perf_counter() - t0)
     dec.set_profiling(False)
-    if dist:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
-    # correctness spot check outside the timed region: the last timed batch
-    # equals a fresh synchronous decode of the same inputs, and repeated
-    # inputs (the batch cycles through `distinct` files) decode identically
+    # correctness outside the timed region: the last timed batch against
+    # the oracle (every distinct image of the slice)
     last = outs[(nsub[0] - 1) % len(outs)]
-    fresh = outs[nsub[0] % len(outs)]
-    dec.decode_batch_device(dev.data_ptr(), dev.numel(), offs, sizes, infos, spec,
-                            fresh.data_ptr(), nbytes_out, stream=stream, sync=True)
-    torch.cuda.synchronize(device)
-    assert torch.equal(last, fresh), "timed batch differs from a fresh decode"
-    if a.batch > a.distinct:
-        assert torch.equal(last[: a.distinct], last[a.distinct : 2 * a.distinct])
+    checked = _oracle_check(datas, last, spec, min(a.batch, a.distinct, a.oracle_check))
 
     stages_ms = {k: v / a.steps / 1000.0 for k, v in stages.items()}
     kernels = {k: v for k, v in stages_ms.items() if k not in ("h2d", "d2h_status")}
@@ -278,7 +386,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "pad224":
-        cpu = _cpu_baseline(datas, a.cpu_threads, a.cpu_images)
+        threads = a.cpu_threads or _cpu_cores()["usable"]
+        cpu = _cpu_baseline(datas, threads, a.cpu_images, a.cpu_images // 2, a.cpu_runs)
 
     if rank == 0:
         value = world * a.batch * a.steps / elapsed
@@ -302,7 +411,8 @@ def main():
                 "per_gpu_batch": a.batch,
                 "mean_jpeg_bytes": round(comp_bytes, 1),
                 "distinct_images": a.distinct,
-                "parallelism": f"{world} independent per-GPU slices, no collective",
+                "parallelism": f"{world} ranks (one process per GPU), contiguous slices of the "
+                               f"global batch, no collective on the data path",
                 "lanes": a.lanes,
             },
             "roofline": {
@@ -313,17 +423,20 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": _pmc_traffic(dominant, a.batch) if a.workload == "pad224" else None,
-                "traffic_source": "profiles/r01_v9/traffic.json (rocprofv3 --pmc FETCH_SIZE, "
-                                  "WRITE_SIZE; separate passes; x1024, FETCH x2 gfx950)",
+                "traffic_source": f"{os.path.relpath(PMC_TRAFFIC, ROOT)} (rocprofv3 --pmc "
+                                  "FETCH_SIZE, WRITE_SIZE; separate passes; x1024, FETCH x2 gfx950)",
                 "algorithmic_bytes_per_image": round(per_image_bytes, 1),
             },
             "stages_ms": {k: round(v, 4) for k, v in stages_ms.items()},
+            "oracle_check": checked,
             "cpu_baseline": cpu,
         }
         if copies is not None:
             rec["with_copies_images_per_sec"] = round(copies, 1)
         print(json.dumps(rec), flush=True)
-    if dist:
+    if world > 1:
+        import torch.distributed as dist
+
         dist.destroy_process_group()
 
 

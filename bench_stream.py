@@ -39,6 +39,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import spdl_amd.io as sio  # noqa: E402
+from spdl_amd.distributed import (  # noqa: E402
+    barrier,
+    init_host_group,
+    launched_world,
+    reduce_max,
+    spawn_ranks,
+)
 from spdl_amd.synthetic import synthetic_batch  # noqa: E402
 
 
@@ -67,15 +74,13 @@ def _make_tar(path: str, n: int, distinct: int, rank: int) -> int:
 
 def main():
     a = _args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rank, world, local = launched_world()
+    if a.gpus > 1 and world == 1:
+        # one process per GPU, started before anything touches a device
+        raise SystemExit(spawn_ranks(a.gpus, [os.path.abspath(__file__), *sys.argv[1:]]))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    init_host_group()  # gloo: barrier + MAX of elapsed seconds only
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -117,23 +122,17 @@ def main():
         for _ in range(a.warmup_passes):
             one_pass()
         torch.cuda.synchronize(device)
-        if dist:
-            dist.barrier()
+        barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         total = 0
         for _ in range(a.passes):
             total += one_pass()
         torch.cuda.synchronize(device)
-        if dist:
-            dist.barrier()
+        barrier()
         torch.cuda.synchronize(device)
-        elapsed = time.perf_counter() - t0
+        elapsed = reduce_max(time.perf_counter() - t0)
         st.close()
-        if dist:
-            t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
         if rank == 0:
             value = world * total / elapsed
             print(json.dumps({
@@ -163,7 +162,9 @@ def main():
             }), flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-        if dist:
+        if world > 1:
+            import torch.distributed as dist
+
             dist.destroy_process_group()
 
 

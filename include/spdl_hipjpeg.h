@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SPDL_HJ_ABI_VERSION 1
+#define SPDL_HJ_ABI_VERSION 2
 
 enum spdl_hj_status {
   SPDL_HJ_OK = 0,
@@ -71,6 +71,12 @@ enum spdl_hj_filter {
 enum spdl_hj_dtype { SPDL_HJ_DTYPE_U8 = 0, SPDL_HJ_DTYPE_F16 = 1, SPDL_HJ_DTYPE_BF16 = 2 };
 /* IDCT: FFmpeg simple_idct (the reference CPU path) or IJG islow (libjpeg). */
 enum spdl_hj_idct { SPDL_HJ_IDCT_SIMPLE = 0, SPDL_HJ_IDCT_ISLOW = 1 };
+/* Colour conversion / scaling: SWSCALE is the reference CPU path's libswscale
+ * (one context: bicubic/bilinear/lanczos scale + yuvj -> rgb24, BT.601 full
+ * range, swscale's chroma siting and fixed-point arithmetic; FilterGraphImpl,
+ * src/libspdl/core/detail/ffmpeg/filter_graph.cpp:280-313).  JFIF is IJG
+ * libjpeg's integer YCbCr -> RGB with nearest chroma (full resolution only). */
+enum spdl_hj_csc { SPDL_HJ_CSC_SWSCALE = 0, SPDL_HJ_CSC_JFIF = 1 };
 
 /* Output specification.  resize == 0: full resolution, every image in the
  * batch must have the same size.  Otherwise the FFmpeg filter chain SPDL
@@ -88,6 +94,7 @@ typedef struct spdl_hj_output {
   int32_t crop_w, crop_h;
   int32_t filter;       /* spdl_hj_filter */
   float mean[3], std[3];
+  int32_t csc;          /* enum spdl_hj_csc, since ABI 2 */
 } spdl_hj_output;
 
 typedef struct spdl_hj_image_info {

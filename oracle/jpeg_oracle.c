@@ -1,5 +1,6 @@
 /*
  * jpeg_oracle.c -- CPU restatement of SPDL's JPEG -> RGB path (test oracle).
+ * The scale / colour-conversion stage is restated in sws_oracle.c.
  *
  * TEST INFRASTRUCTURE ONLY (see jpeg_oracle.h).  Compiled with
  * -ffp-contract=off so the float steps (resize weights, normalisation) are the
@@ -10,7 +11,8 @@
  *            (libavcodec/mjpegdec.c decode_block / mjpeg_decode_dc, simple_idct
  *            template 8-bit: idctRowCondDC, idctSparseColPut).
  *   convert: src/libspdl/core/detail/ffmpeg/filter_graph.cpp:280-313 ->
- *            format=pix_fmts=rgb24 (yuvj4xxp -> rgb24, nearest chroma).
+ *            libswscale yuvj4xxp -> rgb24 (sws_oracle.c); the IJG JFIF
+ *            tables + nearest chroma remain as JO_CSC_JFIF.
  *   resize:  src/spdl/io/_preprocessing.py:214-234 filter string semantics
  *            (scale force_original_aspect_ratio, pad x=-1:y=-1, crop).
  *   norm:    examples/imagenet_classification.py:96-106.
@@ -836,15 +838,81 @@ static int planes_to_rgb(const jo_info* info, const uint8_t* planes, int fmt, ui
   return JO_OK;
 }
 
-int jo_decode_rgb(const uint8_t* d, size_t size, int idct, int fmt, uint8_t* out) {
+/* chroma subsampling shifts of a 3-component frame (the yuvj4xxp format
+ * FFmpeg's mjpeg decoder outputs: 444 / 422 / 420 / 440 / 411 ...) */
+static int chroma_shifts(const jo_info* info, int* hsub, int* vsub) {
+  *hsub = *vsub = 0;
+  if (info->ncomp == 1) return JO_OK;
+  if (info->comp_h[0] != info->hmax || info->comp_v[0] != info->vmax ||
+      info->comp_h[1] != info->comp_h[2] || info->comp_v[1] != info->comp_v[2])
+    return JO_ERR_UNSUPPORTED;
+  int rh = info->hmax / info->comp_h[1], rv = info->vmax / info->comp_v[1];
+  if (rh * info->comp_h[1] != info->hmax || rv * info->comp_v[1] != info->vmax) return JO_ERR_UNSUPPORTED;
+  if ((rh & (rh - 1)) || (rv & (rv - 1)) || rh > 4 || rv > 4) return JO_ERR_UNSUPPORTED;
+  while ((1 << *hsub) < rh) (*hsub)++;
+  while ((1 << *vsub) < rv) (*vsub)++;
+  return JO_OK;
+}
+
+/* swscale the decoded planes to sw x sh rgb24 (scratch slot 7). */
+static int sws_planes(const jo_info* info, const uint8_t* planes, int sw, int sh, int filter,
+                      uint8_t** rgb_out) {
+  int hsub, vsub;
+  int rc = chroma_shifts(info, &hsub, &vsub);
+  if (rc) return rc;
+  const uint8_t* pc[JO_MAX_COMP];
+  int st[JO_MAX_COMP];
+  plane_ptrs(info, planes, pc, st);
+  jo_sws s;
+  if (jo_sws_init(&s, info->width, info->height, hsub, vsub, info->ncomp == 1, sw, sh, filter)) {
+    jo_sws_free(&s);
+    return JO_ERR_BAD_GEOMETRY;
+  }
+  uint8_t* rgb = (uint8_t*)scratch(7, (size_t)sw * sh * 3);
+  rc = rgb ? jo_sws_scale(&s, pc, st, rgb) : -1;
+  jo_sws_free(&s);
+  if (rc) return JO_ERR_BAD_GEOMETRY;
+  *rgb_out = rgb;
+  return JO_OK;
+}
+
+int jo_decode_rgb_csc(const uint8_t* d, size_t size, int idct, int csc, int fmt, uint8_t* out) {
   jo_info info;
   int rc = jo_parse(d, size, &info);
   if (rc) return rc;
   uint8_t* planes = (uint8_t*)scratch(1, jo_planes_size(&info));
   if (!planes) return JO_ERR_BAD_HEADER;
   rc = decode_planes_info(d, size, &info, idct, planes);
-  if (!rc) rc = planes_to_rgb(&info, planes, fmt, out);
-  return rc;
+  if (rc) return rc;
+  if (csc == JO_CSC_JFIF) return planes_to_rgb(&info, planes, fmt, out);
+  uint8_t* rgb;
+  rc = sws_planes(&info, planes, info.width, info.height, JO_FILTER_BICUBIC, &rgb);
+  if (rc) return rc;
+  const int W = info.width, H = info.height;
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) store_px(out, fmt, W, H, x, y, rgb + ((size_t)y * W + x) * 3);
+  return JO_OK;
+}
+
+int jo_decode_rgb(const uint8_t* d, size_t size, int idct, int fmt, uint8_t* out) {
+  return jo_decode_rgb_csc(d, size, idct, JO_CSC_SWSCALE, fmt, out);
+}
+
+int jo_sws_axis(int src, int dst, int kind, int align, int one, int src_pos, int dst_pos,
+                int32_t* pos, int16_t* coef, int cap) {
+  if (src <= 0 || dst <= 0) return -1;
+  const int64_t inc = (((int64_t)src << 16) + (dst >> 1)) / dst;
+  jo_sws_filter f;
+  if (jo_sws_init_filter((int)inc, src, dst, align, one, kind, src_pos, dst_pos, &f)) return -1;
+  int size = f.size;
+  if ((int64_t)size * dst > cap) {
+    jo_sws_filter_free(&f);
+    return -1;
+  }
+  memcpy(pos, f.pos, sizeof(int32_t) * dst);
+  memcpy(coef, f.coef, sizeof(int16_t) * (size_t)size * dst);
+  jo_sws_filter_free(&f);
+  return size;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -897,111 +965,6 @@ int jo_geometry(int w, int h, const jo_resize* rs, jo_geom* g) {
   return JO_OK;
 }
 
-/* Resampling kernel: Keys cubic with a = -0.6 (the B=0, C=0.6 member of the
- * family swscale's SWS_BICUBIC uses), support widened by the downscale factor
- * (anti-aliased); or a triangle (bilinear).  Every float step is one IEEE op. */
-/* sin(pi x) for 0 <= x <= 3 from float adds and multiplies only (odd Taylor
- * polynomial of sin(pi r) to r^13 on the reduced argument |r| <= 1/2), so the
- * GPU kernel (hj_kernels.hip lanczos_eval) evaluates the same IEEE ops and
- * gets the same bits -- a libm sinf would not be reproducible there. */
-static float sinpi_poly(float x) {
-  float k = rintf(x);
-  float r = x - k;
-  float p = r * r;
-  float s = -7.37043094e-3f + p * 4.66302806e-4f;
-  s = 8.21458866e-2f + p * s;
-  s = -5.99264529e-1f + p * s;
-  s = 2.55016404f + p * s;
-  s = -5.16771278f + p * s;
-  s = 3.14159265f + p * s;
-  s = r * s;
-  return ((int)k & 1) ? -s : s;
-}
-
-/* Lanczos-3 windowed sinc, sinc(t) sinc(t/3) = 3 sin(pi t) sin(pi t/3) /
- * (pi^2 t^2): the kernel of NPP's NPPI_INTER_LANCZOS resize that
- * load_image_batch_nvjpeg uses (src/libspdl/cuda/npp/detail/resize.cpp:36-116),
- * and of swscale's flags=lanczos (default parameter 3). */
-static float lanczos_eval(float t) {
-  if (t == 0.0f) return 1.0f;
-  if (t >= 3.0f) return 0.0f;
-  float a = sinpi_poly(t);
-  float b = sinpi_poly(t / 3.0f);
-  float num = 3.0f * a;
-  num = num * b;
-  float den = 9.8696044f * t;
-  den = den * t;
-  return num / den;
-}
-
-static float kernel_eval(int filter, float x) {
-  float t = fabsf(x);
-  if (filter == JO_FILTER_BILINEAR) return t < 1.0f ? 1.0f - t : 0.0f;
-  if (filter == JO_FILTER_LANCZOS) return lanczos_eval(t);
-  float t2 = t * t;
-  float t3 = t2 * t;
-  if (t <= 1.0f) {
-    float a = 1.4f * t3;
-    float b = 2.4f * t2;
-    return (a - b) + 1.0f;
-  }
-  if (t < 2.0f) {
-    float a = -0.6f * t3;
-    float b = 3.0f * t2;
-    float c = 4.8f * t;
-    return ((a + b) - c) + 2.4f;
-  }
-  return 0.0f;
-}
-
-static float filter_radius(int filter) {
-  return filter == JO_FILTER_BILINEAR ? 1.0f : filter == JO_FILTER_LANCZOS ? 3.0f : 2.0f;
-}
-
-int jo_max_taps(int src_len, int dst_len, int filter) {
-  float scale = (float)src_len / (float)dst_len;
-  float fscale = scale > 1.0f ? scale : 1.0f;
-  float support = filter_radius(filter) * fscale;
-  return (int)ceilf(2.0f * support) + 1;
-}
-
-int jo_axis_weights(int src_len, int dst_len, int filter, int maxtaps, int32_t* first, int16_t* w) {
-  float scale = (float)src_len / (float)dst_len;
-  float fscale = scale > 1.0f ? scale : 1.0f;
-  float support = filter_radius(filter) * fscale;
-  int used = 0;
-  float wf[1024];
-  int wq[1024];
-  for (int i = 0; i < dst_len; i++) {
-    float center = ((float)i + 0.5f) * scale;
-    center = center - 0.5f;
-    int lo = (int)ceilf(center - support);
-    int hi = (int)floorf(center + support);
-    int n = hi - lo + 1;
-    if (n > maxtaps || n > 1024) return -1;
-    if (n > used) used = n;
-    float sum = 0.0f;
-    for (int t = 0; t < n; t++) {
-      float x = ((float)(lo + t) - center) / fscale;
-      wf[t] = kernel_eval(filter, x);
-      sum = sum + wf[t];
-    }
-    int qs = 0, am = 0;
-    for (int t = 0; t < n; t++) {
-      float q = wf[t] / sum;
-      q = q * 16384.0f;
-      q = q + 0.5f;
-      wq[t] = (int)floorf(q);
-      qs += wq[t];
-      if (wq[t] > wq[am]) am = t;
-    }
-    wq[am] += 16384 - qs;
-    first[i] = lo;
-    for (int t = 0; t < maxtaps; t++) w[(size_t)i * maxtaps + t] = (int16_t)(t < n ? wq[t] : 0);
-  }
-  return used;
-}
-
 uint16_t jo_f32_to_f16(float f) {
   uint32_t x;
   memcpy(&x, &f, 4);
@@ -1037,53 +1000,6 @@ uint16_t jo_f32_to_bf16(float f) {
   return (uint16_t)(x >> 16);
 }
 
-/* resize one plane (true dims pw x ph, stride st) to sw x sh:
- * horizontal Q14 taps -> Q6 intermediate ((acc + 128) >> 8), then vertical Q14
- * -> (acc + 2^19) >> 20, clamp u8. */
-static int resize_plane(const uint8_t* src, int pw, int ph, int st, int sw, int sh, int filter,
-                        uint8_t* dst) {
-  int mtx = jo_max_taps(pw, sw, filter), mty = jo_max_taps(ph, sh, filter);
-  int32_t* fx = (int32_t*)scratch(2, sizeof(int32_t) * sw);
-  int16_t* wx = (int16_t*)scratch(3, sizeof(int16_t) * (size_t)sw * mtx);
-  int32_t* fy = (int32_t*)scratch(4, sizeof(int32_t) * sh);
-  int16_t* wy = (int16_t*)scratch(5, sizeof(int16_t) * (size_t)sh * mty);
-  int32_t* tmp = (int32_t*)scratch(6, sizeof(int32_t) * (size_t)ph * sw);
-  int rc = JO_OK;
-  if (!fx || !wx || !fy || !wy || !tmp) {
-    rc = JO_ERR_BAD_GEOMETRY;
-    goto done;
-  }
-  if (jo_axis_weights(pw, sw, filter, mtx, fx, wx) < 0 ||
-      jo_axis_weights(ph, sh, filter, mty, fy, wy) < 0) {
-    rc = JO_ERR_BAD_GEOMETRY;
-    goto done;
-  }
-  for (int r = 0; r < ph; r++) {
-    const uint8_t* row = src + (size_t)r * st;
-    for (int x = 0; x < sw; x++) {
-      int32_t acc = 0;
-      for (int t = 0; t < mtx; t++) {
-        int k = fx[x] + t;
-        k = k < 0 ? 0 : k >= pw ? pw - 1 : k;
-        acc += (int32_t)wx[(size_t)x * mtx + t] * row[k];
-      }
-      tmp[(size_t)r * sw + x] = (acc + 128) >> 8;
-    }
-  }
-  for (int y = 0; y < sh; y++)
-    for (int x = 0; x < sw; x++) {
-      int32_t acc = 0;
-      for (int t = 0; t < mty; t++) {
-        int k = fy[y] + t;
-        k = k < 0 ? 0 : k >= ph ? ph - 1 : k;
-        acc += (int32_t)wy[(size_t)y * mty + t] * tmp[(size_t)k * sw + x];
-      }
-      dst[(size_t)y * sw + x] = clip_u8((acc + (1 << 19)) >> 20);
-    }
-done:
-  return rc;
-}
-
 int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize* rs, int fmt,
                      int dtype, const float* mean, const float* stdv, void* out,
                      jo_geom* geom_out) {
@@ -1091,20 +1007,11 @@ int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize
   int rc = jo_geometry(info->width, info->height, rs, &g);
   if (rc) return rc;
   if (geom_out) *geom_out = g;
-  const uint8_t* pc[JO_MAX_COMP];
-  int st[JO_MAX_COMP];
-  plane_ptrs(info, planes, pc, st);
-  uint8_t* rp[JO_MAX_COMP] = {0};
-  for (int c = 0; c < info->ncomp; c++) {
-    rp[c] = (uint8_t*)scratch(7 + c, (size_t)g.sw * g.sh);
-    if (!rp[c] || (rc = resize_plane(pc[c], info->comp_w[c], info->comp_h_px[c], st[c], g.sw,
-                                     g.sh, rs->filter, rp[c]))) {
-      if (!rc) rc = JO_ERR_BAD_GEOMETRY;
-      return rc;
-    }
-  }
-  csc_t t;
-  build_csc(&t);
+  /* one swscale pass to the scaled size (scale filter with rgb24 output),
+   * then pad (black) / crop move pixels */
+  uint8_t* rgbs;
+  rc = sws_planes(info, planes, g.sw, g.sh, rs->filter, &rgbs);
+  if (rc) return rc;
   int planar = (fmt == JO_FMT_RGB || fmt == JO_FMT_BGR);
   int swap = (fmt == JO_FMT_BGR || fmt == JO_FMT_BGR24);
   size_t pl = (size_t)g.ow * g.oh;
@@ -1113,11 +1020,10 @@ int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize
       int cx = x - g.dx, cy = y - g.dy;
       uint8_t rgb[3] = {0, 0, 0};
       if (cx >= 0 && cx < g.sw && cy >= 0 && cy < g.sh) {
-        size_t o = (size_t)cy * g.sw + cx;
-        if (info->ncomp == 1)
-          rgb[0] = rgb[1] = rgb[2] = rp[0][o];
-        else
-          csc_px(&t, rp[0][o], rp[1][o], rp[2][o], rgb);
+        const uint8_t* p = rgbs + ((size_t)cy * g.sw + cx) * 3;
+        rgb[0] = p[0];
+        rgb[1] = p[1];
+        rgb[2] = p[2];
       }
       for (int ch = 0; ch < 3; ch++) {
         int src_ch = swap ? 2 - ch : ch;

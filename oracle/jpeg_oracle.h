@@ -27,9 +27,9 @@
  *   - JO_IDCT_ISLOW + nearest chroma + JFIF integer colour conversion: pinned
  *     bit-exact end-to-end against libjpeg 9d (dct_method=JDCT_ISLOW,
  *     do_fancy_upsampling=FALSE).
- *   - JO_IDCT_SIMPLE (FFmpeg simple_idct) and the resize filter: parity
- *     UNPINNED against FFmpeg (no FFmpeg in this image); restated from the
- *     published algorithm.
+ *   - JO_IDCT_SIMPLE (FFmpeg simple_idct) and the swscale scale / colour
+ *     conversion (sws_oracle.c): parity UNPINNED against FFmpeg (no FFmpeg in
+ *     this image); restated from the published algorithm.
  */
 #ifndef SPDL_JPEG_ORACLE_H
 #define SPDL_JPEG_ORACLE_H
@@ -121,16 +121,10 @@ void jo_idct_islow(const int16_t* in, uint8_t* out, int stride);
 size_t jo_planes_size(const jo_info* info);
 int jo_decode_planes(const uint8_t* data, size_t size, int idct, uint8_t* planes);
 
-/* Full-resolution RGB (nearest chroma replication, JFIF integer CSC). */
+/* Full-resolution RGB through the swscale restatement (JO_CSC_SWSCALE). */
 int jo_decode_rgb(const uint8_t* data, size_t size, int idct, int fmt, uint8_t* out);
 
 int jo_geometry(int w, int h, const jo_resize* rs, jo_geom* g);
-
-/* 1-D resampling table: for each dst index i, first[i] and taps weights
- * (Q14, sum == 16384) in w[i*maxtaps ...]; returns ntaps used (<= maxtaps) or -1. */
-int jo_axis_weights(int src_len, int dst_len, int filter, int maxtaps,
-                    int32_t* first, int16_t* w);
-int jo_max_taps(int src_len, int dst_len, int filter);
 
 /* Decode + resize + csc + pad/crop (+ normalise when dtype == F16).
  * out is ow*oh*3 elements (u8 or IEEE fp16 bits). */
@@ -143,6 +137,49 @@ int jo_decode_resize(const uint8_t* data, size_t size, int idct, const jo_resize
 int jo_resize_planes(const jo_info* info, const uint8_t* planes, const jo_resize* rs,
                      int fmt, int dtype, const float* mean, const float* stdv,
                      void* out, jo_geom* geom_out);
+
+/* ---- libswscale restatement (sws_oracle.c) ------------------------------ */
+
+/* colour conversion of the RGB outputs: the reference CPU path's swscale
+ * (default), or IJG libjpeg's JFIF integer tables with nearest chroma
+ * (full resolution only; pinned against libjpeg 9d) */
+enum { JO_CSC_SWSCALE = 0, JO_CSC_JFIF = 1 };
+
+typedef struct {
+  int size;       /* taps per output sample */
+  int n;          /* output samples */
+  int32_t* pos;   /* first source sample of each output */
+  int16_t* coef;  /* n * size taps, normalised to `one` */
+} jo_sws_filter;
+
+typedef struct {
+  int srcW, srcH, dstW, dstH;
+  int chrSrcW, chrSrcH, chrDstW, chrDstH;
+  int chr_src_hsub, chr_src_vsub;
+  int full;              /* SWS_FULL_CHR_H_INT in effect */
+  int gray;
+  int unscaled_special;  /* yuv2rgb_c_24_rgb (nearest chroma) */
+  jo_sws_filter hl, hc, vl, vc;
+  int32_t crv, cbu, cgu, cgv;                  /* table increments (cy-scaled) */
+  int32_t y_coeff, y_offset, v2r, v2g, u2g, u2b; /* yuv2rgb_write_full */
+} jo_sws;
+
+int jo_sws_init_filter(int xInc, int srcW, int dstW, int filterAlign, int one, int kind, int srcPos,
+                  int dstPos, jo_sws_filter* out);
+void jo_sws_filter_free(jo_sws_filter* f);
+int jo_sws_init(jo_sws* s, int srcW, int srcH, int hsub, int vsub, int gray, int dstW, int dstH,
+                int kind);
+void jo_sws_free(jo_sws* s);
+int jo_sws_scale(const jo_sws* s, const uint8_t* const* planes, const int* stride, uint8_t* rgb);
+
+/* Full-resolution RGB with a chosen colour conversion (JO_CSC_*). */
+int jo_decode_rgb_csc(const uint8_t* data, size_t size, int idct, int csc, int fmt, uint8_t* out);
+
+/* Test helper: the filter swscale builds for one axis (kind = JO_FILTER_*,
+ * align 4/2, one 1<<14 / 1<<12, positions as get_local_pos returns them).
+ * Writes n positions and n*size taps (cap taps max); returns size or -1. */
+int jo_sws_axis(int src, int dst, int kind, int align, int one, int src_pos, int dst_pos,
+                int32_t* pos, int16_t* coef, int cap);
 
 uint16_t jo_f32_to_f16(float f);
 uint16_t jo_f32_to_bf16(float f);

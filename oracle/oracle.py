@@ -127,6 +127,8 @@ def lib() -> ctypes.CDLL:
         L.jo_planes_size.argtypes = [ctypes.POINTER(_Info)]
         L.jo_planes_size.restype = sz
         L.jo_decode_rgb.argtypes = [vp, sz, ip, ip, vp]
+        L.jo_decode_rgb_csc.argtypes = [vp, sz, ip, ip, ip, vp]
+        L.jo_sws_axis.argtypes = [ip, ip, ip, ip, ip, ip, ip, vp, vp, ip]
         L.jo_geometry.argtypes = [ip, ip, ctypes.POINTER(_Resize), ctypes.POINTER(_Geom)]
         L.jo_decode_resize.argtypes = [
             vp, sz, ip, ctypes.POINTER(_Resize), ip, ip, vp, vp, vp, ctypes.POINTER(_Geom)
@@ -135,8 +137,6 @@ def lib() -> ctypes.CDLL:
             ctypes.POINTER(_Info), vp, ctypes.POINTER(_Resize), ip, ip, vp, vp, vp,
             ctypes.POINTER(_Geom),
         ]
-        L.jo_axis_weights.argtypes = [ip, ip, ip, ip, vp, vp]
-        L.jo_max_taps.argtypes = [ip, ip, ip]
         L.jo_idct_simple.argtypes = [vp, vp, ip]
         L.jo_idct_islow.argtypes = [vp, vp, ip]
         L.jo_strerror.restype = ctypes.c_char_p
@@ -231,12 +231,18 @@ def decode_planes(data: bytes, idct: int = IDCT_SIMPLE):
     return planes
 
 
-def decode_rgb(data: bytes, idct: int = IDCT_SIMPLE, pix_fmt: str = "rgb24") -> np.ndarray:
+CSC = {"swscale": 0, "jfif": 1}
+
+
+def decode_rgb(data: bytes, idct: int = IDCT_SIMPLE, pix_fmt: str = "rgb24",
+               csc: str = "swscale") -> np.ndarray:
+    """Full-resolution RGB: FFmpeg's swscale conversion (the reference CPU
+    path, default) or IJG libjpeg's JFIF tables + nearest chroma ("jfif")."""
     info = parse(data)
     W, H = info.width, info.height
     out = np.zeros(W * H * 3, np.uint8)
     _, p = _buf(data)
-    rc = lib().jo_decode_rgb(p, len(data), idct, FMT[pix_fmt], out.ctypes.data)
+    rc = lib().jo_decode_rgb_csc(p, len(data), idct, CSC[csc], FMT[pix_fmt], out.ctypes.data)
     if rc:
         raise OracleError(rc)
     return out.reshape((3, H, W) if pix_fmt in ("rgb", "bgr") else (H, W, 3))
@@ -250,14 +256,18 @@ def geometry(w: int, h: int, rs: Resize) -> dict:
     return {k: getattr(g, k) for k, _ in _Geom._fields_}
 
 
-def axis_weights(src: int, dst: int, filt: str = "bicubic"):
-    mt = lib().jo_max_taps(src, dst, FILTER[filt])
-    first = np.zeros(dst, np.int32)
-    w = np.zeros((dst, mt), np.int16)
-    n = lib().jo_axis_weights(src, dst, FILTER[filt], mt, first.ctypes.data, w.ctypes.data)
+def sws_axis(src: int, dst: int, filt: str = "bicubic", align: int = 4, one: int = 1 << 14,
+             src_pos: int = 128, dst_pos: int = 128):
+    """(positions [dst], taps [dst, size]) of the filter libswscale's
+    initFilter builds for one axis (sws_oracle.c)."""
+    cap = dst * 512
+    pos = np.zeros(dst, np.int32)
+    coef = np.zeros(cap, np.int16)
+    n = lib().jo_sws_axis(src, dst, FILTER[filt], align, one, src_pos, dst_pos, pos.ctypes.data,
+                          coef.ctypes.data, cap)
     if n < 0:
         raise OracleError(7)
-    return first, w
+    return pos, coef[: dst * n].reshape(dst, n)
 
 
 def decode_resize(
@@ -313,6 +323,21 @@ def decode_resize_batch(
         ptrs, sizes, n, idct, ctypes.byref(rs._c()), FMT[pix_fmt], DTYPE_U8,
         m.ctypes.data, s.ctypes.data, out.ctypes.data, per, nthreads, status.ctypes.data,
     )
+    return out, status, failed
+
+
+def decode_rgb_batch(datas, pix_fmt: str = "rgb24", idct: int = IDCT_SIMPLE, nthreads: int = 1):
+    """Threaded full-resolution batch (CPU baseline); equal sizes."""
+    n = len(datas)
+    arrs = [np.frombuffer(d, np.uint8) for d in datas]
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    sizes = (ctypes.c_size_t * n)(*[len(d) for d in datas])
+    info = parse(datas[0])
+    per = info.width * info.height * 3
+    out = np.zeros((n, per), np.uint8)
+    status = np.zeros(n, np.int32)
+    failed = lib().jo_decode_rgb_batch(ptrs, sizes, n, idct, FMT[pix_fmt], out.ctypes.data, per,
+                                       nthreads, status.ctypes.data)
     return out, status, failed
 
 

@@ -15,13 +15,14 @@ from dataclasses import dataclass
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPDL_AMD_LIB") or os.path.join(_HERE, "lib", "libspdl_hipjpeg.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # enums (mirror include/spdl_hipjpeg.h)
 PIX_FMTS = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
 ASPECT = {None: 0, "none": 0, "decrease": 1, "increase": 2}
 FILTERS = {"bicubic": 0, "bilinear": 1, "lanczos": 2}
 IDCT = {"simple": 0, "islow": 1}
+CSC = {"swscale": 0, "jfif": 1}
 DTYPE_U8, DTYPE_F16, DTYPE_BF16 = 0, 1, 2
 NORM_DTYPES = {"float16": DTYPE_F16, "bfloat16": DTYPE_BF16}
 
@@ -78,6 +79,7 @@ class OutputSpec(ctypes.Structure):
         ("filter", ctypes.c_int32),
         ("mean", ctypes.c_float * 3),
         ("std", ctypes.c_float * 3),
+        ("csc", ctypes.c_int32),
     ]
 
 
@@ -107,6 +109,9 @@ class Output:
     mean: tuple = (0.485, 0.456, 0.406)
     std: tuple = (0.229, 0.224, 0.225)
     norm_dtype: str = "float16"  # or "bfloat16"
+    # "swscale": the reference CPU path's libswscale arithmetic (scale +
+    # yuvj -> rgb24); "jfif": IJG libjpeg tables, nearest chroma (full-res)
+    csc: str = "swscale"
 
     def to_c(self) -> OutputSpec:
         if self.pix_fmt not in PIX_FMTS:
@@ -126,6 +131,7 @@ class Output:
             FILTERS[self.filter],
             (ctypes.c_float * 3)(*self.mean),
             (ctypes.c_float * 3)(*self.std),
+            CSC[self.csc],
         )
 
     @property
@@ -213,11 +219,10 @@ def lib() -> ctypes.CDLL:
 
 def get_image_info(data) -> ImageInfo:
     """Host SOF probe (width, height, components, sampling factors)."""
-    mv = memoryview(data).cast("B")
-    buf = (ctypes.c_char * len(mv)).from_buffer_copy(mv) if mv.readonly else (
-        ctypes.c_char * len(mv)).from_buffer(mv)
+    addr, size, keep = buffer_address(data)
     info = ImageInfo()
-    rc = lib().spdl_hj_get_image_info(ctypes.addressof(buf), len(mv), ctypes.byref(info))
+    rc = lib().spdl_hj_get_image_info(addr, size, ctypes.byref(info))
+    del keep
     if rc:
         raise RuntimeError(f"Failed to decode an image. (header probe: status {rc})")
     return info
@@ -242,7 +247,10 @@ def buffer_address(src) -> tuple[int, int, object]:
     if isinstance(src, np.ndarray):
         a = np.ascontiguousarray(src).view(np.uint8).reshape(-1)
         return a.ctypes.data, a.size, a
-    a = np.frombuffer(src, np.uint8)
+    a = np.frombuffer(memoryview(src).cast("B"), np.uint8)
+    if a.size == 0:  # numpy gives empty arrays a dangling address
+        a = np.zeros(1, np.uint8)
+        return a.ctypes.data, 0, a
     return a.ctypes.data, a.size, a
 
 
@@ -337,18 +345,16 @@ class Decoder:
         n = len(datas)
         if n == 0:
             raise RuntimeError("Failed to decode an image. (the batch is empty)")
+        # borrowed for the duration of the call, no copy (the reference binds
+        # memoryviews as string_views, src/spdl/io/lib/cuda/memoryview_utils.h:17-20)
         keep = []
         ptrs = (ctypes.c_void_p * n)()
         sizes = (ctypes.c_size_t * n)()
         for i, d in enumerate(datas):
-            mv = memoryview(d).cast("B")
-            if mv.readonly:
-                b = (ctypes.c_char * len(mv)).from_buffer_copy(mv)
-            else:
-                b = (ctypes.c_char * len(mv)).from_buffer(mv)
-            keep.append(b)
-            ptrs[i] = ctypes.addressof(b)
-            sizes[i] = len(mv)
+            addr, size, k = buffer_address(d)
+            keep.append(k)
+            ptrs[i] = addr
+            sizes[i] = size
         status = (ctypes.c_int32 * n)()
         err = ctypes.create_string_buffer(1024)
         spec = out.to_c()
@@ -458,13 +464,12 @@ class Decoder:
         """Coefficients / destuffed bytes / diagnostics of one image (tests)."""
         import numpy as np
 
-        mv = memoryview(data).cast("B")
-        b = (ctypes.c_char * len(mv)).from_buffer_copy(mv)
+        addr, size, keep = buffer_address(data)
         coefs = np.zeros((nblocks, 64), np.int16)
-        clean = np.zeros(len(mv), np.uint8)
+        clean = np.zeros(size, np.uint8)
         diag = np.zeros(12, np.int32)
         err = ctypes.create_string_buffer(1024)
-        rc = lib().spdl_hj_debug_entropy(self._h, ctypes.addressof(b), len(mv), coefs.ctypes.data,
+        rc = lib().spdl_hj_debug_entropy(self._h, addr, size, coefs.ctypes.data,
                                          coefs.size, clean.ctypes.data, clean.size,
                                          diag.ctypes.data, err, 1024)
         if rc:
@@ -490,10 +495,9 @@ class Decoder:
                 h = -(-info.height * info.v_samp[c] // vmax)
             planes.append(np.zeros((h, w), np.uint8))
         ptrs = (ctypes.c_void_p * 3)(*([p.ctypes.data for p in planes] + [None] * (3 - len(planes))))
-        mv = memoryview(data).cast("B")
-        b = (ctypes.c_char * len(mv)).from_buffer_copy(mv)
+        addr, size, keep = buffer_address(data)
         err = ctypes.create_string_buffer(1024)
-        rc = lib().spdl_hj_decode_planes(self._h, ctypes.addressof(b), len(mv), IDCT[idct],
+        rc = lib().spdl_hj_decode_planes(self._h, addr, size, IDCT[idct],
                                          ptrs, _stream_handle(stream), err, 1024)
         if rc:
             raise RuntimeError(err.value.decode())

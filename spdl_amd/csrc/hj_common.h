@@ -10,7 +10,8 @@
 //   luts    : HuffTable[8] per image (DC0..3, AC0..3)
 //   coefs   : int16 [nblocks][64] per image, natural order, MCU order
 //   planes  : u8 component planes padded to whole blocks
-//   weights : resize tables (first index + Q14 taps) per image/plane/axis
+//   wts     : swscale tables (positions, Q14/Q12 taps, row writers) per
+//             distinct geometry of the batch (host-built, hj_sws.cpp)
 #pragma once
 #include <stdint.h>
 
@@ -25,7 +26,6 @@ constexpr int kMaxBpm = 10;
 constexpr int kLutBits = 10;
 constexpr int kLutSize = 1 << kLutBits;
 constexpr int kDcBias = 1024;  // FFmpeg mjpegdec last_dc start value (4 << bits)
-constexpr int kMaxTaps = 128;
 
 // Parallel Huffman decode: a restart segment is cut into slots of N bits, at
 // most kMaxSlots slots per pass; every slot keeps up to N + kRecPad symbol
@@ -89,6 +89,25 @@ struct HuffTable {
   uint8_t vals[256];
 };
 
+// The swscale conversion of one image (host plan, hj_sws.h): sizes, the
+// offsets of its tables in the per-batch table pool (int32 units from
+// ImageDesc::wt_off) and the sws_kernel tiling.
+// packed_vscale's writer per output row (libswscale/output.c yuv2rgb_{X,2,1}_c
+// and the _full_ variants), table entry: mode | yalpha << 4 | uvalpha << 17
+enum { kSwsX = 0, kSwsOne = 1, kSwsTwo = 2 };
+enum SwsTable { kHlPos = 0, kHlCoef, kHcPos, kHcCoef, kVlPos, kVlCoef, kVcPos, kVcCoef, kVmode, kSwsTables };
+struct SwsDesc {
+  int32_t sw, sh;          // scaled content size (the swscale destination)
+  int32_t chr_w;           // chroma intermediate width (chrDstW)
+  int32_t full, gray;      // SWS_FULL_CHR_H_INT; single-component source
+  int32_t hl_taps, hc_taps, vl_taps, vc_taps;  // taps read per output (trailing zeros cut)
+  int32_t hl_size, hc_size, vl_size, vc_size;  // taps stored per output
+  int32_t off[kSwsTables];
+  int32_t rb;              // output rows per workgroup band
+  int32_t col_chunk;       // output columns per workgroup
+  int32_t pad_;
+};
+
 struct ImageDesc {      // host-filled per image
   int64_t in_off;       // offset into bytes/clean
   int64_t in_size;
@@ -96,49 +115,26 @@ struct ImageDesc {      // host-filled per image
   int64_t plane_off[kMaxComp];
   int64_t seg_off;      // entries into segs
   int64_t out_off;      // elements into the output
-  int64_t wt_off;       // entries into the weights pool (int32 units)
+  int64_t wt_off;       // this image's swscale tables in the table pool (int32 units)
   int32_t seg_cap;
   int32_t width, height, ncomp;
   int32_t h_samp[kMaxComp], v_samp[kMaxComp];
   int32_t nblocks;
   int32_t plane_stride[kMaxComp];
-  // resize geometry (host computed from the probe; device recomputes nothing)
-  int32_t sw, sh, dx, dy, ow, oh;
-  int32_t taps_x[kMaxComp], taps_y[kMaxComp];
-  // resize: visible content [vx0, vx0 + nvis) x [vy0, vy0 + nvy) of the
-  // scaled image; resampled planes (u8 [nvy][rp_stride] per plane) at rp_off;
-  // per-plane band rows r_rb and column chunk r_cols of resize_plane_kernel
-  int32_t vx0, nvis, vy0, nvy;
-  int32_t rp_stride;
-  int32_t r_cols;
-  int32_t r_rb[kMaxComp];
-  int32_t pad2_;
-  int64_t rp_off;
+  // output placement: out(x, y) = scaled(x - dx, y - dy), black outside
+  int32_t dx, dy, ow, oh;
+  SwsDesc sws;
   int64_t ds_off;       // destuff chunk records: offset and count
   int32_t ds_cap;
   int32_t pad3_;
   int64_t rec_off;      // entropy symbol records: offset (u32 units) and capacity
   int64_t rec_cap;
-  // resize weight tables depend only on the geometry: images of the same
-  // (component sizes, scaled size) share one table set at wt_off, computed
-  // by its owner (the first such image of the batch)
-  int32_t src_w[kMaxComp], src_h[kMaxComp];  // component sizes (host probe)
-  int32_t wt_owner;
-  int32_t pad4_;
 };
 
-// resize: source rows are staged kHMaxRows at a time (kHSrcBytes of LDS); the
-// horizontal-pass intermediate of one band holds kTBuf int16 values
-constexpr int kHSrcBytes = 16384;
-constexpr int kHMaxRows = 16;
-constexpr int kTBuf = 16384;
-constexpr int kRMaxRb = 64;
-constexpr int kRMaxCols = 256;
-constexpr int kVTaps = 32;  // vertical taps staged in LDS (more: read from HBM)
-inline HJ_HD int h_rows_per_group(int stride) {
-  const int r = kHSrcBytes / (stride > 0 ? stride : 1);
-  return r < 1 ? 1 : (r > kHMaxRows ? kHMaxRows : r);
-}
+// sws_kernel LDS budget per workgroup (bytes): the horizontal-pass rows of a
+// band (int16 luma + two chroma planes); the host picks the band height
+constexpr int kSwsLdsBudget = 40 * 1024;
+constexpr int kSwsMaxCols = 256;  // output columns per workgroup
 
 struct ImageInfo {      // device-filled by the parse kernel
   int32_t status;
@@ -177,6 +173,9 @@ struct BatchParams {
   int32_t sub_bits;      // Huffman subsequence size (bits, multiple of 32)
   int32_t debug_mask;    // diagnostics: skip kernel phases (timing ablations only)
   float mean[3], std[3];
+  // ff_yuv2rgb_c_init_tables coefficients (hj_sws.h SwsCsc)
+  int32_t crv, cbu, cgu, cgv;
+  int32_t y_coeff, y_offset, v2r, v2g, u2g, u2b;
 };
 
 enum Status {

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <memory>
 #include <tuple>
 #include <mutex>
 #include <string>
@@ -26,6 +27,7 @@
 
 #include "../../include/spdl_hipjpeg.h"
 #include "hj_common.h"
+#include "hj_sws.h"
 
 namespace hj {
 hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageInfo*, HuffTable*, int, hipStream_t);
@@ -37,13 +39,11 @@ hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, Ima
                           hipStream_t);
 hipError_t launch_idct(const int16_t*, const ImageDesc*, const ImageInfo*, uint8_t*, int, int, int,
                        hipStream_t);
-hipError_t launch_weights(const ImageDesc*, const ImageInfo*, int32_t*, int, int, int,
-                          hipStream_t);
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                       const BatchParams&, int64_t, int, hipStream_t);
 hipError_t launch_nv12(const uint8_t*, uint8_t*, int, int, int, int, int, hipStream_t);
-hipError_t launch_resize(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*,
-                         uint8_t*, void*, const BatchParams&, int64_t, int64_t, int, hipStream_t);
+hipError_t launch_sws(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*, void*,
+                      const BatchParams&, int, int, int, int, hipStream_t);
 }  // namespace hj
 
 using namespace hj;
@@ -51,8 +51,8 @@ using namespace hj;
 namespace {
 
 constexpr int kStages = 8;
-const char* kStageNames[kStages] = {"h2d",   "parse", "destuff", "entropy",
-                                    "idct",  "weights", "output", "d2h_status"};
+const char* kStageNames[kStages] = {"h2d",  "parse",  "destuff", "entropy",
+                                    "idct", "tables", "output",  "d2h_status"};
 
 void set_err(char* err, size_t errlen, const char* fmt, ...) {
   if (!err || !errlen) return;
@@ -301,43 +301,145 @@ int geometry(int w, int h, const spdl_hj_output* o, Geom* g) {
   return SPDL_HJ_OK;
 }
 
-int max_taps(int src_len, int dst_len, int filter) {
-  float scale = (float)src_len / (float)dst_len;
-  float fscale = scale > 1.0f ? scale : 1.0f;
-  float support = (filter == SPDL_HJ_FILTER_BILINEAR  ? 1.0f
-                   : filter == SPDL_HJ_FILTER_LANCZOS ? 3.0f
-                                                      : 2.0f) *
-                  fscale;
-  return (int)ceilf(2.0f * support) + 1;
+// ---- swscale plans (hj_sws.h), packed for the device ----------------------
+// One per distinct (source size, sampling, output placement, filter); cached
+// per context so a stream of same-size images plans once.
+struct PlanKey {
+  int w, h, hsub, vsub, gray, filter, sw, sh, dx, dy, ow, oh;
+  bool operator<(const PlanKey& o) const {
+    return std::tie(w, h, hsub, vsub, gray, filter, sw, sh, dx, dy, ow, oh) <
+           std::tie(o.w, o.h, o.hsub, o.vsub, o.gray, o.filter, o.sw, o.sh, o.dx, o.dy, o.ow, o.oh);
+  }
+};
+
+struct PackedPlan {
+  SwsDesc d{};                  // offsets relative to the blob
+  std::vector<int32_t> blob;    // tables, 16-byte aligned sections
+  int bands = 0, chunks = 0, lds = 0;
+};
+
+class PlanCache {
+ public:
+  std::shared_ptr<const PackedPlan> get(const PlanKey& k, int* rc) {
+    auto it = map_.find(k);
+    if (it != map_.end()) return it->second;
+    auto p = build(k, rc);
+    if (!p) return nullptr;
+    if (map_.size() >= 512) map_.clear();  // bounded: a stream of odd sizes replans
+    map_.emplace(k, p);
+    return p;
+  }
+
+ private:
+  static void put(std::vector<int32_t>& blob, int32_t* off, const void* data, size_t bytes) {
+    *off = (int32_t)blob.size();
+    const size_t words = (bytes + 3) / 4;
+    blob.resize(blob.size() + ((words + 3) & ~(size_t)3), 0);
+    if (bytes) memcpy(blob.data() + *off, data, bytes);
+  }
+
+  static std::shared_ptr<const PackedPlan> build(const PlanKey& k, int* rc) {
+    SwsPlan pl;
+    *rc = sws_plan(k.w, k.h, k.hsub, k.vsub, k.gray != 0, k.sw, k.sh, k.filter, &pl);
+    if (*rc) return nullptr;
+    auto pp = std::make_shared<PackedPlan>();
+    SwsDesc& d = pp->d;
+    d.sw = k.sw;
+    d.sh = k.sh;
+    d.chr_w = pl.chrDstW;
+    d.full = pl.full;
+    d.gray = pl.gray;
+    const SwsAxis* ax[4] = {&pl.hl, &pl.hc, &pl.vl, &pl.vc};
+    int32_t* taps[4] = {&d.hl_taps, &d.hc_taps, &d.vl_taps, &d.vc_taps};
+    int32_t* sizes[4] = {&d.hl_size, &d.hc_size, &d.vl_size, &d.vc_size};
+    for (int i = 0; i < 4; i++) {
+      *taps[i] = ax[i]->eff;
+      *sizes[i] = ax[i]->size;
+      put(pp->blob, &d.off[2 * i], ax[i]->pos.data(), ax[i]->pos.size() * 4);
+      put(pp->blob, &d.off[2 * i + 1], ax[i]->coef.data(), ax[i]->coef.size() * 2);
+    }
+    put(pp->blob, &d.off[kVmode], pl.vmode.data(), pl.vmode.size() * 4);
+    // tiling: the tallest band (and widest column chunk) whose horizontal
+    // pass rows fit the LDS budget; bands are in output rows
+    for (int cols = kSwsMaxCols; cols >= 16 && !pp->bands; cols /= 2) {
+      const int chunk = k.ow < cols ? k.ow : cols;
+      static const int kRb[] = {32, 24, 16, 12, 8, 6, 4, 3, 2, 1};
+      for (int rb : kRb) {
+        int64_t lds = 0;
+        for (int yo0 = 0; yo0 < k.oh; yo0 += rb) {
+          const int ys0 = std::max(yo0 - k.dy, 0), ys1 = std::min(yo0 + rb - k.dy, k.sh);
+          if (ys0 >= ys1) continue;
+          const int64_t lrows = pl.vl.pos[ys1 - 1] + pl.vl.eff - pl.vl.pos[ys0];
+          const int64_t crows = pl.gray ? 0 : pl.vc.pos[ys1 - 1] + pl.vc.eff - pl.vc.pos[ys0];
+          for (int xo0 = 0; xo0 < k.ow; xo0 += chunk) {
+            const int xs0 = std::max(xo0 - k.dx, 0), xs1 = std::min(xo0 + chunk - k.dx, k.sw);
+            if (xs0 >= xs1) continue;
+            const int64_t ncl = xs1 - xs0;
+            const int64_t ncc = pl.gray ? 0 : pl.full ? ncl : ((xs1 - 1) >> 1) - (xs0 >> 1) + 1;
+            lds = std::max(lds, 2 * (lrows * ncl + 2 * crows * ncc));
+          }
+        }
+        if (lds <= kSwsLdsBudget || (rb == 1 && lds <= 64 * 1024)) {
+          d.rb = rb;
+          d.col_chunk = chunk;
+          pp->lds = (int)lds;
+          pp->bands = (k.oh + rb - 1) / rb;
+          pp->chunks = (k.ow + chunk - 1) / chunk;
+          break;
+        }
+      }
+    }
+    if (!pp->bands) {
+      *rc = SPDL_HJ_ERR_BAD_GEOMETRY;
+      return nullptr;
+    }
+    return pp;
+  }
+
+  std::map<PlanKey, std::shared_ptr<const PackedPlan>> map_;
+};
+
+// chroma subsampling shifts of the yuvj4xxp frame FFmpeg's mjpeg decoder
+// makes of this sampling (444 / 422 / 420 / 440 / 411 ...); others are not
+// a swscale input format here
+int chroma_shifts(const spdl_hj_image_info& p, int* hs, int* vs) {
+  *hs = *vs = 0;
+  if (p.ncomp == 1) return SPDL_HJ_OK;
+  const int hmax = std::max(p.h_samp[0], std::max(p.h_samp[1], p.h_samp[2]));
+  const int vmax = std::max(p.v_samp[0], std::max(p.v_samp[1], p.v_samp[2]));
+  if (p.h_samp[0] != hmax || p.v_samp[0] != vmax || p.h_samp[1] != p.h_samp[2] ||
+      p.v_samp[1] != p.v_samp[2] || hmax % p.h_samp[1] || vmax % p.v_samp[1])
+    return SPDL_HJ_ERR_UNSUPPORTED;
+  const int rh = hmax / p.h_samp[1], rv = vmax / p.v_samp[1];
+  if ((rh & (rh - 1)) || (rv & (rv - 1))) return SPDL_HJ_ERR_UNSUPPORTED;
+  while ((1 << *hs) < rh) (*hs)++;
+  while ((1 << *vs) < rv) (*vs)++;
+  return SPDL_HJ_OK;
 }
 
 struct Layout {
   std::vector<ImageDesc> desc;
-  int64_t total_blocks = 0, total_planes = 0, total_segs = 0, total_wts = 0, total_recs = 0;
+  std::vector<int32_t> tables;  // the batch's swscale table pool
+  int64_t total_blocks = 0, total_planes = 0, total_segs = 0, total_recs = 0;
   int64_t out_elems_per_image = 0;
-  int max_blocks = 0, max_len = 0;
+  int max_blocks = 0;
   int64_t max_px = 0;
-  int64_t max_bands = 0, max_quads = 0, total_rp = 0;
   int64_t total_ds = 0;
   int max_chunks = 0;
   int ow = 0, oh = 0;
-};
-
-struct WtKey {
-  int ncomp;
-  int cw[3], ch[3];
-  int sw, sh;
-  bool operator<(const WtKey& o) const {
-    return std::tie(ncomp, cw[0], cw[1], cw[2], ch[0], ch[1], ch[2], sw, sh) <
-           std::tie(o.ncomp, o.cw[0], o.cw[1], o.cw[2], o.ch[0], o.ch[1], o.ch[2], o.sw, o.sh);
-  }
+  int sws_bands = 0, sws_chunks = 0, sws_lds = 0;
 };
 
 int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_image_info* infos,
                  int n, const spdl_hj_output* out, int sub_bits, Layout& L, int32_t* status,
-                 char* err, size_t errlen) {
+                 char* err, size_t errlen, PlanCache* plans) {
   L.desc.assign(n, ImageDesc{});
-  std::map<WtKey, int64_t> wt_tables;
+  std::map<const PackedPlan*, int64_t> placed;  // plan -> offset in L.tables
+  auto fail = [&](int i, int rc, const char* what) {
+    if (status) status[i] = rc;
+    set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, what ? what : status_str(rc));
+    return rc;
+  };
   for (int i = 0; i < n; i++) {
     ImageDesc& d = L.desc[i];
     const spdl_hj_image_info& p = infos[i];
@@ -353,11 +455,9 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
       hmax = p.h_samp[c] > hmax ? p.h_samp[c] : hmax;
       vmax = p.v_samp[c] > vmax ? p.v_samp[c] : vmax;
     }
-    int bw[3] = {0, 0, 0}, bh[3] = {0, 0, 0}, cw[3] = {0, 0, 0}, chh[3] = {0, 0, 0};
+    int bw[3] = {0, 0, 0}, bh[3] = {0, 0, 0};
     int64_t nblocks;
     if (p.ncomp == 1) {
-      cw[0] = p.width;
-      chh[0] = p.height;
       bw[0] = (p.width + 7) / 8;
       bh[0] = (p.height + 7) / 8;
       nblocks = (int64_t)bw[0] * bh[0];
@@ -365,30 +465,16 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
       int mcux = (p.width + 8 * hmax - 1) / (8 * hmax), mcuy = (p.height + 8 * vmax - 1) / (8 * vmax);
       int bpm = 0;
       for (int c = 0; c < p.ncomp; c++) {
-        if (hmax % p.h_samp[c] || vmax % p.v_samp[c]) {
-          if (status) status[i] = SPDL_HJ_ERR_UNSUPPORTED;
-          set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i,
-                  status_str(SPDL_HJ_ERR_UNSUPPORTED));
-          return SPDL_HJ_ERR_UNSUPPORTED;
-        }
+        if (hmax % p.h_samp[c] || vmax % p.v_samp[c]) return fail(i, SPDL_HJ_ERR_UNSUPPORTED, nullptr);
         bw[c] = mcux * p.h_samp[c];
         bh[c] = mcuy * p.v_samp[c];
-        cw[c] = (p.width * p.h_samp[c] + hmax - 1) / hmax;
-        chh[c] = (p.height * p.v_samp[c] + vmax - 1) / vmax;
         bpm += p.h_samp[c] * p.v_samp[c];
       }
-      if (bpm > kMaxBpm) {
-        if (status) status[i] = SPDL_HJ_ERR_UNSUPPORTED;
-        set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i,
-                status_str(SPDL_HJ_ERR_UNSUPPORTED));
-        return SPDL_HJ_ERR_UNSUPPORTED;
-      }
+      if (bpm > kMaxBpm) return fail(i, SPDL_HJ_ERR_UNSUPPORTED, nullptr);
       nblocks = (int64_t)mcux * mcuy * bpm;
     }
-    if (nblocks > (1 << 30)) {
-      set_err(err, errlen, "image %d too large", i);
-      return SPDL_HJ_ERR_UNSUPPORTED;
-    }
+    // the entropy kernel's 32-bit coefficient index (blk * 64) must not wrap
+    if (nblocks >= (1 << 26)) return fail(i, SPDL_HJ_ERR_UNSUPPORTED, "image too large");
     d.nblocks = (int)nblocks;
     d.coef_off = L.total_blocks;
     L.total_blocks += nblocks;
@@ -405,22 +491,13 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     d.ds_off = L.total_ds;
     L.total_ds += d.ds_cap;
     if (d.ds_cap > L.max_chunks) L.max_chunks = d.ds_cap;
-    {
-      // entropy slot state (u32 units): two uint4 per slot -- start state,
-      // blocks started, end z, DC sums
-      d.rec_cap = (int64_t)kMaxSlots * 8;
-      d.rec_off = L.total_recs;
-      L.total_recs += d.rec_cap;
-    }
+    // entropy slot state (u32 units): two uint4 per slot
+    d.rec_cap = (int64_t)kMaxSlots * 8;
+    d.rec_off = L.total_recs;
+    L.total_recs += d.rec_cap;
     Geom g;
     int rc = geometry(p.width, p.height, out, &g);
-    if (rc) {
-      if (status) status[i] = rc;
-      set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, status_str(rc));
-      return rc;
-    }
-    d.sw = g.sw;
-    d.sh = g.sh;
+    if (rc) return fail(i, rc, nullptr);
     d.dx = g.dx;
     d.dy = g.dy;
     d.ow = g.ow;
@@ -435,86 +512,25 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
               L.ow, L.oh, i, g.ow, g.oh);
       return SPDL_HJ_ERR_INVALID_ARG;
     }
-    for (int c = 0; c < p.ncomp; c++) {
-      d.src_w[c] = cw[c];
-      d.src_h[c] = chh[c];
-    }
-    d.wt_off = L.total_wts;
-    d.wt_owner = 0;
-    if (out->resize) {
-      for (int c = 0; c < p.ncomp; c++) {
-        d.taps_x[c] = max_taps(cw[c], g.sw, out->filter);
-        d.taps_y[c] = max_taps(chh[c], g.sh, out->filter);
-        if (d.taps_x[c] > kMaxTaps || d.taps_y[c] > kMaxTaps) {
-          if (status) status[i] = SPDL_HJ_ERR_BAD_GEOMETRY;
-          set_err(err, errlen,
-                  "Failed to decode an image. (image %d: downscale factor too large: %dx%d -> "
-                  "%dx%d)",
-                  i, p.width, p.height, g.sw, g.sh);
-          return SPDL_HJ_ERR_BAD_GEOMETRY;
-        }
-      }
-      // one table set per distinct geometry (all images of a uniform batch
-      // share the first one's)
-      WtKey key{p.ncomp, {cw[0], cw[1], cw[2]}, {chh[0], chh[1], chh[2]}, g.sw, g.sh};
-      auto it = wt_tables.find(key);
-      if (it != wt_tables.end()) {
-        d.wt_off = it->second;
-      } else {
-        wt_tables.emplace(key, L.total_wts);
-        d.wt_owner = 1;
-        for (int c = 0; c < p.ncomp; c++)
-          L.total_wts += (int64_t)g.sw * (1 + (d.taps_x[c] + 1) / 2) +
-                         (int64_t)g.sh * (1 + (d.taps_y[c] + 1) / 2);
-      }
-      int ml = g.sw > g.sh ? g.sw : g.sh;
-      if (ml > L.max_len) L.max_len = ml;
-      // visible content of the scaled image and its resampled planes
-      d.vx0 = g.dx < 0 ? -g.dx : 0;
-      const int vx1 = (g.ow - g.dx) < g.sw ? (g.ow - g.dx) : g.sw;
-      d.nvis = vx1 > d.vx0 ? vx1 - d.vx0 : 0;
-      d.vy0 = g.dy < 0 ? -g.dy : 0;
-      const int vy1 = (g.oh - g.dy) < g.sh ? (g.oh - g.dy) : g.sh;
-      d.nvy = vy1 > d.vy0 ? vy1 - d.vy0 : 0;
-      d.rp_stride = (int32_t)round_up(d.nvis > 0 ? d.nvis : 1, 16);
-      d.rp_off = L.total_rp;
-      L.total_rp += round_up((int64_t)p.ncomp * d.nvy * d.rp_stride, 256);
-      // resize_plane_kernel tiling: widest column chunk, then per plane the
-      // tallest band whose intermediate rows fit kTBuf
-      d.r_cols = 0;
-      for (int cand = kRMaxCols; cand >= 64 && d.r_cols == 0; cand -= 64) {
-        const int ncc = cand < d.nvis ? cand : (d.nvis > 0 ? d.nvis : 1);
-        bool all = true;
-        for (int c = 0; c < p.ncomp; c++) {
-          const float sy = (float)chh[c] / (float)g.sh;
-          const int tpy = ((d.taps_y[c] + 1) / 2) * 2;
-          int rb = 0;
-          for (int r = kRMaxRb; r >= 1; r--) {
-            const int rows = (int)ceilf((float)(r - 1) * sy) + 2 + tpy;
-            if ((int64_t)rows * ncc <= kTBuf) {
-              rb = r;
-              break;
-            }
-          }
-          if (rb == 0) all = false;
-          d.r_rb[c] = rb;
-        }
-        if (all) d.r_cols = cand;
-      }
-      if (d.r_cols == 0) {
-        if (status) status[i] = SPDL_HJ_ERR_BAD_GEOMETRY;
-        set_err(err, errlen, "Failed to decode an image. (image %d: resize tile does not fit)", i);
-        return SPDL_HJ_ERR_BAD_GEOMETRY;
-      }
-      for (int c = 0; c < p.ncomp; c++) {
-        const int64_t bands = (d.nvy + d.r_rb[c] - 1) / d.r_rb[c];
-        if (bands > L.max_bands) L.max_bands = bands;
-      }
-      const int64_t quads = (int64_t)((g.ow + 3) / 4) * g.oh;
-      if (quads > L.max_quads) L.max_quads = quads;
-    }
     int64_t px = (int64_t)g.ow * g.oh;
     if (px > L.max_px) L.max_px = px;
+    if (!plans || out->csc == SPDL_HJ_CSC_JFIF) continue;
+    int hs, vs;
+    if ((rc = chroma_shifts(p, &hs, &vs))) return fail(i, rc, nullptr);
+    const PlanKey key{p.width, p.height, hs, vs, p.ncomp == 1, out->resize ? out->filter : 0,
+                      g.sw, g.sh, g.dx, g.dy, g.ow, g.oh};
+    auto plan = plans->get(key, &rc);
+    if (!plan) return fail(i, rc, rc == SPDL_HJ_ERR_BAD_GEOMETRY ? "scale filter too long" : nullptr);
+    auto it = placed.find(plan.get());
+    if (it == placed.end()) {
+      it = placed.emplace(plan.get(), (int64_t)L.tables.size()).first;
+      L.tables.insert(L.tables.end(), plan->blob.begin(), plan->blob.end());
+    }
+    d.wt_off = it->second;
+    d.sws = plan->d;
+    L.sws_bands = std::max(L.sws_bands, plan->bands);
+    L.sws_chunks = std::max(L.sws_chunks, plan->chunks);
+    L.sws_lds = std::max(L.sws_lds, plan->lds);
   }
   L.out_elems_per_image = (int64_t)L.ow * L.oh * 3;
   for (int i = 0; i < n; i++) L.desc[i].out_off = (int64_t)i * L.out_elems_per_image;
@@ -530,7 +546,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
 constexpr int kSlots = 3;
 
 struct Slot {
-  PinBuf pin_in, pin_desc, pin_status;
+  PinBuf pin_in, pin_desc, pin_status, pin_tables;
   DevBuf bytes;
   hipEvent_t h2d_done = nullptr;  // bytes are in HBM
   hipEvent_t done = nullptr;      // the batch's last kernel / status copy finished
@@ -550,7 +566,7 @@ struct Slot {
 constexpr int kMaxLanes = 3;
 
 struct Workspace {
-  DevBuf clean, segs, desc, info, luts, coefs, planes, wts, recs, rplanes, dschunks;
+  DevBuf clean, segs, desc, info, luts, coefs, planes, wts, recs, dschunks;
   hipEvent_t done = nullptr;      // the workspace is free after this
   hipStream_t stream = nullptr;   // lanes > 1 only
 };
@@ -572,6 +588,7 @@ struct spdl_hj_ctx {
   int entropy_threads = 512;
   int warm_slots = 8;  // entropy round 0: slots decoded before a run's first slot
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
+  PlanCache plans;          // swscale plans per distinct geometry
 };
 
 namespace {
@@ -692,10 +709,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   HJ_HIP(W.coefs.ensure((size_t)L.total_blocks * 128 + 256));
   HJ_HIP(W.planes.ensure((size_t)L.total_planes + 256));
   HJ_HIP(W.recs.ensure((size_t)L.total_recs * 4 + 256));
-  if (out->resize) {
-    HJ_HIP(W.wts.ensure((size_t)L.total_wts * 4 + 256));
-    HJ_HIP(W.rplanes.ensure((size_t)L.total_rp + 256));
-  }
+  HJ_HIP(W.wts.ensure(L.tables.size() * 4 + 256));
   HJ_HIP(slot.pin_desc.ensure(sizeof(ImageDesc) * n));
   HJ_HIP(slot.pin_status.ensure(sizeof(int32_t) * n));
   slot.n = n;
@@ -735,15 +749,30 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
     bp.mean[c] = out->mean[c];
     bp.std[c] = out->std[c];
   }
+  const SwsCsc csc = sws_csc();
+  bp.crv = csc.crv;
+  bp.cbu = csc.cbu;
+  bp.cgu = csc.cgu;
+  bp.cgv = csc.cgv;
+  bp.y_coeff = csc.y_coeff;
+  bp.y_offset = csc.y_offset;
+  bp.v2r = csc.v2r;
+  bp.v2g = csc.v2g;
+  bp.u2g = csc.u2g;
+  bp.u2b = csc.u2b;
   if (!planes_only) {
-    if (out->resize) {
-      HJ_HIP(launch_weights(desc, infos, static_cast<int32_t*>(W.wts.p), out->filter, L.max_len,
-                            n, st));
+    if (out->csc == SPDL_HJ_CSC_SWSCALE) {
+      // the batch's swscale tables ride the same stream ahead of the kernel
+      const size_t tb = L.tables.size() * 4;
+      HJ_HIP(slot.pin_tables.ensure(tb + 16));
+      if (tb) {
+        memcpy(slot.pin_tables.p, L.tables.data(), tb);
+        HJ_HIP(hipMemcpyAsync(W.wts.p, slot.pin_tables.p, tb, hipMemcpyHostToDevice, st));
+      }
       mark(ctx, slot, 6, st);
-      HJ_HIP(launch_resize(static_cast<const uint8_t*>(W.planes.p), desc, infos,
-                           static_cast<const int32_t*>(W.wts.p),
-                           static_cast<uint8_t*>(W.rplanes.p), out_dev, bp, L.max_bands,
-                           L.max_quads, n, st));
+      HJ_HIP(launch_sws(static_cast<const uint8_t*>(W.planes.p), desc, infos,
+                        static_cast<const int32_t*>(W.wts.p), out_dev, bp, L.sws_bands,
+                        L.sws_chunks, L.sws_lds, n, st));
     } else {
       mark(ctx, slot, 6, st);
       HJ_HIP(launch_csc(static_cast<const uint8_t*>(W.planes.p), desc, infos, out_dev, bp,
@@ -796,9 +825,11 @@ int stage_h2d(spdl_hj_ctx* ctx, Slot& s, size_t total, hipStream_t st, char* err
 }
 
 bool valid_output(const spdl_hj_output* o) {
+  // the JFIF conversion has no scaler: full resolution only
   return o && o->pix_fmt >= 0 && o->pix_fmt <= 3 && (o->dtype >= 0 && o->dtype <= 2) &&
          (o->idct == 0 || o->idct == 1) && (o->filter >= 0 && o->filter <= 2) &&
-         o->aspect >= 0 && o->aspect <= 2;
+         o->aspect >= 0 && o->aspect <= 2 &&
+         (o->csc == SPDL_HJ_CSC_SWSCALE || (o->csc == SPDL_HJ_CSC_JFIF && !o->resize));
 }
 
 // ---- tar (ustar / GNU 'L' long names / pax 'x' path) ------------------------
@@ -907,7 +938,7 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
   if (c->copy) (void)hipStreamSynchronize(c->copy);
   for (Workspace& w : c->ws) {
     DevBuf* bufs[] = {&w.clean, &w.segs, &w.desc, &w.info, &w.luts, &w.coefs,
-                      &w.planes, &w.wts, &w.recs, &w.rplanes, &w.dschunks};
+                      &w.planes, &w.wts, &w.recs, &w.dschunks};
     for (DevBuf* b : bufs) b->release();
     if (w.done) (void)hipEventDestroy(w.done);
     if (w.stream) (void)hipStreamDestroy(w.stream);
@@ -917,6 +948,7 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
     s.pin_in.release();
     s.pin_desc.release();
     s.pin_status.release();
+    s.pin_tables.release();
     if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.submitted) (void)hipEventDestroy(s.submitted);
@@ -956,7 +988,7 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
   }
   Layout L;
   int rc = build_layout(offs.data(), szs.data(), infos.data(), n, out, ctx->sub_bits, L, status, err,
-                        errlen);
+                        errlen, &ctx->plans);
   if (rc) return rc;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
@@ -985,7 +1017,8 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
   DeviceGuard g(ctx->device);
   hipStream_t st = static_cast<hipStream_t>(stream);
   Layout L;
-  int rc = build_layout(offsets, sizes, infos, n, out, ctx->sub_bits, L, status, err, errlen);
+  int rc = build_layout(offsets, sizes, infos, n, out, ctx->sub_bits, L, status, err, errlen,
+                        &ctx->plans);
   if (rc) return rc;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
@@ -1122,7 +1155,8 @@ int spdl_hj_decode_staged(spdl_hj_ctx* ctx, int64_t ticket, size_t len, const in
     }
   }
   Layout L;
-  int rc = build_layout(offsets, sizes, infos.data(), n, out, ctx->sub_bits, L, status, err, errlen);
+  int rc = build_layout(offsets, sizes, infos.data(), n, out, ctx->sub_bits, L, status, err, errlen,
+                        &ctx->plans);
   if (rc) {
     s->ticket = 0;
     return rc;
@@ -1241,7 +1275,7 @@ int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   o.idct = idct;
   int64_t off = 0, sz = (int64_t)size, total = round_up(sz + 64, 256);
   Layout L;
-  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen);
+  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen, nullptr);
   if (rc) return rc;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
@@ -1294,7 +1328,7 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   spdl_hj_output o{};
   int64_t off = 0, sz = (int64_t)size, total = round_up(sz + 64, 256);
   Layout L;
-  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen);
+  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen, nullptr);
   if (rc) return rc;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);

@@ -1574,419 +1574,289 @@ __global__ void __launch_bounds__(256) csc_kernel(const uint8_t* __restrict__ pl
 }
 
 // ---------------------------------------------------------------------------
-// resize: weights + fused resize/csc/pad/normalise
+// sws_kernel: the reference CPU path's swscale conversion -- scale to the
+// content size + yuvj -> rgb24 in one pass (the graph's scale filter outputs
+// rgb24 itself, src/libspdl/core/detail/ffmpeg/filter_graph.cpp:280-313) --
+// then pad (black) / crop, optional (x/255 - mean)/std, stores in the
+// caller's layout.  Workgroup = (band of output rows, chunk of output
+// columns, image).  The band's source rows are scaled horizontally into LDS
+// (hScale8To15: one thread per column, taps in registers, v_dot2 on int16
+// pairs), then each output pixel runs the vertical taps and the RGB24 writer
+// swscale picks for its row (yuv2rgb_{X,2,1}_c table path or the _full_
+// path, libswscale/output.c).  Tables come from the host plan (hj_sws.cpp);
+// arithmetic: oracle/sws_oracle.c.
 // ---------------------------------------------------------------------------
 
-#pragma clang fp contract(off)
-// sin(pi x), 0 <= x <= 3: odd polynomial to r^13 on r = x - rint(x), the
-// oracle's op sequence (jpeg_oracle.c sinpi_poly), contraction off.
-__device__ float sinpi_poly(float x) {
-  const float k = rintf(x);
-  const float r = x - k;
-  const float p = r * r;
-  float s = -7.37043094e-3f + p * 4.66302806e-4f;
-  s = 8.21458866e-2f + p * s;
-  s = -5.99264529e-1f + p * s;
-  s = 2.55016404f + p * s;
-  s = -5.16771278f + p * s;
-  s = 3.14159265f + p * s;
-  s = r * s;
-  return ((int)k & 1) ? -s : s;
-}
-
-// Lanczos-3 (NPP NPPI_INTER_LANCZOS of resize_npp, swscale flags=lanczos)
-__device__ float lanczos_eval(float t) {
-  if (t == 0.0f) return 1.0f;
-  if (t >= 3.0f) return 0.0f;
-  const float a = sinpi_poly(t);
-  const float b = sinpi_poly(__fdiv_rn(t, 3.0f));
-  float num = 3.0f * a;
-  num = num * b;
-  float den = 9.8696044f * t;
-  den = den * t;
-  return __fdiv_rn(num, den);
-}
-
-__device__ float kernel_eval(int filter, float x) {
-  const float t = fabsf(x);
-  if (filter == 1) return t < 1.0f ? 1.0f - t : 0.0f;
-  if (filter == 2) return lanczos_eval(t);
-  const float t2 = t * t;
-  const float t3 = t2 * t;
-  if (t <= 1.0f) {
-    const float a = 1.4f * t3;
-    const float b = 2.4f * t2;
-    return (a - b) + 1.0f;
-  }
-  if (t < 2.0f) {
-    const float a = -0.6f * t3;
-    const float b = 3.0f * t2;
-    const float c = 4.8f * t;
-    return ((a + b) - c) + 2.4f;
-  }
-  return 0.0f;
-}
-
-// Weight table for one (image, plane, axis): entry i holds first tap index
-// (int32) then `taps` Q14 weights (int16, padded with zero).  Layout in the
-// int32 pool: [first x dst_len][ceil(taps/2) x dst_len] (weights packed 2/int32).
-__global__ void __launch_bounds__(256) weights_kernel(const ImageDesc* __restrict__ desc,
-                                                      const ImageInfo* __restrict__ infos,
-                                                      int32_t* __restrict__ pool,
-                                                      const int filter) {
-  const int img = blockIdx.z, which = blockIdx.y;  // which = plane*2 + axis
-  const ImageDesc& dd = desc[img];
-  // shared tables: only the owner writes them, whatever its decode status
-  // (the table depends on host-known geometry only)
-  if (!dd.wt_owner) return;
-  const int c = which >> 1, axis = which & 1;
-  if (c >= dd.ncomp) return;
-  const int src_len = axis == 0 ? dd.src_w[c] : dd.src_h[c];
-  const int dst_len = axis == 0 ? dd.sw : dd.sh;
-  const int taps = axis == 0 ? dd.taps_x[c] : dd.taps_y[c];
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= dst_len) return;
-  // table offset inside the image's region
-  int64_t off = dd.wt_off;
-  for (int k = 0; k < which; k++) {
-    const int kc = k >> 1, ka = k & 1;
-    if (kc >= dd.ncomp) break;
-    const int dl = ka == 0 ? dd.sw : dd.sh, tp = ka == 0 ? dd.taps_x[kc] : dd.taps_y[kc];
-    off += (int64_t)dl * (1 + (tp + 1) / 2);
-  }
-  int32_t* first = pool + off;
-  int16_t* w = reinterpret_cast<int16_t*>(pool + off + dst_len) + (int64_t)i * ((taps + 1) / 2) * 2;
-  const float scale = __fdiv_rn((float)src_len, (float)dst_len);
-  const float fscale = scale > 1.0f ? scale : 1.0f;
-  const float support = (filter == 1 ? 1.0f : filter == 2 ? 3.0f : 2.0f) * fscale;
-  float center = ((float)i + 0.5f) * scale;
-  center = center - 0.5f;
-  const int lo = (int)ceilf(center - support);
-  const int hi = (int)floorf(center + support);
-  const int n = hi - lo + 1;
-  float wf[kMaxTaps];
-  int wq[kMaxTaps];
-  float sum = 0.0f;
-  for (int t = 0; t < n && t < kMaxTaps; t++) {
-    const float x = __fdiv_rn((float)(lo + t) - center, fscale);
-    wf[t] = kernel_eval(filter, x);
-    sum = sum + wf[t];
-  }
-  int qs = 0, am = 0;
-  for (int t = 0; t < n && t < kMaxTaps; t++) {
-    float q = __fdiv_rn(wf[t], sum);
-    q = q * 16384.0f;
-    q = q + 0.5f;
-    wq[t] = (int)floorf(q);
-    qs += wq[t];
-    if (wq[t] > wq[am]) am = t;
-  }
-  wq[am] += 16384 - qs;
-  first[i] = lo;
-  const int tp2 = ((taps + 1) / 2) * 2;
-  for (int t = 0; t < tp2; t++) w[t] = (int16_t)(t < n ? wq[t] : 0);
-}
-#pragma clang fp contract(on)
-
-// Weight tables of plane c (layout of weights_kernel): first index and
-// Q14 taps (padded to an even count) per destination column / row.
-struct PlaneWeights {
-  const int32_t* fx;
-  const int16_t* wx;
-  const int32_t* fy;
-  const int16_t* wy;
-  int tx, ty;
-};
-
-__device__ __forceinline__ PlaneWeights plane_weights(const ImageDesc& dd, const int32_t* pool,
-                                                      int c) {
-  PlaneWeights w{};
-  int64_t off = dd.wt_off;
-  for (int k = 0; k <= c; k++) {
-    const int tx = ((dd.taps_x[k] + 1) / 2) * 2, ty = ((dd.taps_y[k] + 1) / 2) * 2;
-    if (k == c) {
-      w.tx = tx;
-      w.ty = ty;
-      w.fx = pool + off;
-      w.wx = reinterpret_cast<const int16_t*>(pool + off + dd.sw);
-    }
-    off += (int64_t)dd.sw * (1 + tx / 2);
-    if (k == c) {
-      w.fy = pool + off;
-      w.wy = reinterpret_cast<const int16_t*>(pool + off + dd.sh);
-    }
-    off += (int64_t)dd.sh * (1 + ty / 2);
-  }
-  return w;
-}
-
-// Horizontal taps of one column over nr staged rows, interior case: the
-// 4*NQ bytes from `f` are fetched as NQ+1 aligned dwords, realigned with
-// v_alignbyte, widened to int16 pairs with v_perm and accumulated with
-// v_dot2 against the packed Q14 weights (zeros past the real taps).  Writes
-// the Q6 intermediate ((acc + 128) >> 8) to out[rr * ostride].
 typedef short hj_short2 __attribute__((ext_vector_type(2)));
 
+// sum over taps of row[pos + t] * tap[t] for t < 4 * NQ: 4*NQ bytes from
+// `pos` fetched as NQ+1 aligned dwords, realigned (v_alignbyte), widened to
+// int16 pairs (v_perm) and accumulated with v_dot2 against packed taps.
 template <int NQ>
-__device__ __forceinline__ void h_rows_dot2(const uint8_t* srcb, int stride, int f, int nr,
-                                            const uint32_t* wp, int16_t* out, int ostride) {
-  const int a = f & ~3;
-  const uint32_t sh = (uint32_t)(f & 3);
-#pragma unroll 2
-  for (int rr = 0; rr < nr; rr++) {
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(srcb + rr * stride + a);
-    uint32_t w[NQ + 1];
+__device__ __forceinline__ int32_t hsum(const uint8_t* row, int pos, const uint32_t* wp) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(row + (pos & ~3));
+  const uint32_t sh = (uint32_t)(pos & 3);
+  uint32_t w[NQ + 1];
 #pragma unroll
-    for (int i = 0; i <= NQ; i++) w[i] = q[i];
-    int32_t h = 0;
+  for (int i = 0; i <= NQ; i++) w[i] = q[i];
+  int32_t h = 0;
 #pragma unroll
-    for (int i = 0; i < NQ; i++) {
-      const uint32_t u = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
-      const uint32_t lo = __builtin_amdgcn_perm(0u, u, 0x0C010C00u);  // bytes 0,1 -> int16 x2
-      const uint32_t hi = __builtin_amdgcn_perm(0u, u, 0x0C030C02u);  // bytes 2,3
-      h = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, lo),
-                                 __builtin_bit_cast(hj_short2, wp[2 * i]), h, false);
-      h = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, hi),
-                                 __builtin_bit_cast(hj_short2, wp[2 * i + 1]), h, false);
+  for (int i = 0; i < NQ; i++) {
+    const uint32_t u = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+    const uint32_t lo = __builtin_amdgcn_perm(0u, u, 0x0C010C00u);  // bytes 0,1 -> int16 x2
+    const uint32_t hi = __builtin_amdgcn_perm(0u, u, 0x0C030C02u);  // bytes 2,3
+    h = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, lo),
+                               __builtin_bit_cast(hj_short2, wp[2 * i]), h, false);
+    h = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, hi),
+                               __builtin_bit_cast(hj_short2, wp[2 * i + 1]), h, false);
+  }
+  return h;
+}
+
+// Horizontal pass of one plane: columns [c0, c0 + ncols) of the scaled
+// plane for source rows [r0, r1) into lds[(r - r0) * ncols + (c - c0)].
+// Rows past the plane (only reached by zero taps) read its last row.
+template <int NQ>
+__device__ void hpass_cols(const uint8_t* plane, int stride, int ph, const int32_t* pos,
+                           const int16_t* coef, int size, int taps, int c0, int ncols, int r0,
+                           int r1, int16_t* lds, int tid, int nthreads) {
+  for (int c = tid; c < ncols; c += nthreads) {
+    const int x = c0 + c;
+    const int p = pos[x];
+    uint32_t wp[2 * NQ];
+#pragma unroll
+    for (int k = 0; k < 2 * NQ; k++) {
+      const int t0 = 2 * k, t1 = 2 * k + 1;
+      const uint32_t a = t0 < taps ? (uint16_t)coef[(int64_t)x * size + t0] : 0u;
+      const uint32_t b = t1 < taps ? (uint16_t)coef[(int64_t)x * size + t1] : 0u;
+      wp[k] = a | (b << 16);
     }
-    out[rr * ostride] = (int16_t)((h + 128) >> 8);
+    for (int r = r0; r < r1; r++) {
+      const uint8_t* row = plane + (int64_t)min(r, ph - 1) * stride;
+      const int32_t v = hsum<NQ>(row, p, wp) >> 7;
+      lds[(r - r0) * ncols + c] = (int16_t)min(v, (1 << 15) - 1);
+    }
   }
 }
 
-// Horizontal taps with clamped source columns.  Up to 16 taps: unrolled
-// with constant tap indices (weights stay in registers).  More taps (strong
-// downscale) or rows read in place: a loop over wcol.
-template <bool PACKED>
-__device__ __forceinline__ void h_rows_clamped(const uint8_t* rows, int stride, int f, int pw,
-                                               int nr, int tx, const uint32_t* wp,
-                                               const int16_t* wcol, int16_t* out, int ostride) {
-#pragma unroll 1
-  for (int rr = 0; rr < nr; rr++) {
-    const uint8_t* row = rows + (int64_t)rr * stride;
-    int32_t h = 0;
-    if (PACKED) {
-#pragma unroll
-      for (int t = 0; t < 16; t++) {
-        const int32_t wt = (int32_t)(int16_t)(wp[t >> 1] >> ((t & 1) * 16));
-        h += wt * (int32_t)row[min(max(f + t, 0), pw - 1)];
-      }
-    } else {
-      for (int t = 0; t < tx; t++) h += (int32_t)wcol[t] * row[min(max(f + t, 0), pw - 1)];
+// taps beyond 64: a plain loop over the table
+__device__ void hpass_cols_long(const uint8_t* plane, int stride, int ph, const int32_t* pos,
+                                const int16_t* coef, int size, int taps, int c0, int ncols, int r0,
+                                int r1, int16_t* lds, int tid, int nthreads) {
+  for (int c = tid; c < ncols; c += nthreads) {
+    const int x = c0 + c;
+    const int p = pos[x];
+    const int16_t* cf = coef + (int64_t)x * size;
+    for (int r = r0; r < r1; r++) {
+      const uint8_t* row = plane + (int64_t)min(r, ph - 1) * stride + p;
+      int32_t v = 0;
+      for (int t = 0; t < taps; t++) v += (int32_t)row[t] * cf[t];
+      v >>= 7;
+      lds[(r - r0) * ncols + c] = (int16_t)min(v, (1 << 15) - 1);
     }
-    out[rr * ostride] = (int16_t)((h + 128) >> 8);
   }
 }
 
-// One plane of the scaled image, one band of output rows: workgroup =
-// (band, plane, image).  Source rows the band needs are staged in LDS a
-// group at a time (the next group's loads are issued before the current
-// group is filtered); the horizontal taps (one thread per visible column,
-// v_dot2 on int16 pairs) fill an LDS intermediate (Q6 int16), the vertical
-// taps read it ((acc + 2^19) >> 20, clamp) and the band goes out as u8 rows
-// of the resampled plane.  Arithmetic: oracle/jpeg_oracle.c resize_plane.
-__global__ void __launch_bounds__(256) resize_plane_kernel(const uint8_t* __restrict__ planes,
-                                                           const ImageDesc* __restrict__ desc,
-                                                           ImageInfo* __restrict__ infos,
-                                                           const int32_t* __restrict__ pool,
-                                                           uint8_t* __restrict__ rplanes) {
-  __shared__ __attribute__((aligned(16))) uint8_t srcb[kHSrcBytes + 32];
-  __shared__ int16_t tb[kTBuf];
-  __shared__ __attribute__((aligned(16))) int16_t wys[kRMaxRb * kVTaps];
-  __shared__ int32_t fys[kRMaxRb];
-  const int img = blockIdx.z, c = blockIdx.y, tid = threadIdx.x;
+__device__ void hpass(const uint8_t* plane, int stride, int ph, const int32_t* pos,
+                      const int16_t* coef, int size, int taps, int c0, int ncols, int r0, int r1,
+                      int16_t* lds, int tid, int nthreads) {
+  const int nq = (taps + 3) >> 2;
+#define HJ_HP(N) \
+  hpass_cols<N>(plane, stride, ph, pos, coef, size, taps, c0, ncols, r0, r1, lds, tid, nthreads)
+  if (nq <= 1) HJ_HP(1);
+  else if (nq <= 2) HJ_HP(2);
+  else if (nq <= 3) HJ_HP(3);
+  else if (nq <= 4) HJ_HP(4);
+  else if (nq <= 6) HJ_HP(6);
+  else if (nq <= 8) HJ_HP(8);
+  else if (nq <= 12) HJ_HP(12);
+  else if (nq <= 16) HJ_HP(16);
+  else hpass_cols_long(plane, stride, ph, pos, coef, size, taps, c0, ncols, r0, r1, lds, tid, nthreads);
+#undef HJ_HP
+}
+
+__device__ __forceinline__ int clip_i8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+// yuv2rgb.c fill_table / fill_gv_table: the luma-index offset a chroma value
+// adds through the clipping table (the chroma index saturates to [0, 255])
+__device__ __forceinline__ int tab_off(int32_t inc, int c) {
+  return ((clip_i8(c) * inc) >> 16) - (inc >> 9);
+}
+
+// output.c yuv2rgb_write_full (RGB24): 2^22-scaled sums, 30-bit clip
+__device__ __forceinline__ void full_rgb(const BatchParams& p, int Y, int U, int V, int* rgb) {
+  Y -= p.y_offset;
+  Y *= p.y_coeff;
+  Y += 1 << 21;
+  int R = (int)((uint32_t)Y + (uint32_t)V * (uint32_t)p.v2r);
+  int G = (int)((uint32_t)Y + (uint32_t)V * (uint32_t)p.v2g + (uint32_t)U * (uint32_t)p.u2g);
+  int B = (int)((uint32_t)Y + (uint32_t)U * (uint32_t)p.u2b);
+  if ((R | G | B) & 0xC0000000) {
+    auto c30 = [](int a) { return (a & ~((1 << 30) - 1)) ? ((~a) >> 31) & ((1 << 30) - 1) : a; };
+    R = c30(R);
+    G = c30(G);
+    B = c30(B);
+  }
+  rgb[0] = R >> 22;
+  rgb[1] = G >> 22;
+  rgb[2] = B >> 22;
+}
+
+__global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ planes,
+                                                  const ImageDesc* __restrict__ desc,
+                                                  const ImageInfo* __restrict__ infos,
+                                                  const int32_t* __restrict__ pool,
+                                                  void* __restrict__ out, const BatchParams p) {
+  extern __shared__ int16_t sws_lds[];
+  const int img = blockIdx.z, tid = threadIdx.x, nt = blockDim.x;
   const ImageInfo& in = infos[img];
   if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
-  if (c >= dd.ncomp || dd.nvis <= 0 || dd.nvy <= 0) return;
-  const int RB = dd.r_rb[c];
-  const int yb0 = dd.vy0 + (int)blockIdx.x * RB;  // first content row of the band
-  if (yb0 >= dd.vy0 + dd.nvy) return;
-  const int nyb = min(RB, dd.vy0 + dd.nvy - yb0);
-  const PlaneWeights W = plane_weights(dd, pool, c);
-  const int pw = in.comp_w[c], ph = in.comp_hpx[c], stride = dd.plane_stride[c];
-  const int r_lo = min(max(W.fy[yb0], 0), ph - 1);
-  const int r_hi = min(max(W.fy[yb0 + nyb - 1] + W.ty - 1, 0), ph - 1);
-  const int nrows = r_hi - r_lo + 1;
-  const uint8_t* src_plane = planes + dd.plane_off[c];
-  const bool staged = stride <= kHSrcBytes;
-  const int G = h_rows_per_group(stride);
-  uint8_t* rp = rplanes + dd.rp_off + (int64_t)c * dd.nvy * dd.rp_stride;
-  // the band's vertical taps and first rows, once (read by every column)
-  const bool wy_lds = W.ty <= kVTaps;
-  if (wy_lds)
-    for (int i = tid; i < nyb * W.ty; i += 256) wys[i] = W.wy[(int64_t)yb0 * W.ty + i];
-  for (int i = tid; i < nyb; i += 256) fys[i] = W.fy[yb0 + i];
-  for (int cc0 = 0; cc0 < dd.nvis; cc0 += dd.r_cols) {
-    const int ncc = min(dd.r_cols, dd.nvis - cc0);
-    if (nrows * ncc > kTBuf) {  // the host tiling guarantees this fits
-      if (tid == 0) infos[img].status = kErrBadGeometry;
-      return;
-    }
-    // per-thread column state (a thread owns column cc0 + tid)
-    const bool mine = tid < ncc;
-    const int cx = dd.vx0 + cc0 + tid;
-    int f = 0;
-    const int16_t* wcol = nullptr;
-    uint32_t wp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (mine) {
-      f = W.fx[cx];
-      wcol = W.wx + (int64_t)cx * W.tx;
-      if (W.tx <= 16) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const uint32_t w0 = 2 * k < W.tx ? (uint16_t)wcol[2 * k] : 0u;
-          const uint32_t w1 = 2 * k + 1 < W.tx ? (uint16_t)wcol[2 * k + 1] : 0u;
-          wp[k] = w0 | (w1 << 16);
-        }
-      }
-    }
-    const bool interior = staged && W.tx <= 16 && f >= 0 && f + 16 <= pw;
-    // ---- horizontal taps, a group of G source rows at a time ----
-    uint2 pre[4];
-    auto load_group = [&](int g0) {
-      const uint2* s2 = reinterpret_cast<const uint2*>(src_plane + (int64_t)(r_lo + g0) * stride);
-      const int m8 = min(G, nrows - g0) * stride / 8;
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int i = u * 256 + tid;
-        if (i < m8) pre[u] = s2[i];
-      }
-      return m8;
-    };
-    int m8 = staged ? load_group(0) : 0;
-    for (int g0 = 0; g0 < nrows; g0 += G) {
-      const int ng = min(G, nrows - g0);
-      if (staged) {
-        // finish staging this group (the first 4 x 256 uint2 are prefetched)
-        uint2* d2 = reinterpret_cast<uint2*>(srcb);
-        const uint2* s2 = reinterpret_cast<const uint2*>(src_plane + (int64_t)(r_lo + g0) * stride);
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int i = u * 256 + tid;
-          if (i < m8) d2[i] = pre[u];
-        }
-        for (int i = 4 * 256 + tid; i < m8; i += 256) d2[i] = s2[i];
-      }
-      __syncthreads();
-      if (staged && g0 + G < nrows) m8 = load_group(g0 + G);  // overlaps the taps below
-      if (mine) {
-        int16_t* out = tb + g0 * ncc + tid;
-        if (interior) {
-          if (W.tx <= 8) h_rows_dot2<2>(srcb, stride, f, ng, wp, out, ncc);
-          else h_rows_dot2<4>(srcb, stride, f, ng, wp, out, ncc);
-        } else if (staged && W.tx <= 16) {
-          h_rows_clamped<true>(srcb, stride, f, pw, ng, W.tx, wp, wcol, out, ncc);
-        } else if (staged) {
-          h_rows_clamped<false>(srcb, stride, f, pw, ng, W.tx, wp, wcol, out, ncc);
-        } else {
-          h_rows_clamped<false>(src_plane + (int64_t)(r_lo + g0) * stride, stride, f, pw, ng,
-                                W.tx, wp, wcol, out, ncc);
-        }
-      }
-      __syncthreads();
-    }
-    // ---- vertical taps: nyb output rows of this column ----
-    if (mine) {
-      for (int yy = 0; yy < nyb; yy++) {
-        const int y = yb0 + yy;
-        const int fy = fys[yy];
-        const int16_t* w = wy_lds ? wys + yy * W.ty : W.wy + (int64_t)y * W.ty;
-        int32_t acc = 0;
-        if (wy_lds && fy >= 0 && fy + W.ty <= ph) {
-          const int16_t* tcol = tb + (fy - r_lo) * ncc + tid;
-          for (int t = 0; t < W.ty; t += 2) {
-            const uint32_t wpair = *reinterpret_cast<const uint32_t*>(w + t);
-            const uint32_t vpair = (uint32_t)(uint16_t)tcol[t * ncc] |
-                                   ((uint32_t)(uint16_t)tcol[(t + 1) * ncc] << 16);
-            acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, vpair),
-                                         __builtin_bit_cast(hj_short2, wpair), acc, false);
-          }
-        } else {
-          for (int t = 0; t < W.ty; t++) {
-            const int k = min(max(fy + t, 0), ph - 1) - r_lo;
-            acc += (int32_t)w[t] * tb[k * ncc + tid];
-          }
-        }
-        rp[(int64_t)(y - dd.vy0) * dd.rp_stride + cc0 + tid] = clip_u8((acc + (1 << 19)) >> 20);
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// Colour conversion + pad/crop + (normalise) + store, 4 output pixels of a
-// row per thread: resampled planes (u8, visible content only) -> RGB in the
-// caller's layout; pad pixels are black.  Arithmetic: jo_resize_planes.
-__global__ void __launch_bounds__(256) csc_store_kernel(const uint8_t* __restrict__ rplanes,
-                                                        const ImageDesc* __restrict__ desc,
-                                                        const ImageInfo* __restrict__ infos,
-                                                        void* __restrict__ out,
-                                                        const BatchParams p) {
-  const int img = blockIdx.y;
-  const ImageInfo& in = infos[img];
-  if (in.status != kOk) return;
-  const ImageDesc& dd = desc[img];
-  const int ow = dd.ow, oh = dd.oh;
-  const int qpr = (ow + 3) >> 2;  // pixel quads per row
-  const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= qpr * oh) return;
-  const int y = q / qpr, x0 = (q - y * qpr) * 4;
-  const int np = min(4, ow - x0);
+  const SwsDesc& s = dd.sws;
+  const int yo0 = (int)blockIdx.x * s.rb, xo0 = (int)blockIdx.y * s.col_chunk;
+  if (yo0 >= dd.oh || xo0 >= dd.ow) return;
+  const int yo1 = min(yo0 + s.rb, dd.oh), xo1 = min(xo0 + s.col_chunk, dd.ow);
+  // content of this tile in scaled coordinates
+  const int ys0 = max(yo0 - dd.dy, 0), ys1 = min(yo1 - dd.dy, s.sh);
+  const int xs0 = max(xo0 - dd.dx, 0), xs1 = min(xo1 - dd.dx, s.sw);
   const bool planar = p.pix_fmt == 0 || p.pix_fmt == 1;
   const bool swap = p.pix_fmt == 1 || p.pix_fmt == 3;
-  const int cy = y - dd.dy;
-  const int64_t pl = (int64_t)ow * oh;
-  const uint8_t* r0 = rplanes + dd.rp_off + (int64_t)(cy - dd.vy0) * dd.rp_stride;
-  const int64_t ps = (int64_t)dd.nvy * dd.rp_stride;
-  int v[4][3];
+  const int64_t pl = (int64_t)dd.ow * dd.oh;
+  auto store = [&](int xo, int yo, const int* rgb) {
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    int rgb[3] = {0, 0, 0};
-    const int cx = x0 + k - dd.dx;
-    if (k < np && cy >= dd.vy0 && cy < dd.vy0 + dd.nvy && cx >= dd.vx0 && cx < dd.vx0 + dd.nvis) {
-      const int o = cx - dd.vx0;
-      if (dd.ncomp == 1) rgb[0] = rgb[1] = rgb[2] = r0[o];
-      else ycc_rgb(r0[o], r0[ps + o], r0[2 * ps + o], rgb);
-    }
-#pragma unroll
-    for (int ch = 0; ch < 3; ch++) v[k][ch] = rgb[swap ? 2 - ch : ch];
-  }
-  if (p.dtype == 0) {
-    uint8_t* ob = static_cast<uint8_t*>(out) + dd.out_off;
-    if (!planar) {
-      uint8_t* d = ob + ((int64_t)y * ow + x0) * 3;
-      if (np == 4 && (((uintptr_t)d) & 3) == 0) {
-        uint32_t w0 = v[0][0] | (v[0][1] << 8) | (v[0][2] << 16) | (v[1][0] << 24);
-        uint32_t w1 = v[1][1] | (v[1][2] << 8) | (v[2][0] << 16) | (v[2][1] << 24);
-        uint32_t w2 = v[2][2] | (v[3][0] << 8) | (v[3][1] << 16) | (v[3][2] << 24);
-        reinterpret_cast<uint32_t*>(d)[0] = w0;
-        reinterpret_cast<uint32_t*>(d)[1] = w1;
-        reinterpret_cast<uint32_t*>(d)[2] = w2;
+    for (int ch = 0; ch < 3; ch++) {
+      const int v = rgb[swap ? 2 - ch : ch];
+      const int64_t oi =
+          dd.out_off + (planar ? ch * pl + (int64_t)yo * dd.ow + xo : ((int64_t)yo * dd.ow + xo) * 3 + ch);
+      if (p.dtype == 0) {
+        static_cast<uint8_t*>(out)[oi] = (uint8_t)v;
       } else {
-        for (int k = 0; k < np; k++)
-          for (int ch = 0; ch < 3; ch++) d[3 * k + ch] = (uint8_t)v[k][ch];
-      }
-    } else {
-#pragma unroll
-      for (int ch = 0; ch < 3; ch++) {
-        uint8_t* d = ob + ch * pl + (int64_t)y * ow + x0;
-        if (np == 4 && (((uintptr_t)d) & 3) == 0)
-          *reinterpret_cast<uint32_t*>(d) = v[0][ch] | (v[1][ch] << 8) | (v[2][ch] << 16) | (v[3][ch] << 24);
-        else
-          for (int k = 0; k < np; k++) d[k] = (uint8_t)v[k][ch];
+        float f = __fdiv_rn((float)v, 255.0f);
+        f = __fsub_rn(f, p.mean[ch]);
+        f = __fdiv_rn(f, p.std[ch]);
+        static_cast<uint16_t*>(out)[oi] = to_f16_bits(f, p.dtype);
       }
     }
-  } else {
-    uint16_t* ob = static_cast<uint16_t*>(out) + dd.out_off;
-    for (int k = 0; k < np; k++)
-#pragma unroll
-      for (int ch = 0; ch < 3; ch++) {
-        float fv = __fdiv_rn((float)v[k][ch], 255.0f);
-        fv = __fsub_rn(fv, p.mean[ch]);
-        fv = __fdiv_rn(fv, p.std[ch]);
-        const int64_t oi = planar ? ch * pl + (int64_t)y * ow + x0 + k : ((int64_t)y * ow + x0 + k) * 3 + ch;
-        ob[oi] = to_f16_bits(fv, p.dtype);
+  };
+  // pad: output pixels of the tile outside the scaled image are black
+  {
+    const int tw = xo1 - xo0, npx = (yo1 - yo0) * tw;
+    const int zero[3] = {0, 0, 0};
+    for (int i = tid; i < npx; i += nt) {
+      const int yo = yo0 + i / tw, xo = xo0 + i % tw;
+      const int ys = yo - dd.dy, xs = xo - dd.dx;
+      if (ys < 0 || ys >= s.sh || xs < 0 || xs >= s.sw) store(xo, yo, zero);
+    }
+  }
+  if (ys0 >= ys1 || xs0 >= xs1) return;
+  const int32_t* T = pool + dd.wt_off;
+  const int32_t* vl_pos = T + s.off[kVlPos];
+  const int16_t* vl_coef = reinterpret_cast<const int16_t*>(T + s.off[kVlCoef]);
+  const int32_t* vmode = T + s.off[kVmode];
+  const int lr0 = vl_pos[ys0], lr1 = vl_pos[ys1 - 1] + s.vl_taps;
+  const int ncl = xs1 - xs0;
+  int16_t* hl = sws_lds;
+  hpass(planes + dd.plane_off[0], dd.plane_stride[0], in.comp_hpx[0], T + s.off[kHlPos],
+        reinterpret_cast<const int16_t*>(T + s.off[kHlCoef]), s.hl_size, s.hl_taps, xs0, ncl, lr0,
+        lr1, hl, tid, nt);
+  int cr0 = 0, cx0 = 0, ncc = 0;
+  int16_t *hu = nullptr, *hv = nullptr;
+  const int32_t* vc_pos = T + s.off[kVcPos];
+  const int16_t* vc_coef = reinterpret_cast<const int16_t*>(T + s.off[kVcCoef]);
+  if (!s.gray) {
+    cr0 = vc_pos[ys0];
+    const int cr1 = vc_pos[ys1 - 1] + s.vc_taps;
+    cx0 = s.full ? xs0 : xs0 >> 1;
+    ncc = (s.full ? xs1 - 1 : (xs1 - 1) >> 1) + 1 - cx0;
+    hu = hl + (lr1 - lr0) * ncl;
+    hv = hu + (cr1 - cr0) * ncc;
+    const int32_t* hc_pos = T + s.off[kHcPos];
+    const int16_t* hc_coef = reinterpret_cast<const int16_t*>(T + s.off[kHcCoef]);
+    // the two chroma planes share the tables: threads split over both
+    const int half = nt >> 1, t2 = tid < half ? tid : tid - half;
+    const int c = tid < half ? 1 : 2;
+    hpass(planes + dd.plane_off[c], dd.plane_stride[c], in.comp_hpx[c], hc_pos, hc_coef, s.hc_size,
+          s.hc_taps, cx0, ncc, cr0, cr1, c == 1 ? hu : hv, t2, half);
+  }
+  __syncthreads();
+  // vertical taps + RGB24 writer, one output column per thread
+  for (int cl = tid; cl < ncl; cl += nt) {
+    const int xs = xs0 + cl;
+    const int cc = (s.full ? xs : xs >> 1) - cx0;
+    for (int ys = ys0; ys < ys1; ys++) {
+      const int m = vmode[ys];
+      const int mode = m & 15, ya = (m >> 4) & 8191, ua = (m >> 17) & 8191;
+      const int lp = vl_pos[ys] - lr0;
+      const int16_t* lf = vl_coef + (int64_t)ys * s.vl_size;
+      const int16_t* lcol = hl + lp * ncl + cl;
+      int rgb[3];
+      int Y, U = 0, V = 0;
+      int cp = 0;
+      const int16_t* cf = nullptr;
+      if (!s.gray) {
+        cp = vc_pos[ys] - cr0;
+        cf = vc_coef + (int64_t)ys * s.vc_size;
       }
+      if (s.full) {
+        if (mode == kSwsTwo) {
+          Y = ((int)lcol[0] * (4096 - ya) + (int)lcol[ncl] * ya) >> 10;
+        } else if (mode == kSwsOne) {
+          Y = (int)lcol[0] * 4;
+        } else {
+          Y = 1 << 9;
+          for (int j = 0; j < s.vl_taps; j++) Y += (int)lcol[j * ncl] * lf[j];
+          Y >>= 10;
+        }
+        if (!s.gray) {
+          const int16_t* ucol = hu + cp * ncc + cc;
+          const int16_t* vcol = hv + cp * ncc + cc;
+          if (mode == kSwsX) {
+            U = (1 << 9) - (128 << 19);
+            V = (1 << 9) - (128 << 19);
+            for (int j = 0; j < s.vc_taps; j++) {
+              U += (int)ucol[j * ncc] * cf[j];
+              V += (int)vcol[j * ncc] * cf[j];
+            }
+            U >>= 10;
+            V >>= 10;
+          } else {
+            const int o1 = ua ? ncc : 0;
+            U = ((int)ucol[0] * (4096 - ua) + (int)ucol[o1] * ua - (128 << 19)) >> 10;
+            V = ((int)vcol[0] * (4096 - ua) + (int)vcol[o1] * ua - (128 << 19)) >> 10;
+          }
+        }
+        full_rgb(p, Y, U, V, rgb);
+      } else {
+        const int16_t* ucol = hu + cp * ncc + cc;
+        const int16_t* vcol = hv + cp * ncc + cc;
+        if (mode == kSwsX) {
+          Y = 1 << 18;
+          U = 1 << 18;
+          V = 1 << 18;
+          for (int j = 0; j < s.vl_taps; j++) Y += (int)lcol[j * ncl] * lf[j];
+          for (int j = 0; j < s.vc_taps; j++) {
+            U += (int)ucol[j * ncc] * cf[j];
+            V += (int)vcol[j * ncc] * cf[j];
+          }
+          Y >>= 19;
+          U >>= 19;
+          V >>= 19;
+        } else if (mode == kSwsTwo) {
+          Y = ((int)lcol[0] * (4096 - ya) + (int)lcol[ncl] * ya) >> 19;
+          U = ((int)ucol[0] * (4096 - ua) + (int)ucol[ncc] * ua) >> 19;
+          V = ((int)vcol[0] * (4096 - ua) + (int)vcol[ncc] * ua) >> 19;
+        } else {
+          const int o1 = ua ? ncc : 0;
+          Y = ((int)lcol[0] + 64) >> 7;
+          U = ((int)ucol[0] * (4096 - ua) + (int)ucol[o1] * ua + (128 << 11)) >> 19;
+          V = ((int)vcol[0] * (4096 - ua) + (int)vcol[o1] * ua + (128 << 11)) >> 19;
+        }
+        rgb[0] = clip_i8(Y + tab_off(p.crv, V));
+        rgb[1] = clip_i8(Y + tab_off(p.cgu, U) + tab_off(p.cgv, V));
+        rgb[2] = clip_i8(Y + tab_off(p.cbu, U));
+      }
+      store(xs + dd.dx, ys + dd.dy, rgb);
+    }
   }
 }
 
@@ -2061,12 +1931,6 @@ hipError_t launch_idct(const int16_t* coefs, const ImageDesc* desc, const ImageI
     hipLaunchKernelGGL(idct_kernel<0>, grid, dim3(256), 0, st, coefs, desc, infos, planes);
   return hipGetLastError();
 }
-hipError_t launch_weights(const ImageDesc* desc, const ImageInfo* infos, int32_t* pool,
-                          int filter, int max_len, int n, hipStream_t st) {
-  dim3 grid((max_len + 255) / 256, 6, n);
-  hipLaunchKernelGGL(weights_kernel, grid, dim3(256), 0, st, desc, infos, pool, filter);
-  return hipGetLastError();
-}
 hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
                       void* out, const BatchParams& p, int64_t max_px, int n, hipStream_t st) {
   int64_t gx64 = (max_px + 255) / 256;
@@ -2134,13 +1998,11 @@ hipError_t launch_nv12(const uint8_t* src, uint8_t* dst, int frames, int height,
   return hipGetLastError();
 }
 
-hipError_t launch_resize(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
-                         const int32_t* pool, uint8_t* rplanes, void* out, const BatchParams& p,
-                         int64_t max_bands, int64_t max_quads, int n, hipStream_t st) {
-  hipLaunchKernelGGL(resize_plane_kernel, dim3((int)max_bands, kMaxComp, n), dim3(256), 0, st,
-                     planes, desc, const_cast<ImageInfo*>(infos), pool, rplanes);
-  hipLaunchKernelGGL(csc_store_kernel, dim3((int)((max_quads + 255) / 256), n), dim3(256), 0, st,
-                     rplanes, desc, infos, out, p);
+hipError_t launch_sws(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
+                      const int32_t* pool, void* out, const BatchParams& p, int bands, int chunks,
+                      int lds_bytes, int n, hipStream_t st) {
+  hipLaunchKernelGGL(sws_kernel, dim3(bands, chunks, n), dim3(256), lds_bytes, st, planes, desc,
+                     infos, pool, out, p);
   return hipGetLastError();
 }
 hipError_t launch_planes_copy(const uint8_t* planes, const ImageDesc* desc,

@@ -185,11 +185,32 @@ def load_image_batch(
         filter_desc = get_video_filter_desc(
             scale_width=width, scale_height=height, pix_fmt=pix_fmt
         )
+    cfg = device_config or CUDAConfig(0)
+    if filter_desc is None:
+        # no scale and no output format: the decoder's own planes, batched as
+        # the reference's convert_frames stacks them ([B, 3, H, W] yuvj444p,
+        # [B, 1, 1.5H, W] yuvj420p, [B, H, W, 1] gray; same size and format)
+        dec = _lib.thread_decoder(cfg.device_index)
+        arrs = []
+        for i, s in enumerate(srcs):
+            try:
+                arrs.append(_native_planes(dec.decode_planes(_read(s), stream=_stream(cfg))))
+            except Exception as err:  # reference: log, skip, raise later if strict
+                _LG.error("Failed to load image %d: %s", i, err)
+        if strict and len(arrs) != len(srcs):
+            raise RuntimeError("Failed to load some images.")
+        if not arrs:
+            raise RuntimeError("Failed to load all the images.")
+        if any(a.shape != arrs[0].shape for a in arrs):
+            raise RuntimeError("The input images must have the same size and pixel format.")
+        arr = np.stack(arrs)
+        if device_config is not None:
+            return CUDABuffer(torch.from_numpy(arr).to(f"cuda:{cfg.device_index}"))
+        return CPUBuffer(arr)
     out = parse_image_filter(filter_desc, default_pix_fmt=pix_fmt or "rgb24")
     if normalize:
         out = Output(**{**out.__dict__, "normalize": True, "mean": tuple(mean),
                         "std": tuple(std), "norm_dtype": norm_dtype})
-    cfg = device_config or CUDAConfig(0)
     datas, keep = [], []
     for i, s in enumerate(srcs):
         try:
@@ -230,6 +251,36 @@ def load_image_batch(
     return buf
 
 
+def _native_planes(planes: list) -> np.ndarray:
+    """The buffer the reference's convert_frames makes of an unfiltered
+    frame (src/libspdl/core/detail/ffmpeg/conversion.cpp:172-303,411-454,
+    single-frame form conversion.h:45-53): av_image_copy_to_buffer packs Y,
+    then all of U, then all of V, each plane tightly, into
+      gray8     [H, W, 1]        (convert_interleaved)
+      yuvj444p  [3, H, W]        (convert_planer)
+      yuvj420p  [1, H + H/2, W]  (convert_yuv420p)
+      yuvj422p  [1, 2H, W]       (convert_yuv422p)
+    A frame whose planes do not fit that shape (odd 4:2:0 / 4:2:2 sizes)
+    fails the copy there ("Failed to copy image data."); other samplings
+    (yuvj440p, yuvj411p) are "Unsupported pixel format"."""
+    if len(planes) == 1:
+        return np.ascontiguousarray(planes[0])[:, :, None]
+    (H, W), (ch, cw) = planes[0].shape, planes[1].shape
+    flat = np.concatenate([np.ascontiguousarray(p).reshape(-1) for p in planes])
+    if (ch, cw) == (H, W):
+        return flat.reshape(3, H, W)
+    if cw == (W + 1) // 2 and ch == (H + 1) // 2:
+        shape = (1, H + H // 2, W)
+    elif cw == (W + 1) // 2 and ch == H:
+        shape = (1, 2 * H, W)
+    else:
+        raise RuntimeError(
+            f"Unsupported pixel format: chroma {cw}x{ch} for a {W}x{H} image")
+    if flat.size != shape[1] * shape[2]:
+        raise RuntimeError("Failed to copy image data.")
+    return flat.reshape(shape)
+
+
 def load_image(
     src,
     *,
@@ -238,9 +289,11 @@ def load_image(
     pix_fmt: str = "rgb24",
     **kwargs,
 ):
-    """Single image.  ``filter_desc=None`` returns the raw decoded planes
-    (yuvj4xxp, ``[1, 1.5H, W]`` for 4:2:0 like the reference's
-    convert_frames of an unfiltered frame); otherwise RGB per the filter."""
+    """Single image.  ``filter_desc=None`` returns the decoded planes in the
+    layout of the reference's convert_frames of an unfiltered frame (Y, U, V
+    back to back: ``[1, 1.5H, W]`` yuvj420p, ``[1, 2H, W]`` yuvj422p,
+    ``[3, H, W]`` yuvj444p, ``[H, W, 1]`` gray; see :func:`_native_planes`);
+    otherwise RGB per the filter."""
     for k in ("demux_config", "decode_config", "name"):
         kwargs.pop(k, None)
     if kwargs:
@@ -249,17 +302,7 @@ def load_image(
     data = _read(src)
     if filter_desc is None:
         dec = _lib.thread_decoder(cfg.device_index)
-        planes = dec.decode_planes(data, stream=_stream(cfg))
-        if len(planes) == 3 and planes[1].shape[1] * 2 == planes[0].shape[1] and (
-                planes[1].shape[0] * 2 == planes[0].shape[0]):
-            H, W = planes[0].shape
-            arr = np.concatenate(
-                [planes[0], np.concatenate([planes[1], planes[2]], axis=1)], axis=0
-            ).reshape(1, H * 3 // 2, W)
-        elif len(planes) == 1:
-            arr = planes[0][None]
-        else:  # 4:4:4 / 4:2:2: stacked planes
-            arr = np.concatenate([p.reshape(1, -1) for p in planes], axis=1)
+        arr = _native_planes(dec.decode_planes(data, stream=_stream(cfg)))
         if device_config is not None:
             return CUDABuffer(torch.from_numpy(arr).to(f"cuda:{cfg.device_index}"))
         return CPUBuffer(arr)

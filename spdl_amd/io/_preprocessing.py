@@ -17,6 +17,16 @@ _FILTERS = {"bicubic": "bicubic", "bilinear": "bilinear", "fast_bilinear": "bili
             "lanczos": "lanczos"}
 
 
+# scale_mode -> scale's force_original_aspect_ratio and the filter that
+# brings the fitted image to the requested box
+_FIT = {None: (None, None), "pad": ("decrease", "pad"), "crop": ("increase", "crop")}
+
+
+def _node(name: str, **opts) -> str:
+    """One filter of an FFmpeg chain: ``name=k1=v1:k2=v2``."""
+    return name + "=" + ":".join(f"{k}={v}" for k, v in opts.items())
+
+
 def get_video_filter_desc(
     *,
     scale_width: int | None = None,
@@ -30,39 +40,34 @@ def get_video_filter_desc(
     filter_desc: str | None = None,
     **unsupported: object,
 ) -> str | None:
-    """Same output as the reference for the image arguments."""
-    for k, v in unsupported.items():
-        if v is not None:
-            raise ValueError(f"`{k}` is not supported by the image path")
-    parts = []
-    if scale_width is not None or scale_height is not None:
-        w = scale_width or 0
-        h = scale_height or 0
-        scale = [f"{w=}", f"{h=}", f"flags={scale_algo}"]
-        if scale_mode is None:
-            parts.append(f"scale={':'.join(scale)}")
-        elif scale_mode == "pad":
-            scale.append("force_original_aspect_ratio=decrease")
-            parts.append(f"scale={':'.join(scale)}")
-            parts.append(f"pad={w=}:{h=}:x=-1:y=-1:color={pad_mode or 'black'}")
-        elif scale_mode == "crop":
-            scale.append("force_original_aspect_ratio=increase")
-            parts.append(f"scale={':'.join(scale)}")
-            parts.append(f"crop={w=}:{h=}")
-        else:
-            raise ValueError(
-                f"Unexpected `scale_mode` value ({scale_mode}). "
-                'Expected values are "pad", "crop", or None.'
-            )
-    if crop_width is not None or crop_height is not None:
-        parts.append(f"crop=w={crop_width or 0}:h={crop_height or 0}")
+    """The filter chain the reference builds for these image arguments
+    (src/spdl/io/_preprocessing.py:122-254; byte-for-byte, pinned by
+    tests/golden/filter_desc.json): optional scale (+ pad / crop to the box),
+    optional centre crop, a caller chain, then the output pixel format."""
+    extra = sorted(k for k, v in unsupported.items() if v is not None)
+    if extra:
+        raise ValueError(f"image filter arguments not supported here: {extra}")
+    if scale_mode not in _FIT:
+        raise ValueError(f"scale_mode must be 'pad', 'crop' or None, got {scale_mode!r}")
+    chain: list[str] = []
+    if (scale_width, scale_height) != (None, None):
+        box = {"w": scale_width or 0, "h": scale_height or 0}
+        ratio, follow = _FIT[scale_mode]
+        scale = {**box, "flags": scale_algo}
+        if ratio:
+            scale["force_original_aspect_ratio"] = ratio
+        chain.append(_node("scale", **scale))
+        if follow == "pad":
+            chain.append(_node("pad", **box, x=-1, y=-1, color=pad_mode or "black"))
+        elif follow == "crop":
+            chain.append(_node("crop", **box))
+    if (crop_width, crop_height) != (None, None):
+        chain.append(_node("crop", w=crop_width or 0, h=crop_height or 0))
     if filter_desc is not None:
-        parts.append(filter_desc)
+        chain.append(filter_desc)
     if pix_fmt is not None:
-        parts.append(f"format=pix_fmts={pix_fmt}")
-    if parts:
-        return ",".join(parts)
-    return None
+        chain.append(_node("format", pix_fmts=pix_fmt))
+    return ",".join(chain) or None
 
 
 def _kv(args: str) -> dict:

@@ -58,3 +58,17 @@ def synthetic_batch(n: int, distinct: int = 32, **kw) -> list[bytes]:
     """n JPEGs cycling through `distinct` seeded images."""
     base = [synthetic_jpeg(1000 + i, **kw) for i in range(min(n, distinct))]
     return [base[i % len(base)] for i in range(n)]
+
+
+def synthetic_slice(indices, distinct: int = 32, **kw) -> list[bytes]:
+    """Images ``indices`` of the global synthetic dataset whose image i is
+    ``synthetic_batch``'s image i (seed 1000 + i % distinct): one rank's slice
+    of a global batch (BASELINE configs[2]: 2048 -> 8 x 256)."""
+    cache: dict[int, bytes] = {}
+    out = []
+    for i in indices:
+        k = int(i) % distinct
+        if k not in cache:
+            cache[k] = synthetic_jpeg(1000 + k, **kw)
+        out.append(cache[k])
+    return out

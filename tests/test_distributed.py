@@ -65,3 +65,49 @@ def test_two_rank_gloo_sharding():
         assert t == 2.0
         flat = sorted(sum(gathered, []))
         assert flat == list(range(100))
+
+
+def _last_json(out: str) -> dict:
+    import json
+
+    for line in reversed(out.strip().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError(f"no JSON line in output:\n{out}")
+
+
+@pytest.mark.parametrize("launcher", ["self", "torchrun"])
+def test_bench_launcher_spawns_ranks(launcher):
+    """`python bench.py --gpus 2` starts two rank processes itself (the
+    reference's examples/image_dataloading.py:291-317 one-worker-per-GPU
+    launch), and under torch.distributed.run it joins the launched ranks;
+    either way each rank gets a disjoint contiguous slice of the global
+    batch (2048 -> 2 x 1024) and the reported time is the MAX over ranks
+    (rank 1 sleeps twice as long as rank 0).  CPU-only (--dry-run, gloo)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = ["bench.py", "--gpus", "2", "--dry-run", "--batch", "1024"]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+               "2", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
+    else:
+        cmd = [sys.executable, *args]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = _last_json(r.stdout)
+    assert rec["n_gpus"] == 2 and rec["global_batch"] == 2048
+    assert rec["slices"] == [[0, 1024], [1024, 2048]]
+    assert rec["elapsed"] >= 0.1  # rank 1's 2 x 50 ms, not rank 0's 50 ms
+
+
+def test_bench_rejects_mismatched_world():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--dry-run"], cwd=root,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)

@@ -53,7 +53,8 @@ def test_islow_matches_libjpeg_fixture(decoder, oracle, name):
     if oracle.ljpin() is None:
         pytest.skip("libjpeg 9 not available on this host")
     info = oracle.parse(d)
-    hyp = _decode(decoder, [d], Output(pix_fmt="rgb24", idct="islow"), (info.height, info.width, 3))
+    hyp = _decode(decoder, [d], Output(pix_fmt="rgb24", idct="islow", csc="jfif"),
+                  (info.height, info.width, 3))
     ref = oracle.lj_decode_rgb(d)
     np.testing.assert_array_equal(hyp[0].numpy(), ref, strict=True)
 

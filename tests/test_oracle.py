@@ -36,7 +36,7 @@ def test_islow_pipeline_matches_libjpeg(oracle, name):
     """IDCT islow + nearest chroma + JFIF integer CSC: bit-exact vs libjpeg 9d
     (dct_method=JDCT_ISLOW, do_fancy_upsampling=FALSE)."""
     ref = np.load(os.path.join(GOLD, name + ".libjpeg.npz"))["rgb_islow"]
-    hyp = oracle.decode_rgb(_jpeg(name), oracle.IDCT_ISLOW, "rgb24")
+    hyp = oracle.decode_rgb(_jpeg(name), oracle.IDCT_ISLOW, "rgb24", csc="jfif")
     np.testing.assert_array_equal(hyp, ref, strict=True)
 
 
@@ -166,13 +166,6 @@ def test_geometry_ffmpeg_semantics(oracle, w, h, kw, expect):
     assert oracle.geometry(w, h, oracle.Resize(**kw)) == expect
 
 
-def test_resize_weights_sum_and_identity(oracle):
-    first, w = oracle.axis_weights(640, 224)
-    assert (w.astype(np.int32).sum(axis=1) == 16384).all()
-    first, w = oracle.axis_weights(100, 100)
-    assert (w.max(axis=1) == 16384).all()  # identity at scale 1
-
-
 def test_filter_desc_strings_match_reference():
     """Our filter-string builder reproduces the reference's
     get_video_filter_desc (fixture generated by importing the reference)."""
@@ -215,45 +208,156 @@ def test_bf16_rounding_matches_torch(oracle):
     np.testing.assert_array_equal(hyp, ref)
 
 
-def _lanczos3(x):
-    x = np.abs(np.asarray(x, dtype=np.float64))
-    with np.errstate(invalid="ignore", divide="ignore"):
-        v = 3.0 * np.sin(np.pi * x) * np.sin(np.pi * x / 3.0) / (np.pi ** 2 * x * x)
-    return np.where(x == 0, 1.0, np.where(x < 3.0, v, 0.0))
+# ---- libswscale restatement (oracle/sws_oracle.c) ---------------------------
 
 
-@pytest.mark.parametrize("src,dst", [(640, 224), (480, 168), (320, 224), (333, 256), (100, 700),
-                                     (1920, 224), (8, 8)])
-def test_lanczos_weights_follow_the_formula(oracle, src, dst):
-    """Lanczos-3 taps (NPP NPPI_INTER_LANCZOS / swscale flags=lanczos kernel):
-    the float-polynomial evaluation the GPU shares, quantised to Q14, stays
-    within one LSB of the float64 taps from sin() (bar the tap that absorbs
-    the rounding residual)."""
-    first, w = oracle.axis_weights(src, dst, "lanczos")
-    scale = src / dst
-    fs = max(scale, 1.0)
+def _keys(x, a=-0.6):
+    """Keys cubic: Mitchell-Netravali with B = 0, C = 0.6 (swscale's default
+    SWS_BICUBIC parameters), in float64."""
+    x = np.abs(np.asarray(x, np.float64))
+    return np.where(x < 1, (a + 2) * x ** 3 - (a + 3) * x ** 2 + 1,
+                    np.where(x < 2, a * x ** 3 - 5 * a * x ** 2 + 8 * a * x - 4 * a, 0.0))
+
+
+@pytest.mark.parametrize("src,dst,align,one", [
+    (640, 224, 4, 1 << 14), (480, 168, 2, 1 << 12), (320, 112, 4, 1 << 14), (240, 168, 2, 1 << 12),
+    (1920, 224, 4, 1 << 14), (167, 333, 4, 1 << 14), (114, 227, 2, 1 << 12), (1, 224, 4, 1 << 14),
+    (100, 100, 4, 1 << 14), (100, 100, 2, 1 << 12)])
+@pytest.mark.parametrize("filt", ["bicubic", "bilinear", "lanczos"])
+def test_sws_filter_invariants(oracle, src, dst, align, one, filt):
+    """initFilter's output contract: every row sums to `one` (the
+    error-diffusing normalisation), positions are non-decreasing and keep
+    every non-zero tap inside the source, sizes are aligned (x86: 4
+    horizontal, 2 vertical, unpadded when unscaled), unscaled is identity."""
+    pos, coef = oracle.sws_axis(src, dst, filt, align, one)
+    size = coef.shape[1]
+    assert (coef.astype(np.int64).sum(axis=1) == one).all()
+    assert (np.diff(pos) >= 0).all() and pos.min() >= 0
     for i in range(dst):
-        c = (i + 0.5) * scale - 0.5
-        n = int(np.floor(c + 3 * fs)) - int(np.ceil(c - 3 * fs)) + 1
-        lo = int(first[i])
-        wf = _lanczos3((np.arange(lo, lo + n) - c) / fs)
-        ref = wf / wf.sum() * 16384.0
-        got = w[i, :n].astype(np.float64)
-        assert got.sum() == 16384
-        # every tap rounds to nearest; the largest one also takes the
-        # rounding residual that makes the taps sum to 16384
-        err = np.abs(got - ref)
-        # (float vs float64 evaluation may flip a tap that sits at x.5)
-        assert (err > 1.01).sum() <= 1 and err.max() <= 0.5 * n + 1.01, (i, err)
-        assert not w[i, n:].any()
+        nz = np.nonzero(coef[i])[0]
+        assert pos[i] + nz.max() < max(src, 1)
+    if src == dst:  # horizontal filters stay padded to 4 on x86
+        assert size == (4 if align == 4 else 1)
+        dense = np.zeros((dst, src), np.int64)
+        for i in range(dst):
+            dense[i, pos[i]:pos[i] + size] += coef[i]
+        np.testing.assert_array_equal(dense, np.eye(dst, dtype=np.int64) * one)
+    else:
+        assert size % align == 0
 
 
-def test_lanczos_resize_close_to_bicubic(oracle):
-    """Sanity: Lanczos-3 and bicubic resamplings of the same picture agree to
-    a few levels (both are interpolating, antialiased kernels)."""
-    d = _jpeg("q90_444")
-    kw = dict(fit_w=160, fit_h=120)
-    a = oracle.decode_resize(d, oracle.Resize(filter="lanczos", **kw), "rgb24").astype(int)
-    b = oracle.decode_resize(d, oracle.Resize(filter="bicubic", **kw), "rgb24").astype(int)
-    assert a.shape == b.shape == (120, 160, 3)
-    assert np.abs(a - b).mean() < 2.0 and (a != b).any()
+@pytest.mark.parametrize("src,dst", [(640, 224), (480, 168), (320, 112), (1920, 224)])
+def test_sws_bicubic_taps_follow_the_kernel(oracle, src, dst):
+    """Interior rows of the fixed-point bicubic filter equal the float64
+    Keys(-0.6) kernel, widened by the downscale factor and normalised, to
+    within 2 LSB of 1<<14 (the int64 coefficient arithmetic and rounding
+    residual are the only differences)."""
+    pos, coef = oracle.sws_axis(src, dst, "bicubic")
+    s = ((src << 16) + dst // 2) // dst / 65536.0
+    for i in range(4, dst - 4):
+        c = (i + 0.5) * s - 0.5
+        idx = pos[i] + np.arange(coef.shape[1])
+        w = _keys((idx - c) / s)
+        ref = w / w.sum() * (1 << 14)
+        assert np.abs(coef[i] - ref).max() <= 2.0, (i, coef[i], np.rint(ref))
+
+
+def _float_swscale(planes, sw, sh):
+    """Independent float64 model of the scale path swscale runs for a
+    yuvj420p frame -> rgb24 (bicubic, centred chroma siting, half-width
+    chroma shared by pixel pairs, BT.601 full-range matrix, round)."""
+    Y, U, V = [p.astype(np.float64) for p in planes]
+    H, W = Y.shape
+
+    def res(p, n_out, axis, s, off=0.0):
+        f = max(s, 1.0)
+        out = []
+        for i in range(n_out):
+            c = (i + 0.5) * s - 0.5 + off
+            idx = np.arange(int(np.floor(c - 2 * f)), int(np.ceil(c + 2 * f)) + 1)
+            w = _keys((idx - c) / f)
+            out.append(np.tensordot(w / w.sum(), np.take(p, np.clip(idx, 0, p.shape[axis] - 1),
+                                                         axis=axis), axes=([0], [axis])))
+        return np.stack(out, axis=axis)
+
+    inc = lambda a, b: ((a << 16) + b // 2) // b / 65536.0  # noqa: E731
+    Yr = res(res(Y, sw, 1, inc(W, sw)), sh, 0, inc(H, sh))
+    cw, ch = U.shape[1], U.shape[0]
+
+    def chroma(P):
+        h = res(P, sw // 2, 1, inc(cw, sw // 2))
+        # output row y (luma grid, centre 128) -> chroma rows (centre 128 at half res)
+        s = inc(ch, sh)
+        return np.repeat(res(h, sh, 0, s), 2, axis=1)
+
+    Ur, Vr = chroma(U) - 128, chroma(V) - 128
+    rgb = np.stack([Yr + 1.402 * Vr, Yr - 0.344136 * Ur - 0.714136 * Vr, Yr + 1.772 * Ur], -1)
+    return np.clip(np.rint(rgb), 0, 255)
+
+
+@pytest.mark.parametrize("name", ["q90_420", "odd_227x333"])
+def test_sws_resize_matches_float_model(oracle, name):
+    """The fixed-point restatement agrees with a float64 statement of the same
+    algorithm to within 2 levels (fixed-point taps, 15-bit intermediates and
+    the table CSC's truncations)."""
+    from tests import cases
+
+    d = cases.case(name)
+    planes = oracle.decode_planes(d)
+    info = oracle.parse(d)
+    rs = oracle.Resize(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224)
+    g = oracle.geometry(info.width, info.height, rs)
+    hyp = oracle.decode_resize(d, rs, "rgb24").astype(int)
+    hyp = hyp[g["dy"]:g["dy"] + g["sh"], g["dx"]:g["dx"] + g["sw"]]
+    ref = _float_swscale(planes, g["sw"], g["sh"])
+    # the first chroma rows/cols see swscale's truncating window start
+    diff = np.abs(hyp - ref)[4:-4, 4:-4]
+    assert diff.max() <= 2 and diff.mean() < 0.8, (diff.max(), diff.mean())
+
+
+def test_sws_unscaled_420_is_nearest_chroma_tables(oracle):
+    """Same-size yuvj420p -> rgb24 (even size) is the unscaled converter:
+    nearest chroma through the yuv2rgb tables, within 2 of the JFIF (IJG)
+    conversion of the same planes and exactly R = G = B = Y for gray."""
+    from tests import cases
+
+    d = cases.case("q90_420")
+    a = oracle.decode_rgb(d).astype(int)
+    b = oracle.decode_rgb(d, csc="jfif").astype(int)
+    assert np.abs(a - b).max() <= 2
+    g = cases.case("gray")
+    rgb = oracle.decode_rgb(g)
+    (y,) = oracle.decode_planes(g)
+    for ch in range(3):
+        np.testing.assert_array_equal(rgb[..., ch], y)
+
+
+def _edge_jpeg(subsampling=2, quality=95):
+    """A 96x64 JPEG of three 32-px pure red / green / blue columns -- the
+    reference's edge-value sample (ffmpeg lavfi color=0xff0000|0x00ff00|
+    0x0000ff, hstack, tests/io/image_decoding_test.py:130-166), encoded by
+    Pillow here (no ffmpeg CLI)."""
+    import io as _io
+
+    from PIL import Image
+
+    px = np.zeros((64, 96, 3), np.uint8)
+    px[:, :32, 0] = 255
+    px[:, 32:64, 1] = 255
+    px[:, 64:, 2] = 255
+    b = _io.BytesIO()
+    Image.fromarray(px).save(b, "JPEG", quality=quality, subsampling=subsampling)
+    return b.getvalue()
+
+
+def check_edge_values(hyp):
+    """The reference's assertions (image_decoding_test.py:154-166)."""
+    red, green, blue = hyp[:, :32], hyp[:, 32:64], hyp[:, 64:]
+    assert np.all(red[..., 0] >= 254) and np.all(red[..., 1] <= 1) and np.all(red[..., 2] == 0)
+    assert np.all(green[..., 0] == 0) and np.all(green[..., 1] >= 253)
+    assert np.all(green[..., 2] <= 1)
+    assert np.all(blue[..., 0] <= 1) and np.all(blue[..., 1] <= 1) and np.all(blue[..., 2] >= 254)
+
+
+def test_edge_values_oracle(oracle):
+    check_edge_values(oracle.decode_rgb(_edge_jpeg()))
