@@ -8,6 +8,7 @@
 // hipMemcpyAsync from pinned staging.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -180,6 +181,33 @@ class CopyPool {
   bool stop_ = false;
 };
 
+// Copier threads per context: the host cores this process may use (affinity,
+// capped by a cgroup v2 CPU quota) shared among the ranks of this node
+// (LOCAL_WORLD_SIZE), at most 8 with the caller; SPDL_HJ_COPY_THREADS
+// overrides.  8 ranks x 8 copiers would oversubscribe a 16-core share.
+int copy_workers() {
+  if (const char* e = getenv("SPDL_HJ_COPY_THREADS")) {
+    const int v = atoi(e);
+    return v < 1 ? 0 : (v > 16 ? 15 : v - 1);
+  }
+  int cores = (int)sysconf(_SC_NPROCESSORS_ONLN);
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) cores = CPU_COUNT(&set);
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long per = 0;
+    if (fscanf(f, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+      const long long c = atoll(q) / per;
+      if (c >= 1 && c < cores) cores = (int)c;
+    }
+    fclose(f);
+  }
+  int ranks = 1;
+  if (const char* e = getenv("LOCAL_WORLD_SIZE")) ranks = atoi(e) > 0 ? atoi(e) : 1;
+  const int share = cores / ranks;
+  return share <= 1 ? 0 : (share - 1 > 7 ? 7 : share - 1);
+}
+
 // Copy n items of (dst_off, src, len) into `base`, zero-filling each item's
 // tail [len, padded) -- split by bytes over the pool when the total is large.
 struct CopyItem {
@@ -207,7 +235,7 @@ void parallel_pack(CopyPool* pool, uint8_t* base, const std::vector<CopyItem>& i
       if (e > zs) memset(base + it.dst_off + zs, 0, (size_t)(e - zs));
     }
   };
-  if (!pool || total < (4 << 20)) body(0, 1);
+  if (!pool || pool->workers() < 2 || total < (4 << 20)) body(0, 1);
   else pool->run(body);
 }
 
@@ -922,7 +950,7 @@ spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen) {
     spdl_hj_destroy(c);
     return nullptr;
   }
-  c->pool = new CopyPool(7);  // + the calling thread: 8 copiers
+  c->pool = new CopyPool(copy_workers());  // + the calling thread
   return c;
 }
 
@@ -1114,7 +1142,7 @@ int spdl_hj_staging_read(spdl_hj_ctx* ctx, int64_t ticket, size_t dst_off, int f
       lo += (size_t)r;
     }
   };
-  if (len < (4u << 20)) body(0, 1);
+  if (len < (4u << 20) || ctx->pool->workers() < 2) body(0, 1);
   else ctx->pool->run(body);
   if (bad) {
     set_err(err, errlen, "pread failed or hit end of file (offset %lld, %zu bytes)",

@@ -168,65 +168,111 @@ def transfer_buffer_cpu(buffer) -> CPUBuffer:
     return CPUBuffer(host.numpy())
 
 
-def _recursive_apply(fn, obj):
-    """Apply ``fn`` to the leaves of lists, tuples, namedtuples, dicts and
-    dataclasses, rebuilding the containers (reference _transfer.py)."""
+# ---- transfer_tensor: one coalesced pinned H2D per batch -----------------------
+#
+# The reference (src/spdl/io/_transfer.py:82-177) pins and copies each CPU
+# tensor of a nested batch separately on a per-thread stream.  Here the
+# batch is flattened, every CPU tensor is packed into ONE page-locked staging
+# area (a per-thread ring of `num_caches` slots), the staging goes to the
+# device in ONE spdl_hj_copy (hipMemcpyAsync on the thread's stream + sync),
+# and the returned device tensors are views of that one allocation.  The
+# last `num_caches` device allocations stay referenced, the reference's
+# guard against the caching allocator handing their memory to another
+# stream while a consumer still reads it
+# (docs/source/notes/pytorch_cuda_race_condition.rst).
+
+
+def _flatten(obj, leaves: list):
+    """Leaves of lists / tuples / namedtuples / mappings / dataclasses into
+    `leaves`; returns a function rebuilding the same structure from an
+    iterator over (possibly replaced) leaves."""
     cls = type(obj)
-    if isinstance(obj, list):
-        return cls(_recursive_apply(fn, v) for v in obj)
-    if isinstance(obj, tuple):
-        if hasattr(obj, "_fields"):
-            return cls(**{k: _recursive_apply(fn, v) for k, v in obj._asdict().items()})
-        return cls(_recursive_apply(fn, v) for v in obj)
-    if isinstance(obj, defaultdict):
-        return cls(obj.default_factory, {k: _recursive_apply(fn, v) for k, v in obj.items()})
-    if isinstance(obj, Mapping):
-        return cls({k: _recursive_apply(fn, v) for k, v in obj.items()})
     if is_dataclass(obj) and not isinstance(obj, type):
-        new = cls(**{f.name: _recursive_apply(fn, getattr(obj, f.name))
-                     for f in fields(obj) if f.init})
-        for f in fields(obj):
-            if not f.init:
-                setattr(new, f.name, _recursive_apply(fn, getattr(obj, f.name)))
-        return new
-    return fn(obj)
+        parts = [(f.name, f.init, _flatten(getattr(obj, f.name), leaves)) for f in fields(obj)]
+
+        def build_dc(it):
+            vals = [(n, init, b(it)) for n, init, b in parts]
+            new = cls(**{n: v for n, init, v in vals if init})
+            for n, init, v in vals:
+                if not init:
+                    setattr(new, n, v)
+            return new
+
+        return build_dc
+    if isinstance(obj, Mapping):
+        items = [(k, _flatten(v, leaves)) for k, v in obj.items()]
+        if isinstance(obj, defaultdict):
+            return lambda it: cls(obj.default_factory, {k: b(it) for k, b in items})
+        return lambda it: cls({k: b(it) for k, b in items})
+    if isinstance(obj, (list, tuple)):
+        items = [_flatten(v, leaves) for v in obj]
+        if hasattr(obj, "_fields"):  # namedtuple
+            return lambda it: cls(*[b(it) for b in items])
+        return lambda it: cls([b(it) for b in items])
+    leaves.append(obj)
+    return lambda it: next(it)
 
 
-class _TensorTransfer:
-    def __init__(self, device: torch.device, num_caches: int):
-        self._device = device
-        self._stream = torch.cuda.Stream(device)
-        self._cache: list = [None] * num_caches
+class _BatchMover:
+    """Per-thread mover: a stream, a ring of pinned staging slots and the
+    device allocations of the last `num_caches` batches."""
+
+    _ALIGN = 256
+
+    def __init__(self, device: int, num_caches: int):
+        self.device = device
+        self.stream = torch.cuda.Stream(torch.device("cuda", device))
+        self.ring: list = [None] * max(1, num_caches)
+        self.keep: list = [None] * max(1, num_caches)
+        self.k = 0
 
     def __call__(self, batch):
-        pinned = []
-
-        def move(x):
-            if isinstance(x, torch.Tensor) and x.is_cpu:
-                p = x.pin_memory()
-                pinned.append(p)
-                return p.to(self._device, non_blocking=True)
-            return x
-
-        with torch.cuda.stream(self._stream):
-            batch = _recursive_apply(move, batch)
-        self._stream.synchronize()
-        self._cache.append(batch)
-        self._cache.pop(0)
-        return batch
+        leaves: list = []
+        rebuild = _flatten(batch, leaves)
+        moved = [i for i, x in enumerate(leaves) if isinstance(x, torch.Tensor) and x.is_cpu]
+        if not moved:
+            return batch
+        offs, total = [], 0
+        for i in moved:
+            offs.append(total)
+            nb = leaves[i].numel() * leaves[i].element_size()
+            total += (nb + self._ALIGN - 1) // self._ALIGN * self._ALIGN
+        slot = self.k % len(self.ring)
+        self.k += 1
+        stage = self.ring[slot]
+        if stage is None or stage.numel() < total:
+            stage = self.ring[slot] = torch.empty(max(total, 1), dtype=torch.uint8,
+                                                  pin_memory=True)
+        for i, o in zip(moved, offs):  # pack (torch's multi-threaded copy)
+            t = leaves[i].contiguous()
+            nb = t.numel() * t.element_size()
+            stage[o:o + nb].copy_(t.reshape(-1).view(torch.uint8))
+        dev = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{self.device}")
+        _copy(dev.data_ptr(), stage.data_ptr(), total, _H2D, self.device,
+              self.stream.cuda_stream, True)
+        self.keep[slot] = dev
+        out = list(leaves)
+        for i, o in zip(moved, offs):
+            t = leaves[i]
+            nb = t.numel() * t.element_size()
+            out[i] = dev[o:o + nb].view(t.dtype).view(t.shape)
+        return rebuild(iter(out))
 
 
 _TLS = threading.local()
 
 
 def transfer_tensor(batch, /, *, num_caches: int = 4):
-    """Move the CPU tensors of a (nested) batch to ``cuda:$LOCAL_RANK`` on a
-    dedicated per-thread stream: pin, copy non-blocking, synchronise.  The
-    last ``num_caches`` batches stay referenced so the caller's consumer
-    stream cannot see their memory recycled early."""
-    if not hasattr(_TLS, "transfer"):
+    """Move every CPU tensor of a (nested) batch to ``cuda:$LOCAL_RANK``
+    (reference src/spdl/io/_transfer.py:82-177): one coalesced pinned
+    host-to-device copy per batch on this thread's stream, complete when the
+    call returns; the result has the batch's structure with device tensors
+    in place of the CPU ones."""
+    mover = getattr(_TLS, "mover", None)
+    if mover is None:
         rank = int(os.environ.get("LOCAL_RANK", "0"))
-        if rank >= torch.cuda.device_count():
-            raise RuntimeError("The local rank is larger than the number of available GPUs.")
-        _TLS.transfer = _TensorTransfer(torch.device(f"cuda:{rank}"), num_caches)
-    return _TLS.transfer(batch)
+        count = torch.cuda.device_count()
+        if rank >= count:
+            raise RuntimeError(f"LOCAL_RANK={rank} but only {count} GPU(s) are visible.")
+        mover = _TLS.mover = _BatchMover(rank, num_caches)
+    return mover(batch)

@@ -141,3 +141,45 @@ def test_transfer_tensor_nested():
     assert out.x.is_cuda and out.meta["y"][0].is_cuda
     assert out.meta["y"][1] == 3 and out.meta["s"] == "k"
     assert torch.equal(out.x.cpu(), b.x)
+
+
+def test_transfer_tensor_structure_roundtrip():
+    """The batch flattening used by transfer_tensor rebuilds every container
+    kind the reference handles (list, tuple, namedtuple, defaultdict,
+    Mapping, dataclass incl. non-init fields) -- CPU only."""
+    from collections import defaultdict, namedtuple
+    from dataclasses import dataclass, field
+
+    from spdl_amd.io._transfer import _flatten
+
+    P = namedtuple("P", "a b")
+
+    @dataclass
+    class D:
+        x: object
+        y: list
+        z: int = field(init=False, default=0)
+
+    dd = defaultdict(list, {"k": [1, (2, 3)]})
+    d = D(P(1, [2, 3]), [dd, {"m": 4}])
+    d.z = 5
+    leaves = []
+    build = _flatten(d, leaves)
+    assert leaves == [1, 2, 3, 1, 2, 3, 4, 5]
+    out = build(iter(v * 10 for v in leaves))
+    assert isinstance(out, D) and isinstance(out.x, P) and isinstance(out.y[0], defaultdict)
+    assert out.x == P(10, [20, 30]) and out.y[0]["k"] == [10, (20, 30)] and out.y[1] == {"m": 40}
+    assert out.z == 50 and out.y[0].default_factory is list
+
+
+@pytest.mark.gpu
+def test_transfer_tensor_dtypes_one_copy():
+    ts = [torch.arange(10, dtype=torch.bfloat16), torch.tensor([True, False, True]),
+          torch.randn(3, 5), torch.tensor(7), torch.randint(0, 255, (33,), dtype=torch.uint8)]
+    out = sio.transfer_tensor(ts)
+    for a, b in zip(ts, out):
+        assert b.is_cuda and b.dtype == a.dtype and b.shape == a.shape
+        assert torch.equal(b.cpu(), a)
+    # views of one allocation
+    base = {o.untyped_storage().data_ptr() for o in out}
+    assert len(base) == 1

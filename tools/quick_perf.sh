@@ -3,7 +3,7 @@
 set -o pipefail
 timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/t.log; exit 1; }
 tail -2 gpurun_out/t.log
-timeout -k 10 120 python tests/debug_phases3.py > gpurun_out/ph.log 2>&1 || exit 1
+timeout -k 10 120 python tools/debug/debug_phases3.py > gpurun_out/ph.log 2>&1 || exit 1
 grep "T=512" gpurun_out/ph.log
 for cfg in "--lanes 2" "--lanes 1"; do
   timeout -k 10 120 python bench.py --steps 200 --no-cpu-baseline $cfg > gpurun_out/l.log 2>&1 || { tail -5 gpurun_out/l.log; exit 1; }
