@@ -107,6 +107,8 @@ def _args():
     p.add_argument("--cpu-runs", type=int, default=5)
     p.add_argument("--oracle-check", type=int, default=32,
                    help="images of the last timed batch compared with the oracle")
+    p.add_argument("--debug-mask", type=int, default=0,
+                   help="kernel phase ablations for timing (outputs are wrong; no oracle check)")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU-only rehearsal of the multi-rank launch and timing reduction")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -299,6 +301,8 @@ def main():
     if a.warm_slots >= 0:
         dec.set_param("warmup_slots", a.warm_slots)
     dec.set_param("lanes", a.lanes)
+    if a.debug_mask:
+        dec.set_param("debug_mask", a.debug_mask)
     if a.workload == "imagenet":
         spec = Output(**{**IMAGENET_SPEC.__dict__, "norm_dtype": a.norm_dtype})
         outs = [torch.empty((a.batch, 3, 224, 224), dtype=spec.torch_dtype, device=device)
@@ -361,7 +365,8 @@ def main():
     # correctness outside the timed region: the last timed batch against
     # the oracle (every distinct image of the slice)
     last = outs[(nsub[0] - 1) % len(outs)]
-    checked = _oracle_check(datas, last, spec, min(a.batch, a.distinct, a.oracle_check))
+    checked = ("skipped (--debug-mask ablation)" if a.debug_mask else
+               _oracle_check(datas, last, spec, min(a.batch, a.distinct, a.oracle_check)))
 
     stages_ms = {k: v / a.steps / 1000.0 for k, v in stages.items()}
     kernels = {k: v for k, v in stages_ms.items() if k not in ("h2d", "d2h_status")}

@@ -101,7 +101,7 @@ struct SwsDesc {
   int32_t chr_w;           // chroma intermediate width (chrDstW)
   int32_t full, gray;      // SWS_FULL_CHR_H_INT; single-component source
   int32_t hl_taps, hc_taps, vl_taps, vc_taps;  // taps read per output (trailing zeros cut)
-  int32_t hl_size, hc_size, vl_size, vc_size;  // taps stored per output
+  int32_t hl_size, hc_size, vl_size, vc_size;  // tap row stride (taps, multiple of 4)
   int32_t off[kSwsTables];
   int32_t rb;              // output rows per workgroup band
   int32_t col_chunk;       // output columns per workgroup
@@ -132,8 +132,9 @@ struct ImageDesc {      // host-filled per image
 };
 
 // sws_kernel LDS budget per workgroup (bytes): the horizontal-pass rows of a
-// band (int16 luma + two chroma planes); the host picks the band height
-constexpr int kSwsLdsBudget = 40 * 1024;
+// band (int16 luma + two chroma planes) and the u8 output tile; the host
+// picks the band height (three workgroups per CU at 48 KiB)
+constexpr int kSwsLdsBudget = 48 * 1024;
 constexpr int kSwsMaxCols = 256;  // output columns per workgroup
 
 struct ImageInfo {      // device-filled by the parse kernel

@@ -381,14 +381,27 @@ class PlanCache {
     int32_t* taps[4] = {&d.hl_taps, &d.hc_taps, &d.vl_taps, &d.vc_taps};
     int32_t* sizes[4] = {&d.hl_size, &d.hc_size, &d.vl_size, &d.vc_size};
     for (int i = 0; i < 4; i++) {
-      *taps[i] = ax[i]->eff;
-      *sizes[i] = ax[i]->size;
-      put(pp->blob, &d.off[2 * i], ax[i]->pos.data(), ax[i]->pos.size() * 4);
-      put(pp->blob, &d.off[2 * i + 1], ax[i]->coef.data(), ax[i]->coef.size() * 2);
+      // rows cut to the taps that are ever non-zero, padded to a multiple
+      // of 4 (the kernel reads taps 4 at a time)
+      const SwsAxis& a = *ax[i];
+      const int eff = a.eff;
+      // horizontal rows: padded to the kernel's register bucket of taps
+      // (hpass: 4, 8, 12, 16, 24, 32, 48, 64; longer rows use a plain loop)
+      int q = (eff + 3) / 4;
+      if (i < 2) q = q <= 4 ? q : q <= 6 ? 6 : q <= 8 ? 8 : q <= 12 ? 12 : q <= 16 ? 16 : q;
+      const int stride = 4 * q;
+      *taps[i] = eff;
+      *sizes[i] = stride;
+      std::vector<int16_t> rows((size_t)a.n * stride, 0);
+      for (int r = 0; r < a.n; r++)
+        for (int t = 0; t < eff; t++) rows[(size_t)r * stride + t] = a.coef[(size_t)r * a.size + t];
+      put(pp->blob, &d.off[2 * i], a.pos.data(), a.pos.size() * 4);
+      put(pp->blob, &d.off[2 * i + 1], rows.data(), rows.size() * 2);
     }
     put(pp->blob, &d.off[kVmode], pl.vmode.data(), pl.vmode.size() * 4);
     // tiling: the tallest band (and widest column chunk) whose horizontal
-    // pass rows fit the LDS budget; bands are in output rows
+    // pass rows (+ 4 slack rows) and u8 output tile fit the LDS budget;
+    // bands are in output rows
     for (int cols = kSwsMaxCols; cols >= 16 && !pp->bands; cols /= 2) {
       const int chunk = k.ow < cols ? k.ow : cols;
       static const int kRb[] = {32, 24, 16, 12, 8, 6, 4, 3, 2, 1};
@@ -404,13 +417,15 @@ class PlanCache {
             if (xs0 >= xs1) continue;
             const int64_t ncl = xs1 - xs0;
             const int64_t ncc = pl.gray ? 0 : pl.full ? ncl : ((xs1 - 1) >> 1) - (xs0 >> 1) + 1;
-            lds = std::max(lds, 2 * (lrows * ncl + 2 * crows * ncc));
+            const int64_t h = 2 * (lrows * ncl + 2 * crows * ncc + 4 * std::max(ncl, ncc));
+            lds = std::max(lds, (h + 15) & ~(int64_t)15);
           }
         }
-        if (lds <= kSwsLdsBudget || (rb == 1 && lds <= 64 * 1024)) {
+        const int64_t tile = (int64_t)rb * chunk * 3;
+        if (lds + tile <= kSwsLdsBudget || (rb == 1 && lds + tile <= 64 * 1024)) {
           d.rb = rb;
           d.col_chunk = chunk;
-          pp->lds = (int)lds;
+          pp->lds = (int)(lds + tile);
           pp->bands = (k.oh + rb - 1) / rb;
           pp->chunks = (k.ow + chunk - 1) / chunk;
           break;

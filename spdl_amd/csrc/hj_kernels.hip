@@ -633,6 +633,7 @@ constexpr int kWinWords = HJ_WIN_WORDS;  // bit-reader window per thread (words)
 // distinct tables is left to the NTAB = 6 instance launched after it.
 template <int NT, int NTAB>
 struct EntShared {
+  static constexpr int kTabs = NTAB;
   uint32_t lut[NTAB][kLutSize];
   uint32_t sub[kSubPool];
   int32_t maxcode[NTAB][18];
@@ -656,6 +657,10 @@ struct EntShared {
   };
   int32_t flag;
   int32_t err;
+  // tables past the NTAB LDS slots (5-6 distinct tables, rare): read from
+  // the parse kernel's HBM copy
+  const HuffTable* gtab;
+  int32_t gslot[kMaxTabs];
 };
 static_assert(sizeof(EntShared<512, 4>) <= 160 * 1024 / 3,
               "entropy LDS must allow 3 workgroups per CU");
@@ -675,7 +680,7 @@ static_assert(sizeof(EntShared<512, 4>) <= 160 * 1024 / 3,
 #define HJ_POS_READER 1
 #endif
 struct Dec {
-#if !HJ_POS_READER
+#if HJ_POS_READER != 1
   uint64_t buf;  // the next 33..64 bits MSB-first
   uint32_t nxt;  // the word after them
   uint32_t wi;   // absolute word index of nxt
@@ -713,7 +718,7 @@ __device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, 
   }
 }
 
-#if HJ_POS_READER
+#if HJ_POS_READER == 1
 template <int NT>
 __device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
                                          uint32_t z, uint32_t bs) {
@@ -741,6 +746,48 @@ __device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32
 }
 
 __device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) { d.pos += nbits; }
+#elif HJ_POS_READER == 2
+// 64-bit register buffer (>= 33 valid bits at every peek), refilled
+// branch-free from a word read from the window one step ahead: the symbol
+// chain carries no window read, only the Huffman table lookup.
+template <int NT>
+__device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
+                                         uint32_t z, uint32_t bs) {
+  const uint32_t w0 = p >> 5;
+  d.wb = w0 & ~3u;
+  win_stage<NT>(win, words, d.wb);
+  const uint64_t hi = win[(w0 - d.wb) * NT];
+  const uint64_t lo = win[(w0 + 1 - d.wb) * NT];
+  d.buf = ((hi << 32) | lo) << (p & 31);
+  d.cnt = 64 - (int)(p & 31);
+  d.wi = w0 + 2;
+  d.nxt = win[(d.wi - d.wb) * NT];
+  d.pos = p;
+  d.z = z;
+  d.bs = bs;
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
+  if (__any((d.wi - d.wb) >= (uint32_t)(kWinWords - 1))) {
+    d.wb = d.wi & ~3u;
+    win_stage<NT>(win, words, d.wb);
+    d.nxt = win[(d.wi - d.wb) * NT];
+  }
+  return (uint32_t)(d.buf >> 32);
+}
+
+template <int NT>
+__device__ __forceinline__ void dec_skip2(Dec& d, const uint32_t* win, uint32_t nbits) {
+  d.buf <<= nbits;
+  d.cnt -= (int)nbits;
+  d.pos += nbits;
+  const bool r = d.cnt <= 32;
+  d.buf |= r ? ((uint64_t)d.nxt << (32 - d.cnt)) : 0ull;
+  d.cnt += r ? 32 : 0;
+  d.wi += r ? 1u : 0u;
+  d.nxt = win[(d.wi - d.wb) * NT];
+}
 #else
 template <int NT>
 __device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
@@ -798,16 +845,25 @@ __device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) {
 }
 #endif
 
+#if HJ_POS_READER == 2
+#define HJ_DEC_SKIP(d, n) dec_skip2<NT>(d, win, n)
+#else
+#define HJ_DEC_SKIP(d, n) dec_skip(d, n)
+#endif
+
 // Canonical decode of a code that is not fully resolved by the LUT (longer
 // than kLutBits, or a DC size > 15): returns a kKindCode entry, 0 if invalid.
 template <class SH>
 __device__ __attribute__((noinline)) uint32_t slow_symbol(const SH& S, int t, uint32_t hi,
                                                           bool is_dc) {
+  const bool g = t >= SH::kTabs;
+  const HuffTable* G = g ? S.gtab + S.gslot[t] : nullptr;
+  const int tl = g ? 0 : t;
   const uint32_t w16 = hi >> 16;
   for (int l = 1; l <= 16; l++) {
     const int code = (int)(w16 >> (16 - l));
-    if (code <= S.maxcode[t][l]) {
-      const int sym = S.vals[t][S.valoff[t][l] + code];
+    if (code <= (g ? G->maxcode[l] : S.maxcode[tl][l])) {
+      const int sym = g ? G->vals[G->valoff[l] + code] : S.vals[tl][S.valoff[tl][l] + code];
       if (is_dc && sym > 15) return 0;
       return hj_entry(kKindCode, l, sym, is_dc, 0);
     }
@@ -821,6 +877,17 @@ __device__ __attribute__((noinline)) uint32_t slow_symbol(const SH& S, int t, ui
 // entry is 0 (invalid code) and the canonical fallback is not needed.
 template <bool SLOW, class SH>
 __device__ __forceinline__ uint32_t lookup(const SH& S, uint32_t t, uint32_t hi, bool is_dc) {
+  if constexpr (SLOW) {
+    if (t >= (uint32_t)SH::kTabs) {  // a table past the LDS slots: its HBM copy
+      const HuffTable& G = S.gtab[S.gslot[t]];
+      uint32_t e = G.lut[hi >> (32 - kLutBits)];
+      if (((e >> 5) & 3) == kKindSub)
+        e = G.sub[((e >> kEntHiShift) << kSubBits) |
+                  ((hi >> (32 - kLutBits - kSubBits)) & ((1u << kSubBits) - 1))];
+      if (((e >> 5) & 3) == kKindSlow) e = slow_symbol(S, (int)t, hi, is_dc);
+      return e;
+    }
+  }
   uint32_t e = S.lut[t][hi >> (32 - kLutBits)];
   if (((e >> 5) & 3) == kKindSub)
     e = S.sub[((e >> kEntHiShift) << kSubBits) |
@@ -854,7 +921,7 @@ __device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     // entry 0 (invalid) takes one bit, advances nothing and starts no block
     const uint32_t nbits = max((e & 31u) + __builtin_amdgcn_ubfe(e, 7, 5), 1u);  // <= 31
     nblk += is_dc ? (int)__builtin_amdgcn_ubfe(e, 19, 1) : 0;  // DC: coef bit = valid
-    dec_skip(d, nbits);
+    HJ_DEC_SKIP(d, nbits);
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool bend = zn >= 64u;
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
@@ -903,7 +970,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
     const uint32_t msk = (1u << sz) - 1u;
     const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
-    dec_skip(d, nbits);
+    HJ_DEC_SKIP(d, nbits);
     const int blk = is_dc ? nb : nb - 1;
 #if HJ_U32_STORE
     // 32-bit element index (blk >= 0 here): an SGPR base + VGPR offset store
@@ -931,7 +998,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
     const uint32_t msk = (1u << sz) - 1u;
     const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
-    dec_skip(d, nbits);
+    HJ_DEC_SKIP(d, nbits);
     const uint32_t zinc = __builtin_amdgcn_ubfe(e, 12, 7);
     const bool coef = valid && ((e >> 19) & 1u);
     const uint32_t zz = (z + zinc - 1u) & 63u;  // coefficient index (DC: 0)
@@ -985,8 +1052,11 @@ __device__ void seg_scan(SH& S, int tid, int flag, const int (&v)[3]) {
   }
 }
 
-// One image's scan, decoded by the whole workgroup.
-template <int NT, int NTAB>
+// One image's scan, decoded by the whole workgroup.  kSlow: the scan has
+// more distinct tables than LDS slots, or long codes outside the LDS
+// sub-table pool (parse_kernel's ent_wide): lookups may go to HBM copies
+// and the canonical fallback.
+template <int NT, int NTAB, bool kSlow>
 __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
                               const uint8_t* __restrict__ clean, const uint32_t* __restrict__ segs,
                               const ImageDesc* __restrict__ desc, ImageInfo* __restrict__ infos,
@@ -1001,8 +1071,6 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   // The NTAB = 4 instance takes the images whose scan uses <= 4 distinct
   // tables with every long code in sub-tables that fit the LDS pool (no
   // canonical fallback in its loops); the NTAB = 6 instance takes the rest.
-  constexpr bool kSlow = NTAB > 4;
-  if (kSlow != (in.ent_wide != 0)) return;  // (parse_kernel decides the instance)
   const int bpm = in.bpm, ri = in.ri, nmcu = in.mcux * in.mcuy;
   const int nblocks = in.nblocks;
   const uint32_t* words = reinterpret_cast<const uint32_t*>(clean + dd.in_off);
@@ -1029,8 +1097,13 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       }
     }
     const HuffTable* tabs = luts + (size_t)img * 8;
+    if (tid == 0) S.gtab = tabs;
     int pool = 0;  // in units of 64-entry sub-tables
     for (int i = 0; i < ns; i++) {
+      if (i >= NTAB) {  // kept in HBM (kSlow images only)
+        if (tid == 0) S.gslot[i] = slots[i];
+        continue;
+      }
       const HuffTable& T = tabs[slots[i]];
       const int nsub = T.nsub;
       const bool fits = (pool + nsub) << kSubBits <= kSubPool;
@@ -1366,11 +1439,10 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   }
 }
 
-// The NTAB = 4 instance runs one workgroup per image.  The NTAB = 6 instance
-// (images with 5-6 distinct tables or long codes outside the LDS pool, rare)
-// runs a few workgroups that stride over the batch: every other image exits
-// at once, and the small grid does not wait for LDS behind the other lane's
-// entropy workgroups.
+// One workgroup per image (grid-stride).  The common scan (<= 4 distinct
+// tables, every long code in the LDS sub-table pool) runs the LDS-only
+// decode loops; a wide one (parse_kernel's ent_wide) the loops that may read
+// HBM table copies and the canonical fallback.  One launch serves both.
 template <int NT, int NTAB>
 __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
                                                      const uint32_t* __restrict__ segs,
@@ -1382,30 +1454,14 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
                                                      const int sub_bits_param, const int warm_slots,
                                                      const int n) {
   __shared__ EntShared<NT, NTAB> S;
-  if constexpr (NTAB > 4) {
-    // Strided instance: the workgroup first tests the flags of its next NT
-    // images at once (one load per thread) and skips the chunk when none of
-    // them needs this instance -- the common case, where the launch is then
-    // one flag read per image instead of NT serial per-image checks.
-    const int tid = threadIdx.x;
-    for (int base = blockIdx.x; base < n; base += gridDim.x * NT) {
-      const int mine = base + tid * gridDim.x;
-      const bool need = mine < n && infos[mine].status == kOk && infos[mine].ent_wide != 0;
-      if (!__syncthreads_or(need)) continue;
-      for (int j = 0; j < NT; j++) {
-        const int img = base + j * gridDim.x;
-        if (img >= n) break;
-        entropy_image<NT, NTAB>(S, img, clean, segs, desc, infos, luts, coefs, recs,
-                                sub_bits_param, warm_slots);
-        __syncthreads();  // LDS is reused by the next image
-      }
-    }
-  } else {
-    for (int img = blockIdx.x; img < n; img += gridDim.x) {
-      entropy_image<NT, NTAB>(S, img, clean, segs, desc, infos, luts, coefs, recs, sub_bits_param,
-                              warm_slots);
-      __syncthreads();  // LDS is reused by the next image
-    }
+  for (int img = blockIdx.x; img < n; img += gridDim.x) {
+    if (infos[img].ent_wide)
+      entropy_image<NT, NTAB, true>(S, img, clean, segs, desc, infos, luts, coefs, recs,
+                                    sub_bits_param, warm_slots);
+    else
+      entropy_image<NT, NTAB, false>(S, img, clean, segs, desc, infos, luts, coefs, recs,
+                                     sub_bits_param, warm_slots);
+    __syncthreads();  // LDS is reused by the next image
   }
 }
 
@@ -1588,17 +1644,28 @@ __global__ void __launch_bounds__(256) csc_kernel(const uint8_t* __restrict__ pl
 // ---------------------------------------------------------------------------
 
 typedef short hj_short2 __attribute__((ext_vector_type(2)));
+// 16-byte vector load from a 4-byte aligned address (gfx950 global loads
+// allow it): one global_load_dwordx4 instead of four dword loads
+typedef uint32_t hj_u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 
-// sum over taps of row[pos + t] * tap[t] for t < 4 * NQ: 4*NQ bytes from
-// `pos` fetched as NQ+1 aligned dwords, realigned (v_alignbyte), widened to
-// int16 pairs (v_perm) and accumulated with v_dot2 against packed taps.
-template <int NQ>
-__device__ __forceinline__ int32_t hsum(const uint8_t* row, int pos, const uint32_t* wp) {
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(row + (pos & ~3));
-  const uint32_t sh = (uint32_t)(pos & 3);
-  uint32_t w[NQ + 1];
+// NW dwords (NW % 4 == 0) from a 4-byte aligned address, 16 bytes at a time
+template <int NW>
+__device__ __forceinline__ void load_words(const uint8_t* p, uint32_t (&w)[NW]) {
+  static_assert(NW % 4 == 0, "whole 16-byte loads");
 #pragma unroll
-  for (int i = 0; i <= NQ; i++) w[i] = q[i];
+  for (int i = 0; i < NW; i += 4) {
+    const hj_u32x4a v = *reinterpret_cast<const hj_u32x4a*>(p + 4 * i);
+    w[i] = v.x;
+    w[i + 1] = v.y;
+    w[i + 2] = v.z;
+    w[i + 3] = v.w;
+  }
+}
+
+// sum over t < 4*NQ of byte (sh + t) of w times tap t: realign (v_alignbyte),
+// widen to int16 pairs (v_perm), accumulate with v_dot2 against packed taps
+template <int NQ, int NW>
+__device__ __forceinline__ int32_t hdot(const uint32_t (&w)[NW], uint32_t sh, const uint32_t* wp) {
   int32_t h = 0;
 #pragma unroll
   for (int i = 0; i < NQ; i++) {
@@ -1613,56 +1680,73 @@ __device__ __forceinline__ int32_t hsum(const uint8_t* row, int pos, const uint3
   return h;
 }
 
-// Horizontal pass of one plane: columns [c0, c0 + ncols) of the scaled
-// plane for source rows [r0, r1) into lds[(r - r0) * ncols + (c - c0)].
-// Rows past the plane (only reached by zero taps) read its last row.
+__device__ __forceinline__ int16_t h15(int32_t h) {  // hScale8To15: (sum >> 7), capped
+  return (int16_t)min(h >> 7, (1 << 15) - 1);
+}
+
+// Horizontal pass of one plane: scaled columns [c0, c0 + ncols) for source
+// rows [r0, r1) into lds[(r - r0) * ncols + (c - c0)].  One thread per
+// column, its taps in registers (rows of the tap table are padded to a
+// multiple of 4 taps, `cstride` int16 apart), one or two 16-byte loads per
+// source row, the next row's load issued before the current row's taps.
+// Rows past the plane (reached by zero taps only) read its last row.
 template <int NQ>
 __device__ void hpass_cols(const uint8_t* plane, int stride, int ph, const int32_t* pos,
-                           const int16_t* coef, int size, int taps, int c0, int ncols, int r0,
-                           int r1, int16_t* lds, int tid, int nthreads) {
+                           const int16_t* coef, int cstride, int c0, int ncols, int r0, int r1,
+                           int16_t* lds, int tid, int nthreads) {
+  constexpr int NW = (NQ + 1 + 3) / 4 * 4;
   for (int c = tid; c < ncols; c += nthreads) {
     const int x = c0 + c;
     const int p = pos[x];
+    const uint32_t sh = (uint32_t)(p & 3);
     uint32_t wp[2 * NQ];
+    const uint2* cp = reinterpret_cast<const uint2*>(coef + (int64_t)x * cstride);
 #pragma unroll
-    for (int k = 0; k < 2 * NQ; k++) {
-      const int t0 = 2 * k, t1 = 2 * k + 1;
-      const uint32_t a = t0 < taps ? (uint16_t)coef[(int64_t)x * size + t0] : 0u;
-      const uint32_t b = t1 < taps ? (uint16_t)coef[(int64_t)x * size + t1] : 0u;
-      wp[k] = a | (b << 16);
+    for (int k = 0; k < NQ; k++) {
+      const uint2 t = cp[k];
+      wp[2 * k] = t.x;
+      wp[2 * k + 1] = t.y;
     }
-    for (int r = r0; r < r1; r++) {
-      const uint8_t* row = plane + (int64_t)min(r, ph - 1) * stride;
-      const int32_t v = hsum<NQ>(row, p, wp) >> 7;
-      lds[(r - r0) * ncols + c] = (int16_t)min(v, (1 << 15) - 1);
+    const uint8_t* base = plane + (p & ~3);
+    int16_t* out = lds + c;
+    // rows in groups of G: the G loads are issued back to back, so one
+    // memory latency is exposed per group instead of per row
+    constexpr int G = NW <= 4 ? 8 : (NW <= 8 ? 4 : 2);
+    for (int r = r0; r < r1; r += G) {
+      uint32_t w[G][NW];
+#pragma unroll
+      for (int g = 0; g < G; g++)
+        if (r + g < r1) load_words<NW>(base + (int64_t)min(r + g, ph - 1) * stride, w[g]);
+#pragma unroll
+      for (int g = 0; g < G; g++)
+        if (r + g < r1) out[(r + g - r0) * ncols] = h15(hdot<NQ>(w[g], sh, wp));
     }
   }
 }
 
 // taps beyond 64: a plain loop over the table
 __device__ void hpass_cols_long(const uint8_t* plane, int stride, int ph, const int32_t* pos,
-                                const int16_t* coef, int size, int taps, int c0, int ncols, int r0,
-                                int r1, int16_t* lds, int tid, int nthreads) {
+                                const int16_t* coef, int cstride, int taps, int c0, int ncols,
+                                int r0, int r1, int16_t* lds, int tid, int nthreads) {
   for (int c = tid; c < ncols; c += nthreads) {
     const int x = c0 + c;
     const int p = pos[x];
-    const int16_t* cf = coef + (int64_t)x * size;
+    const int16_t* cf = coef + (int64_t)x * cstride;
     for (int r = r0; r < r1; r++) {
       const uint8_t* row = plane + (int64_t)min(r, ph - 1) * stride + p;
       int32_t v = 0;
       for (int t = 0; t < taps; t++) v += (int32_t)row[t] * cf[t];
-      v >>= 7;
-      lds[(r - r0) * ncols + c] = (int16_t)min(v, (1 << 15) - 1);
+      lds[(r - r0) * ncols + c] = h15(v);
     }
   }
 }
 
 __device__ void hpass(const uint8_t* plane, int stride, int ph, const int32_t* pos,
-                      const int16_t* coef, int size, int taps, int c0, int ncols, int r0, int r1,
+                      const int16_t* coef, int cstride, int taps, int c0, int ncols, int r0, int r1,
                       int16_t* lds, int tid, int nthreads) {
   const int nq = (taps + 3) >> 2;
 #define HJ_HP(N) \
-  hpass_cols<N>(plane, stride, ph, pos, coef, size, taps, c0, ncols, r0, r1, lds, tid, nthreads)
+  hpass_cols<N>(plane, stride, ph, pos, coef, cstride, c0, ncols, r0, r1, lds, tid, nthreads)
   if (nq <= 1) HJ_HP(1);
   else if (nq <= 2) HJ_HP(2);
   else if (nq <= 3) HJ_HP(3);
@@ -1671,8 +1755,23 @@ __device__ void hpass(const uint8_t* plane, int stride, int ph, const int32_t* p
   else if (nq <= 8) HJ_HP(8);
   else if (nq <= 12) HJ_HP(12);
   else if (nq <= 16) HJ_HP(16);
-  else hpass_cols_long(plane, stride, ph, pos, coef, size, taps, c0, ncols, r0, r1, lds, tid, nthreads);
+  else hpass_cols_long(plane, stride, ph, pos, coef, cstride, taps, c0, ncols, r0, r1, lds, tid, nthreads);
 #undef HJ_HP
+}
+
+// vertical taps over an LDS column (`st` int16 apart), 4 taps at a time
+// (the tap rows are padded to a multiple of 4 with zeros; the LDS holds 4
+// slack rows past the last plane so the padded reads stay inside it)
+__device__ __forceinline__ int32_t vdot(const int16_t* col, int st, const int16_t* f, int taps) {
+  int32_t acc = 0;
+  for (int j = 0; j < taps; j += 4) {
+    const uint2 cf = *reinterpret_cast<const uint2*>(f + j);
+    const int32_t a0 = col[j * st], a1 = col[(j + 1) * st];
+    const int32_t a2 = col[(j + 2) * st], a3 = col[(j + 3) * st];
+    acc += a0 * (int32_t)(int16_t)cf.x + a1 * ((int32_t)cf.x >> 16) +
+           a2 * (int32_t)(int16_t)cf.y + a3 * ((int32_t)cf.y >> 16);
+  }
+  return acc;
 }
 
 __device__ __forceinline__ int clip_i8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
@@ -1707,7 +1806,7 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
                                                   const ImageInfo* __restrict__ infos,
                                                   const int32_t* __restrict__ pool,
                                                   void* __restrict__ out, const BatchParams p) {
-  extern __shared__ int16_t sws_lds[];
+  extern __shared__ __attribute__((aligned(16))) int16_t sws_lds[];
   const int img = blockIdx.z, tid = threadIdx.x, nt = blockDim.x;
   const ImageInfo& in = infos[img];
   if (in.status != kOk) return;
@@ -1716,146 +1815,168 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
   const int yo0 = (int)blockIdx.x * s.rb, xo0 = (int)blockIdx.y * s.col_chunk;
   if (yo0 >= dd.oh || xo0 >= dd.ow) return;
   const int yo1 = min(yo0 + s.rb, dd.oh), xo1 = min(xo0 + s.col_chunk, dd.ow);
+  const int th = yo1 - yo0, tw = xo1 - xo0;
   // content of this tile in scaled coordinates
   const int ys0 = max(yo0 - dd.dy, 0), ys1 = min(yo1 - dd.dy, s.sh);
   const int xs0 = max(xo0 - dd.dx, 0), xs1 = min(xo1 - dd.dx, s.sw);
+  const bool content = ys0 < ys1 && xs0 < xs1;
   const bool planar = p.pix_fmt == 0 || p.pix_fmt == 1;
   const bool swap = p.pix_fmt == 1 || p.pix_fmt == 3;
+  const bool u8 = p.dtype == 0;
   const int64_t pl = (int64_t)dd.ow * dd.oh;
-  auto store = [&](int xo, int yo, const int* rgb) {
+  // LDS: horizontal-pass rows (luma, then the two chroma planes), 4 slack
+  // rows, then (u8 output) the tile in output layout for wide stores
+  const int32_t* T = pool + dd.wt_off;
+  const int32_t* vl_pos = T + s.off[kVlPos];
+  const int32_t* vc_pos = T + s.off[kVcPos];
+  int lr0 = 0, lr1 = 0, cr0 = 0, cr1 = 0, cx0 = 0, ncc = 0;
+  const int ncl = content ? xs1 - xs0 : 0;
+  if (content) {
+    lr0 = vl_pos[ys0];
+    lr1 = vl_pos[ys1 - 1] + s.vl_taps;
+    if (!s.gray) {
+      cr0 = vc_pos[ys0];
+      cr1 = vc_pos[ys1 - 1] + s.vc_taps;
+      cx0 = s.full ? xs0 : xs0 >> 1;
+      ncc = (s.full ? xs1 - 1 : (xs1 - 1) >> 1) + 1 - cx0;
+    }
+  }
+  int16_t* hl = sws_lds;
+  int16_t* hu = hl + (lr1 - lr0) * ncl;
+  int16_t* hv = hu + (cr1 - cr0) * ncc;
+  const int hrow_end = (int)((hv + (cr1 - cr0) * ncc) - sws_lds) + 4 * max(ncl, ncc);
+  uint8_t* tile = reinterpret_cast<uint8_t*>(sws_lds) + ((2 * hrow_end + 15) & ~15);
+  auto put = [&](int xo, int yo, const int* rgb) {
+    if (u8) {
+#pragma unroll
+      for (int ch = 0; ch < 3; ch++) {
+        const int v = rgb[swap ? 2 - ch : ch];
+        const int ti = planar ? (ch * th + (yo - yo0)) * tw + (xo - xo0)
+                              : ((yo - yo0) * tw + (xo - xo0)) * 3 + ch;
+        tile[ti] = (uint8_t)v;
+      }
+      return;
+    }
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
       const int v = rgb[swap ? 2 - ch : ch];
       const int64_t oi =
           dd.out_off + (planar ? ch * pl + (int64_t)yo * dd.ow + xo : ((int64_t)yo * dd.ow + xo) * 3 + ch);
-      if (p.dtype == 0) {
-        static_cast<uint8_t*>(out)[oi] = (uint8_t)v;
-      } else {
-        float f = __fdiv_rn((float)v, 255.0f);
-        f = __fsub_rn(f, p.mean[ch]);
-        f = __fdiv_rn(f, p.std[ch]);
-        static_cast<uint16_t*>(out)[oi] = to_f16_bits(f, p.dtype);
-      }
+      float f = __fdiv_rn((float)v, 255.0f);
+      f = __fsub_rn(f, p.mean[ch]);
+      f = __fdiv_rn(f, p.std[ch]);
+      static_cast<uint16_t*>(out)[oi] = to_f16_bits(f, p.dtype);
     }
   };
-  // pad: output pixels of the tile outside the scaled image are black
+  // pad: tile pixels outside the scaled image are black
   {
-    const int tw = xo1 - xo0, npx = (yo1 - yo0) * tw;
+    const int npx = th * tw;
     const int zero[3] = {0, 0, 0};
     for (int i = tid; i < npx; i += nt) {
       const int yo = yo0 + i / tw, xo = xo0 + i % tw;
       const int ys = yo - dd.dy, xs = xo - dd.dx;
-      if (ys < 0 || ys >= s.sh || xs < 0 || xs >= s.sw) store(xo, yo, zero);
+      if (ys < 0 || ys >= s.sh || xs < 0 || xs >= s.sw) put(xo, yo, zero);
     }
   }
-  if (ys0 >= ys1 || xs0 >= xs1) return;
-  const int32_t* T = pool + dd.wt_off;
-  const int32_t* vl_pos = T + s.off[kVlPos];
-  const int16_t* vl_coef = reinterpret_cast<const int16_t*>(T + s.off[kVlCoef]);
-  const int32_t* vmode = T + s.off[kVmode];
-  const int lr0 = vl_pos[ys0], lr1 = vl_pos[ys1 - 1] + s.vl_taps;
-  const int ncl = xs1 - xs0;
-  int16_t* hl = sws_lds;
-  hpass(planes + dd.plane_off[0], dd.plane_stride[0], in.comp_hpx[0], T + s.off[kHlPos],
-        reinterpret_cast<const int16_t*>(T + s.off[kHlCoef]), s.hl_size, s.hl_taps, xs0, ncl, lr0,
-        lr1, hl, tid, nt);
-  int cr0 = 0, cx0 = 0, ncc = 0;
-  int16_t *hu = nullptr, *hv = nullptr;
-  const int32_t* vc_pos = T + s.off[kVcPos];
-  const int16_t* vc_coef = reinterpret_cast<const int16_t*>(T + s.off[kVcCoef]);
-  if (!s.gray) {
-    cr0 = vc_pos[ys0];
-    const int cr1 = vc_pos[ys1 - 1] + s.vc_taps;
-    cx0 = s.full ? xs0 : xs0 >> 1;
-    ncc = (s.full ? xs1 - 1 : (xs1 - 1) >> 1) + 1 - cx0;
-    hu = hl + (lr1 - lr0) * ncl;
-    hv = hu + (cr1 - cr0) * ncc;
-    const int32_t* hc_pos = T + s.off[kHcPos];
-    const int16_t* hc_coef = reinterpret_cast<const int16_t*>(T + s.off[kHcCoef]);
-    // the two chroma planes share the tables: threads split over both
-    const int half = nt >> 1, t2 = tid < half ? tid : tid - half;
-    const int c = tid < half ? 1 : 2;
-    hpass(planes + dd.plane_off[c], dd.plane_stride[c], in.comp_hpx[c], hc_pos, hc_coef, s.hc_size,
-          s.hc_taps, cx0, ncc, cr0, cr1, c == 1 ? hu : hv, t2, half);
+  if (content && !(p.debug_mask & 0x100)) {  // (debug_mask: timing ablations only)
+    hpass(planes + dd.plane_off[0], dd.plane_stride[0], in.comp_hpx[0], T + s.off[kHlPos],
+          reinterpret_cast<const int16_t*>(T + s.off[kHlCoef]), s.hl_size, s.hl_taps, xs0, ncl,
+          lr0, lr1, hl, tid, nt);
+    if (!s.gray) {
+      // the two chroma planes share the tables: half the threads each
+      const int half = nt >> 1, t2 = tid < half ? tid : tid - half;
+      const int c = tid < half ? 1 : 2;
+      hpass(planes + dd.plane_off[c], dd.plane_stride[c], in.comp_hpx[c], T + s.off[kHcPos],
+            reinterpret_cast<const int16_t*>(T + s.off[kHcCoef]), s.hc_size, s.hc_taps, cx0, ncc,
+            cr0, cr1, c == 1 ? hu : hv, t2, half);
+    }
   }
   __syncthreads();
-  // vertical taps + RGB24 writer, one output column per thread
-  for (int cl = tid; cl < ncl; cl += nt) {
-    const int xs = xs0 + cl;
-    const int cc = (s.full ? xs : xs >> 1) - cx0;
-    for (int ys = ys0; ys < ys1; ys++) {
-      const int m = vmode[ys];
-      const int mode = m & 15, ya = (m >> 4) & 8191, ua = (m >> 17) & 8191;
-      const int lp = vl_pos[ys] - lr0;
-      const int16_t* lf = vl_coef + (int64_t)ys * s.vl_size;
-      const int16_t* lcol = hl + lp * ncl + cl;
-      int rgb[3];
-      int Y, U = 0, V = 0;
-      int cp = 0;
-      const int16_t* cf = nullptr;
-      if (!s.gray) {
-        cp = vc_pos[ys] - cr0;
-        cf = vc_coef + (int64_t)ys * s.vc_size;
-      }
-      if (s.full) {
-        if (mode == kSwsTwo) {
-          Y = ((int)lcol[0] * (4096 - ya) + (int)lcol[ncl] * ya) >> 10;
-        } else if (mode == kSwsOne) {
-          Y = (int)lcol[0] * 4;
-        } else {
-          Y = 1 << 9;
-          for (int j = 0; j < s.vl_taps; j++) Y += (int)lcol[j * ncl] * lf[j];
-          Y >>= 10;
-        }
+  if (content && !(p.debug_mask & 0x200)) {
+    const int16_t* vl_coef = reinterpret_cast<const int16_t*>(T + s.off[kVlCoef]);
+    const int16_t* vc_coef = reinterpret_cast<const int16_t*>(T + s.off[kVcCoef]);
+    const int32_t* vmode = T + s.off[kVmode];
+    // vertical taps + RGB24 writer, one scaled column per thread
+    for (int cl = tid; cl < ncl; cl += nt) {
+      const int xs = xs0 + cl;
+      const int cc = (s.full ? xs : xs >> 1) - cx0;
+      for (int ys = ys0; ys < ys1; ys++) {
+        const int m = vmode[ys];
+        const int mode = m & 15, ya = (m >> 4) & 8191, ua = (m >> 17) & 8191;
+        const int16_t* lcol = hl + (vl_pos[ys] - lr0) * ncl + cl;
+        int rgb[3];
+        int Y, U = 0, V = 0;
+        const int16_t* ucol = hu;
+        const int16_t* vcol = hv;
+        const int16_t* cf = vc_coef;
         if (!s.gray) {
-          const int16_t* ucol = hu + cp * ncc + cc;
-          const int16_t* vcol = hv + cp * ncc + cc;
-          if (mode == kSwsX) {
-            U = (1 << 9) - (128 << 19);
-            V = (1 << 9) - (128 << 19);
-            for (int j = 0; j < s.vc_taps; j++) {
-              U += (int)ucol[j * ncc] * cf[j];
-              V += (int)vcol[j * ncc] * cf[j];
+          const int cp = vc_pos[ys] - cr0;
+          ucol = hu + cp * ncc + cc;
+          vcol = hv + cp * ncc + cc;
+          cf = vc_coef + (int64_t)ys * s.vc_size;
+        }
+        if (s.full) {
+          if (mode == kSwsTwo) {
+            Y = ((int)lcol[0] * (4096 - ya) + (int)lcol[ncl] * ya) >> 10;
+          } else if (mode == kSwsOne) {
+            Y = (int)lcol[0] * 4;
+          } else {
+            Y = ((1 << 9) + vdot(lcol, ncl, vl_coef + (int64_t)ys * s.vl_size, s.vl_taps)) >> 10;
+          }
+          if (!s.gray) {
+            if (mode == kSwsX) {
+              U = ((1 << 9) - (128 << 19) + vdot(ucol, ncc, cf, s.vc_taps)) >> 10;
+              V = ((1 << 9) - (128 << 19) + vdot(vcol, ncc, cf, s.vc_taps)) >> 10;
+            } else {
+              const int o1 = ua ? ncc : 0;
+              U = ((int)ucol[0] * (4096 - ua) + (int)ucol[o1] * ua - (128 << 19)) >> 10;
+              V = ((int)vcol[0] * (4096 - ua) + (int)vcol[o1] * ua - (128 << 19)) >> 10;
             }
-            U >>= 10;
-            V >>= 10;
+          }
+          full_rgb(p, Y, U, V, rgb);
+        } else {
+          if (mode == kSwsX) {
+            Y = ((1 << 18) + vdot(lcol, ncl, vl_coef + (int64_t)ys * s.vl_size, s.vl_taps)) >> 19;
+            U = ((1 << 18) + vdot(ucol, ncc, cf, s.vc_taps)) >> 19;
+            V = ((1 << 18) + vdot(vcol, ncc, cf, s.vc_taps)) >> 19;
+          } else if (mode == kSwsTwo) {
+            Y = ((int)lcol[0] * (4096 - ya) + (int)lcol[ncl] * ya) >> 19;
+            U = ((int)ucol[0] * (4096 - ua) + (int)ucol[ncc] * ua) >> 19;
+            V = ((int)vcol[0] * (4096 - ua) + (int)vcol[ncc] * ua) >> 19;
           } else {
             const int o1 = ua ? ncc : 0;
-            U = ((int)ucol[0] * (4096 - ua) + (int)ucol[o1] * ua - (128 << 19)) >> 10;
-            V = ((int)vcol[0] * (4096 - ua) + (int)vcol[o1] * ua - (128 << 19)) >> 10;
+            Y = ((int)lcol[0] + 64) >> 7;
+            U = ((int)ucol[0] * (4096 - ua) + (int)ucol[o1] * ua + (128 << 11)) >> 19;
+            V = ((int)vcol[0] * (4096 - ua) + (int)vcol[o1] * ua + (128 << 11)) >> 19;
           }
+          rgb[0] = clip_i8(Y + tab_off(p.crv, V));
+          rgb[1] = clip_i8(Y + tab_off(p.cgu, U) + tab_off(p.cgv, V));
+          rgb[2] = clip_i8(Y + tab_off(p.cbu, U));
         }
-        full_rgb(p, Y, U, V, rgb);
-      } else {
-        const int16_t* ucol = hu + cp * ncc + cc;
-        const int16_t* vcol = hv + cp * ncc + cc;
-        if (mode == kSwsX) {
-          Y = 1 << 18;
-          U = 1 << 18;
-          V = 1 << 18;
-          for (int j = 0; j < s.vl_taps; j++) Y += (int)lcol[j * ncl] * lf[j];
-          for (int j = 0; j < s.vc_taps; j++) {
-            U += (int)ucol[j * ncc] * cf[j];
-            V += (int)vcol[j * ncc] * cf[j];
-          }
-          Y >>= 19;
-          U >>= 19;
-          V >>= 19;
-        } else if (mode == kSwsTwo) {
-          Y = ((int)lcol[0] * (4096 - ya) + (int)lcol[ncl] * ya) >> 19;
-          U = ((int)ucol[0] * (4096 - ua) + (int)ucol[ncc] * ua) >> 19;
-          V = ((int)vcol[0] * (4096 - ua) + (int)vcol[ncc] * ua) >> 19;
-        } else {
-          const int o1 = ua ? ncc : 0;
-          Y = ((int)lcol[0] + 64) >> 7;
-          U = ((int)ucol[0] * (4096 - ua) + (int)ucol[o1] * ua + (128 << 11)) >> 19;
-          V = ((int)vcol[0] * (4096 - ua) + (int)vcol[o1] * ua + (128 << 11)) >> 19;
-        }
-        rgb[0] = clip_i8(Y + tab_off(p.crv, V));
-        rgb[1] = clip_i8(Y + tab_off(p.cgu, U) + tab_off(p.cgv, V));
-        rgb[2] = clip_i8(Y + tab_off(p.cbu, U));
+        put(xs + dd.dx, ys + dd.dy, rgb);
       }
-      store(xs + dd.dx, ys + dd.dy, rgb);
+    }
+  }
+  if (!u8 || (p.debug_mask & 0x400)) return;
+  __syncthreads();
+  // the u8 tile out with wide stores: whole rows of an interleaved image are
+  // one contiguous run, planar ones three
+  const int nplane = planar ? 3 : 1;
+  const int run = planar ? th * tw : th * tw * 3;  // bytes per plane run
+  for (int pc = 0; pc < nplane; pc++) {
+    const uint8_t* src = tile + pc * run;
+    uint8_t* dst = static_cast<uint8_t*>(out) + dd.out_off + pc * pl +
+                   (planar ? (int64_t)yo0 * dd.ow + xo0 : ((int64_t)yo0 * dd.ow + xo0) * 3);
+    if (tw == dd.ow && ((uintptr_t)dst & 15) == 0 && (run & 15) == 0) {
+      for (int i = tid; i < run / 16; i += nt)
+        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else {
+      const int rowb = planar ? tw : tw * 3;
+      const int64_t ostride = planar ? dd.ow : (int64_t)dd.ow * 3;
+      for (int i = tid; i < run; i += nt) {
+        const int r = i / rowb, k = i - r * rowb;
+        dst[r * ostride + k] = src[i];
+      }
     }
   }
 }
@@ -1902,22 +2023,17 @@ hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const Imag
                           ImageInfo* infos, const HuffTable* luts, int16_t* coefs, uint32_t* recs,
                           int sub_bits, int warm_slots, int threads, int lds_pad, int n,
                           hipStream_t st) {
-  // two instances per batch: <=4 distinct tables (nearly every JPEG, one
-  // workgroup per image), then the images that need 5-6 (at most 16
-  // workgroups striding over the batch)
+  // one workgroup per image; wide scans take the HBM-table loops inside
 #define HJ_ENT(T, NTAB)                                                                   \
-  hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(NTAB > 4 ? (n < 16 ? n : 16) : n), dim3(T), \
-                     NTAB > 4 ? 0 : lds_pad, st, clean, segs, desc, infos, luts, coefs, recs,    \
+  hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(n), dim3(T), lds_pad, st, clean, segs, \
+                     desc, infos, luts, coefs, recs,                                        \
                      sub_bits, warm_slots, n)
   if (threads == 1024) {
     HJ_ENT(1024, 4);
-    HJ_ENT(1024, 6);
   } else if (threads == 512) {
     HJ_ENT(512, 4);
-    HJ_ENT(512, 6);
   } else {
     HJ_ENT(256, 4);
-    HJ_ENT(256, 6);
   }
 #undef HJ_ENT
   return hipGetLastError();
