@@ -36,10 +36,10 @@ hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, DsChunk*
                           uint32_t*, int, int,
                           hipStream_t);
 hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
-                          const HuffTable*, int16_t*, uint32_t*, int, int, int, int, int,
+                          const HuffTable*, uint32_t*, uint2*, uint32_t*, int, int, int, int, int,
                           hipStream_t);
-hipError_t launch_idct(const int16_t*, const ImageDesc*, const ImageInfo*, uint8_t*, int, int, int,
-                       hipStream_t);
+hipError_t launch_idct(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, uint8_t*,
+                       int, int, int, hipStream_t);
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                       const BatchParams&, int64_t, int, hipStream_t);
 hipError_t launch_nv12(const uint8_t*, uint8_t*, int, int, int, int, int, hipStream_t);
@@ -516,8 +516,9 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
       if (bpm > kMaxBpm) return fail(i, SPDL_HJ_ERR_UNSUPPORTED, nullptr);
       nblocks = (int64_t)mcux * mcuy * bpm;
     }
-    // the entropy kernel's 32-bit coefficient index (blk * 64) must not wrap
-    if (nblocks >= (1 << 26)) return fail(i, SPDL_HJ_ERR_UNSUPPORTED, "image too large");
+    // the entropy kernel's 32-bit byte offsets into an image's coefficient
+    // lists (4 bytes x 64 entries per block) must not wrap
+    if (nblocks >= (1 << 24)) return fail(i, SPDL_HJ_ERR_UNSUPPORTED, "image too large");
     d.nblocks = (int)nblocks;
     d.coef_off = L.total_blocks;
     L.total_blocks += nblocks;
@@ -609,7 +610,7 @@ struct Slot {
 constexpr int kMaxLanes = 3;
 
 struct Workspace {
-  DevBuf clean, segs, desc, info, luts, coefs, planes, wts, recs, dschunks;
+  DevBuf clean, segs, desc, info, luts, ents, bdesc, planes, wts, recs, dschunks;
   hipEvent_t done = nullptr;      // the workspace is free after this
   hipStream_t stream = nullptr;   // lanes > 1 only
 };
@@ -749,7 +750,8 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   HJ_HIP(W.desc.ensure(sizeof(ImageDesc) * n));
   HJ_HIP(W.info.ensure(sizeof(ImageInfo) * n));
   HJ_HIP(W.luts.ensure(sizeof(HuffTable) * 8 * n));
-  HJ_HIP(W.coefs.ensure((size_t)L.total_blocks * 128 + 256));
+  HJ_HIP(W.ents.ensure((size_t)L.total_blocks * 256 + 256));
+  HJ_HIP(W.bdesc.ensure((size_t)L.total_blocks * 8 + 64));
   HJ_HIP(W.planes.ensure((size_t)L.total_planes + 256));
   HJ_HIP(W.recs.ensure((size_t)L.total_recs * 4 + 256));
   HJ_HIP(W.wts.ensure(L.tables.size() * 4 + 256));
@@ -771,10 +773,12 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   HJ_HIP(launch_entropy(static_cast<const uint8_t*>(W.clean.p),
                         static_cast<const uint32_t*>(W.segs.p), desc, infos,
                         static_cast<const HuffTable*>(W.luts.p),
-                        static_cast<int16_t*>(W.coefs.p), static_cast<uint32_t*>(W.recs.p),
+                        static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
+                        static_cast<uint32_t*>(W.recs.p),
                         ctx->sub_bits, ctx->warm_slots, ctx->entropy_threads, ctx->entropy_lds_pad, n, st));
   mark(ctx, slot, 4, st);
-  HJ_HIP(launch_idct(static_cast<const int16_t*>(W.coefs.p), desc, infos,
+  HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
+                     static_cast<const uint2*>(W.bdesc.p), desc, infos,
                      static_cast<uint8_t*>(W.planes.p), out->idct, L.max_blocks, n, st));
   mark(ctx, slot, 5, st);
   BatchParams bp{};
@@ -980,7 +984,7 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
   }
   if (c->copy) (void)hipStreamSynchronize(c->copy);
   for (Workspace& w : c->ws) {
-    DevBuf* bufs[] = {&w.clean, &w.segs, &w.desc, &w.info, &w.luts, &w.coefs,
+    DevBuf* bufs[] = {&w.clean, &w.segs, &w.desc, &w.info, &w.luts, &w.ents, &w.bdesc,
                       &w.planes, &w.wts, &w.recs, &w.dschunks};
     for (DevBuf* b : bufs) b->release();
     if (w.done) (void)hipEventDestroy(w.done);
@@ -1394,9 +1398,25 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   diag[3] = hi.sync_rounds;
   for (int i = 0; i < 4; i++) diag[4 + i] = (int32_t)hi.tphase[i];
   for (int i = 0; i < 4; i++) diag[8 + i] = (int32_t)hi.dbg[i];
-  size_t nc = (size_t)L.desc[0].nblocks * 64;
-  if (coefs) HJ_HIP(hipMemcpy(coefs, W.coefs.p, 2 * (nc < coef_cap ? nc : coef_cap),
-                              hipMemcpyDeviceToHost));
+  // expand the coefficient lists (see BlockOut in hj_kernels.hip) to the dense
+  // natural-order blocks the IDCT consumes
+  const size_t nbk = (size_t)L.desc[0].nblocks;
+  if (coefs && hi.status == SPDL_HJ_OK) {
+    std::vector<uint2> bd(nbk);
+    std::vector<uint32_t> ents(nbk * 64);
+    HJ_HIP(hipMemcpy(bd.data(), W.bdesc.p, nbk * sizeof(uint2), hipMemcpyDeviceToHost));
+    HJ_HIP(hipMemcpy(ents.data(), W.ents.p, nbk * 256, hipMemcpyDeviceToHost));
+    std::vector<int16_t> dense(nbk * 64, 0);
+    for (size_t j = 0; j < nbk; j++) {
+      dense[j * 64] = (int16_t)(bd[j].y >> 16);
+      const uint32_t cnt = bd[j].y & 0xFFFFu;
+      for (uint32_t i = 0; i < cnt && bd[j].x + i < nbk * 64; i++) {
+        const uint32_t e = ents[bd[j].x + i];
+        dense[j * 64 + (e & 63u)] = (int16_t)(e >> 16);  // natural index, dequantised
+      }
+    }
+    memcpy(coefs, dense.data(), 2 * (dense.size() < coef_cap ? dense.size() : coef_cap));
+  }
   if (clean && hi.clean_len > 0) {
     size_t n = (size_t)hi.clean_len < clean_cap ? (size_t)hi.clean_len : clean_cap;
     HJ_HIP(hipMemcpy(clean, W.clean.p, n, hipMemcpyDeviceToHost));

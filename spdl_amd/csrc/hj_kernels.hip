@@ -621,6 +621,12 @@ __global__ void __launch_bounds__(kDsThreads) destuff_write_kernel(
 // ---------------------------------------------------------------------------
 
 constexpr int kMaxTabs = 2 * kMaxComp;  // distinct (DC, AC) tables of a scan
+// natural (row-major) index of each zig-zag position
+__constant__ uint8_t kNatOrder[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
+                                      11, 4,  5,  12, 19, 26, 33, 40, 48, 41, 34, 27, 20,
+                                      13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43,
+                                      36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45,
+                                      38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 #ifndef HJ_WIN_WORDS
 #define HJ_WIN_WORDS 8
 #endif
@@ -642,6 +648,7 @@ struct EntShared {
   uint32_t run_pos[NT];
   uint32_t run_zb[NT];
   uint32_t qdc[kMaxComp];  // DC quantiser per component
+  uint32_t qn[kMaxComp][64];  // per zig-zag index: natural index | quantiser << 16
   int32_t tdc[kMaxBpm], tac[kMaxBpm], bcomp[kMaxBpm];
   // The bit-reader windows are dead outside round 0 / the sync rounds, so the
   // reduction and scan scratch share their storage (keeps the workgroup at
@@ -931,61 +938,112 @@ __device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
   return nblk;
 }
 
-// Full decode of the symbols that start in [d.pos, end) from a synchronised
-// state: dequantise, scatter in natural order, and apply the sequential
-// decoder's stop / error rules of the segment (blocks [.., seg_end_blk),
-// scan bits [.., seg_end)) -- oracle jo_decode_coefs.  nb = blocks started so
-// far (absolute).  DC coefficients are stored as raw differences; the
-// predictors are applied after the pass.  Returns the status; sets `done`
-// once the segment's last block is complete.
-#ifndef HJ_U32_STORE
-#define HJ_U32_STORE 1
-#endif
+// The block in progress at a run's synchronised start belongs to the run
+// its DC symbol lies in (that run finishes it past its own slots): skip the
+// rest of it, state only, bounded by the segment end.
 template <int NT, bool SLOW, class SH>
-__device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
-                            const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
-                            const uint32_t end, const uint32_t seg_end, const int seg_end_blk,
-                            int16_t* __restrict__ coef_img, int& nb, bool& done) {
-  int rc = kOk;
-  // Fast path: a symbol that can trigger none of the rules below -- a valid
-  // code, no run past coefficient 63, not running past the segment end, and
-  // not after the segment's last block started (nb < seg_end_blk) -- is
-  // decoded without them.  A lane leaves at the first symbol that could,
-  // before consuming it, and the careful loop continues from that state.
-  while (d.pos < end && nb < seg_end_blk) {
+__device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
+                                const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
+                                const uint32_t seg_end) {
+  while (d.z != 0u && d.pos < seg_end) {
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
-    const bool is_dc = z == 0;
     const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
-    const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
-    const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
-    const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
-    const uint32_t nbits = (e & 31u) + sz;
-    const uint32_t zinc = __builtin_amdgcn_ubfe(e, 12, 7);
-    const bool coef = (e >> 19) & 1u;
-    // (bitwise, not short-circuit: one exit test instead of nested branches)
-    if ((e == 0u) | (((e >> 20) & 1u) != 0u) | (coef & (z + zinc > 64u)) |
-        (d.pos + nbits > seg_end))
-      break;
-    const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
-    const uint32_t msk = (1u << sz) - 1u;
-    const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
+    const uint32_t t = __builtin_amdgcn_ubfe(tmap, 9u + c * 3u, 3);
+    const uint32_t e = lookup<SLOW>(S, t, hi, false);
+    const uint32_t nbits = max((e & 31u) + __builtin_amdgcn_ubfe(e, 7, 5), 1u);
     HJ_DEC_SKIP(d, nbits);
-    const int blk = is_dc ? nb : nb - 1;
-#if HJ_U32_STORE
-    // 32-bit element index (blk >= 0 here): an SGPR base + VGPR offset store
-    if (coef) coef_img[(uint32_t)blk * 64u + ((z + zinc - 1u) & 63u)] = (int16_t)v;
-#else
-    if (coef) coef_img[(size_t)blk * 64 + ((z + zinc - 1u) & 63u)] = (int16_t)v;
-#endif
-    nb += is_dc ? 1 : 0;
-    const uint32_t zn = z + zinc;
+    const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool bend = zn >= 64u;
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
-  while (d.pos < end && !done && rc == kOk) {
+}
+
+// Coefficient lists, the write pass's output (read by idct_kernel): block j
+// of an image keeps its non-zero AC coefficients, dequantised (the int16
+// product the sequential decoder stores), as u32 entries (value << 16 |
+// natural index) in ents[bd.x, bd.x + (bd.y & 0xFFFF)), bd = bdesc[j];
+// bd.y >> 16 holds the block's raw DC difference until the DC pass replaces
+// it by the final dequantised DC.  Each block is written by the one run its DC
+// symbol lies in, entries appended from that run's region start (first block
+// * 64; a block has at most 63 AC entries, its list starts 16-byte aligned),
+// so no buffer needs clearing and nothing is scattered: HBM sees ~4 bytes per
+// non-zero coefficient.
+struct BlockOut {
+  uint32_t* ents;
+  uint2* bdesc;
+  uint32_t cur;   // next entry
+  uint32_t last;  // the image's last entry (a clamp that keeps a failed scan's stores in place)
+  uint32_t bstart;  // first entry of the open block
+  int dcv;          // its DC difference
+  bool open;        // a block of this run is being decoded
+};
+
+__device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e) {
+  *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.ents) + (min(o.cur, o.last) << 2)) = e;
+}
+
+__device__ __forceinline__ void close_block(BlockOut& o, int blk) {
+  o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
+  o.cur = (o.cur + 3u) & ~3u;
+  o.open = false;
+}
+
+// Full decode from a synchronised state (z == 0: at a block start) of the
+// blocks whose DC symbol starts before `end`, each to its end (past `end` if
+// needed); the sequential decoder's stop / error rules of the segment (blocks
+// [.., seg_end_blk), scan bits [.., seg_end)) -- oracle jo_decode_coefs.  nb =
+// blocks started so far (absolute).  Returns the status; sets `done` once the
+// segment's last block is complete.
+template <int NT, bool SLOW, class SH>
+__device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
+                            const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
+                            const uint32_t end, const uint32_t seg_end, const int seg_end_blk,
+                            BlockOut& o, int& nb, bool& done) {
+  int rc = kOk;
+  // Fast path, straight-line: a symbol that can trigger none of the rules
+  // below -- a valid code, no run past coefficient 63, not running past the
+  // segment end, not a DC symbol once the segment's last block started -- is
+  // decoded without them.  A lane leaves at the first symbol that could,
+  // before consuming it, and the careful loop continues from that state.
+  for (;;) {
+    const uint32_t z = d.z;
+    const bool is_dc = z == 0;
+    if (is_dc & ((d.pos >= end) | (nb >= seg_end_blk))) break;
+    const uint32_t hi = dec_peek<NT>(d, win, words);
+    const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
+    const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
+    const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
+    const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
+    const uint32_t nbits = (e & 31u) + sz;
+    const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
+    const bool coef = (e >> 19) & 1u;
+    // (bitwise, not short-circuit: one exit test instead of nested branches)
+    if ((e == 0u) | (((e >> 20) & 1u) != 0u) | (coef & (zn > 64u)) | (d.pos + nbits > seg_end))
+      break;
+    const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
+    const uint32_t msk = (1u << sz) - 1u;
+    const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
+    HJ_DEC_SKIP(d, nbits);
+    const bool ac = coef & !is_dc;
+    if (ac) {
+      const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
+      put_entry(o, ((uint32_t)v * (qn >> 16)) << 16 | (qn & 63u));
+    }
+    o.cur += ac ? 1u : 0u;
+    o.bstart = is_dc ? o.cur : o.bstart;
+    o.dcv = is_dc ? v : o.dcv;
+    nb += is_dc ? 1 : 0;
+    const bool bend = zn >= 64u;
+    if (bend) close_block(o, nb - 1);
+    o.open = !bend;
+    const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
+    d.z = bend ? 0u : zn;
+    d.bs = bend ? bsn : d.bs;
+  }
+  while (!done && rc == kOk && !(d.z == 0u && d.pos >= end)) {
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
@@ -1001,7 +1059,6 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     HJ_DEC_SKIP(d, nbits);
     const uint32_t zinc = __builtin_amdgcn_ubfe(e, 12, 7);
     const bool coef = valid && ((e >> 19) & 1u);
-    const uint32_t zz = (z + zinc - 1u) & 63u;  // coefficient index (DC: 0)
     const bool bad = !valid || (coef && z + zinc > 64u) || ((e >> 20) & 1u);
     // The sequential decoder's rules, branch-free (the lanes of a wave sit
     // at unrelated symbols): it stops at the segment's last block and never
@@ -1010,23 +1067,33 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const bool good = coef && !bad;
     const bool stop = good && (is_dc ? nb : nb - 1) >= seg_end_blk;
     const bool wr = good && !stop;
-    const int blk = is_dc ? nb : nb - 1;
-    if (wr) coef_img[(size_t)blk * 64 + zz] = (int16_t)v;
+    const uint32_t zn = valid ? z + zinc : z;
+    if (wr && is_dc) {
+      o.bstart = o.cur;
+      o.dcv = v;
+      o.open = true;
+    }
+    if (wr && !is_dc) {
+      const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
+      put_entry(o, ((uint32_t)v * (qn >> 16)) << 16 | (qn & 63u));
+      o.cur++;
+    }
     nb += (wr && is_dc) ? 1 : 0;
     // a symbol running past the segment end (after the rule above)
     const bool trunc = !bad && !stop && d.pos > seg_end;
     const bool past_b = nb > seg_end_blk || (nb == seg_end_blk && z == 0u);
     done = (bad && past_a) || stop || (trunc && past_b);
     rc = (bad && !past_a) ? kErrBadHuffman : ((trunc && !past_b) ? kErrTruncated : kOk);
-    const uint32_t zn = valid ? z + zinc : z;
     const bool bend = zn >= 64u;
+    if (bend && !stop && o.open) close_block(o, nb - 1);
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
+  // the segment ended (or failed) inside a block: keep what it decoded
+  if (o.open && d.z != 0u) close_block(o, nb - 1);
   return rc;
 }
-
 
 // Segmented inclusive scan over the workgroup's runs (Hillis-Steele): a run
 // with `flag` set restarts the sums.  Results in S.sc.scan_v[tid][0, NV).
@@ -1060,8 +1127,9 @@ template <int NT, int NTAB, bool kSlow>
 __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
                               const uint8_t* __restrict__ clean, const uint32_t* __restrict__ segs,
                               const ImageDesc* __restrict__ desc, ImageInfo* __restrict__ infos,
-                              const HuffTable* __restrict__ luts, int16_t* __restrict__ coefs,
-                              uint32_t* __restrict__ recs, const int sub_bits_param,
+                              const HuffTable* __restrict__ luts, uint32_t* __restrict__ ents,
+                              uint2* __restrict__ bdesc, uint32_t* __restrict__ recs,
+                              const int sub_bits_param,
                               const int warm_slots) {
   const int tid = threadIdx.x;
   uint32_t* win = &S.win[0][tid];
@@ -1121,8 +1189,10 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       if (tid < 17) S.valoff[i][tid] = T.valoff[tid];
       if (tid < 256) S.vals[i][tid] = T.vals[tid];
     }
-    for (int k = tid; k < kMaxComp * 64; k += NT)
+    for (int k = tid; k < kMaxComp * 64; k += NT) {
       if (k % 64 == 0) S.qdc[k / 64] = in.qt[k / 64][0];
+      S.qn[k / 64][k % 64] = kNatOrder[k % 64] | ((uint32_t)in.qt[k / 64][k % 64] << 16);
+    }
     for (int b = 0; b < bpm; b++) bcomp |= (uint32_t)in.mcu_comp[b] << (2 * b);
     for (int c = 0; c < kMaxComp; c++)
       tmap |= ((uint32_t)ldc[c] << (3 * c)) | ((uint32_t)lac[c] << (9 + 3 * c));
@@ -1160,7 +1230,8 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   }
   const int cmax = max(1, (int)((maxbits + N - 1) / N));
   const int seg_per_chunk = max(1, kMaxSlots / cmax);
-  int16_t* coef_img = coefs + (size_t)dd.coef_off * 64;
+  uint32_t* ents_img = ents + (size_t)dd.coef_off * 64;
+  uint2* bdesc_img = bdesc + dd.coef_off;
   // per-slot state, one uint4 per slot: {start pos, start z | bs << 8, blocks
   // started, end z}; each slot is only ever touched by the thread that owns it
   uint4* sst = reinterpret_cast<uint4*>(recs + dd.rec_off);
@@ -1324,21 +1395,21 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
         b1 = min(min(run_end_blk, seg_end_blk(slot_seg(r1 - 1))), nblocks);
       }
     }
-    // ---- clear this run's blocks (replaces a memset of the coefficient
-    // buffer): the write pass may scatter into a block another run started,
-    // so the clears finish (barrier) before any coefficient is written ----
-    {
-      uint4* z4 = reinterpret_cast<uint4*>(coef_img);
-      for (int i = b0 * 8; i < b1 * 8; i++) z4[i] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    __syncthreads();
     // ---- write pass: decode each run once more from its synchronised
-    // start, dequantise, scatter to natural order; the sequential decoder's
+    // start, appending its blocks' coefficient lists; the sequential decoder's
     // stop and error rules per segment ----
     {
       int rc = kOk;
       bool done = false;  // the segment's last block is complete
       bool have = false;  // the decoder holds this run's state
+      BlockOut o;
+      o.ents = ents_img;
+      o.bdesc = bdesc_img;
+      o.cur = (uint32_t)b0 * 64u;
+      o.last = (uint32_t)nblocks * 64u - 1u;
+      o.bstart = o.cur;
+      o.dcv = 0;
+      o.open = false;
       Dec d;
       for (int k = r0; k < r1 && rc == kOk; k++) {
         if (slot_empty(k)) {
@@ -1354,12 +1425,14 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
         } else if (!have) {
           const uint4 q = sst[k];
           dec_init<NT>(d, win, words, q.x, q.y & 0xFF, q.y >> 8);
+          skip_open_block<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm,
+                                     seg_end_bits(s));
           have = true;
         }
         if (done) continue;
         const int seb = seg_end_blk(s);
         rc = decode_write<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm,
-                                     slot_end(k), seg_end_bits(s), seb, coef_img, nb, done);
+                                     slot_end(k), seg_end_bits(s), seb, o, nb, done);
         // last slot of its segment: every block of the segment must be done
         const bool last = (k + 1 >= nslots) || slot_j(k + 1) == 0 || slot_empty(k + 1);
         if (rc == kOk && !done && last && (nb < seb || (nb == seb && d.z != 0)))
@@ -1391,7 +1464,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
             reset += rblk;
           }
           const uint32_t c = __builtin_amdgcn_ubfe(bcomp, 2u * (uint32_t)bs, 2);
-          const int dv = coef_img[(size_t)b * 64];
+          const int dv = (int32_t)bdesc_img[b].y >> 16;
           v[0] += c == 0u ? dv : 0;
           v[1] += c == 1u ? dv : 0;
           v[2] += c == 2u ? dv : 0;
@@ -1413,14 +1486,16 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
           reset += rblk;
         }
         const uint32_t c = __builtin_amdgcn_ubfe(bcomp, 2u * (uint32_t)bs, 2);
-        const int dv = coef_img[(size_t)b * 64];
+        const uint32_t by = bdesc_img[b].y;
+        const int dv = (int32_t)by >> 16;
         const int cur = (c == 0u ? p0 : (c == 1u ? p1 : p2)) + dv;
         p0 = c == 0u ? cur : p0;
         p1 = c == 1u ? cur : p1;
         p2 = c == 2u ? cur : p2;
         const uint32_t q = S.qdc[c];
         const int32_t dqi = (int32_t)((uint32_t)kDcBias + q * (uint32_t)cur);
-        coef_img[(size_t)b * 64] = (int16_t)(dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi));
+        const int32_t dc = dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi);
+        bdesc_img[b].y = (by & 0xFFFFu) | ((uint32_t)dc << 16);
         bs = bs + 1 == bpm ? 0 : bs + 1;
       }
     }
@@ -1449,17 +1524,18 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
                                                      const ImageDesc* __restrict__ desc,
                                                      ImageInfo* __restrict__ infos,
                                                      const HuffTable* __restrict__ luts,
-                                                     int16_t* __restrict__ coefs,
+                                                     uint32_t* __restrict__ ents,
+                                                     uint2* __restrict__ bdesc,
                                                      uint32_t* __restrict__ recs,
                                                      const int sub_bits_param, const int warm_slots,
                                                      const int n) {
   __shared__ EntShared<NT, NTAB> S;
   for (int img = blockIdx.x; img < n; img += gridDim.x) {
     if (infos[img].ent_wide)
-      entropy_image<NT, NTAB, true>(S, img, clean, segs, desc, infos, luts, coefs, recs,
+      entropy_image<NT, NTAB, true>(S, img, clean, segs, desc, infos, luts, ents, bdesc, recs,
                                     sub_bits_param, warm_slots);
     else
-      entropy_image<NT, NTAB, false>(S, img, clean, segs, desc, infos, luts, coefs, recs,
+      entropy_image<NT, NTAB, false>(S, img, clean, segs, desc, infos, luts, ents, bdesc, recs,
                                      sub_bits_param, warm_slots);
     __syncthreads();  // LDS is reused by the next image
   }
@@ -1469,30 +1545,23 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
 // idct_kernel
 // ---------------------------------------------------------------------------
 
-typedef unsigned short hj_u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_mul_lo16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t,
-                            __builtin_bit_cast(hj_u16x2, a) * __builtin_bit_cast(hj_u16x2, b));
-}
+// Per-thread dense block in LDS: 64 int16 in natural order in a 144-byte
+// slot (36 words: the uint4 accesses of 16 consecutive threads fall on
+// disjoint banks).
+constexpr int kIdctThreads = 256;
+constexpr int kBlkWords = 36;
 
 template <int IDCT>
-__global__ void __launch_bounds__(256) idct_kernel(const int16_t* __restrict__ coefs,
-                                                   const ImageDesc* __restrict__ desc,
-                                                   const ImageInfo* __restrict__ infos,
-                                                   uint8_t* __restrict__ planes) {
-  // quantisers in zig-zag order as u16 pairs, DC 1 (its coefficient is final)
-  __shared__ __attribute__((aligned(16))) uint32_t sq[kMaxComp][32];
+__global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __restrict__ ents,
+                                                            const uint2* __restrict__ bdesc,
+                                                            const ImageDesc* __restrict__ desc,
+                                                            const ImageInfo* __restrict__ infos,
+                                                            uint8_t* __restrict__ planes) {
+  __shared__ __attribute__((aligned(16))) uint32_t sblk[kIdctThreads][kBlkWords];
   const int img = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const ImageInfo& in = infos[img];
-  if (in.status != kOk) return;
-  for (int k = threadIdx.x; k < kMaxComp * 32; k += blockDim.x) {
-    const int cc = k / 32, i = k % 32;
-    const uint32_t q0 = i == 0 ? 1u : in.qt[cc][2 * i];
-    sq[cc][i] = q0 | ((uint32_t)in.qt[cc][2 * i + 1] << 16);
-  }
-  __syncthreads();
-  if (j >= in.nblocks) return;
+  if (in.status != kOk || j >= in.nblocks) return;
   const ImageDesc& dd = desc[img];
   const int bpm = in.bpm;
   const int mcu = j / bpm, b = j - mcu * bpm;
@@ -1506,30 +1575,43 @@ __global__ void __launch_bounds__(256) idct_kernel(const int16_t* __restrict__ c
     bx = mx * in.comp_h[c] + in.mcu_dx[b];
     by = my * in.comp_v[c] + in.mcu_dy[b];
   }
-  // The entropy kernel stores raw levels in zig-zag order (DC final).  Dequantise
-  // two at a time (v_pk_mul_lo_u16: the int16 product the sequential decoder
-  // stores), then place them in natural order -- a compile-time permutation.
-  constexpr uint8_t kZigOf[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16,
-                                  26, 29, 42, 3,  8,  12, 17, 25, 30, 41, 43, 9,  11,
-                                  18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52,
-                                  54, 20, 22, 33, 38, 46, 51, 55, 60, 21, 34, 37, 47,
-                                  50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
-  uint32_t zw[32];
-  const uint4* src = reinterpret_cast<const uint4*>(coefs + ((size_t)dd.coef_off + j) * 64);
-  const uint4* qv = reinterpret_cast<const uint4*>(sq[c]);
+  // The entropy kernel's list for this block (see BlockOut): DC final, AC
+  // dequantised with their natural index; placed in the thread's LDS block.
+  const uint2 bd = bdesc[(size_t)dd.coef_off + j];
+  const uint32_t cap = (uint32_t)in.nblocks * 64u;
+  uint32_t start = bd.x & ~3u, count = min(bd.y & 0xFFFFu, 63u);
+  if (start > cap - 64u) count = 0;  // only an unwritten list (a failed scan)
+  const uint4* e4 = reinterpret_cast<const uint4*>(ents + (size_t)dd.coef_off * 64 + start);
+  uint32_t* my_blk = sblk[threadIdx.x];
+  uint4* my4 = reinterpret_cast<uint4*>(my_blk);
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint4 lv = src[i], qq = qv[i];
-    zw[4 * i + 0] = pk_mul_lo16(lv.x, qq.x);
-    zw[4 * i + 1] = pk_mul_lo16(lv.y, qq.y);
-    zw[4 * i + 2] = pk_mul_lo16(lv.z, qq.z);
-    zw[4 * i + 3] = pk_mul_lo16(lv.w, qq.w);
+  for (int i = 0; i < 8; i++) my4[i] = make_uint4(0u, 0u, 0u, 0u);
+  int16_t* my16 = reinterpret_cast<int16_t*>(my_blk);
+  my16[0] = (int16_t)(bd.y >> 16);
+  const uint32_t n4 = (count + 3u) >> 2;
+  for (uint32_t i = 0; i < n4; i += 4) {
+    // unconditional loads (index clamped into the list), then the scatter
+    uint4 q[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) q[u] = e4[min(i + u, n4 - 1u)];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+      for (int h = 0; h < 4; h++)  // (past the list: into the slot's padding)
+        my16[4u * (i + u) + h < count ? (w[h] & 63u) : 64u] = (int16_t)(w[h] >> 16);
+    }
   }
   int32_t blk[64];
 #pragma unroll
-  for (int k = 0; k < 64; k++) {
-    const int zi = kZigOf[k];
-    blk[k] = sext16(zw[zi >> 1] >> ((zi & 1) * 16));
+  for (int i = 0; i < 8; i++) {
+    const uint4 q = my4[i];
+    const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+      blk[8 * i + 2 * h] = sext16(wv[h]);
+      blk[8 * i + 2 * h + 1] = sext16(wv[h] >> 16);
+    }
   }
   int32_t px[64];
   if (IDCT == 0) {
@@ -2020,13 +2102,13 @@ hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo
   return hipGetLastError();
 }
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
-                          ImageInfo* infos, const HuffTable* luts, int16_t* coefs, uint32_t* recs,
-                          int sub_bits, int warm_slots, int threads, int lds_pad, int n,
+                          ImageInfo* infos, const HuffTable* luts, uint32_t* ents, uint2* bdesc,
+                          uint32_t* recs, int sub_bits, int warm_slots, int threads, int lds_pad, int n,
                           hipStream_t st) {
   // one workgroup per image; wide scans take the HBM-table loops inside
 #define HJ_ENT(T, NTAB)                                                                   \
   hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(n), dim3(T), lds_pad, st, clean, segs, \
-                     desc, infos, luts, coefs, recs,                                        \
+                     desc, infos, luts, ents, bdesc, recs,                                  \
                      sub_bits, warm_slots, n)
   if (threads == 1024) {
     HJ_ENT(1024, 4);
@@ -2038,13 +2120,16 @@ hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const Imag
 #undef HJ_ENT
   return hipGetLastError();
 }
-hipError_t launch_idct(const int16_t* coefs, const ImageDesc* desc, const ImageInfo* infos,
-                       uint8_t* planes, int idct, int max_blocks, int n, hipStream_t st) {
-  dim3 grid((max_blocks + 255) / 256, n);
+hipError_t launch_idct(const uint32_t* ents, const uint2* bdesc, const ImageDesc* desc,
+                       const ImageInfo* infos, uint8_t* planes, int idct, int max_blocks, int n,
+                       hipStream_t st) {
+  dim3 grid((max_blocks + kIdctThreads - 1) / kIdctThreads, n);
   if (idct == 1)
-    hipLaunchKernelGGL(idct_kernel<1>, grid, dim3(256), 0, st, coefs, desc, infos, planes);
+    hipLaunchKernelGGL(idct_kernel<1>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
+                       planes);
   else
-    hipLaunchKernelGGL(idct_kernel<0>, grid, dim3(256), 0, st, coefs, desc, infos, planes);
+    hipLaunchKernelGGL(idct_kernel<0>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
+                       planes);
   return hipGetLastError();
 }
 hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
