@@ -107,6 +107,8 @@ def _args():
     p.add_argument("--cpu-runs", type=int, default=5)
     p.add_argument("--oracle-check", type=int, default=32,
                    help="images of the last timed batch compared with the oracle")
+    p.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
+                   help="extra decoder parameter (spdl_hj_set_param), for A/B runs")
     p.add_argument("--debug-mask", type=int, default=0,
                    help="kernel phase ablations for timing (outputs are wrong; no oracle check)")
     p.add_argument("--dry-run", action="store_true",
@@ -301,6 +303,9 @@ def main():
     if a.warm_slots >= 0:
         dec.set_param("warmup_slots", a.warm_slots)
     dec.set_param("lanes", a.lanes)
+    for kv in a.param:
+        k, v = kv.split("=", 1)
+        dec.set_param(k, int(v))
     if a.debug_mask:
         dec.set_param("debug_mask", a.debug_mask)
     if a.workload == "imagenet":

@@ -136,6 +136,10 @@ struct ImageDesc {      // host-filled per image
 // picks the band height (three workgroups per CU at 48 KiB)
 constexpr int kSwsLdsBudget = 48 * 1024;
 constexpr int kSwsMaxCols = 256;  // output columns per workgroup
+// sws_kernel's LDS holds the horizontal pass column-major: a column of `rows`
+// int16 samples (+ 4 slack rows read by zero taps) takes an odd number of
+// words, so the 64 columns of a wave fall on distinct banks.  In int16 units.
+inline HJ_HD int sws_col_stride(int rows) { return 2 * (((rows + 5) >> 1) | 1); }
 
 struct ImageInfo {      // device-filled by the parse kernel
   int32_t status;

@@ -31,7 +31,8 @@
 #include "hj_sws.h"
 
 namespace hj {
-hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageInfo*, HuffTable*, int, hipStream_t);
+hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageDesc*, ImageInfo*, HuffTable*,
+                        const void*, void*, int64_t, int, hipStream_t);
 hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, DsChunk*, uint8_t*,
                           uint32_t*, int, int,
                           hipStream_t);
@@ -41,10 +42,10 @@ hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, Ima
 hipError_t launch_idct(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, uint8_t*,
                        int, int, int, hipStream_t);
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
-                      const BatchParams&, int64_t, int, hipStream_t);
+                      const BatchParams&, int64_t, int, int32_t*, hipStream_t);
 hipError_t launch_nv12(const uint8_t*, uint8_t*, int, int, int, int, int, hipStream_t);
 hipError_t launch_sws(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*, void*,
-                      const BatchParams&, int, int, int, int, hipStream_t);
+                      const BatchParams&, int, int, int, int, int32_t*, hipStream_t);
 }  // namespace hj
 
 using namespace hj;
@@ -104,20 +105,29 @@ struct DevBuf {
 
 struct PinBuf {
   void* p = nullptr;
+  void* dev = nullptr;  // the same pages as the device sees them (kernels read / write them)
   size_t cap = 0;
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
+    release();
     size_t want = n + n / 4 + 4096;
     hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-    if (e == hipSuccess) cap = want;
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    e = hipHostGetDevicePointer(&dev, p, 0);
+    if (e != hipSuccess) {
+      release();
+      return e;
+    }
+    cap = want;
     return e;
   }
   void release() {
     if (p) (void)hipHostFree(p);
     p = nullptr;
+    dev = nullptr;
     cap = 0;
   }
 };
@@ -417,11 +427,14 @@ class PlanCache {
             if (xs0 >= xs1) continue;
             const int64_t ncl = xs1 - xs0;
             const int64_t ncc = pl.gray ? 0 : pl.full ? ncl : ((xs1 - 1) >> 1) - (xs0 >> 1) + 1;
-            const int64_t h = 2 * (lrows * ncl + 2 * crows * ncc + 4 * std::max(ncl, ncc));
+            const int64_t h = 2 * (ncl * sws_col_stride((int)lrows) +
+                                   (pl.gray ? 0 : 2 * ncc * sws_col_stride((int)crows)));
             lds = std::max(lds, (h + 15) & ~(int64_t)15);
           }
         }
-        const int64_t tile = (int64_t)rb * chunk * 3;
+        // + the u8 output tile and the band's staged vertical tables
+        const int64_t tile = (((int64_t)rb * chunk * 3 + 15) & ~(int64_t)15) +
+                             (int64_t)rb * (16 + 2 * (d.vl_size + d.vc_size));
         if (lds + tile <= kSwsLdsBudget || (rb == 1 && lds + tile <= 64 * 1024)) {
           d.rb = rb;
           d.col_chunk = chunk;
@@ -629,6 +642,9 @@ struct spdl_hj_ctx {
   int ntimings = 0;
   int sub_bits = 512;
   int debug_mask = 0;
+  // the first kernel pulls descriptors + tables from pinned memory and the
+  // last writes statuses back (1), or DMA copies do it (0; kept for A/B)
+  int host_staging = 1;
   int entropy_threads = 512;
   int warm_slots = 8;  // entropy round 0: slots decoded before a run's first slot
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
@@ -759,12 +775,24 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   HJ_HIP(slot.pin_status.ensure(sizeof(int32_t) * n));
   slot.n = n;
   memcpy(slot.pin_desc.p, L.desc.data(), sizeof(ImageDesc) * n);
-  HJ_HIP(hipMemcpyAsync(W.desc.p, slot.pin_desc.p, sizeof(ImageDesc) * n,
-                        hipMemcpyHostToDevice, st));
+  // the batch's swscale tables travel with the descriptors
+  const bool swscale = !planes_only && out->csc == SPDL_HJ_CSC_SWSCALE;
+  const size_t tb = swscale ? L.tables.size() * 4 : 0;
+  HJ_HIP(slot.pin_tables.ensure(tb + 16));
+  if (tb) memcpy(slot.pin_tables.p, L.tables.data(), tb);
+  const bool hs = ctx->host_staging != 0;
+  if (!hs) {
+    HJ_HIP(hipMemcpyAsync(W.desc.p, slot.pin_desc.p, sizeof(ImageDesc) * n,
+                          hipMemcpyHostToDevice, st));
+    if (tb) HJ_HIP(hipMemcpyAsync(W.wts.p, slot.pin_tables.p, tb, hipMemcpyHostToDevice, st));
+  }
   mark(ctx, slot, 1, st);
   auto* desc = static_cast<const ImageDesc*>(W.desc.p);
   auto* infos = static_cast<ImageInfo*>(W.info.p);
-  HJ_HIP(launch_parse(d_bytes, desc, infos, static_cast<HuffTable*>(W.luts.p), n, st));
+  HJ_HIP(launch_parse(d_bytes, hs ? static_cast<const ImageDesc*>(slot.pin_desc.dev) : nullptr,
+                      static_cast<ImageDesc*>(W.desc.p), infos,
+                      static_cast<HuffTable*>(W.luts.p), hs ? slot.pin_tables.dev : nullptr,
+                      W.wts.p, hs ? (int64_t)tb : 0, n, st));
   mark(ctx, slot, 2, st);
   HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<DsChunk*>(W.dschunks.p),
                         static_cast<uint8_t*>(W.clean.p), static_cast<uint32_t*>(W.segs.p),
@@ -807,31 +835,24 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   bp.v2g = csc.v2g;
   bp.u2g = csc.u2g;
   bp.u2b = csc.u2b;
+  // the output kernel writes each image's status into the pinned array itself
+  int32_t* hstat = hs && !planes_only ? static_cast<int32_t*>(slot.pin_status.dev) : nullptr;
+  mark(ctx, slot, 6, st);
   if (!planes_only) {
-    if (out->csc == SPDL_HJ_CSC_SWSCALE) {
-      // the batch's swscale tables ride the same stream ahead of the kernel
-      const size_t tb = L.tables.size() * 4;
-      HJ_HIP(slot.pin_tables.ensure(tb + 16));
-      if (tb) {
-        memcpy(slot.pin_tables.p, L.tables.data(), tb);
-        HJ_HIP(hipMemcpyAsync(W.wts.p, slot.pin_tables.p, tb, hipMemcpyHostToDevice, st));
-      }
-      mark(ctx, slot, 6, st);
+    if (swscale) {
       HJ_HIP(launch_sws(static_cast<const uint8_t*>(W.planes.p), desc, infos,
                         static_cast<const int32_t*>(W.wts.p), out_dev, bp, L.sws_bands,
-                        L.sws_chunks, L.sws_lds, n, st));
+                        L.sws_chunks, L.sws_lds, n, hstat, st));
     } else {
-      mark(ctx, slot, 6, st);
       HJ_HIP(launch_csc(static_cast<const uint8_t*>(W.planes.p), desc, infos, out_dev, bp,
-                        L.max_px, n, st));
+                        L.max_px, n, hstat, st));
     }
-  } else {
-    mark(ctx, slot, 6, st);
   }
   mark(ctx, slot, 7, st);
   // per-image status: strided D2H of ImageInfo::status
-  HJ_HIP(hipMemcpy2DAsync(slot.pin_status.p, sizeof(int32_t), W.info.p, sizeof(ImageInfo),
-                          sizeof(int32_t), n, hipMemcpyDeviceToHost, st));
+  if (!hstat)
+    HJ_HIP(hipMemcpy2DAsync(slot.pin_status.p, sizeof(int32_t), W.info.p, sizeof(ImageInfo),
+                            sizeof(int32_t), n, hipMemcpyDeviceToHost, st));
   mark(ctx, slot, 8, st);
   HJ_HIP(hipEventRecord(W.done, st));
   HJ_HIP(hipEventRecord(slot.done, st));
@@ -1516,6 +1537,10 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "lanes")) {  // concurrent pipelines (workspaces + streams)
     if (value < 1 || value > kMaxLanes) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->lanes = (int)value;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "host_staging")) {  // 1: kernels move descriptors / statuses; 0: DMA copies
+    ctx->host_staging = value != 0;
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "debug_mask")) {  // timing ablations only: output is wrong

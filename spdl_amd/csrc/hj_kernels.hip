@@ -62,9 +62,12 @@ struct ParseScratch {
 // from there and only reaches into HBM for headers past that window.
 constexpr int kHdrBytes = 4096;
 
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;  // an LDS byte
+
 struct Bytes {
   const uint8_t* g;  // file in HBM
-  const uint8_t* l;  // its first nl bytes in LDS
+  lds_u8* l;         // its first nl bytes in LDS (typed so: a generic pointer
+                     // would make every header read a flat load)
   int nl;
   __device__ uint8_t operator[](int i) const { return i < nl ? l[i] : g[i]; }
 };
@@ -229,15 +232,31 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
   }
 }
 
+// The batch's host-built inputs arrive with the first kernel: each
+// workgroup pulls its image's descriptor, and all of them the swscale table
+// pool, straight from the slot's pinned staging (mapped host memory) into the
+// workspace -- no DMA-engine copy and no cross-queue sync ahead of the batch.
 __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict__ bytes,
-                                                    const ImageDesc* __restrict__ desc,
+                                                    const ImageDesc* __restrict__ host_desc,
+                                                    ImageDesc* __restrict__ desc,
                                                     ImageInfo* __restrict__ infos,
-                                                    HuffTable* __restrict__ luts) {
+                                                    HuffTable* __restrict__ luts,
+                                                    const uint4* __restrict__ host_tables,
+                                                    uint4* __restrict__ tables, int64_t ntab16) {
   __shared__ ParseScratch s;
   __shared__ int st;
   __shared__ __attribute__((aligned(16))) uint8_t hdr[kHdrBytes];
   const int img = blockIdx.x, tid = threadIdx.x;
-  const ImageDesc dd = desc[img];
+  if (host_desc) {
+    static_assert(sizeof(ImageDesc) % 8 == 0, "descriptor copied in 8-byte words");
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(host_desc + img);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(desc + img);
+    for (int i = tid; i < (int)(sizeof(ImageDesc) / 8); i += blockDim.x) dst[i] = src[i];
+    for (int64_t i = (int64_t)img * blockDim.x + tid; i < ntab16;
+         i += (int64_t)gridDim.x * blockDim.x)
+      tables[i] = host_tables[i];
+  }
+  const ImageDesc dd = (host_desc ? host_desc : desc)[img];
   {
     int* z = reinterpret_cast<int*>(&s);
     for (int i = tid; i < (int)(sizeof(ParseScratch) / 4); i += blockDim.x) z[i] = 0;
@@ -247,7 +266,7 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     reinterpret_cast<uint4*>(hdr)[i] = reinterpret_cast<const uint4*>(bytes + dd.in_off)[i];
   __syncthreads();
   if (tid == 0) {
-    const Bytes file{bytes + dd.in_off, hdr, nh};
+    const Bytes file{bytes + dd.in_off, (lds_u8*)hdr, nh};
     int rc = parse_headers(file, (int)dd.in_size, s);
     if (rc == kOk) {
       // the host probe sized every buffer; it must agree with the device parse
@@ -289,7 +308,7 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
   }
   {
     // table payloads: every thread copies a share
-    const Bytes file{bytes + dd.in_off, hdr, nh};
+    const Bytes file{bytes + dd.in_off, (lds_u8*)hdr, nh};
     for (int i = tid; i < 8 * 256; i += blockDim.x) {
       const int t = i >> 8, k = i & 255;
       if (s.have[t]) s.vals[t][k] = k < s.dht_n[t] ? file[s.dht_off[t] + k] : 0;
@@ -1686,9 +1705,11 @@ __device__ __forceinline__ void store_rgb(void* out, int64_t base, int fmt, int 
 __global__ void __launch_bounds__(256) csc_kernel(const uint8_t* __restrict__ planes,
                                                   const ImageDesc* __restrict__ desc,
                                                   const ImageInfo* __restrict__ infos,
-                                                  void* __restrict__ out, const BatchParams p) {
+                                                  void* __restrict__ out, const BatchParams p,
+                                                  int32_t* __restrict__ host_status) {
   const int img = blockIdx.y;
   const ImageInfo& in = infos[img];
+  if (host_status && blockIdx.x == 0 && threadIdx.x == 0) host_status[img] = in.status;
   if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
   const int W = in.width, H = in.height;
@@ -1726,6 +1747,9 @@ __global__ void __launch_bounds__(256) csc_kernel(const uint8_t* __restrict__ pl
 // ---------------------------------------------------------------------------
 
 typedef short hj_short2 __attribute__((ext_vector_type(2)));
+#ifndef HJ_HG4
+#define HJ_HG4 8  // rows per load group of the short horizontal filters
+#endif
 // 16-byte vector load from a 4-byte aligned address (gfx950 global loads
 // allow it): one global_load_dwordx4 instead of four dword loads
 typedef uint32_t hj_u32x4a __attribute__((ext_vector_type(4), aligned(4)));
@@ -1766,16 +1790,18 @@ __device__ __forceinline__ int16_t h15(int32_t h) {  // hScale8To15: (sum >> 7),
   return (int16_t)min(h >> 7, (1 << 15) - 1);
 }
 
+// (Inlined: through a call the plane and LDS pointers turn generic and the
+// loads / stores into flat ones.)
 // Horizontal pass of one plane: scaled columns [c0, c0 + ncols) for source
-// rows [r0, r1) into lds[(r - r0) * ncols + (c - c0)].  One thread per
+// rows [r0, r1) into lds[(c - c0) * cst + (r - r0)] (column-major).  One thread per
 // column, its taps in registers (rows of the tap table are padded to a
 // multiple of 4 taps, `cstride` int16 apart), one or two 16-byte loads per
 // source row, the next row's load issued before the current row's taps.
 // Rows past the plane (reached by zero taps only) read its last row.
 template <int NQ>
-__device__ void hpass_cols(const uint8_t* plane, int stride, int ph, const int32_t* pos,
+__device__ __forceinline__ void hpass_cols(const uint8_t* plane, int stride, int ph, const int32_t* pos,
                            const int16_t* coef, int cstride, int c0, int ncols, int r0, int r1,
-                           int16_t* lds, int tid, int nthreads) {
+                           int16_t* lds, int cst, int tid, int nthreads) {
   constexpr int NW = (NQ + 1 + 3) / 4 * 4;
   for (int c = tid; c < ncols; c += nthreads) {
     const int x = c0 + c;
@@ -1790,10 +1816,10 @@ __device__ void hpass_cols(const uint8_t* plane, int stride, int ph, const int32
       wp[2 * k + 1] = t.y;
     }
     const uint8_t* base = plane + (p & ~3);
-    int16_t* out = lds + c;
+    int16_t* out = lds + c * cst;
     // rows in groups of G: the G loads are issued back to back, so one
     // memory latency is exposed per group instead of per row
-    constexpr int G = NW <= 4 ? 8 : (NW <= 8 ? 4 : 2);
+    constexpr int G = NW <= 4 ? HJ_HG4 : (NW <= 8 ? 4 : 1);
     for (int r = r0; r < r1; r += G) {
       uint32_t w[G][NW];
 #pragma unroll
@@ -1801,15 +1827,15 @@ __device__ void hpass_cols(const uint8_t* plane, int stride, int ph, const int32
         if (r + g < r1) load_words<NW>(base + (int64_t)min(r + g, ph - 1) * stride, w[g]);
 #pragma unroll
       for (int g = 0; g < G; g++)
-        if (r + g < r1) out[(r + g - r0) * ncols] = h15(hdot<NQ>(w[g], sh, wp));
+        if (r + g < r1) out[r + g - r0] = h15(hdot<NQ>(w[g], sh, wp));
     }
   }
 }
 
 // taps beyond 64: a plain loop over the table
-__device__ void hpass_cols_long(const uint8_t* plane, int stride, int ph, const int32_t* pos,
+__device__ __forceinline__ void hpass_cols_long(const uint8_t* plane, int stride, int ph, const int32_t* pos,
                                 const int16_t* coef, int cstride, int taps, int c0, int ncols,
-                                int r0, int r1, int16_t* lds, int tid, int nthreads) {
+                                int r0, int r1, int16_t* lds, int cst, int tid, int nthreads) {
   for (int c = tid; c < ncols; c += nthreads) {
     const int x = c0 + c;
     const int p = pos[x];
@@ -1818,17 +1844,17 @@ __device__ void hpass_cols_long(const uint8_t* plane, int stride, int ph, const 
       const uint8_t* row = plane + (int64_t)min(r, ph - 1) * stride + p;
       int32_t v = 0;
       for (int t = 0; t < taps; t++) v += (int32_t)row[t] * cf[t];
-      lds[(r - r0) * ncols + c] = h15(v);
+      lds[c * cst + (r - r0)] = h15(v);
     }
   }
 }
 
-__device__ void hpass(const uint8_t* plane, int stride, int ph, const int32_t* pos,
+__device__ __forceinline__ void hpass(const uint8_t* plane, int stride, int ph, const int32_t* pos,
                       const int16_t* coef, int cstride, int taps, int c0, int ncols, int r0, int r1,
-                      int16_t* lds, int tid, int nthreads) {
+                      int16_t* lds, int cst, int tid, int nthreads) {
   const int nq = (taps + 3) >> 2;
 #define HJ_HP(N) \
-  hpass_cols<N>(plane, stride, ph, pos, coef, cstride, c0, ncols, r0, r1, lds, tid, nthreads)
+  hpass_cols<N>(plane, stride, ph, pos, coef, cstride, c0, ncols, r0, r1, lds, cst, tid, nthreads)
   if (nq <= 1) HJ_HP(1);
   else if (nq <= 2) HJ_HP(2);
   else if (nq <= 3) HJ_HP(3);
@@ -1837,23 +1863,39 @@ __device__ void hpass(const uint8_t* plane, int stride, int ph, const int32_t* p
   else if (nq <= 8) HJ_HP(8);
   else if (nq <= 12) HJ_HP(12);
   else if (nq <= 16) HJ_HP(16);
-  else hpass_cols_long(plane, stride, ph, pos, coef, cstride, taps, c0, ncols, r0, r1, lds, tid, nthreads);
+  else hpass_cols_long(plane, stride, ph, pos, coef, cstride, taps, c0, ncols, r0, r1, lds, cst, tid, nthreads);
 #undef HJ_HP
 }
 
-// vertical taps over an LDS column (`st` int16 apart), 4 taps at a time
-// (the tap rows are padded to a multiple of 4 with zeros; the LDS holds 4
-// slack rows past the last plane so the padded reads stay inside it)
-__device__ __forceinline__ int32_t vdot(const int16_t* col, int st, const int16_t* f, int taps) {
+// Vertical taps over an LDS column (column-major int16 words): the tap
+// pairs (row p + 2i, p + 2i + 1) realigned from the column's words
+// (v_alignbit by 16 when p is odd) against packed tap pairs, v_dot2 4 taps a
+// step (tap rows are padded to a multiple of 4 with zeros; the 4 slack rows
+// keep the padded reads inside the column).
+__device__ __forceinline__ int32_t vdot_pairs(const uint32_t* col, int p, const uint32_t* f,
+                                              int np) {
+  const uint32_t* c = col + (p >> 1);
+  const uint32_t sh = (uint32_t)(p & 1) * 16u;
   int32_t acc = 0;
-  for (int j = 0; j < taps; j += 4) {
-    const uint2 cf = *reinterpret_cast<const uint2*>(f + j);
-    const int32_t a0 = col[j * st], a1 = col[(j + 1) * st];
-    const int32_t a2 = col[(j + 2) * st], a3 = col[(j + 3) * st];
-    acc += a0 * (int32_t)(int16_t)cf.x + a1 * ((int32_t)cf.x >> 16) +
-           a2 * (int32_t)(int16_t)cf.y + a3 * ((int32_t)cf.y >> 16);
+  uint32_t w0 = c[0];
+  for (int i = 0; i < np; i += 2) {
+    const uint32_t w1 = c[i + 1], w2 = c[i + 2];
+    const uint2 ff = *reinterpret_cast<const uint2*>(f + i);
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, __builtin_amdgcn_alignbit(w1, w0, sh)),
+                                 __builtin_bit_cast(hj_short2, ff.x), acc, false);
+    acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_short2, __builtin_amdgcn_alignbit(w2, w1, sh)),
+                                 __builtin_bit_cast(hj_short2, ff.y), acc, false);
+    w0 = w2;
   }
   return acc;
+}
+
+// rows p and p + 1 of a column as (lo, hi) int16
+__device__ __forceinline__ void vpair(const uint32_t* col, int p, int& a, int& b) {
+  const uint32_t* c = col + (p >> 1);
+  const uint32_t w = __builtin_amdgcn_alignbit(c[1], c[0], (uint32_t)(p & 1) * 16u);
+  a = (int32_t)(int16_t)(w & 0xFFFFu);
+  b = (int32_t)w >> 16;
 }
 
 __device__ __forceinline__ int clip_i8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
@@ -1887,10 +1929,13 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
                                                   const ImageDesc* __restrict__ desc,
                                                   const ImageInfo* __restrict__ infos,
                                                   const int32_t* __restrict__ pool,
-                                                  void* __restrict__ out, const BatchParams p) {
+                                                  void* __restrict__ out, const BatchParams p,
+                                                  int32_t* __restrict__ host_status) {
   extern __shared__ __attribute__((aligned(16))) int16_t sws_lds[];
   const int img = blockIdx.z, tid = threadIdx.x, nt = blockDim.x;
   const ImageInfo& in = infos[img];
+  // the image's final status, straight into the slot's pinned status array
+  if (host_status && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) host_status[img] = in.status;
   if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
   const SwsDesc& s = dd.sws;
@@ -1923,16 +1968,42 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
       ncc = (s.full ? xs1 - 1 : (xs1 - 1) >> 1) + 1 - cx0;
     }
   }
+  // horizontal-pass output, column-major (sws_col_stride)
+  const int lst = sws_col_stride(lr1 - lr0), cst = sws_col_stride(cr1 - cr0);
   int16_t* hl = sws_lds;
-  int16_t* hu = hl + (lr1 - lr0) * ncl;
-  int16_t* hv = hu + (cr1 - cr0) * ncc;
-  const int hrow_end = (int)((hv + (cr1 - cr0) * ncc) - sws_lds) + 4 * max(ncl, ncc);
+  int16_t* hu = hl + ncl * lst;
+  int16_t* hv = hu + (s.gray ? 0 : ncc * cst);
+  const int hrow_end = (int)((hv + (s.gray ? 0 : ncc * cst)) - sws_lds);
   uint8_t* tile = reinterpret_cast<uint8_t*>(sws_lds) + ((2 * hrow_end + 15) & ~15);
+  // the band's vertical tables, staged once (the per-row loads of the V pass
+  // are then LDS broadcasts): per output row {mode, first luma row, first
+  // chroma row (both band-relative), 0, luma taps, chroma taps}
+  const int vrw = 4 + (s.vl_size + s.vc_size) / 2;
+  uint32_t* vt = reinterpret_cast<uint32_t*>(tile + ((s.rb * s.col_chunk * 3 + 15) & ~15));
+  if (content) {
+    const int32_t* vmode = T + s.off[kVmode];
+    const uint32_t* vlw = reinterpret_cast<const uint32_t*>(T + s.off[kVlCoef]);
+    const uint32_t* vcw = reinterpret_cast<const uint32_t*>(T + s.off[kVcCoef]);
+    const int nl = s.vl_size / 2, nc = s.vc_size / 2;
+    for (int i = tid; i < (ys1 - ys0) * vrw; i += nt) {
+      const int r = i / vrw, w = i - r * vrw, ys = ys0 + r;
+      uint32_t v = 0;
+      if (w == 0) v = (uint32_t)vmode[ys];
+      else if (w == 1) v = (uint32_t)(vl_pos[ys] - lr0);
+      else if (w == 2) v = s.gray ? 0u : (uint32_t)(vc_pos[ys] - cr0);
+      else if (w >= 4 && w < 4 + nl) v = vlw[(int64_t)ys * nl + (w - 4)];
+      else if (w >= 4 + nl) v = vcw[(int64_t)ys * nc + (w - 4 - nl)];
+      vt[i] = v;
+    }
+  }
   auto put = [&](int xo, int yo, const int* rgb) {
+    // (selects, not a dynamically indexed array: that would live in scratch)
+    const int c0v = swap ? rgb[2] : rgb[0], c2v = swap ? rgb[0] : rgb[2];
+    const int cv[3] = {c0v, rgb[1], c2v};
     if (u8) {
 #pragma unroll
       for (int ch = 0; ch < 3; ch++) {
-        const int v = rgb[swap ? 2 - ch : ch];
+        const int v = cv[ch];
         const int ti = planar ? (ch * th + (yo - yo0)) * tw + (xo - xo0)
                               : ((yo - yo0) * tw + (xo - xo0)) * 3 + ch;
         tile[ti] = (uint8_t)v;
@@ -1941,7 +2012,7 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
     }
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
-      const int v = rgb[swap ? 2 - ch : ch];
+      const int v = cv[ch];
       const int64_t oi =
           dd.out_off + (planar ? ch * pl + (int64_t)yo * dd.ow + xo : ((int64_t)yo * dd.ow + xo) * 3 + ch);
       float f = __fdiv_rn((float)v, 255.0f);
@@ -1963,73 +2034,88 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
   if (content && !(p.debug_mask & 0x100)) {  // (debug_mask: timing ablations only)
     hpass(planes + dd.plane_off[0], dd.plane_stride[0], in.comp_hpx[0], T + s.off[kHlPos],
           reinterpret_cast<const int16_t*>(T + s.off[kHlCoef]), s.hl_size, s.hl_taps, xs0, ncl,
-          lr0, lr1, hl, tid, nt);
+          lr0, lr1, hl, lst, tid, nt);
     if (!s.gray) {
       // the two chroma planes share the tables: half the threads each
       const int half = nt >> 1, t2 = tid < half ? tid : tid - half;
       const int c = tid < half ? 1 : 2;
       hpass(planes + dd.plane_off[c], dd.plane_stride[c], in.comp_hpx[c], T + s.off[kHcPos],
             reinterpret_cast<const int16_t*>(T + s.off[kHcCoef]), s.hc_size, s.hc_taps, cx0, ncc,
-            cr0, cr1, c == 1 ? hu : hv, t2, half);
+            cr0, cr1, c == 1 ? hu : hv, cst, t2, half);
     }
   }
   __syncthreads();
   if (content && !(p.debug_mask & 0x200)) {
-    const int16_t* vl_coef = reinterpret_cast<const int16_t*>(T + s.off[kVlCoef]);
-    const int16_t* vc_coef = reinterpret_cast<const int16_t*>(T + s.off[kVcCoef]);
-    const int32_t* vmode = T + s.off[kVmode];
     // vertical taps + RGB24 writer, one scaled column per thread
+    const int npl = s.vl_size / 2, npc = s.vc_size / 2;  // tap pairs per row
     for (int cl = tid; cl < ncl; cl += nt) {
       const int xs = xs0 + cl;
       const int cc = (s.full ? xs : xs >> 1) - cx0;
+      const uint32_t* lcol = reinterpret_cast<const uint32_t*>(hl + cl * lst);
+      const uint32_t* ucol = reinterpret_cast<const uint32_t*>(hu + cc * cst);
+      const uint32_t* vcol = reinterpret_cast<const uint32_t*>(hv + cc * cst);
       for (int ys = ys0; ys < ys1; ys++) {
-        const int m = vmode[ys];
+        const uint32_t* row = vt + (ys - ys0) * vrw;
+        const uint4 hdr = *reinterpret_cast<const uint4*>(row);
+        const int m = (int)hdr.x;
         const int mode = m & 15, ya = (m >> 4) & 8191, ua = (m >> 17) & 8191;
-        const int16_t* lcol = hl + (vl_pos[ys] - lr0) * ncl + cl;
+        const uint32_t* lf = row + 4;  // luma tap pairs, then chroma
+        const uint32_t* cf = lf + npl;
+        const int lp = (int)hdr.y, cp = (int)hdr.z;
         int rgb[3];
         int Y, U = 0, V = 0;
-        const int16_t* ucol = hu;
-        const int16_t* vcol = hv;
-        const int16_t* cf = vc_coef;
-        if (!s.gray) {
-          const int cp = vc_pos[ys] - cr0;
-          ucol = hu + cp * ncc + cc;
-          vcol = hv + cp * ncc + cc;
-          cf = vc_coef + (int64_t)ys * s.vc_size;
-        }
         if (s.full) {
           if (mode == kSwsTwo) {
-            Y = ((int)lcol[0] * (4096 - ya) + (int)lcol[ncl] * ya) >> 10;
+            int a, b;
+            vpair(lcol, lp, a, b);
+            Y = (a * (4096 - ya) + b * ya) >> 10;
           } else if (mode == kSwsOne) {
-            Y = (int)lcol[0] * 4;
+            int a, b;
+            vpair(lcol, lp, a, b);
+            Y = a * 4;
           } else {
-            Y = ((1 << 9) + vdot(lcol, ncl, vl_coef + (int64_t)ys * s.vl_size, s.vl_taps)) >> 10;
+            Y = ((1 << 9) + vdot_pairs(lcol, lp, lf, npl)) >> 10;
           }
           if (!s.gray) {
             if (mode == kSwsX) {
-              U = ((1 << 9) - (128 << 19) + vdot(ucol, ncc, cf, s.vc_taps)) >> 10;
-              V = ((1 << 9) - (128 << 19) + vdot(vcol, ncc, cf, s.vc_taps)) >> 10;
+              U = ((1 << 9) - (128 << 19) + vdot_pairs(ucol, cp, cf, npc)) >> 10;
+              V = ((1 << 9) - (128 << 19) + vdot_pairs(vcol, cp, cf, npc)) >> 10;
             } else {
-              const int o1 = ua ? ncc : 0;
-              U = ((int)ucol[0] * (4096 - ua) + (int)ucol[o1] * ua - (128 << 19)) >> 10;
-              V = ((int)vcol[0] * (4096 - ua) + (int)vcol[o1] * ua - (128 << 19)) >> 10;
+              int u0, u1, v0, v1;
+              vpair(ucol, cp, u0, u1);
+              vpair(vcol, cp, v0, v1);
+              if (!ua) {
+                u1 = u0;
+                v1 = v0;
+              }
+              U = (u0 * (4096 - ua) + u1 * ua - (128 << 19)) >> 10;
+              V = (v0 * (4096 - ua) + v1 * ua - (128 << 19)) >> 10;
             }
           }
           full_rgb(p, Y, U, V, rgb);
         } else {
           if (mode == kSwsX) {
-            Y = ((1 << 18) + vdot(lcol, ncl, vl_coef + (int64_t)ys * s.vl_size, s.vl_taps)) >> 19;
-            U = ((1 << 18) + vdot(ucol, ncc, cf, s.vc_taps)) >> 19;
-            V = ((1 << 18) + vdot(vcol, ncc, cf, s.vc_taps)) >> 19;
-          } else if (mode == kSwsTwo) {
-            Y = ((int)lcol[0] * (4096 - ya) + (int)lcol[ncl] * ya) >> 19;
-            U = ((int)ucol[0] * (4096 - ua) + (int)ucol[ncc] * ua) >> 19;
-            V = ((int)vcol[0] * (4096 - ua) + (int)vcol[ncc] * ua) >> 19;
+            Y = ((1 << 18) + vdot_pairs(lcol, lp, lf, npl)) >> 19;
+            U = ((1 << 18) + vdot_pairs(ucol, cp, cf, npc)) >> 19;
+            V = ((1 << 18) + vdot_pairs(vcol, cp, cf, npc)) >> 19;
           } else {
-            const int o1 = ua ? ncc : 0;
-            Y = ((int)lcol[0] + 64) >> 7;
-            U = ((int)ucol[0] * (4096 - ua) + (int)ucol[o1] * ua + (128 << 11)) >> 19;
-            V = ((int)vcol[0] * (4096 - ua) + (int)vcol[o1] * ua + (128 << 11)) >> 19;
+            int y0, y1, u0, u1, v0, v1;
+            vpair(lcol, lp, y0, y1);
+            vpair(ucol, cp, u0, u1);
+            vpair(vcol, cp, v0, v1);
+            if (mode == kSwsTwo) {
+              Y = (y0 * (4096 - ya) + y1 * ya) >> 19;
+              U = (u0 * (4096 - ua) + u1 * ua) >> 19;
+              V = (v0 * (4096 - ua) + v1 * ua) >> 19;
+            } else {
+              if (!ua) {
+                u1 = u0;
+                v1 = v0;
+              }
+              Y = (y0 + 64) >> 7;
+              U = (u0 * (4096 - ua) + u1 * ua + (128 << 11)) >> 19;
+              V = (v0 * (4096 - ua) + v1 * ua + (128 << 11)) >> 19;
+            }
           }
           rgb[0] = clip_i8(Y + tab_off(p.crv, V));
           rgb[1] = clip_i8(Y + tab_off(p.cgu, U) + tab_off(p.cgv, V));
@@ -2086,9 +2172,12 @@ __global__ void planes_copy_kernel(const uint8_t* __restrict__ planes,
 // launchers (host side, same TU)
 // ---------------------------------------------------------------------------
 
-hipError_t launch_parse(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
-                        HuffTable* luts, int n, hipStream_t st) {
-  hipLaunchKernelGGL(parse_kernel, dim3(n), dim3(256), 0, st, bytes, desc, infos, luts);
+hipError_t launch_parse(const uint8_t* bytes, const ImageDesc* host_desc, ImageDesc* desc,
+                        ImageInfo* infos, HuffTable* luts, const void* host_tables, void* tables,
+                        int64_t table_bytes, int n, hipStream_t st) {
+  hipLaunchKernelGGL(parse_kernel, dim3(n), dim3(256), 0, st, bytes, host_desc, desc, infos, luts,
+                     static_cast<const uint4*>(host_tables), static_cast<uint4*>(tables),
+                     (table_bytes + 15) / 16);
   return hipGetLastError();
 }
 hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
@@ -2133,10 +2222,12 @@ hipError_t launch_idct(const uint32_t* ents, const uint2* bdesc, const ImageDesc
   return hipGetLastError();
 }
 hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
-                      void* out, const BatchParams& p, int64_t max_px, int n, hipStream_t st) {
+                      void* out, const BatchParams& p, int64_t max_px, int n, int32_t* host_status,
+                      hipStream_t st) {
   int64_t gx64 = (max_px + 255) / 256;
   int gx = (int)(gx64 < 4096 ? gx64 : 4096);
-  hipLaunchKernelGGL(csc_kernel, dim3(gx, n), dim3(256), 0, st, planes, desc, infos, out, p);
+  hipLaunchKernelGGL(csc_kernel, dim3(gx, n), dim3(256), 0, st, planes, desc, infos, out, p,
+                     host_status);
   return hipGetLastError();
 }
 // ---------------------------------------------------------------------------
@@ -2201,9 +2292,9 @@ hipError_t launch_nv12(const uint8_t* src, uint8_t* dst, int frames, int height,
 
 hipError_t launch_sws(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
                       const int32_t* pool, void* out, const BatchParams& p, int bands, int chunks,
-                      int lds_bytes, int n, hipStream_t st) {
+                      int lds_bytes, int n, int32_t* host_status, hipStream_t st) {
   hipLaunchKernelGGL(sws_kernel, dim3(bands, chunks, n), dim3(256), lds_bytes, st, planes, desc,
-                     infos, pool, out, p);
+                     infos, pool, out, p, host_status);
   return hipGetLastError();
 }
 hipError_t launch_planes_copy(const uint8_t* planes, const ImageDesc* desc,
