@@ -43,7 +43,7 @@ inline HJ_HD uint32_t slot_bits(uint32_t maxbits, int sub_bits) {
 }
 
 // LUT entry (u32), everything a decode step needs precomputed:
-//   [0,5)   bits taken by the code (Full: code + value bits)
+//   [0,5)   bits the symbol takes: code + value bits (<= 16 + 15)
 //   [5,7)   kind
 //   [7,12)  value bits that follow the code (0 for Full)
 //   [12,19) z advance: DC 1, AC coefficient run+1, ZRL 16, EOB or any other
@@ -75,7 +75,7 @@ inline HJ_HD uint32_t hj_entry(uint32_t kind, int len, int sym, bool is_dc, int 
     bad = run != 0;
   }
   const uint32_t sz = kind == kKindFull ? 0u : (uint32_t)size;
-  return (uint32_t)len | (kind << 5) | (sz << 7) | (zinc << 12) | (coef << 19) | (bad << 20) |
+  return ((uint32_t)len + sz) | (kind << 5) | (sz << 7) | (zinc << 12) | (coef << 19) | (bad << 20) |
          (((uint32_t)v & 0x7FFu) << kEntHiShift);
 }
 

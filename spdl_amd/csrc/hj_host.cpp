@@ -640,13 +640,13 @@ struct spdl_hj_ctx {
   bool profiling = false;
   float timings[kStages] = {};
   int ntimings = 0;
-  int sub_bits = 512;
+  int sub_bits = 384;
   int debug_mask = 0;
   // the first kernel pulls descriptors + tables from pinned memory and the
   // last writes statuses back (1), or DMA copies do it (0; kept for A/B)
   int host_staging = 1;
   int entropy_threads = 512;
-  int warm_slots = 8;  // entropy round 0: slots decoded before a run's first slot
+  int warm_slots = 12;  // entropy round 0: slots decoded before a run's first slot
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
   PlanCache plans;          // swscale plans per distinct geometry
 };

@@ -652,10 +652,9 @@ __constant__ uint8_t kNatOrder[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32
 constexpr int kWinWords = HJ_WIN_WORDS;  // bit-reader window per thread (words)
 
 
-// NTAB = distinct Huffman tables the workgroup holds in LDS.  The common case
-// (luma + chroma DC/AC: 4 tables, gray: 2) runs the NTAB = 4 instance, small
-// enough for three entropy workgroups per CU; an image whose scan uses 5-6
-// distinct tables is left to the NTAB = 6 instance launched after it.
+// NTAB = distinct Huffman tables the workgroup holds in LDS: 4 covers luma +
+// chroma DC/AC (gray: 2) and keeps three entropy workgroups per CU; a scan
+// with 5-6 distinct tables reads the extra ones from their HBM copies.
 template <int NT, int NTAB>
 struct EntShared {
   static constexpr int kTabs = NTAB;
@@ -698,25 +697,19 @@ static_assert(sizeof(EntShared<512, 4>) <= 160 * 1024 / 3,
 // never stall it (on gfx9 a vmcnt wait for a load also waits for older
 // stores).
 //
-// HJ_POS_READER (default): the state is the bit position alone; each step
-// reads the two window words holding bits [pos, pos + 32) (one
-// ds_read2st64) and funnel-shifts them -- no bit buffer to refill, no
-// branch.  Otherwise a 64-bit buffer with a refill step (kept for A/B).
-#ifndef HJ_POS_READER
-#define HJ_POS_READER 1
-#endif
+// The state is the bit position alone; each step reads the two window words
+// holding bits [pos, pos + 32) (one ds_read2st64) and shifts them -- no bit
+// buffer to refill, no branch.  The window is stored in reverse word order
+// so the pair lands in a register pair as (lo, hi) = (word w + 1, word w),
+// ready for one 64-bit shift.
 struct Dec {
-#if HJ_POS_READER != 1
-  uint64_t buf;  // the next 33..64 bits MSB-first
-  uint32_t nxt;  // the word after them
-  uint32_t wi;   // absolute word index of nxt
-  int cnt;
-#endif
   uint32_t wb;   // absolute word index of the window's first word
   uint32_t pos;  // absolute bit position of the next symbol
   uint32_t z;    // next coefficient index (0 = DC)
   uint32_t bs;   // 2 * block-in-MCU
 };
+
+__device__ __forceinline__ constexpr int win_slot(int i) { return kWinWords - 1 - i; }
 
 template <int NT>
 __device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, uint32_t wb) {
@@ -725,26 +718,16 @@ __device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, 
   uint4 q[kWinWords / 4];
 #pragma unroll
   for (int i = 0; i < kWinWords / 4; i++) q[i] = src[i];
-#if HJ_POS_READER
   // stored MSB-first (byte-swapped once here instead of at every read)
 #pragma unroll
   for (int i = 0; i < kWinWords / 4; i++) {
-    q[i].x = __builtin_bswap32(q[i].x);
-    q[i].y = __builtin_bswap32(q[i].y);
-    q[i].z = __builtin_bswap32(q[i].z);
-    q[i].w = __builtin_bswap32(q[i].w);
-  }
-#endif
-#pragma unroll
-  for (int i = 0; i < kWinWords / 4; i++) {
-    win[(4 * i + 0) * NT] = q[i].x;
-    win[(4 * i + 1) * NT] = q[i].y;
-    win[(4 * i + 2) * NT] = q[i].z;
-    win[(4 * i + 3) * NT] = q[i].w;
+    win[win_slot(4 * i + 0) * NT] = __builtin_bswap32(q[i].x);
+    win[win_slot(4 * i + 1) * NT] = __builtin_bswap32(q[i].y);
+    win[win_slot(4 * i + 2) * NT] = __builtin_bswap32(q[i].z);
+    win[win_slot(4 * i + 3) * NT] = __builtin_bswap32(q[i].w);
   }
 }
 
-#if HJ_POS_READER == 1
 template <int NT>
 __device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
                                          uint32_t z, uint32_t bs) {
@@ -767,115 +750,13 @@ __device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32
     win_stage<NT>(win, words, d.wb);
     w = (d.pos >> 5) - d.wb;
   }
-  const uint32_t lo = win[(w + 1) * NT], hi = win[w * NT];
-  return (uint32_t)(((((uint64_t)hi << 32) | lo) << (d.pos & 31u)) >> 32);
+  const uint32_t* pw = win + (kWinWords - 2 - (int)w) * NT;  // word w + 1, then word w
+  const uint64_t lohi = (uint64_t)pw[0] | ((uint64_t)pw[NT] << 32);
+  return (uint32_t)((lohi << (d.pos & 31u)) >> 32);
 }
 
 __device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) { d.pos += nbits; }
-#elif HJ_POS_READER == 2
-// 64-bit register buffer (>= 33 valid bits at every peek), refilled
-// branch-free from a word read from the window one step ahead: the symbol
-// chain carries no window read, only the Huffman table lookup.
-template <int NT>
-__device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
-                                         uint32_t z, uint32_t bs) {
-  const uint32_t w0 = p >> 5;
-  d.wb = w0 & ~3u;
-  win_stage<NT>(win, words, d.wb);
-  const uint64_t hi = win[(w0 - d.wb) * NT];
-  const uint64_t lo = win[(w0 + 1 - d.wb) * NT];
-  d.buf = ((hi << 32) | lo) << (p & 31);
-  d.cnt = 64 - (int)(p & 31);
-  d.wi = w0 + 2;
-  d.nxt = win[(d.wi - d.wb) * NT];
-  d.pos = p;
-  d.z = z;
-  d.bs = bs;
-}
-
-template <int NT>
-__device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
-  if (__any((d.wi - d.wb) >= (uint32_t)(kWinWords - 1))) {
-    d.wb = d.wi & ~3u;
-    win_stage<NT>(win, words, d.wb);
-    d.nxt = win[(d.wi - d.wb) * NT];
-  }
-  return (uint32_t)(d.buf >> 32);
-}
-
-template <int NT>
-__device__ __forceinline__ void dec_skip2(Dec& d, const uint32_t* win, uint32_t nbits) {
-  d.buf <<= nbits;
-  d.cnt -= (int)nbits;
-  d.pos += nbits;
-  const bool r = d.cnt <= 32;
-  d.buf |= r ? ((uint64_t)d.nxt << (32 - d.cnt)) : 0ull;
-  d.cnt += r ? 32 : 0;
-  d.wi += r ? 1u : 0u;
-  d.nxt = win[(d.wi - d.wb) * NT];
-}
-#else
-template <int NT>
-__device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
-                                         uint32_t z, uint32_t bs) {
-  const uint32_t w0 = p >> 5;
-  d.wb = w0 & ~3u;
-  win_stage<NT>(win, words, d.wb);
-  const uint64_t hi = __builtin_bswap32(win[(w0 - d.wb) * NT]);
-  const uint64_t lo = __builtin_bswap32(win[(w0 + 1 - d.wb) * NT]);
-  d.buf = ((hi << 32) | lo) << (p & 31);
-  d.cnt = 64 - (int)(p & 31);
-  d.wi = w0 + 2;
-  d.nxt = win[(d.wi - d.wb) * NT];
-  d.pos = p;
-  d.z = z;
-  d.bs = bs;
-}
-
-template <int NT>
-__device__ __forceinline__ void dec_refill(Dec& d, const uint32_t* win) {
-  if (d.cnt <= 32) {
-    d.buf |= (uint64_t)__builtin_bswap32(d.nxt) << (32 - d.cnt);
-    d.cnt += 32;
-    d.wi++;
-    d.nxt = win[(d.wi - d.wb) * NT];  // in the window: see dec_restage
-  }
-}
-
-// Wave-uniform window restage: when any active lane is about to read past its
-// window, every active lane restages from its own position.  The global load
-// and its vmcnt wait (which on gfx9 also waits for the lane's older record
-// stores) then happen once per ~40 symbol steps of the wave instead of in
-// most steps (a per-lane restage fires in ~3/4 of the iterations of a
-// 64-lane wave).  Keeps wi - wb <= kWinWords - 1 after the next refill.
-template <int NT>
-__device__ __forceinline__ void dec_restage(Dec& d, uint32_t* win, const uint32_t* words) {
-  if (__any((d.wi - d.wb) >= (uint32_t)(kWinWords - 1))) {
-    d.wb = d.wi & ~3u;
-    win_stage<NT>(win, words, d.wb);
-    d.nxt = win[(d.wi - d.wb) * NT];
-  }
-}
-
-template <int NT>
-__device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
-  dec_restage<NT>(d, win, words);
-  dec_refill<NT>(d, win);
-  return (uint32_t)(d.buf >> 32);
-}
-
-__device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) {
-  d.buf <<= nbits;
-  d.cnt -= (int)nbits;
-  d.pos += nbits;
-}
-#endif
-
-#if HJ_POS_READER == 2
-#define HJ_DEC_SKIP(d, n) dec_skip2<NT>(d, win, n)
-#else
 #define HJ_DEC_SKIP(d, n) dec_skip(d, n)
-#endif
 
 // Canonical decode of a code that is not fully resolved by the LUT (longer
 // than kLutBits, or a DC size > 15): returns a kKindCode entry, 0 if invalid.
@@ -945,7 +826,7 @@ __device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
     const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
     // entry 0 (invalid) takes one bit, advances nothing and starts no block
-    const uint32_t nbits = max((e & 31u) + __builtin_amdgcn_ubfe(e, 7, 5), 1u);  // <= 31
+    const uint32_t nbits = max(e & 31u, 1u);  // code + value bits, <= 31
     nblk += is_dc ? (int)__builtin_amdgcn_ubfe(e, 19, 1) : 0;  // DC: coef bit = valid
     HJ_DEC_SKIP(d, nbits);
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
@@ -970,7 +851,7 @@ __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32
     const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
     const uint32_t t = __builtin_amdgcn_ubfe(tmap, 9u + c * 3u, 3);
     const uint32_t e = lookup<SLOW>(S, t, hi, false);
-    const uint32_t nbits = max((e & 31u) + __builtin_amdgcn_ubfe(e, 7, 5), 1u);
+    const uint32_t nbits = max(e & 31u, 1u);
     HJ_DEC_SKIP(d, nbits);
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool bend = zn >= 64u;
@@ -1001,11 +882,19 @@ struct BlockOut {
 };
 
 __device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e) {
+#if HJ_XP_NOENT
+  if (e == 0x12345u) o.ents[0] = e;
+#else
   *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.ents) + (min(o.cur, o.last) << 2)) = e;
+#endif
 }
 
 __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
+#if HJ_XP_NOBD
+  if (o.dcv == 0x12345) o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
+#else
   o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
+#endif
   o.cur = (o.cur + 3u) & ~3u;
   o.open = false;
 }
@@ -1036,7 +925,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 9u) + c * 3u, 3);
     const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
-    const uint32_t nbits = (e & 31u) + sz;
+    const uint32_t nbits = e & 31u;
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool coef = (e >> 19) & 1u;
     // (bitwise, not short-circuit: one exit test instead of nested branches)
@@ -1071,7 +960,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
     const bool valid = e != 0u;
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
-    const uint32_t nbits = valid ? (e & 31u) + sz : 1u;
+    const uint32_t nbits = valid ? e & 31u : 1u;
     const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
     const uint32_t msk = (1u << sz) - 1u;
     const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
