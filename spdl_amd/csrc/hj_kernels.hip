@@ -871,6 +871,11 @@ __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32
 // * 64; a block has at most 63 AC entries, its list starts 16-byte aligned),
 // so no buffer needs clearing and nothing is scattered: HBM sees ~4 bytes per
 // non-zero coefficient.
+#ifndef HJ_ENT_PACK
+#define HJ_ENT_PACK 4  // entries per store (1, 2 or 4; lists start 16-byte aligned)
+#endif
+constexpr uint32_t kEntPack = HJ_ENT_PACK;
+
 struct BlockOut {
   uint32_t* ents;
   uint2* bdesc;
@@ -879,17 +884,40 @@ struct BlockOut {
   uint32_t bstart;  // first entry of the open block
   int dcv;          // its DC difference
   bool open;        // a block of this run is being decoded
+  uint32_t pk[kEntPack];  // entries not yet stored (kEntPack > 1)
 };
 
+__device__ __forceinline__ void store_pack(BlockOut& o) {
+  const uint32_t base = min(o.cur & ~(kEntPack - 1u), o.last & ~(kEntPack - 1u));
+  char* a = reinterpret_cast<char*>(o.ents) + (base << 2);
+  if constexpr (kEntPack == 4)
+    *reinterpret_cast<uint4*>(a) = make_uint4(o.pk[0], o.pk[1], o.pk[2], o.pk[3]);
+  else if constexpr (kEntPack == 2)
+    *reinterpret_cast<uint2*>(a) = make_uint2(o.pk[0], o.pk[1]);
+  else
+    *reinterpret_cast<uint32_t*>(a) = o.pk[0];
+}
+
+// entry e at o.cur (the caller advances o.cur)
 __device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e) {
 #if HJ_XP_NOENT
   if (e == 0x12345u) o.ents[0] = e;
 #else
-  *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.ents) + (min(o.cur, o.last) << 2)) = e;
+  if constexpr (kEntPack == 1) {
+    *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.ents) + (min(o.cur, o.last) << 2)) = e;
+  } else {
+    const uint32_t k = o.cur & (kEntPack - 1u);
+#pragma unroll
+    for (uint32_t i = 0; i < kEntPack; i++) o.pk[i] = k == i ? e : o.pk[i];
+    if (k == kEntPack - 1u) store_pack(o);
+  }
 #endif
 }
 
 __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
+  if constexpr (kEntPack > 1) {
+    if (o.cur & (kEntPack - 1u)) store_pack(o);  // the partial pack (its tail is unused)
+  }
 #if HJ_XP_NOBD
   if (o.dcv == 0x12345) o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
 #else
@@ -1318,6 +1346,8 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       o.bstart = o.cur;
       o.dcv = 0;
       o.open = false;
+#pragma unroll
+      for (uint32_t i = 0; i < kEntPack; i++) o.pk[i] = 0u;
       Dec d;
       for (int k = r0; k < r1 && rc == kOk; k++) {
         if (slot_empty(k)) {
