@@ -49,7 +49,7 @@ const char* jo_strerror(int code) {
   switch (code) {
     case JO_OK: return "ok";
     case JO_ERR_NOT_JPEG: return "not a JPEG (missing SOI)";
-    case JO_ERR_UNSUPPORTED: return "unsupported JPEG (progressive/arithmetic/12-bit/CMYK/multi-scan)";
+    case JO_ERR_UNSUPPORTED: return "unsupported JPEG (arithmetic/lossless/12-bit/CMYK)";
     case JO_ERR_BAD_HEADER: return "corrupt JPEG header";
     case JO_ERR_BAD_HUFFMAN: return "corrupt entropy-coded data";
     case JO_ERR_TRUNCATED: return "truncated entropy-coded data";
@@ -126,7 +126,8 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
         s += 17 + total;
         n -= 17 + total;
       }
-    } else if (m == 0xC0 || m == 0xC1) { /* SOF0 / SOF1 (Huffman, sequential) */
+    } else if (m == 0xC0 || m == 0xC1 || m == 0xC2) { /* SOF0/1 sequential, SOF2 progressive */
+      info->progressive = m == 0xC2;
       if (n < 6) return JO_ERR_BAD_HEADER;
       if (s[0] != 8) return JO_ERR_UNSUPPORTED;
       info->height = be16(s + 1);
@@ -147,16 +148,19 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
           return JO_ERR_BAD_HEADER;
       }
       have_sof = 1;
-    } else if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) ||
-               (m >= 0xC9 && m <= 0xCB) || (m >= 0xCD && m <= 0xCF)) {
-      return JO_ERR_UNSUPPORTED; /* progressive, lossless, hierarchical, arithmetic */
+    } else if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
+               (m >= 0xCD && m <= 0xCF)) {
+      return JO_ERR_UNSUPPORTED; /* lossless, hierarchical, arithmetic */
     } else if (m == 0xDD) { /* DRI */
       if (n < 2) return JO_ERR_BAD_HEADER;
       info->restart_interval = be16(s);
     } else if (m == 0xDA) { /* SOS */
       if (!have_sof) return JO_ERR_BAD_HEADER;
       int ns = s[0];
-      if (ns != info->ncomp) return JO_ERR_UNSUPPORTED; /* multi-scan sequential */
+      if (ns < 1 || ns > info->ncomp) return JO_ERR_BAD_HEADER;
+      /* progressive, or sequential with non-interleaved scans: the first scan
+       * fixes nothing beyond the frame; every scan is walked at decode time */
+      info->multiscan = info->progressive || ns != info->ncomp;
       if (n < 1 + 2 * ns + 3) return JO_ERR_BAD_HEADER;
       int order[JO_MAX_COMP];
       for (int i = 0; i < ns; i++) {
@@ -170,8 +174,10 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
         if (info->comp_td[c] > 3 || info->comp_ta[c] > 3) return JO_ERR_BAD_HEADER;
       }
       int ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahal = s[3 + 2 * ns];
-      if (ss != 0 || se != 63 || ahal != 0) return JO_ERR_UNSUPPORTED;
+      if (!info->multiscan && (ss != 0 || se != 63 || ahal != 0)) return JO_ERR_UNSUPPORTED;
       info->scan_start = pos;
+      if (info->multiscan) /* blocks of an MCU in frame component order */
+        for (int i = 0; i < info->ncomp; i++) order[i] = i;
       /* geometry */
       int hmax = 1, vmax = 1;
       for (int c = 0; c < info->ncomp; c++) {
@@ -182,8 +188,8 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
       info->vmax = vmax;
       for (int c = 0; c < info->ncomp; c++) {
         if (hmax % info->comp_h[c] || vmax % info->comp_v[c]) return JO_ERR_UNSUPPORTED;
-        if (!qt_have[info->comp_tq[c]] || !dc_have[info->comp_td[c]] ||
-            !ac_have[info->comp_ta[c]])
+        if (!info->multiscan && (!qt_have[info->comp_tq[c]] || !dc_have[info->comp_td[c]] ||
+                                 !ac_have[info->comp_ta[c]]))
           return JO_ERR_BAD_HEADER;
         info->comp_w[c] = (info->width * info->comp_h[c] + hmax - 1) / hmax;
         info->comp_h_px[c] = (info->height * info->comp_v[c] + vmax - 1) / vmax;
@@ -199,7 +205,7 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
         info->mcux = (info->width + 8 * hmax - 1) / (8 * hmax);
         info->mcuy = (info->height + 8 * vmax - 1) / (8 * vmax);
         int b = 0;
-        for (int i = 0; i < ns; i++) {
+        for (int i = 0; i < (info->multiscan ? info->ncomp : ns); i++) {
           int c = order[i];
           info->comp_bw[c] = info->mcux * info->comp_h[c];
           info->comp_bh[c] = info->mcuy * info->comp_v[c];
@@ -350,8 +356,326 @@ static inline int16_t clip16(int32_t v) {
   return v < -32768 ? -32768 : v > 32767 ? 32767 : (int16_t)v;
 }
 
+/* ------------------------------------------------------------------------ */
+/* Multi-scan images: progressive (SOF2) and sequential with non-interleaved */
+/* scans.  Every scan adds to one level accumulator per coefficient (zig-zag */
+/* index, per block in MCU order); the levels are dequantised FFmpeg-style at */
+/* the end (block[j] = level * q, DC biased by 1024, int16).                 */
+/* Scan semantics: T.81 G.1.2 as libjpeg 9d implements them (jdphuff.c      */
+/* decode_mcu_DC_first / DC_refine / AC_first / AC_refine; jdhuff.c for the  */
+/* sequential scans), which is what tests/golden pins; FFmpeg's mjpegdec     */
+/* (decode_dc_progressive, decode_block_progressive, decode_block_refinement)*/
+/* computes the same values on valid streams.                                */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+  int ns, comp[JO_MAX_COMP], td[JO_MAX_COMP], ta[JO_MAX_COMP];
+  int ss, se, ah, al;
+} scan_t;
+
+/* MCU-order block index of component c's block (bx, by) in its block grid */
+static size_t ms_block(const jo_info* info, int c, int bx, int by) {
+  if (info->ncomp == 1) return (size_t)by * info->mcux + bx;
+  int b0 = 0;
+  for (int k = 0; k < c; k++) b0 += info->comp_h[k] * info->comp_v[k];
+  int mx = bx / info->comp_h[c], my = by / info->comp_v[c];
+  int b = b0 + (by % info->comp_v[c]) * info->comp_h[c] + (bx % info->comp_h[c]);
+  return ((size_t)my * info->mcux + mx) * info->bpm + b;
+}
+
+/* one block of one scan; lev: the block's 64 levels (zig-zag index) */
+static int ms_block_decode(bitrd_t* br, const jo_info* info, const scan_t* sc, int progressive,
+                           const huff_t* dh, const huff_t* ah, int32_t* pred, int32_t* lev,
+                           int* eobrun) {
+  if (!progressive) { /* sequential scan: DC + AC of the block */
+    int s = huff_decode(br, dh);
+    if (s < 0 || s > 15) return JO_ERR_BAD_HUFFMAN;
+    *pred += s ? extend(br_get(br, s), s) : 0;
+    lev[0] = *pred;
+    for (int k = 1; k < 64;) {
+      int rs = huff_decode(br, ah);
+      if (rs < 0) return JO_ERR_BAD_HUFFMAN;
+      int r = rs >> 4;
+      s = rs & 15;
+      if (s == 0) {
+        if (r == 15) { k += 16; continue; }
+        if (r != 0) return JO_ERR_BAD_HUFFMAN;
+        break;
+      }
+      k += r;
+      if (k > 63) return JO_ERR_BAD_HUFFMAN;
+      lev[k++] = extend(br_get(br, s), s);
+    }
+    return JO_OK;
+  }
+  const int al = sc->al;
+  if (sc->ss == 0) {
+    if (sc->ah == 0) { /* DC first: the difference, scaled by 2^Al */
+      int s = huff_decode(br, dh);
+      if (s < 0 || s > 15) return JO_ERR_BAD_HUFFMAN;
+      *pred += s ? extend(br_get(br, s), s) : 0;
+      lev[0] = (int32_t)((uint32_t)*pred << al);
+    } else if (br_get(br, 1)) { /* DC refine: one bit */
+      lev[0] |= 1 << al;
+    }
+    return JO_OK;
+  }
+  if (sc->ah == 0) { /* AC first */
+    if (*eobrun > 0) {
+      (*eobrun)--;
+      return JO_OK;
+    }
+    for (int k = sc->ss; k <= sc->se; k++) {
+      int rs = huff_decode(br, ah);
+      if (rs < 0) return JO_ERR_BAD_HUFFMAN;
+      int r = rs >> 4, s = rs & 15;
+      if (s) {
+        k += r;
+        if (k > sc->se) return JO_ERR_BAD_HUFFMAN;
+        lev[k] = (int32_t)((uint32_t)extend(br_get(br, s), s) << al);
+      } else if (r == 15) {
+        k += 15;
+      } else {
+        *eobrun = (1 << r) - 1;
+        if (r) *eobrun += (int)br_get(br, r);
+        break;
+      }
+    }
+    return JO_OK;
+  }
+  /* AC refine: new coefficients are +-1 at bit Al; every coefficient already
+   * non-zero that the scan passes gets one correction bit */
+  const int32_t p1 = 1 << al, m1 = -(1 << al);
+  int k = sc->ss;
+  if (*eobrun <= 0) {
+    for (; k <= sc->se; k++) {
+      int rs = huff_decode(br, ah);
+      if (rs < 0) return JO_ERR_BAD_HUFFMAN;
+      int r = rs >> 4, s = rs & 15;
+      int32_t v = 0;
+      if (s) {
+        if (s != 1) return JO_ERR_BAD_HUFFMAN;
+        v = br_get(br, 1) ? p1 : m1;
+      } else if (r != 15) {
+        *eobrun = 1 << r;
+        if (r) *eobrun += (int)br_get(br, r);
+        break; /* the rest of the block refines below */
+      }
+      /* skip r zero-history coefficients, refining the non-zero ones */
+      for (; k <= sc->se; k++) {
+        int32_t* c = &lev[k];
+        if (*c != 0) {
+          if (br_get(br, 1) && (*c & p1) == 0) *c += *c >= 0 ? p1 : m1;
+        } else {
+          if (r == 0) break;
+          r--;
+        }
+      }
+      if (k > sc->se) {
+        if (v) return JO_ERR_BAD_HUFFMAN; /* a new coefficient past Se */
+        break;
+      }
+      if (v) lev[k] = v;
+    }
+  }
+  if (*eobrun > 0) {
+    for (; k <= sc->se; k++) {
+      int32_t* c = &lev[k];
+      if (*c != 0 && br_get(br, 1) && (*c & p1) == 0) *c += *c >= 0 ? p1 : m1;
+    }
+    (*eobrun)--;
+  }
+  return JO_OK;
+}
+
+/* Decode one scan whose entropy data starts at `pos`; returns the byte
+ * position after it (the next marker) in *end. */
+static int ms_scan(const uint8_t* d, size_t size, size_t pos, const jo_info* info,
+                   const scan_t* sc, int ri, const huff_t* dct, const huff_t* act, int32_t* lev,
+                   size_t* end) {
+  bitrd_t br;
+  memset(&br, 0, sizeof(br));
+  br.d = d;
+  br.size = size;
+  br.pos = pos;
+  int32_t pred[JO_MAX_COMP] = {0};
+  int eobrun = 0;
+  const int prog = info->progressive;
+  /* interleaved: MCUs of the frame; one component: its blocks in raster
+   * order over its own (unpadded) block grid, one block per MCU */
+  int nmcu, bw1 = 0;
+  if (sc->ns > 1) {
+    nmcu = info->mcux * info->mcuy;
+  } else {
+    int c = sc->comp[0];
+    bw1 = info->ncomp == 1 ? info->mcux : (info->comp_w[c] + 7) / 8;
+    int bh1 = info->ncomp == 1 ? info->mcuy : (info->comp_h_px[c] + 7) / 8;
+    nmcu = bw1 * bh1;
+  }
+  for (int mcu = 0; mcu < nmcu; mcu++) {
+    if (ri && mcu && mcu % ri == 0) {
+      if (br.used_bits > br.real_bits) return JO_ERR_TRUNCATED;
+      size_t p = br.pos;
+      for (;;) {
+        if (p >= size) return JO_ERR_BAD_RESTART;
+        if (d[p] == 0xFF && p + 1 < size && d[p + 1] == 0x00) { p += 2; continue; }
+        if (d[p] == 0xFF) break;
+        p++;
+      }
+      while (p < size && d[p] == 0xFF) p++;
+      if (p >= size || d[p] < 0xD0 || d[p] > 0xD7) return JO_ERR_BAD_RESTART;
+      br.pos = p + 1;
+      br.buf = 0;
+      br.cnt = 0;
+      br.hit_marker = 0;
+      br.real_bits = br.used_bits = 0;
+      for (int c = 0; c < JO_MAX_COMP; c++) pred[c] = 0;
+      eobrun = 0;
+    }
+    for (int i = 0; i < sc->ns; i++) {
+      const int c = sc->comp[i];
+      const huff_t* dh = &dct[sc->td[i]];
+      const huff_t* ah = &act[sc->ta[i]];
+      if (sc->ns > 1) {
+        int mx = mcu % info->mcux, my = mcu / info->mcux;
+        for (int y = 0; y < info->comp_v[c]; y++)
+          for (int x = 0; x < info->comp_h[c]; x++) {
+            size_t b = ms_block(info, c, mx * info->comp_h[c] + x, my * info->comp_v[c] + y);
+            int rc = ms_block_decode(&br, info, sc, prog, dh, ah, &pred[c], lev + b * 64, &eobrun);
+            if (rc) return rc;
+          }
+      } else {
+        size_t b = ms_block(info, c, mcu % bw1, mcu / bw1);
+        int rc = ms_block_decode(&br, info, sc, prog, dh, ah, &pred[c], lev + b * 64, &eobrun);
+        if (rc) return rc;
+      }
+    }
+  }
+  if (br.used_bits > br.real_bits) return JO_ERR_TRUNCATED;
+  /* the next marker: past the bytes the reader took (stuffed 0xFF00 pairs
+   * included), then skip to a marker that is not RSTn */
+  size_t p = br.pos;
+  for (;;) {
+    while (p < size && d[p] != 0xFF) p++;
+    if (p + 1 >= size) break;
+    if (d[p + 1] == 0x00 || (d[p + 1] >= 0xD0 && d[p + 1] <= 0xD7)) { p += 2; continue; }
+    break;
+  }
+  *end = p;
+  return JO_OK;
+}
+
+static int ms_decode(const uint8_t* d, size_t size, const jo_info* info, int16_t* coefs,
+                     int16_t* levels) {
+  int32_t* lev = (int32_t*)calloc((size_t)info->nblocks * 64, sizeof(int32_t));
+  if (!lev) return JO_ERR_UNSUPPORTED;
+  huff_t dct[4], act[4];
+  memset(dct, 0, sizeof(dct));
+  memset(act, 0, sizeof(act));
+  int comp_id[JO_MAX_COMP] = {0};
+  int ri = 0, rc = JO_OK, nscan = 0;
+  size_t pos = 2;
+  for (;;) {
+    while (pos < size && d[pos] != 0xFF) pos++;
+    while (pos < size && d[pos] == 0xFF) pos++;
+    if (pos >= size) break; /* no EOI: what was decoded stands */
+    int m = d[pos++];
+    if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+    if (m == 0xD9) break;
+    if (pos + 2 > size) { rc = JO_ERR_BAD_HEADER; break; }
+    int len = be16(d + pos);
+    if (len < 2 || pos + (size_t)len > size) { rc = JO_ERR_BAD_HEADER; break; }
+    const uint8_t* s = d + pos + 2;
+    int n = len - 2;
+    pos += (size_t)len;
+    if (m == 0xC4) {
+      while (n >= 17) {
+        int tc = s[0] >> 4, th = s[0] & 15, total = 0;
+        uint8_t bits[17], vals[256];
+        bits[0] = 0;
+        for (int l = 1; l <= 16; l++) { bits[l] = s[l]; total += s[l]; }
+        if (tc > 1 || th > 3 || total > 256 || n < 17 + total || !check_huff(bits)) {
+          rc = JO_ERR_BAD_HEADER;
+          break;
+        }
+        memset(vals, 0, sizeof(vals));
+        memcpy(vals, s + 17, (size_t)total);
+        build_huff(bits, vals, tc ? &act[th] : &dct[th]);
+        s += 17 + total;
+        n -= 17 + total;
+      }
+      if (rc) break;
+    } else if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
+      for (int c = 0; c < info->ncomp && 8 + 3 * c < len; c++) comp_id[c] = s[6 + 3 * c];
+    } else if (m == 0xDD) {
+      if (n >= 2) ri = be16(s);
+    } else if (m == 0xDA) {
+      scan_t sc;
+      sc.ns = s[0];
+      if (sc.ns < 1 || sc.ns > info->ncomp || n < 1 + 2 * sc.ns + 3) { rc = JO_ERR_BAD_HEADER; break; }
+      for (int i = 0; i < sc.ns; i++) {
+        int cs = s[1 + 2 * i], c = -1;
+        for (int k = 0; k < info->ncomp; k++)
+          if (comp_id[k] == cs) c = k;
+        if (c < 0) { rc = JO_ERR_BAD_HEADER; break; }
+        sc.comp[i] = c;
+        sc.td[i] = s[2 + 2 * i] >> 4;
+        sc.ta[i] = s[2 + 2 * i] & 15;
+        if (sc.td[i] > 3 || sc.ta[i] > 3) { rc = JO_ERR_BAD_HEADER; break; }
+      }
+      if (rc) break;
+      sc.ss = s[1 + 2 * sc.ns];
+      sc.se = s[2 + 2 * sc.ns];
+      sc.ah = s[3 + 2 * sc.ns] >> 4;
+      sc.al = s[3 + 2 * sc.ns] & 15;
+      if (info->progressive) {
+        /* T.81 G.1.1.1.1: DC scans Ss = Se = 0; AC scans one component */
+        if (sc.ss > sc.se || sc.se > 63 || sc.al > 13 || (sc.ss == 0 && sc.se != 0) ||
+            (sc.ss > 0 && sc.ns != 1)) { rc = JO_ERR_BAD_HEADER; break; }
+      } else if (sc.ss != 0 || sc.se != 63 || sc.ah || sc.al) {
+        rc = JO_ERR_BAD_HEADER;
+        break;
+      }
+      size_t end = pos;
+      rc = ms_scan(d, size, pos, info, &sc, ri, dct, act, lev, &end);
+      if (rc) break;
+      pos = end;
+      nscan++;
+    }
+  }
+  if (!rc && !nscan) rc = JO_ERR_BAD_HEADER;
+  if (!rc) {
+    for (int b = 0; b < info->nblocks; b++) {
+      const int c = info->mcu_comp[b % info->bpm];
+      const uint16_t* q = info->qt[info->comp_tq[c]];
+      const int32_t* lv = lev + (size_t)b * 64;
+      int16_t* blk = coefs + (size_t)b * 64;
+      blk[0] = (int16_t)(JO_DC_BIAS + lv[0] * (int32_t)q[0]);
+      for (int k = 1; k < 64; k++) blk[kNatural[k]] = (int16_t)(lv[k] * (int32_t)q[k]);
+    }
+    if (levels) {
+      size_t o = 0;
+      for (int c = 0; c < info->ncomp; c++) {
+        for (int by = 0; by < info->comp_bh[c]; by++)
+          for (int bx = 0; bx < info->comp_bw[c]; bx++) {
+            const int32_t* lv = lev + ms_block(info, c, bx, by) * 64;
+            int16_t* out = levels + o + ((size_t)by * info->comp_bw[c] + bx) * 64;
+            for (int k = 0; k < 64; k++) out[kNatural[k]] = (int16_t)lv[k];
+          }
+        o += (size_t)info->comp_bw[c] * info->comp_bh[c] * 64;
+      }
+    }
+  }
+  free(lev);
+  return rc;
+}
+
 int jo_decode_coefs(const uint8_t* d, size_t size, const jo_info* info, int16_t* coefs,
                     int16_t* levels) {
+  if (info->multiscan) {
+    memset(coefs, 0, (size_t)info->nblocks * 64 * sizeof(int16_t));
+    return ms_decode(d, size, info, coefs, levels);
+  }
   huff_t dct[4], act[4];
   for (int t = 0; t < 4; t++) {
     build_huff(info->dc_bits[t], info->dc_vals[t], &dct[t]);

@@ -44,7 +44,7 @@ extern "C" {
 enum {
   JO_OK = 0,
   JO_ERR_NOT_JPEG = 1,
-  JO_ERR_UNSUPPORTED = 2,   /* progressive / arithmetic / 12-bit / CMYK ... */
+  JO_ERR_UNSUPPORTED = 2,   /* arithmetic / lossless / 12-bit / CMYK ...   */
   JO_ERR_BAD_HEADER = 3,
   JO_ERR_BAD_HUFFMAN = 4,   /* invalid code / run past coefficient 63     */
   JO_ERR_TRUNCATED = 5,     /* entropy data ended before the last MCU      */
@@ -83,6 +83,10 @@ typedef struct {
   uint8_t dc_bits[4][17], dc_vals[4][256];
   uint8_t ac_bits[4][17], ac_vals[4][256];
   size_t scan_start;         /* byte offset of the entropy-coded data */
+  int progressive;           /* SOF2 */
+  int multiscan;             /* the image takes more than one scan (progressive,
+                                or sequential with non-interleaved scans):
+                                jo_decode_coefs walks every scan */
 } jo_info;
 
 typedef struct {

@@ -139,3 +139,65 @@ int lj_decode_rgb(const uint8_t* d, size_t n, uint8_t* out, size_t cap, int* w, 
   jpeg_destroy_decompress(&c);
   return 0;
 }
+
+/* ---- fixture encoder: a sequential (SOF0) JPEG whose components are coded
+ * in separate, non-interleaved scans (one scan per component, Ss=0 Se=63),
+ * the multi-scan sequential layout Pillow cannot write.  rgb: h*w*ncomp
+ * (ncomp 1 or 3), h_samp/v_samp of component 0 (chroma 1x1).  Returns the
+ * JPEG size, or -1 / -(needed) when out_cap is too small. */
+static void dst_init(j_compress_ptr c) { (void)c; }
+static boolean dst_empty(j_compress_ptr c) { (void)c; return FALSE; }
+static void dst_term(j_compress_ptr c) { (void)c; }
+
+long lj_encode_multiscan(const uint8_t* px, int w, int h, int ncomp, int quality, int h0, int v0,
+                         int restart_blocks, uint8_t* out, size_t out_cap) {
+  struct jpeg_compress_struct c;
+  err_t e;
+  struct jpeg_destination_mgr dst;
+  c.err = jpeg_std_error(&e.pub);
+  e.pub.error_exit = on_error;
+  e.pub.emit_message = on_message;
+  if (setjmp(e.jb)) {
+    jpeg_destroy_compress(&c);
+    return -1;
+  }
+  jpeg_create_compress(&c);
+  dst.init_destination = dst_init;
+  dst.empty_output_buffer = dst_empty;
+  dst.term_destination = dst_term;
+  dst.next_output_byte = out;
+  dst.free_in_buffer = out_cap;
+  c.dest = &dst;
+  c.image_width = (JDIMENSION)w;
+  c.image_height = (JDIMENSION)h;
+  c.input_components = ncomp;
+  c.in_color_space = ncomp == 3 ? JCS_RGB : JCS_GRAYSCALE;
+  jpeg_set_defaults(&c);
+  jpeg_set_quality(&c, quality, TRUE);
+  if (ncomp == 3) {
+    c.comp_info[0].h_samp_factor = h0;
+    c.comp_info[0].v_samp_factor = v0;
+  }
+  c.restart_in_rows = 0;
+  c.restart_interval = (unsigned)restart_blocks;
+  static jpeg_scan_info scans[3];
+  for (int i = 0; i < ncomp; i++) {
+    scans[i].comps_in_scan = 1;
+    scans[i].component_index[0] = ncomp - 1 - i; /* reverse order: not the frame order */
+    scans[i].Ss = 0;
+    scans[i].Se = 63;
+    scans[i].Ah = 0;
+    scans[i].Al = 0;
+  }
+  c.scan_info = scans;
+  c.num_scans = ncomp;
+  jpeg_start_compress(&c, TRUE);
+  while (c.next_scanline < c.image_height) {
+    JSAMPROW row = (JSAMPROW)(px + (size_t)c.next_scanline * w * ncomp);
+    jpeg_write_scanlines(&c, &row, 1);
+  }
+  jpeg_finish_compress(&c);
+  long n = (long)(out_cap - dst.free_in_buffer);
+  jpeg_destroy_compress(&c);
+  return n;
+}

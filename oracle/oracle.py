@@ -57,6 +57,8 @@ class _Info(ctypes.Structure):
         ("ac_bits", (ctypes.c_uint8 * 17) * 4),
         ("ac_vals", (ctypes.c_uint8 * 256) * 4),
         ("scan_start", ctypes.c_size_t),
+        ("progressive", ctypes.c_int),
+        ("multiscan", ctypes.c_int),
     ]
 
 
@@ -400,3 +402,24 @@ def lj_decode_rgb(data: bytes) -> np.ndarray:
     if rc:
         raise RuntimeError(f"libjpeg failed ({rc})")
     return out[: w.value * h.value * 3].reshape(h.value, w.value, 3).copy()
+
+
+def lj_encode_multiscan(px: np.ndarray, quality: int = 90, h0: int = 2, v0: int = 2,
+                        restart_blocks: int = 0) -> bytes:
+    """Fixture encoder (libjpeg 9): sequential JPEG with one non-interleaved
+    scan per component, in reverse component order."""
+    L = ljpin()
+    if L is None:
+        raise RuntimeError("libjpeg 9 pin helper not available")
+    px = np.ascontiguousarray(px, np.uint8)
+    h, w = px.shape[:2]
+    nc = 1 if px.ndim == 2 else px.shape[2]
+    cap = h * w * nc * 4 + 65536
+    out = np.zeros(cap, np.uint8)
+    f = L.lj_encode_multiscan
+    f.restype = ctypes.c_long
+    f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_size_t]
+    n = f(px.ctypes.data, w, h, nc, quality, h0, v0, restart_blocks, out.ctypes.data, cap)
+    if n <= 0:
+        raise RuntimeError(f"libjpeg encode failed ({n})")
+    return out[:n].tobytes()

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import functools
 import io
+import os
 
 import numpy as np
 from PIL import Image
@@ -69,13 +70,48 @@ def case(name: str) -> bytes:
         return six_tables(case("q90_444"))
     if name == "large_1080p":
         return _enc(synthetic_pixels(18, 1080, 1920), quality=90, subsampling=2)
+    # progressive (SOF2): DC first/refine + spectral-selection and
+    # successive-approximation AC scans (libjpeg's default script via Pillow)
+    if name == "prog_420":
+        return _enc(synthetic_pixels(19, 240, 320), quality=90, subsampling=2, progressive=True)
+    if name == "prog_444_odd":
+        return _enc(synthetic_pixels(20, 101, 67), quality=85, subsampling=0, progressive=True)
+    if name == "prog_422":
+        return _enc(synthetic_pixels(21, 120, 200), quality=92, subsampling=1, progressive=True)
+    if name == "prog_gray":
+        return _enc(synthetic_pixels(22, 77, 131)[..., 0], quality=80, progressive=True)
+    if name == "prog_optimized":  # per-scan Huffman tables (a DHT before every scan)
+        return _enc(synthetic_pixels(23, 240, 320), quality=90, progressive=True, optimize=True)
+    if name == "prog_restart":
+        return _enc(synthetic_pixels(24, 227, 333), quality=90, progressive=True,
+                    restart_marker_blocks=5)
+    if name == "prog_noise_q100":
+        return _enc(_noise(25, 96, 128), quality=100, subsampling=0, progressive=True)
+    # sequential, one non-interleaved scan per component (reverse order);
+    # Pillow cannot write these: libjpeg 9 wrote the committed files
+    # (tests/gen_golden.py, oracle.lj_encode_multiscan)
+    if name in MULTISCAN:
+        with open(os.path.join(GOLD_JPEG, name + ".jpg"), "rb") as f:
+            return f.read()
     raise KeyError(name)
+
+
+GOLD_JPEG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "jpeg")
+# name -> (pixels seed, h, w, quality, h0, v0, restart blocks)
+MULTISCAN = {
+    "multiscan_420": (30, 240, 320, 90, 2, 2, 0),
+    "multiscan_444_odd": (31, 101, 67, 85, 1, 1, 0),
+    "multiscan_422_rst": (32, 120, 200, 90, 2, 1, 7),
+}
+PROGRESSIVE = ["prog_420", "prog_444_odd", "prog_422", "prog_gray", "prog_optimized",
+               "prog_restart", "prog_noise_q100"]
 
 
 VALID = [
     "q90_420", "q75_420", "q95_420", "q90_444", "q90_422", "odd_227x333", "odd_444_101x67",
     "gray", "gray_odd", "noise_420", "noise_q100", "restart_rows", "restart_blocks",
     "restart_every_mcu", "tiny_8x8", "tiny_1x1", "optimized", "six_tables", "large_1080p",
+    *PROGRESSIVE, *MULTISCAN,
 ]
 
 
@@ -112,6 +148,21 @@ def six_tables(data: bytes) -> bytes:
 
 def progressive() -> bytes:
     return _enc(synthetic_pixels(20, 64, 64), quality=90, progressive=True)
+
+
+def arithmetic() -> bytes:
+    """A baseline file re-labelled SOF9 (arithmetic coding): unsupported."""
+    d = bytearray(case("q90_420"))
+    i = d.index(b"\xff\xc0")
+    d[i + 1] = 0xC9
+    return bytes(d)
+
+
+def cmyk() -> bytes:
+    """A 4-component (Adobe CMYK) JPEG: unsupported."""
+    b = io.BytesIO()
+    Image.fromarray(synthetic_pixels(26, 64, 64)).convert("CMYK").save(b, "JPEG", quality=90)
+    return b.getvalue()
 
 
 def truncated() -> bytes:

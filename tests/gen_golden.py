@@ -38,6 +38,7 @@ CASES = [
     "q90_444", "q90_422", "odd_227x333", "odd_444_101x67", "gray", "gray_odd",
     "noise_q100", "restart_rows", "restart_blocks", "restart_every_mcu", "tiny_8x8",
     "tiny_1x1", "optimized", "six_tables",
+    *cases.PROGRESSIVE, *cases.MULTISCAN,
 ]
 
 PAD224 = O.Resize(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224)
@@ -60,7 +61,13 @@ def main() -> None:
     for name in CASES:
         if only and name not in only:
             continue
-        data = cases.case(name)
+        if name in cases.MULTISCAN:  # libjpeg 9 writes these inputs
+            seed, h, w, q, h0, v0, rst = cases.MULTISCAN[name]
+            from spdl_amd.synthetic import synthetic_pixels
+
+            data = O.lj_encode_multiscan(synthetic_pixels(seed, h, w), q, h0, v0, rst)
+        else:
+            data = cases.case(name)
         with open(os.path.join(GOLD, "jpeg", f"{name}.jpg"), "wb") as f:
             f.write(data)
         comps = O.lj_read_coefs(data)

@@ -63,7 +63,9 @@ def test_host_probe_rejects_garbage():
     with pytest.raises(RuntimeError, match="Failed to decode"):
         _lib.get_image_info(b"\x00" * 64)
     with pytest.raises(RuntimeError, match="Failed to decode"):
-        _lib.get_image_info(cases.progressive())  # unsupported SOF2
+        _lib.get_image_info(cases.arithmetic())  # unsupported SOF9
+    with pytest.raises(RuntimeError, match="Failed to decode"):
+        _lib.get_image_info(cases.cmyk())  # unsupported 4 components
 
 
 @pytest.mark.parametrize("w,h", [(640, 480), (480, 640), (333, 227), (1, 1), (1920, 1080)])

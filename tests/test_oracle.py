@@ -179,7 +179,9 @@ def test_oracle_errors(oracle):
     from tests import cases
 
     with pytest.raises(oracle.OracleError):
-        oracle.decode_rgb(cases.progressive())
+        oracle.decode_rgb(cases.arithmetic())
+    with pytest.raises(oracle.OracleError):
+        oracle.decode_rgb(cases.cmyk())
     with pytest.raises(oracle.OracleError):
         oracle.decode_rgb(cases.truncated())
     with pytest.raises(oracle.OracleError):
