@@ -35,7 +35,7 @@ extern "C" {
 enum spdl_hj_status {
   SPDL_HJ_OK = 0,
   SPDL_HJ_ERR_NOT_JPEG = 1,
-  SPDL_HJ_ERR_UNSUPPORTED = 2,  /* progressive, arithmetic, 12-bit, CMYK, multi-scan */
+  SPDL_HJ_ERR_UNSUPPORTED = 2,  /* arithmetic, lossless, 12-bit, CMYK */
   SPDL_HJ_ERR_BAD_HEADER = 3,
   SPDL_HJ_ERR_BAD_HUFFMAN = 4,
   SPDL_HJ_ERR_TRUNCATED = 5,

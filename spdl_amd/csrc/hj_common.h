@@ -8,7 +8,9 @@
 //   segs    : restart-segment start offsets (bytes into clean), seg_cap each
 //   info    : ImageInfo (device parse result + status)
 //   luts    : HuffTable[8] per image (DC0..3, AC0..3)
-//   coefs   : int16 [nblocks][64] per image, natural order, MCU order
+//   ents    : per block 64 u32 coefficient-list entries (BlockOut in
+//             hj_kernels.hip); multiscan_kernel's int32 levels before that
+//   bdesc   : per block {list start, count | DC << 16}
 //   planes  : u8 component planes padded to whole blocks
 //   wts     : swscale tables (positions, Q14/Q12 taps, row writers) per
 //             distinct geometry of the batch (host-built, hj_sws.cpp)
@@ -155,8 +157,11 @@ struct ImageInfo {      // device-filled by the parse kernel
   int32_t clean_len;    // destuffed bytes
   int32_t sync_rounds;  // diagnostics: rounds the Huffman sync took
   int32_t scan_end;     // destuff: first byte past the entropy-coded data
-  int32_t ent_wide;     // parse: scan needs the NTAB = 6 entropy instance (5-6 distinct
+  int32_t ent_wide;     // parse: the scan needs the entropy kernel's wide path (5-6 distinct
                         // tables, long codes outside the LDS sub-table pool or slow codes)
+  int32_t multiscan;    // parse: progressive, or sequential with non-interleaved scans
+                        // (multiscan_kernel decodes it; destuff / entropy skip it)
+  int32_t progressive;  // parse: SOF2
   int32_t pad_;
   int64_t tphase[4];    // diagnostics: wall_clock64 ticks of the entropy phases
   int64_t dbg[4];       // diagnostics: symbols (round 0), wave iterations, shader clocks, rt ticks

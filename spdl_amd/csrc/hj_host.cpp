@@ -41,6 +41,8 @@ hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, Ima
                           hipStream_t);
 hipError_t launch_idct(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, uint8_t*,
                        int, int, int, hipStream_t);
+hipError_t launch_multiscan(const uint8_t*, const ImageDesc*, ImageInfo*, uint32_t*, uint2*, int,
+                            hipStream_t);
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                       const BatchParams&, int64_t, int, int32_t*, hipStream_t);
 hipError_t launch_nv12(const uint8_t*, uint8_t*, int, int, int, int, int, hipStream_t);
@@ -68,7 +70,7 @@ const char* status_str(int s) {
   switch (s) {
     case SPDL_HJ_OK: return "OK";
     case SPDL_HJ_ERR_NOT_JPEG: return "not a JPEG";
-    case SPDL_HJ_ERR_UNSUPPORTED: return "unsupported JPEG (progressive, arithmetic, 12-bit, CMYK or multi-scan)";
+    case SPDL_HJ_ERR_UNSUPPORTED: return "unsupported JPEG (arithmetic, lossless, 12-bit or CMYK)";
     case SPDL_HJ_ERR_BAD_HEADER: return "corrupt JPEG header";
     case SPDL_HJ_ERR_BAD_HUFFMAN: return "corrupt entropy-coded data";
     case SPDL_HJ_ERR_TRUNCATED: return "truncated entropy-coded data";
@@ -266,7 +268,7 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
     if (len < 2 || pos + (size_t)len > size) return SPDL_HJ_ERR_BAD_HEADER;
     const uint8_t* s = d + pos + 2;
     pos += (size_t)len;
-    if (m == 0xC0 || m == 0xC1) {
+    if (m == 0xC0 || m == 0xC1 || m == 0xC2) {  // sequential or progressive Huffman
       if (len < 8) return SPDL_HJ_ERR_BAD_HEADER;
       if (s[0] != 8) return SPDL_HJ_ERR_UNSUPPORTED;
       info->height = (s[1] << 8) | s[2];
@@ -285,9 +287,9 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
       }
       return SPDL_HJ_OK;
     }
-    if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
+    if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
         (m >= 0xCD && m <= 0xCF))
-      return SPDL_HJ_ERR_UNSUPPORTED;
+      return SPDL_HJ_ERR_UNSUPPORTED;  // lossless, hierarchical, arithmetic
   }
 }
 
@@ -804,6 +806,9 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
                         static_cast<uint32_t*>(W.recs.p),
                         ctx->sub_bits, ctx->warm_slots, ctx->entropy_threads, ctx->entropy_lds_pad, n, st));
+  // progressive / non-interleaved images (the kernels above skipped them)
+  HJ_HIP(launch_multiscan(d_bytes, desc, infos, static_cast<uint32_t*>(W.ents.p),
+                          static_cast<uint2*>(W.bdesc.p), n, st));
   mark(ctx, slot, 4, st);
   HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
                      static_cast<const uint2*>(W.bdesc.p), desc, infos,

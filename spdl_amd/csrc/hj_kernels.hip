@@ -88,7 +88,7 @@ __device__ static int be16(BPtr p) { return (p[0] << 8) | p[1]; }
 __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
   ImageInfo& in = s.info;
   if (size < 4 || d[0] != 0xFF || d[1] != 0xD8) return kErrNotJpeg;
-  int have_sof = 0;
+  int have_sof = 0, prog = 0;
   int comp_id[kMaxComp] = {0, 0, 0};
   int comp_tq[kMaxComp] = {0, 0, 0};
   int pos = 2;
@@ -138,7 +138,8 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
         p += 17 + total;
         n -= 17 + total;
       }
-    } else if (m == 0xC0 || m == 0xC1) {
+    } else if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
+      prog = m == 0xC2;
       if (n < 6) return kErrBadHeader;
       if (p[0] != 8) return kErrUnsupported;
       in.height = be16(p + 1);
@@ -159,8 +160,8 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
           return kErrBadHeader;
       }
       have_sof = 1;
-    } else if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) ||
-               (m >= 0xC9 && m <= 0xCB) || (m >= 0xCD && m <= 0xCF)) {
+    } else if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
+               (m >= 0xCD && m <= 0xCF)) {
       return kErrUnsupported;
     } else if (m == 0xDD) {
       if (n < 2) return kErrBadHeader;
@@ -168,7 +169,11 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
     } else if (m == 0xDA) {
       if (!have_sof) return kErrBadHeader;
       int ns = p[0];
-      if (ns != in.ncomp) return kErrUnsupported;
+      if (ns < 1 || ns > in.ncomp) return kErrBadHeader;
+      // progressive, or sequential with non-interleaved scans: multiscan_kernel
+      // walks every scan; the MCU holds the components in frame order
+      in.multiscan = prog || ns != in.ncomp;
+      in.progressive = prog;
       if (n < 1 + 2 * ns + 3) return kErrBadHeader;
       int order[kMaxComp] = {0, 0, 0};
       for (int i = 0; i < ns; i++) {
@@ -182,8 +187,10 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
         if (in.dc_tab[c] > 3 || in.ac_tab[c] > 3) return kErrBadHeader;
       }
       int ss = p[1 + 2 * ns], se = p[2 + 2 * ns], ahal = p[3 + 2 * ns];
-      if (ss != 0 || se != 63 || ahal != 0) return kErrUnsupported;
+      if (!in.multiscan && (ss != 0 || se != 63 || ahal != 0)) return kErrUnsupported;
       in.scan_start = pos;
+      if (in.multiscan)
+        for (int i = 0; i < in.ncomp; i++) order[i] = i;
       int hmax = 1, vmax = 1;
       for (int c = 0; c < in.ncomp; c++) {
         hmax = max(hmax, in.comp_h[c]);
@@ -193,7 +200,8 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
       in.vmax = vmax;
       for (int c = 0; c < in.ncomp; c++) {
         if (hmax % in.comp_h[c] || vmax % in.comp_v[c]) return kErrUnsupported;
-        if (!s.qhave[comp_tq[c]] || !s.have[in.dc_tab[c]] || !s.have[4 + in.ac_tab[c]])
+        if (!s.qhave[comp_tq[c]] ||
+            (!in.multiscan && (!s.have[in.dc_tab[c]] || !s.have[4 + in.ac_tab[c]])))
           return kErrBadHeader;
         in.comp_w[c] = (in.width * in.comp_h[c] + hmax - 1) / hmax;
         in.comp_hpx[c] = (in.height * in.comp_v[c] + vmax - 1) / vmax;
@@ -211,7 +219,7 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
         in.mcux = (in.width + 8 * hmax - 1) / (8 * hmax);
         in.mcuy = (in.height + 8 * vmax - 1) / (8 * vmax);
         int b = 0;
-        for (int i = 0; i < ns; i++) {
+        for (int i = 0; i < (in.multiscan ? in.ncomp : ns); i++) {
           int c = order[i];
           in.comp_bw[c] = in.mcux * in.comp_h[c];
           in.comp_bh[c] = in.mcuy * in.comp_v[c];
@@ -326,7 +334,9 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     // the image's quantisation tables by component (as the thread-0 pass did)
     for (int c = 0; c < s.info.ncomp; c++)
       for (int i = 0; i < 64; i++) s.info.qt[c][i] = s.qt[s.qtsel[c]][i];
+    if (s.info.multiscan) infos[img] = s.info;  // tables are built per scan later
   }
+  if (s.info.multiscan) return;
   HuffTable* tabs = luts + (size_t)img * 8;
   int tab_nsub[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tab_slow = 0;  // per table slot (thread 0 uses)
   for (int t = 0; t < 8; t++) {
@@ -520,7 +530,7 @@ __global__ void __launch_bounds__(kDsThreads) destuff_count_kernel(
   __shared__ int sh[8];
   __shared__ int shterm;
   const int img = blockIdx.y, k = blockIdx.x, tid = threadIdx.x;
-  if (infos[img].status != kOk) return;
+  if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc& dd = desc[img];
   const int size = (int)dd.in_size, start = infos[img].scan_start;
   const int cbase = (start & ~15) + k * kDsChunk;
@@ -549,7 +559,7 @@ __global__ void __launch_bounds__(kDsThreads) destuff_prefix_kernel(
   __shared__ int sh[8];
   __shared__ int shterm;
   const int img = blockIdx.x, tid = threadIdx.x;
-  if (infos[img].status != kOk) return;
+  if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc& dd = desc[img];
   const int size = (int)dd.in_size, start = infos[img].scan_start;
   const int base = start & ~15;
@@ -584,7 +594,7 @@ __global__ void __launch_bounds__(kDsThreads) destuff_write_kernel(
   __shared__ int sh[8];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kDsChunk];
   const int img = blockIdx.y, k = blockIdx.x, tid = threadIdx.x;
-  if (infos[img].status != kOk) return;
+  if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc& dd = desc[img];
   const int size = (int)dd.in_size, start = infos[img].scan_start, end = infos[img].scan_end;
   const int base = start & ~15;
@@ -1069,7 +1079,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
                               const int warm_slots) {
   const int tid = threadIdx.x;
   uint32_t* win = &S.win[0][tid];
-  if (infos[img].status != kOk) return;
+  if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc dd = desc[img];
   const ImageInfo& in = infos[img];
   // The NTAB = 4 instance takes the images whose scan uses <= 4 distinct
@@ -1477,6 +1487,631 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
                                      sub_bits_param, warm_slots);
     __syncthreads();  // LDS is reused by the next image
   }
+}
+
+// ---------------------------------------------------------------------------
+// multiscan_kernel: progressive (SOF2) and sequential non-interleaved JPEGs.
+// One workgroup per image.  The whole workgroup finds the marker candidates
+// (one coalesced pass over the file), thread 0 walks the segments and records
+// every scan, the workgroup builds each scan's Huffman tables in LDS, and
+// thread 0 decodes the scan (a progressive scan's meaning depends on every
+// earlier scan of its blocks, so it is one sequential pass per scan; images
+// run in parallel, one per CU).  Levels accumulate as int32 in the image's
+// coefficient-list region, which the final pass turns into the lists
+// idct_kernel reads.  Arithmetic: oracle ms_decode (jpeg_oracle.c), libjpeg
+// jdphuff.c semantics, FFmpeg-style dequantisation.
+// ---------------------------------------------------------------------------
+
+constexpr int kMsMaxScans = 64;
+constexpr int kMsMaxMarks = 512;
+constexpr int kMsLook = 9;
+
+struct MsTable {
+  uint16_t look[1 << kMsLook];  // (len << 8) | sym for codes <= kMsLook bits, else 0
+  int32_t maxcode[18];
+  int32_t valoff[17];
+  uint8_t vals[256];
+  uint8_t bits[17];
+};
+
+struct MsScan {
+  int32_t ns, comp[kMaxComp], td[kMaxComp], ta[kMaxComp];
+  int32_t ss, se, ah, al, ri;
+  int32_t start, end;  // entropy-coded bytes [start, end) of the file
+  int32_t dht[8];      // file offset of the DHT entry in effect per slot (-1: none)
+};
+
+struct MsShared {
+  MsTable tab[8];  // DC 0..3, AC 0..3 (slot 4 + id)
+  MsScan scan[kMsMaxScans];
+  int32_t marks[kMsMaxMarks];
+  __attribute__((aligned(16))) int32_t blk[64];  // thread 0's block of levels (AC refinement)
+  int32_t dht[8], comp_id[kMaxComp];  // segment walk state (thread 0)
+  int32_t nmarks, nscans, err;
+};
+
+// Sequential byte source over the file with a two-chunk (32 B) look-ahead:
+// the next 16-byte chunk is already in flight when the reader reaches it.
+// (Scalar words, not uint4 members: the state must stay in registers.)
+struct MsBytes {
+  const uint8_t* d;
+  int size, base;
+  uint32_t a0, a1, a2, a3, b0, b1, b2, b3;  // chunk at base, chunk at base + 16
+  __device__ __forceinline__ void load(int b, uint32_t& x, uint32_t& y, uint32_t& z,
+                                       uint32_t& w) const {
+    if (b + 16 <= size) {
+      const uint4 q = *reinterpret_cast<const uint4*>(d + b);
+      x = q.x, y = q.y, z = q.z, w = q.w;
+      return;
+    }
+    // the file's last partial chunk, a byte at a time (into locals: a select
+    // between references to the members would put the reader in scratch)
+    uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+#pragma unroll 1
+    for (int i = 0; i < 16 && b + i < size; i++) {
+      const uint32_t v = (uint32_t)d[b + i] << (8 * (i & 3));
+      v0 |= i < 4 ? v : 0u;
+      v1 |= i >= 4 && i < 8 ? v : 0u;
+      v2 |= i >= 8 && i < 12 ? v : 0u;
+      v3 |= i >= 12 ? v : 0u;
+    }
+    x = v0, y = v1, z = v2, w = v3;
+  }
+  __device__ __forceinline__ void seek(int p) {
+    base = p & ~15;
+    load(base, a0, a1, a2, a3);
+    load(base + 16, b0, b1, b2, b3);
+  }
+  __device__ __forceinline__ uint32_t at(int i) {
+    if (i < base) seek(i);  // a step back (a marker found by look-ahead): reload
+    while (i >= base + 16) {
+      base += 16;
+      a0 = b0, a1 = b1, a2 = b2, a3 = b3;
+      load(base + 16, b0, b1, b2, b3);
+    }
+    const int k = i - base;
+    // masks, not selects: a select between members becomes a load from a
+    // selected address, which keeps the reader in scratch memory
+    const uint32_t q = (uint32_t)k >> 2;
+    const uint32_t w = (a0 & (0u - (uint32_t)(q == 0))) | (a1 & (0u - (uint32_t)(q == 1))) |
+                       (a2 & (0u - (uint32_t)(q == 2))) | (a3 & (0u - (uint32_t)(q == 3)));
+    return (w >> (8 * (k & 3))) & 0xFFu;
+  }
+};
+
+// Bit reader over stuffed entropy data: 0xFF00 -> 0xFF; any other marker (or
+// the scan end) stops the data, zeros follow (oracle bitrd_t).
+struct MsBits {
+  MsBytes src;
+  int pos, end;
+  uint64_t buf;
+  int cnt;
+  bool marker;
+  int64_t real, used;
+  __device__ __forceinline__ void start(int p, int e) {
+    pos = p;
+    end = e;
+    buf = 0;
+    cnt = 0;
+    marker = false;
+    real = used = 0;
+    src.seek(p);
+  }
+  __device__ __forceinline__ void fill() {
+    while (cnt <= 56) {
+      uint32_t byte = 0;
+      if (!marker) {
+        if (pos >= end) {
+          marker = true;
+        } else {
+          const uint32_t c = src.at(pos);
+          if (c == 0xFFu) {
+            const uint32_t nx = pos + 1 < end ? src.at(pos + 1) : 0xD9u;
+            if (nx == 0u) {
+              pos += 2;
+              byte = 0xFFu;
+              real += 8;
+            } else {
+              marker = true;
+            }
+          } else {
+            pos++;
+            byte = c;
+            real += 8;
+          }
+        }
+      }
+      buf |= (uint64_t)byte << (56 - cnt);
+      cnt += 8;
+    }
+  }
+  __device__ __forceinline__ uint32_t peek16() {
+    if (cnt < 32) fill();
+    return (uint32_t)(buf >> 48);
+  }
+  __device__ __forceinline__ void skip(int n) {
+    buf <<= n;
+    cnt -= n;
+    used += n;
+  }
+  __device__ __forceinline__ uint32_t get(int n) {
+    if (n == 0) return 0u;
+    if (cnt < 32) fill();
+    const uint32_t v = (uint32_t)(buf >> (64 - n));
+    skip(n);
+    return v;
+  }
+  // symbol, or -1 for an invalid code
+  __device__ __forceinline__ int decode(const MsTable& t) {
+    const uint32_t w = peek16();
+    const uint32_t e = t.look[w >> (16 - kMsLook)];
+    if (e) {
+      skip((int)(e >> 8));
+      return (int)(e & 0xFFu);
+    }
+    for (int l = kMsLook + 1; l <= 16; l++) {
+      const int code = (int)(w >> (16 - l));
+      if (code <= t.maxcode[l]) {
+        skip(l);
+        return t.vals[t.valoff[l] + code];
+      }
+    }
+    return -1;
+  }
+};
+
+__device__ __forceinline__ int ms_extend(uint32_t v, int s) {
+  return v < (1u << (s - 1)) ? (int)v - ((1 << s) - 1) : (int)v;
+}
+
+// MCU-order block index of component c's block (bx, by)
+__device__ __forceinline__ int ms_block(const ImageInfo& in, int c, int bx, int by) {
+  if (in.ncomp == 1) return by * in.mcux + bx;
+  int b0 = 0;
+  for (int k = 0; k < c; k++) b0 += in.comp_h[k] * in.comp_v[k];
+  const int mx = bx / in.comp_h[c], my = by / in.comp_v[c];
+  const int b = b0 + (by % in.comp_v[c]) * in.comp_h[c] + (bx % in.comp_h[c]);
+  return (my * in.mcux + mx) * in.bpm + b;
+}
+
+// One block of one scan (thread 0).  lev: the block's levels in HBM (zig-zag
+// index); AC refinement works on the copy ms_scan staged in S.blk.
+__device__ __forceinline__ int ms_block_decode(MsShared& S, MsBits& br, const MsScan& sc, bool prog,
+                               const MsTable& dh, const MsTable& ah, int32_t& pred,
+                               int32_t* __restrict__ lev, int& eobrun) {
+  if (!prog) {  // sequential scan: the whole block
+    int s = br.decode(dh);
+    if (s < 0 || s > 15) return kErrBadHuffman;
+    pred += s ? ms_extend(br.get(s), s) : 0;
+    lev[0] = pred;
+    for (int k = 1; k < 64;) {
+      const int rs = br.decode(ah);
+      if (rs < 0) return kErrBadHuffman;
+      const int r = rs >> 4;
+      s = rs & 15;
+      if (s == 0) {
+        if (r == 15) {
+          k += 16;
+          continue;
+        }
+        if (r != 0) return kErrBadHuffman;
+        break;
+      }
+      k += r;
+      if (k > 63) return kErrBadHuffman;
+      lev[k++] = ms_extend(br.get(s), s);
+    }
+    return kOk;
+  }
+  const int al = sc.al;
+  if (sc.ss == 0) {
+    if (sc.ah == 0) {  // DC first
+      const int s = br.decode(dh);
+      if (s < 0 || s > 15) return kErrBadHuffman;
+      pred += s ? ms_extend(br.get(s), s) : 0;
+      lev[0] = (int32_t)((uint32_t)pred << al);
+    } else if (br.get(1)) {  // DC refine
+      atomicOr(reinterpret_cast<unsigned int*>(lev), 1u << al);
+    }
+    return kOk;
+  }
+  if (sc.ah == 0) {  // AC first (spectral selection)
+    if (eobrun > 0) {
+      eobrun--;
+      return kOk;
+    }
+    for (int k = sc.ss; k <= sc.se; k++) {
+      const int rs = br.decode(ah);
+      if (rs < 0) return kErrBadHuffman;
+      const int r = rs >> 4, s = rs & 15;
+      if (s) {
+        k += r;
+        if (k > sc.se) return kErrBadHuffman;
+        lev[k] = (int32_t)((uint32_t)ms_extend(br.get(s), s) << al);
+      } else if (r == 15) {
+        k += 15;
+      } else {
+        eobrun = (1 << r) - 1;
+        if (r) eobrun += (int)br.get(r);
+        break;
+      }
+    }
+    return kOk;
+  }
+  // AC refinement (successive approximation) on the LDS copy of the block
+  int32_t* b = S.blk;
+  const int32_t p1 = 1 << al, m1 = -(1 << al);
+  int k = sc.ss;
+  if (eobrun <= 0) {
+    for (; k <= sc.se; k++) {
+      const int rs = br.decode(ah);
+      if (rs < 0) return kErrBadHuffman;
+      int r = rs >> 4;
+      const int s = rs & 15;
+      int32_t v = 0;
+      if (s) {
+        if (s != 1) return kErrBadHuffman;
+        v = br.get(1) ? p1 : m1;
+      } else if (r != 15) {
+        eobrun = 1 << r;
+        if (r) eobrun += (int)br.get(r);
+        break;
+      }
+      for (; k <= sc.se; k++) {
+        const int32_t c = b[k];
+        if (c != 0) {
+          if (br.get(1) && (c & p1) == 0) b[k] = c + (c >= 0 ? p1 : m1);
+        } else {
+          if (r == 0) break;
+          r--;
+        }
+      }
+      if (k > sc.se) {
+        if (v) return kErrBadHuffman;
+        break;
+      }
+      if (v) b[k] = v;
+    }
+  }
+  if (eobrun > 0) {
+    for (; k <= sc.se; k++) {
+      const int32_t c = b[k];
+      if (c != 0 && br.get(1) && (c & p1) == 0) b[k] = c + (c >= 0 ? p1 : m1);
+    }
+    eobrun--;
+  }
+  return kOk;
+}
+
+// One scan (thread 0): restart intervals, interleaved MCUs or one
+// component's blocks in raster order over its own (unpadded) block grid.
+// (Everything here is inlined into the kernel: through a call the reader
+// state would live in scratch memory and the LDS tables behind flat loads.)
+__device__ __forceinline__ int ms_scan(MsShared& S, const uint8_t* d, int size, const ImageInfo& in,
+                       const MsScan& sc, bool prog, int32_t* __restrict__ lv) {
+  MsBits br;
+  br.src.d = d;
+  br.src.size = size;
+  br.start(sc.start, sc.end);
+  int32_t pred0 = 0, pred1 = 0, pred2 = 0;  // (scalars: an indexed array would be scratch)
+  int eobrun = 0;
+  int nmcu, bw1 = 1;
+  if (sc.ns > 1) {
+    nmcu = in.mcux * in.mcuy;
+  } else {
+    const int c = sc.comp[0];
+    bw1 = in.ncomp == 1 ? in.mcux : (in.comp_w[c] + 7) / 8;
+    const int bh1 = in.ncomp == 1 ? in.mcuy : (in.comp_hpx[c] + 7) / 8;
+    nmcu = bw1 * bh1;
+  }
+  const bool refine = prog && sc.ss > 0 && sc.ah > 0;  // reads its blocks: staged in S.blk
+  for (int mcu = 0; mcu < nmcu; mcu++) {
+    if (sc.ri && mcu && mcu % sc.ri == 0) {
+      if (br.used > br.real) return kErrTruncated;
+      int p = br.pos;
+      for (;;) {  // the next marker must be RSTn
+        if (p >= sc.end) return kErrBadRestart;
+        const uint32_t c = br.src.at(p);
+        if (c == 0xFFu && p + 1 < size && br.src.at(p + 1) == 0u) {
+          p += 2;
+          continue;
+        }
+        if (c == 0xFFu) break;
+        p++;
+      }
+      while (p < size && br.src.at(p) == 0xFFu) p++;
+      if (p >= size || br.src.at(p) < 0xD0u || br.src.at(p) > 0xD7u) return kErrBadRestart;
+      br.start(p + 1, sc.end);
+      pred0 = pred1 = pred2 = 0;
+      eobrun = 0;
+    }
+    const int mx = mcu % in.mcux, my = mcu / in.mcux;
+    for (int i = 0; i < sc.ns; i++) {
+      const int c = sc.comp[i];
+      const MsTable& dh = S.tab[sc.td[i]];
+      const MsTable& ah = S.tab[4 + sc.ta[i]];
+      int32_t pred = c == 0 ? pred0 : (c == 1 ? pred1 : pred2);
+      const int hc = in.comp_h[c], nb = sc.ns > 1 ? hc * in.comp_v[c] : 1;
+      for (int u = 0; u < nb; u++) {
+        const int b = sc.ns > 1 ? ms_block(in, c, mx * hc + u % hc, my * in.comp_v[c] + u / hc)
+                                : ms_block(in, c, mcu % bw1, mcu / bw1);
+        int32_t* lev = lv + (size_t)b * 64;
+        if (refine) {
+          const uint4* src = reinterpret_cast<const uint4*>(lev);
+#pragma unroll
+          for (int q = 0; q < 16; q++) reinterpret_cast<uint4*>(S.blk)[q] = src[q];
+        }
+        const int rc = ms_block_decode(S, br, sc, prog, dh, ah, pred, lev, eobrun);
+        if (rc != kOk) return rc;
+        if (refine) {
+          uint4* dst = reinterpret_cast<uint4*>(lev);
+#pragma unroll
+          for (int q = 0; q < 16; q++) dst[q] = reinterpret_cast<const uint4*>(S.blk)[q];
+        }
+      }
+      pred0 = c == 0 ? pred : pred0;
+      pred1 = c == 1 ? pred : pred1;
+      pred2 = c == 2 ? pred : pred2;
+    }
+  }
+  return br.used > br.real ? kErrTruncated : kOk;
+}
+
+__global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restrict__ bytes,
+                                                        const ImageDesc* __restrict__ desc,
+                                                        ImageInfo* __restrict__ infos,
+                                                        uint32_t* __restrict__ ents,
+                                                        uint2* __restrict__ bdesc) {
+  __shared__ MsShared S;
+  const int img = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  ImageInfo& in = infos[img];
+  if (in.status != kOk || !in.multiscan) return;
+  const ImageDesc& dd = desc[img];
+  const uint8_t* d = bytes + dd.in_off;
+  const int size = (int)dd.in_size;
+  const bool prog = in.progressive != 0;
+  int32_t* lv = reinterpret_cast<int32_t*>(ents + (size_t)dd.coef_off * 64);
+  const int nblocks = in.nblocks;
+  int64_t t0 = wall_clock64(), tph[4] = {0, 0, 0, 0};
+  if (tid == 0) {
+    S.nmarks = 0;
+    S.nscans = 0;
+    S.err = kOk;
+  }
+  __syncthreads();
+  // ---- marker candidates: 0xFF followed by neither 0x00, 0xFF nor RSTn ----
+  for (int g = tid; g * 16 < size; g += nt) {
+    const int b = g * 16;
+    uint32_t w[5];
+    if (b + 20 <= size) {
+      const uint4 q = *reinterpret_cast<const uint4*>(d + b);
+      w[0] = q.x, w[1] = q.y, w[2] = q.z, w[3] = q.w;
+      w[4] = *reinterpret_cast<const uint32_t*>(d + b + 16);
+    } else {
+      for (int i = 0; i < 5; i++) w[i] = 0;
+      for (int i = 0; i < 20 && b + i < size; i++) w[i >> 2] |= (uint32_t)d[b + i] << (8 * (i & 3));
+    }
+    for (int i = 0; i < 16 && b + i + 1 < size; i++) {
+      const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      const uint32_t nx = (w[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 0xFFu;
+      if (c == 0xFFu && nx != 0u && nx != 0xFFu && (nx < 0xD0u || nx > 0xD7u)) {
+        const int k = atomicAdd(&S.nmarks, 1);
+        if (k < kMsMaxMarks) S.marks[k] = b + i;
+      }
+    }
+  }
+  for (int i = tid; i < nblocks * 16; i += nt)
+    reinterpret_cast<uint4*>(lv)[i] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  // ---- thread 0: sort the candidates, walk the segments, record the scans ----
+  if (tid == 0) {
+    const int nm = min(S.nmarks, kMsMaxMarks);
+    for (int i = 1; i < nm; i++) {
+      const int v = S.marks[i];
+      int j = i - 1;
+      while (j >= 0 && S.marks[j] > v) {
+        S.marks[j + 1] = S.marks[j];
+        j--;
+      }
+      S.marks[j + 1] = v;
+    }
+    int err = S.nmarks > kMsMaxMarks ? kErrUnsupported : kOk;
+    int* dht = S.dht;
+    int* comp_id = S.comp_id;
+    for (int t = 0; t < 8; t++) dht[t] = -1;
+    for (int c = 0; c < kMaxComp; c++) comp_id[c] = 0;
+    int ri = 0, ns = 0;
+    int pos = 2;
+    while (err == kOk) {
+      while (pos < size && d[pos] != 0xFF) pos++;
+      while (pos < size && d[pos] == 0xFF) pos++;
+      if (pos >= size) break;
+      const int m = d[pos++];
+      if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+      if (m == 0xD9) break;
+      if (pos + 2 > size) {
+        err = kErrBadHeader;
+        break;
+      }
+      const int len = (d[pos] << 8) | d[pos + 1];
+      if (len < 2 || pos + len > size) {
+        err = kErrBadHeader;
+        break;
+      }
+      int p = pos + 2;
+      const int seg_end = pos + len;
+      pos = seg_end;
+      if (m == 0xC4) {
+        while (p + 17 <= seg_end) {
+          const int tc = d[p] >> 4, th = d[p] & 15;
+          int total = 0;
+          for (int l = 1; l <= 16; l++) total += d[p + l];
+          if (tc > 1 || th > 3 || total > 256 || p + 17 + total > seg_end) {
+            err = kErrBadHeader;
+            break;
+          }
+          dht[tc * 4 + th] = p;
+          p += 17 + total;
+        }
+      } else if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
+        for (int c = 0; c < in.ncomp && p + 6 + 3 * c < seg_end; c++) comp_id[c] = d[p + 6 + 3 * c];
+      } else if (m == 0xDD) {
+        if (len >= 4) ri = (d[p] << 8) | d[p + 1];
+      } else if (m == 0xDA) {
+        if (ns >= kMsMaxScans) {
+          err = kErrUnsupported;
+          break;
+        }
+        MsScan& sc = S.scan[ns];
+        sc.ns = d[p];
+        if (sc.ns < 1 || sc.ns > in.ncomp || p + 1 + 2 * sc.ns + 3 > seg_end) {
+          err = kErrBadHeader;
+          break;
+        }
+        for (int i = 0; i < sc.ns; i++) {
+          const int cs = d[p + 1 + 2 * i];
+          int c = -1;
+          for (int k = 0; k < in.ncomp; k++)
+            if (comp_id[k] == cs) c = k;
+          sc.comp[i] = c;
+          sc.td[i] = d[p + 2 + 2 * i] >> 4;
+          sc.ta[i] = d[p + 2 + 2 * i] & 15;
+          if (c < 0 || sc.td[i] > 3 || sc.ta[i] > 3) err = kErrBadHeader;
+        }
+        if (err != kOk) break;
+        sc.ss = d[p + 1 + 2 * sc.ns];
+        sc.se = d[p + 2 + 2 * sc.ns];
+        sc.ah = d[p + 3 + 2 * sc.ns] >> 4;
+        sc.al = d[p + 3 + 2 * sc.ns] & 15;
+        if (prog ? (sc.ss > sc.se || sc.se > 63 || sc.al > 13 || (sc.ss == 0 && sc.se != 0) ||
+                    (sc.ss > 0 && sc.ns != 1))
+                 : (sc.ss != 0 || sc.se != 63 || sc.ah || sc.al)) {
+          err = kErrBadHeader;
+          break;
+        }
+        sc.ri = ri;
+        for (int t = 0; t < 8; t++) sc.dht[t] = dht[t];
+        sc.start = seg_end;
+        int e = size;  // the scan's data ends at the first marker past its start
+        for (int i = 0; i < nm; i++)
+          if (S.marks[i] >= seg_end) {
+            e = S.marks[i];
+            break;
+          }
+        sc.end = e;
+        pos = e;
+        ns++;
+      }
+    }
+    if (err == kOk && ns == 0) err = kErrBadHeader;
+    S.nscans = ns;
+    S.err = err;
+  }
+  __syncthreads();
+  tph[0] = wall_clock64() - t0;  // marker candidates + segment walk
+  // ---- the scans, in order ----
+  const bool progressive = prog;
+  for (int si = 0; si < S.nscans && S.err == kOk; si++) {
+    const MsScan& sc = S.scan[si];
+    // tables this scan reads: DC for DC-first / sequential, AC for AC scans
+    const bool need_dc = !progressive || (sc.ss == 0 && sc.ah == 0);
+    const bool need_ac = !progressive || sc.ss > 0;
+    for (int t = 0; t < 8; t++) {
+      bool used = false;
+      for (int i = 0; i < sc.ns; i++)
+        used |= (t < 4 && need_dc && sc.td[i] == t) || (t >= 4 && need_ac && sc.ta[i] == t - 4);
+      if (!used) continue;  // (uniform: every thread reads the same scan record)
+      const int o = sc.dht[t];
+      if (o < 0) {
+        if (tid == 0) S.err = kErrBadHeader;
+        continue;
+      }
+      MsTable& T = S.tab[t];
+      if (tid < 17) T.bits[tid] = tid == 0 ? 0 : d[o + tid];
+      __syncthreads();
+      if (tid == 0) {
+        int code = 0, k = 0;
+        for (int l = 1; l <= 16; l++) {
+          if (T.bits[l]) {
+            T.valoff[l] = k - code;
+            code += T.bits[l];
+            k += T.bits[l];
+            T.maxcode[l] = code - 1;
+          } else {
+            T.maxcode[l] = -1;
+            T.valoff[l] = 0;
+          }
+          if (code > (1 << l)) S.err = kErrBadHeader;
+          code <<= 1;
+        }
+        T.maxcode[17] = 0x7FFFFFFF;
+      }
+      int total = 0;
+      for (int l = 1; l <= 16; l++) total += T.bits[l];
+      for (int i = tid; i < 256; i += nt) T.vals[i] = i < total ? d[o + 17 + i] : 0;
+      __syncthreads();
+      for (int idx = tid; idx < (1 << kMsLook); idx += nt) {
+        uint16_t e = 0;
+        for (int l = 1; l <= kMsLook; l++) {
+          const int code = idx >> (kMsLook - l);
+          if (code <= T.maxcode[l]) {
+            e = (uint16_t)((l << 8) | T.vals[T.valoff[l] + code]);
+            break;
+          }
+        }
+        T.look[idx] = e;
+      }
+      __syncthreads();
+    }
+    const int64_t ts = wall_clock64();
+    if (tid == 0 && S.err == kOk) S.err = ms_scan(S, d, size, in, sc, progressive, lv);
+    __syncthreads();
+    tph[2] += wall_clock64() - ts;  // decode
+  }
+  tph[1] = wall_clock64() - t0 - tph[0] - tph[2];  // table builds
+  if (S.err != kOk) {
+    if (tid == 0) in.status = S.err;
+    return;
+  }
+  // ---- levels -> coefficient lists (BlockOut layout), dequantised ----
+  for (int j = tid; j < nblocks; j += nt) {
+    const int c = in.mcu_comp[j % in.bpm];
+    uint4 q[16];
+    const uint4* src = reinterpret_cast<const uint4*>(lv + (size_t)j * 64);
+#pragma unroll
+    for (int i = 0; i < 16; i++) q[i] = src[i];
+    int32_t l[64];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      l[4 * i] = (int32_t)q[i].x;
+      l[4 * i + 1] = (int32_t)q[i].y;
+      l[4 * i + 2] = (int32_t)q[i].z;
+      l[4 * i + 3] = (int32_t)q[i].w;
+    }
+    uint32_t* out = ents + ((size_t)dd.coef_off + j) * 64;
+    uint32_t n = 0;
+#pragma unroll
+    for (int k = 1; k < 64; k++) {
+      if (l[k] != 0) {
+        const uint32_t v = (uint32_t)l[k] * (uint32_t)in.qt[c][k];
+        out[n++] = (v << 16) | kNatOrder[k];
+      }
+    }
+    const int32_t dc = (int32_t)(int16_t)(uint16_t)((uint32_t)kDcBias + (uint32_t)l[0] * in.qt[c][0]);
+    bdesc[(size_t)dd.coef_off + j] = make_uint2((uint32_t)j * 64u, n | ((uint32_t)dc << 16));
+  }
+  __syncthreads();
+  if (tid == 0) {
+    tph[3] = wall_clock64() - t0 - tph[0] - tph[1] - tph[2];  // lists
+    for (int i = 0; i < 4; i++) in.tphase[i] = tph[i];
+    in.sync_rounds = S.nscans;
+  }
+}
+
+hipError_t launch_multiscan(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
+                            uint32_t* ents, uint2* bdesc, int n, hipStream_t st) {
+  hipLaunchKernelGGL(multiscan_kernel, dim3(n), dim3(256), 0, st, bytes, desc, infos, ents, bdesc);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

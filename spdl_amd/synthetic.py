@@ -30,14 +30,16 @@ def synthetic_pixels(seed: int, height: int = 480, width: int = 640) -> np.ndarr
 
 
 def encode_jpeg(
-    pixels: np.ndarray, quality: int = 90, subsampling: int = 2, optimize: bool = False
+    pixels: np.ndarray, quality: int = 90, subsampling: int = 2, optimize: bool = False,
+    progressive: bool = False,
 ) -> bytes:
-    """Pillow baseline JPEG. subsampling: 0=4:4:4, 1=4:2:2, 2=4:2:0."""
+    """Pillow JPEG (baseline unless `progressive`). subsampling: 0=4:4:4,
+    1=4:2:2, 2=4:2:0."""
     from PIL import Image
 
     mode = "L" if pixels.ndim == 2 else "RGB"
     buf = io.BytesIO()
-    kw = dict(quality=quality, optimize=optimize, progressive=False)
+    kw = dict(quality=quality, optimize=optimize, progressive=progressive)
     if mode == "RGB":
         kw["subsampling"] = subsampling
     Image.fromarray(pixels, mode).save(buf, format="JPEG", **kw)
@@ -50,8 +52,10 @@ def synthetic_jpeg(
     width: int = 640,
     quality: int = 90,
     subsampling: int = 2,
+    progressive: bool = False,
 ) -> bytes:
-    return encode_jpeg(synthetic_pixels(seed, height, width), quality, subsampling)
+    return encode_jpeg(synthetic_pixels(seed, height, width), quality, subsampling,
+                       progressive=progressive)
 
 
 def synthetic_batch(n: int, distinct: int = 32, **kw) -> list[bytes]:

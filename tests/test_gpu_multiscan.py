@@ -1,0 +1,91 @@
+"""GPU tests of progressive and non-interleaved multi-scan JPEGs (-m gpu).
+
+The per-case parity (planes, rgb24, JFIF) runs in test_gpu_parity.py over
+cases.VALID, which includes cases.PROGRESSIVE and cases.MULTISCAN (their
+oracle is pinned to libjpeg 9 coefficients in test_oracle.py).  Here: mixed
+batches -- progressive and baseline images in one call, through the resize
+chain and the device-resident entry point -- and the unsupported formats.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import spdl_amd.io as sio
+from spdl_amd import _lib
+from spdl_amd._lib import Output
+from tests import cases
+
+pytestmark = pytest.mark.gpu
+
+PAD224 = dict(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224)
+
+
+def _mixed():
+    names = ["q90_420", "prog_420", "multiscan_420", "prog_gray", "q90_444", "prog_restart",
+             "multiscan_422_rst", "prog_optimized"]
+    return [cases.case(n) for n in names]
+
+
+def test_mixed_batch_pad224(oracle):
+    datas = _mixed()
+    hyp = sio.to_numpy(sio.load_image_batch(datas, width=224, height=224))
+    rs = oracle.Resize(**PAD224)
+    for i, d in enumerate(datas):
+        np.testing.assert_array_equal(hyp[i], oracle.decode_resize(d, rs, "rgb24"), strict=True)
+
+
+def test_mixed_batch_device_resident(oracle):
+    """decode_batch_device (bytes already in HBM) with two batches in flight."""
+    datas = _mixed() * 4
+    offs, sizes, total = [], [], 0
+    for d in datas:
+        offs.append(total)
+        sizes.append(len(d))
+        total += (len(d) + 64 + 255) // 256 * 256
+    host = np.zeros(total, np.uint8)
+    for o, d in zip(offs, datas):
+        host[o:o + len(d)] = np.frombuffer(d, np.uint8)
+    dev = torch.from_numpy(host).to("cuda:0")
+    infos = (_lib.ImageInfo * len(datas))(*[_lib.get_image_info(d) for d in datas])
+    spec = Output(pix_fmt="rgb24", resize=True, **PAD224)
+    dec = _lib.Decoder(0)
+    dec.set_param("lanes", 2)
+    outs = [torch.zeros((len(datas), 224, 224, 3), dtype=torch.uint8, device="cuda:0")
+            for _ in range(2)]
+    tickets = []
+    for o in outs:
+        dec.decode_batch_device(dev.data_ptr(), dev.numel(), np.asarray(offs, np.int64),
+                                np.asarray(sizes, np.int64), infos, spec, o.data_ptr(), o.numel(),
+                                stream=torch.cuda.current_stream(), sync=False)
+        tickets.append(dec.last_ticket())
+    for t in tickets:
+        assert not any(dec.wait(t, len(datas)))
+    torch.cuda.synchronize()
+    rs = oracle.Resize(**PAD224)
+    refs = [oracle.decode_resize(d, rs, "rgb24") for d in datas[:8]]
+    for o in outs:
+        hyp = o.cpu().numpy()
+        for i in range(len(datas)):
+            np.testing.assert_array_equal(hyp[i], refs[i % 8], strict=True)
+    dec.close()
+
+
+@pytest.mark.parametrize("name", ["prog_420", "multiscan_444_odd", "prog_gray"])
+def test_native_planes(oracle, name):
+    """load_image(filter_desc=None) of a multi-scan image: the planes."""
+    d = cases.case(name)
+    hyp = sio.to_numpy(sio.load_image(d, filter_desc=None))
+    ref = np.concatenate([p.reshape(-1) for p in oracle.decode_planes(d)])
+    np.testing.assert_array_equal(hyp.reshape(-1), ref, strict=True)
+
+
+@pytest.mark.parametrize("bad", ["arithmetic", "cmyk"])
+def test_unsupported_fails_per_image(bad):
+    """An unsupported image fails alone: strict=False keeps the others."""
+    d = getattr(cases, bad)()
+    good = [cases.case("prog_420"), cases.case("q90_420")]
+    with pytest.raises(RuntimeError):
+        sio.load_image_batch([d, *good], width=64, height=64, strict=True)
+    buf = sio.load_image_batch([d, *good], width=64, height=64, strict=False)
+    assert sio.to_numpy(buf).shape == (2, 64, 64, 3)
