@@ -48,7 +48,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # Per-launch HBM-side bytes per kernel from the committed rocprofv3 --pmc
 # passes of this same command (tools/pmc_passes.sh + tools/pmc_traffic.py):
 # FETCH_SIZE / WRITE_SIZE cannot be read from inside the timed process.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_v2", "traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_v3", "traffic.json")
 # bench stage -> kernels launched in it
 STAGE_KERNELS = {
     "parse": ["hj::parse_kernel"],
@@ -72,7 +72,7 @@ def _pmc_traffic(stage: str, batch: int):
     tot, hit = 0, False
     for name, v in rec["kernels"].items():
         if any(name.startswith(k) for k in STAGE_KERNELS.get(stage, [])):
-            tot += v["traffic_bytes"] / max(1, v.get("dispatches", 1))
+            tot += v["traffic_bytes"]  # already per dispatch (tools/pmc_traffic.py)
             hit = True
     return int(tot) if hit else None
 
