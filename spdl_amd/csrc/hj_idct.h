@@ -1,6 +1,6 @@
-// hj_idct.h -- 8x8 IDCTs shared by the gfx950 kernel and the host unit test
-// (tests/test_idct_host.py builds this header for the CPU and compares it with
-// the oracle).  HJ_HD marks functions compiled for both sides.
+// hj_idct.h -- 8x8 IDCTs of idct_kernel (FFmpeg simple_idct 8-bit and IJG
+// islow), bit-exact to the oracle's (tests/test_gpu_parity.py planes tests).
+// HJ_HD marks functions that also compile for the host.
 #pragma once
 #include <stdint.h>
 
