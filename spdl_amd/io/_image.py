@@ -104,8 +104,14 @@ def decode_image_nvjpeg(
         datas = [_read(s) for s in src]
         if not datas:
             raise RuntimeError("No input is provided.")
-        if scale_width <= 0 or scale_height <= 0:
+        # the reference rejects only when both are missing
+        # (nvjpeg/decoding.cpp:219-221); one missing size would size its
+        # output buffer with a non-positive dimension and fail there
+        if scale_width <= 0 and scale_height <= 0:
             raise RuntimeError("Both `scale_width` and `scale_height` must be specified.")
+        if scale_width <= 0 or scale_height <= 0:
+            raise RuntimeError(
+                f"Failed to allocate the output buffer: invalid size {scale_width}x{scale_height}.")
         out = Output(pix_fmt=pix_fmt, resize=True, fit_w=scale_width, fit_h=scale_height,
                      filter=scale_algo)
         return _decode(datas, out, device_config, _shape(out, scale_width, scale_height), True)

@@ -169,3 +169,45 @@ def test_bench_path_bit_exact(bench_batch, lanes, warm):
         for i in range(256):
             np.testing.assert_array_equal(hyp[i], refs[i % 32], strict=True)
     dec.close()
+
+
+def test_decode_outputs_use_the_allocator_hook(oracle):
+    """cuda_config(allocator=...) serves the decode outputs too (reference
+    cuda/storage.cpp:71-100): called once per batch, freed with the buffer."""
+    import gc
+
+    calls = {"alloc": 0, "free": 0}
+
+    def alloc(size, device, stream):
+        calls["alloc"] += 1
+        return torch.cuda.caching_allocator_alloc(size, device, stream)
+
+    def free(ptr):
+        calls["free"] += 1
+        torch.cuda.caching_allocator_delete(ptr)
+
+    def run():
+        cfg = sio.cuda_config(0, allocator=(alloc, free))
+        d = cases.case("q90_420")
+        buf = sio.load_image_batch([d, d], width=64, height=48, device_config=cfg)
+        assert calls == {"alloc": 1, "free": 0}
+        hyp = sio.to_torch(buf).cpu().numpy()
+        ref = oracle.decode_resize(d, oracle.Resize(fit_w=64, fit_h=48, aspect="decrease",
+                                                    pad_w=64, pad_h=48), "rgb24")
+        for h in hyp:
+            np.testing.assert_array_equal(h, ref, strict=True)
+        buf2 = sio.decode_image_nvjpeg(d, device_config=cfg)
+        assert calls["alloc"] == 2
+        del buf, buf2
+
+    run()
+    gc.collect()
+    assert calls["free"] == 2
+
+
+def test_nvjpeg_batch_scale_size_errors(cfg):
+    d = cases.case("q90_420")
+    with pytest.raises(RuntimeError, match="Both"):
+        sio.decode_image_nvjpeg([d], device_config=cfg)
+    with pytest.raises(RuntimeError):
+        sio.decode_image_nvjpeg([d], device_config=cfg, scale_width=32)
