@@ -647,7 +647,10 @@ struct spdl_hj_ctx {
   // the first kernel pulls descriptors + tables from pinned memory and the
   // last writes statuses back (1), or DMA copies do it (0; kept for A/B)
   int host_staging = 1;
-  int entropy_threads = 512;
+  // Huffman workgroup size; 0 = by schedule: 512 with one lane (shortest
+  // kernel), 256 with two or more (the smaller workgroups leave the other
+  // lane's kernels more room: +3 % in the 2-lane bench, r02 A/B)
+  int entropy_threads = 0;
   int warm_slots = 12;  // entropy round 0: slots decoded before a run's first slot
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
   PlanCache plans;          // swscale plans per distinct geometry
@@ -805,7 +808,9 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<const HuffTable*>(W.luts.p),
                         static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
                         static_cast<uint32_t*>(W.recs.p),
-                        ctx->sub_bits, ctx->warm_slots, ctx->entropy_threads, ctx->entropy_lds_pad, n, st));
+                        ctx->sub_bits, ctx->warm_slots,
+                        ctx->entropy_threads ? ctx->entropy_threads : (ctx->lanes > 1 ? 256 : 512),
+                        ctx->entropy_lds_pad, n, st));
   // progressive / non-interleaved images (the kernels above skipped them)
   HJ_HIP(launch_multiscan(d_bytes, desc, infos, static_cast<uint32_t*>(W.ents.p),
                           static_cast<uint2*>(W.bdesc.p), n, st));
@@ -1525,7 +1530,7 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "entropy_threads")) {  // workgroup size of the Huffman kernel
-    if (value != 256 && value != 512 && value != 1024) return SPDL_HJ_ERR_INVALID_ARG;
+    if (value != 0 && value != 256 && value != 512 && value != 1024) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->entropy_threads = (int)value;
     return SPDL_HJ_OK;
   }
