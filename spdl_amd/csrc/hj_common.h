@@ -133,10 +133,15 @@ struct ImageDesc {      // host-filled per image
   int64_t rec_cap;
 };
 
-// sws_kernel LDS budget per workgroup (bytes): the horizontal-pass rows of a
-// band (int16 luma + two chroma planes) and the u8 output tile; the host
-// picks the band height (three workgroups per CU at 48 KiB)
-constexpr int kSwsLdsBudget = 48 * 1024;
+// sws_kernel LDS budget per workgroup (bytes): the horizontal-pass columns of
+// a band (int16 luma + two chroma planes), the u8 output tile and the band's
+// vertical tables; the host picks the tallest band that fits.  32 KiB: the
+// 2-lane schedule runs 3.6 % faster than at 48 KiB (smaller bands leave room
+// for the other lane's workgroups; r02 A/B, 24 and 64 KiB slower)
+#ifndef HJ_SWS_LDS_KB
+#define HJ_SWS_LDS_KB 32
+#endif
+constexpr int kSwsLdsBudget = HJ_SWS_LDS_KB * 1024;
 constexpr int kSwsMaxCols = 256;  // output columns per workgroup
 // sws_kernel's LDS holds the horizontal pass column-major: a column of `rows`
 // int16 samples (+ 4 slack rows read by zero taps) takes an odd number of

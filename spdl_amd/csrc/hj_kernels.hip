@@ -289,9 +289,14 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
         rc = kErrBadRestart;
     }
     s.info.status = rc;
-    // canonical-code decode arrays (T.81 F.2.2.3 / libjpeg jdhuff.c)
-    for (int t = 0; t < 8 && rc == kOk; t++) {
-      if (!s.have[t]) continue;
+    st = rc;
+  }
+  __syncthreads();
+  // canonical-code decode arrays (T.81 F.2.2.3 / libjpeg jdhuff.c), one
+  // thread per table slot
+  if (tid < 8 && st == kOk && s.have[tid]) {
+    const int t = tid;
+    {
       int code = 0, k = 0;
       for (int l = 1; l <= 16; l++) {
         if (s.bits[t][l]) {
@@ -307,7 +312,6 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
       }
       s.maxcode[t][17] = 0x7FFFFFFF;
     }
-    st = rc;
   }
   __syncthreads();
   if (st != kOk) {
@@ -330,13 +334,14 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    // the image's quantisation tables by component (as the thread-0 pass did)
-    for (int c = 0; c < s.info.ncomp; c++)
-      for (int i = 0; i < 64; i++) s.info.qt[c][i] = s.qt[s.qtsel[c]][i];
-    if (s.info.multiscan) infos[img] = s.info;  // tables are built per scan later
+  // the image's quantisation tables by component
+  for (int i = tid; i < s.info.ncomp * 64; i += blockDim.x)
+    s.info.qt[i / 64][i % 64] = s.qt[s.qtsel[i / 64]][i % 64];
+  __syncthreads();
+  if (s.info.multiscan) {  // tables are built per scan later
+    if (tid == 0) infos[img] = s.info;
+    return;
   }
-  if (s.info.multiscan) return;
   HuffTable* tabs = luts + (size_t)img * 8;
   int tab_nsub[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tab_slow = 0;  // per table slot (thread 0 uses)
   for (int t = 0; t < 8; t++) {
@@ -416,7 +421,13 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
         seen |= 1 << slot;
       }
     s.info.ent_wide = !(ns <= 4 && (subs << kSubBits) <= kSubPool && !slow);
-    infos[img] = s.info;
+  }
+  __syncthreads();
+  static_assert(sizeof(ImageInfo) % 4 == 0, "ImageInfo copied in words");
+  {  // the parse result out, a word per thread
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&s.info);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(infos + img);
+    for (int i = tid; i < (int)(sizeof(ImageInfo) / 4); i += blockDim.x) dst[i] = src[i];
   }
 }
 
@@ -648,6 +659,14 @@ __global__ void __launch_bounds__(kDsThreads) destuff_write_kernel(
 // ---------------------------------------------------------------------------
 // entropy_kernel
 // ---------------------------------------------------------------------------
+
+typedef unsigned short hj_u16x2 __attribute__((ext_vector_type(2)));
+// low 16 bits of two u16 products at once (v_pk_mul_lo_u16, full rate; a
+// 32-bit multiply is quarter rate)
+__device__ __forceinline__ uint32_t pk_mul_lo16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t,
+                            __builtin_bit_cast(hj_u16x2, a) * __builtin_bit_cast(hj_u16x2, b));
+}
 
 constexpr int kMaxTabs = 2 * kMaxComp;  // distinct (DC, AC) tables of a scan
 // natural (row-major) index of each zig-zag position
@@ -976,7 +995,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const bool ac = coef & !is_dc;
     if (ac) {
       const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-      put_entry(o, ((uint32_t)v * (qn >> 16)) << 16 | (qn & 63u));
+      put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
     }
     o.cur += ac ? 1u : 0u;
     o.bstart = is_dc ? o.cur : o.bstart;
@@ -1021,7 +1040,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     }
     if (wr && !is_dc) {
       const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-      put_entry(o, ((uint32_t)v * (qn >> 16)) << 16 | (qn & 63u));
+      put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
       o.cur++;
     }
     nb += (wr && is_dc) ? 1 : 0;
