@@ -602,7 +602,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
 // descriptor/status staging, and the events that say when each may be reused.
 // kSlots of them form the ring that lets batch k+1 be packed on the host and
 // copied (on the context's copy stream) while batch k's kernels run.
-constexpr int kSlots = 3;
+constexpr int kSlots = 10;
 
 struct Slot {
   PinBuf pin_in, pin_desc, pin_status, pin_tables;
@@ -622,7 +622,7 @@ struct Slot {
 // batches alternate between workspaces and run on the lanes' own streams, so
 // batch k+1's kernels can occupy the CUs that batch k's latency-bound
 // entropy kernel leaves idle (its sync rounds park most waves at barriers).
-constexpr int kMaxLanes = 3;
+constexpr int kMaxLanes = 8;
 
 struct Workspace {
   DevBuf clean, segs, desc, info, luts, ents, bdesc, planes, wts, recs, dschunks;
@@ -808,7 +808,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<const HuffTable*>(W.luts.p),
                         static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
                         static_cast<uint32_t*>(W.recs.p),
-                        ctx->sub_bits, ctx->warm_slots,
+                        ctx->sub_bits, ctx->warm_slots | (((ctx->debug_mask >> 12) & 0xF) << 16),
                         ctx->entropy_threads ? ctx->entropy_threads : (ctx->lanes > 1 ? 256 : 512),
                         ctx->entropy_lds_pad, n, st));
   // progressive / non-interleaved images (the kernels above skipped them)
@@ -817,7 +817,8 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   mark(ctx, slot, 4, st);
   HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
                      static_cast<const uint2*>(W.bdesc.p), desc, infos,
-                     static_cast<uint8_t*>(W.planes.p), out->idct, L.max_blocks, n, st));
+                     static_cast<uint8_t*>(W.planes.p), (ctx->debug_mask & 0x800) ? 2 : out->idct,
+                     L.max_blocks, n, st));
   mark(ctx, slot, 5, st);
   BatchParams bp{};
   bp.n = n;

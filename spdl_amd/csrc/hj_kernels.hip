@@ -678,8 +678,25 @@ __constant__ uint8_t kNatOrder[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32
 #ifndef HJ_WIN_WORDS
 #define HJ_WIN_WORDS 8
 #endif
+#ifndef HJ_REG_READER
+#define HJ_REG_READER 0  // 1: register bit buffer with a read-ahead word (see dec_skip)
+#endif
 constexpr int kWinWords = HJ_WIN_WORDS;  // bit-reader window per thread (words)
+#ifndef HJ_WIN_ALIGN
+#define HJ_WIN_ALIGN 1
+#endif
+// window start: a multiple of HJ_WIN_ALIGN words (1: the word holding the
+// reader's position -- a full window of runway after every restage; the
+// 16-byte loads need only dword alignment)
+constexpr uint32_t kWinAlign = ~(uint32_t)(HJ_WIN_ALIGN - 1);
 
+
+#ifndef HJ_STAGE
+#define HJ_STAGE 0  // write-pass LDS staging line per run, entries (0: register packs; 16/32 measured 3%/15% slower)
+#endif
+__host__ __device__ constexpr int stage_entries(int nt) {
+  return HJ_STAGE == 0 ? 0 : (nt >= 1024 ? 8 : (nt >= 512 && HJ_STAGE > 16 ? 16 : HJ_STAGE));
+}
 
 // NTAB = distinct Huffman tables the workgroup holds in LDS: 4 covers luma +
 // chroma DC/AC (gray: 2) and keeps three entropy workgroups per CU; a scan
@@ -709,6 +726,11 @@ struct EntShared {
       int32_t red[NT];
     } sc;
   };
+  // write pass: each run's coefficient entries are staged here and leave as
+  // whole kStage-entry lines (partially written lines cost ~3x their bytes
+  // in HBM writes: many concurrently appending streams)
+  static constexpr int kStage = stage_entries(NT);
+  uint32_t stage[kStage > 0 ? kStage : 1][NT];
   int32_t flag;
   int32_t err;
   // tables past the NTAB LDS slots (5-6 distinct tables, rare): read from
@@ -716,8 +738,10 @@ struct EntShared {
   const HuffTable* gtab;
   int32_t gslot[kMaxTabs];
 };
-static_assert(sizeof(EntShared<512, 4>) <= 160 * 1024 / 3,
-              "entropy LDS must allow 3 workgroups per CU");
+static_assert(sizeof(EntShared<512, 4>) <= 160 * 1024 / 2,
+              "entropy LDS must allow 2 workgroups per CU");
+static_assert(HJ_STAGE > 16 || sizeof(EntShared<256, 4>) <= 160 * 1024 / 3,
+              "entropy LDS must allow 3 workgroups per CU at 256 threads");
 
 // Per-thread bit reader over the destuffed stream (big-endian bytes read as
 // 32-bit words).  Words come from an 8-word LDS window per thread
@@ -736,6 +760,12 @@ struct Dec {
   uint32_t pos;  // absolute bit position of the next symbol
   uint32_t z;    // next coefficient index (0 = DC)
   uint32_t bs;   // 2 * block-in-MCU
+#if HJ_REG_READER
+  uint64_t acc;  // the bits at pos, MSB-aligned (cnt of them valid)
+  uint32_t cnt;  // valid bits in acc (>= 32 between symbols)
+  uint32_t nw;   // absolute index of the next word to shift into acc
+  uint32_t pre;  // that word, read ahead from the LDS window
+#endif
 };
 
 __device__ __forceinline__ constexpr int win_slot(int i) { return kWinWords - 1 - i; }
@@ -743,8 +773,9 @@ __device__ __forceinline__ constexpr int win_slot(int i) { return kWinWords - 1 
 template <int NT>
 __device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, uint32_t wb) {
   static_assert(kWinWords % 4 == 0, "window is staged in uint4 units");
-  const uint4* src = reinterpret_cast<const uint4*>(words + wb);  // wb % 4 == 0
-  uint4 q[kWinWords / 4];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+  const u32x4* src = reinterpret_cast<const u32x4*>(words + wb);  // dword-aligned 16-B loads
+  u32x4 q[kWinWords / 4];
 #pragma unroll
   for (int i = 0; i < kWinWords / 4; i++) q[i] = src[i];
   // stored MSB-first (byte-swapped once here instead of at every read)
@@ -758,24 +789,66 @@ __device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, 
 }
 
 template <int NT>
+__device__ __forceinline__ uint32_t win_word(const uint32_t* win, uint32_t i) {  // window word i
+  return win[(kWinWords - 1 - (int)i) * NT];
+}
+
+template <int NT>
 __device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
                                          uint32_t z, uint32_t bs) {
-  d.wb = (p >> 5) & ~3u;
+  d.wb = (p >> 5) & kWinAlign;
   win_stage<NT>(win, words, d.wb);
   d.pos = p;
   d.z = z;
   d.bs = bs;
+#if HJ_REG_READER
+  const uint32_t w = (p >> 5) - d.wb;  // 0..3: words w, w + 1, w + 2 are in the window
+  const uint64_t two = ((uint64_t)win_word<NT>(win, w) << 32) | win_word<NT>(win, w + 1);
+  d.acc = two << (p & 31u);
+  d.cnt = 64u - (p & 31u);
+  d.nw = d.wb + w + 2;
+  d.pre = win_word<NT>(win, w + 2);
+#endif
 }
 
 // The 32 bits at d.pos, MSB-first.  Wave-uniform window restage: when any
 // active lane is about to read past its window, every active lane restages
 // from its own position, so the global load and its vmcnt wait happen once
 // per ~25 symbol steps of the wave.
+#if HJ_REG_READER
+// Register bit buffer: the symbol's bits are the top of acc (no LDS read on
+// the symbol chain).  Consuming bits shifts acc; when fewer than 32 remain the
+// read-ahead word is shifted in and the next one is read from the LDS window
+// (its latency overlaps the following symbols: LDS returns in order, so the
+// table lookup's wait covers it).  Wave-uniform window restage as below.
+template <int NT>
+__device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
+  return (uint32_t)(d.acc >> 32);
+}
+
+template <int NT>
+__device__ __forceinline__ void dec_skip(Dec& d, uint32_t* win, const uint32_t* words,
+                                         uint32_t nbits) {
+  d.pos += nbits;
+  d.acc <<= nbits;
+  d.cnt -= nbits;
+  const bool need = d.cnt < 32u;
+  d.acc |= need ? (uint64_t)d.pre << (32u - d.cnt) : 0ull;
+  d.cnt += need ? 32u : 0u;
+  d.nw += need ? 1u : 0u;
+  if (__any(d.nw - d.wb >= (uint32_t)kWinWords)) {
+    d.wb = d.nw & kWinAlign;
+    win_stage<NT>(win, words, d.wb);
+  }
+  d.pre = win_word<NT>(win, d.nw - d.wb);
+}
+#define HJ_DEC_SKIP(d, n) dec_skip<NT>(d, win, words, n)
+#else
 template <int NT>
 __device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
   uint32_t w = (d.pos >> 5) - d.wb;
   if (__any(w >= (uint32_t)(kWinWords - 1))) {
-    d.wb = (d.pos >> 5) & ~3u;
+    d.wb = (d.pos >> 5) & kWinAlign;
     win_stage<NT>(win, words, d.wb);
     w = (d.pos >> 5) - d.wb;
   }
@@ -786,6 +859,7 @@ __device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32
 
 __device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) { d.pos += nbits; }
 #define HJ_DEC_SKIP(d, n) dec_skip(d, n)
+#endif
 
 // Canonical decode of a code that is not fully resolved by the LUT (longer
 // than kLutBits, or a DC size > 15): returns a kKindCode entry, 0 if invalid.
@@ -903,7 +977,7 @@ __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32
 #ifndef HJ_ENT_PACK
 #define HJ_ENT_PACK 4  // entries per store (1, 2 or 4; lists start 16-byte aligned)
 #endif
-constexpr uint32_t kEntPack = HJ_ENT_PACK;
+[[maybe_unused]] constexpr uint32_t kEntPack = HJ_ENT_PACK;
 
 struct BlockOut {
   uint32_t* ents;
@@ -913,9 +987,29 @@ struct BlockOut {
   uint32_t bstart;  // first entry of the open block
   int dcv;          // its DC difference
   bool open;        // a block of this run is being decoded
+#if HJ_STAGE
+  uint32_t* stg;  // this run's LDS staging line (stride NT words)
+#else
   uint32_t pk[kEntPack];  // entries not yet stored (kEntPack > 1)
+#endif
 };
 
+#if HJ_STAGE
+// The staged line holding entry c leaves as kStage / 4 16-byte stores
+// (LDS reads strided by NT: conflict-free across the wave).
+template <int NT, int KS>
+__device__ __forceinline__ void flush_line(BlockOut& o, uint32_t c) {
+  static_assert(KS % 4 == 0 && 64 % KS == 0, "lines tile the 64-entry block regions");
+  const uint32_t base = min(c & ~(uint32_t)(KS - 1), o.last & ~(uint32_t)(KS - 1));
+  uint4* dst = reinterpret_cast<uint4*>(o.ents + base);
+#pragma unroll
+  for (int i = 0; i < KS / 4; i++)
+    dst[i] = make_uint4(o.stg[(4 * i) * NT], o.stg[(4 * i + 1) * NT], o.stg[(4 * i + 2) * NT],
+                        o.stg[(4 * i + 3) * NT]);
+}
+#endif
+
+#if !HJ_STAGE
 __device__ __forceinline__ void store_pack(BlockOut& o) {
   const uint32_t base = min(o.cur & ~(kEntPack - 1u), o.last & ~(kEntPack - 1u));
   char* a = reinterpret_cast<char*>(o.ents) + (base << 2);
@@ -927,10 +1021,18 @@ __device__ __forceinline__ void store_pack(BlockOut& o) {
     *reinterpret_cast<uint32_t*>(a) = o.pk[0];
 }
 
+#endif
+
 // entry e at o.cur (the caller advances o.cur)
+template <int NT>
 __device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e) {
 #if HJ_XP_NOENT
   if (e == 0x12345u) o.ents[0] = e;
+#elif HJ_STAGE
+  constexpr int KS = stage_entries(NT);
+  const uint32_t k = o.cur & (uint32_t)(KS - 1);
+  o.stg[k * NT] = e;
+  if (k == (uint32_t)(KS - 1)) flush_line<NT, KS>(o, o.cur);
 #else
   if constexpr (kEntPack == 1) {
     *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.ents) + (min(o.cur, o.last) << 2)) = e;
@@ -943,17 +1045,35 @@ __device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e) {
 #endif
 }
 
+template <int NT>
 __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
+  const uint32_t nc = (o.cur + 3u) & ~3u;  // the next list starts 16-byte aligned
+#if HJ_STAGE
+  constexpr int KS = stage_entries(NT);
+  // the list's padding completes the staged line: it leaves now
+  if ((o.cur & (uint32_t)(KS - 1)) != 0u && (nc & (uint32_t)(KS - 1)) == 0u)
+    flush_line<NT, KS>(o, o.cur);
+#else
   if constexpr (kEntPack > 1) {
     if (o.cur & (kEntPack - 1u)) store_pack(o);  // the partial pack (its tail is unused)
   }
+#endif
 #if HJ_XP_NOBD
   if (o.dcv == 0x12345) o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
 #else
   o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
 #endif
-  o.cur = (o.cur + 3u) & ~3u;
+  o.cur = nc;
   o.open = false;
+}
+
+// the run's last, partial staged line
+template <int NT>
+__device__ __forceinline__ void flush_tail(BlockOut& o) {
+#if HJ_STAGE
+  constexpr int KS = stage_entries(NT);
+  if (o.cur & (uint32_t)(KS - 1)) flush_line<NT, KS>(o, o.cur);
+#endif
 }
 
 // Full decode from a synchronised state (z == 0: at a block start) of the
@@ -995,14 +1115,14 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const bool ac = coef & !is_dc;
     if (ac) {
       const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-      put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
+      put_entry<NT>(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
     }
     o.cur += ac ? 1u : 0u;
     o.bstart = is_dc ? o.cur : o.bstart;
     o.dcv = is_dc ? v : o.dcv;
     nb += is_dc ? 1 : 0;
     const bool bend = zn >= 64u;
-    if (bend) close_block(o, nb - 1);
+    if (bend) close_block<NT>(o, nb - 1);
     o.open = !bend;
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
     d.z = bend ? 0u : zn;
@@ -1040,7 +1160,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     }
     if (wr && !is_dc) {
       const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-      put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
+      put_entry<NT>(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
       o.cur++;
     }
     nb += (wr && is_dc) ? 1 : 0;
@@ -1050,13 +1170,13 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     done = (bad && past_a) || stop || (trunc && past_b);
     rc = (bad && !past_a) ? kErrBadHuffman : ((trunc && !past_b) ? kErrTruncated : kOk);
     const bool bend = zn >= 64u;
-    if (bend && !stop && o.open) close_block(o, nb - 1);
+    if (bend && !stop && o.open) close_block<NT>(o, nb - 1);
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
   // the segment ended (or failed) inside a block: keep what it decoded
-  if (o.open && d.z != 0u) close_block(o, nb - 1);
+  if (o.open && d.z != 0u) close_block<NT>(o, nb - 1);
   return rc;
 }
 
@@ -1095,8 +1215,13 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
                               const HuffTable* __restrict__ luts, uint32_t* __restrict__ ents,
                               uint2* __restrict__ bdesc, uint32_t* __restrict__ recs,
                               const int sub_bits_param,
-                              const int warm_slots) {
+                              const int warm_param) {
   const int tid = threadIdx.x;
+  // warm_param: warm-up slots; bits 16-19 = timing ablations (BatchParams
+  // debug_mask >> 12: 1 skips the write and DC passes, 2 the sync rounds,
+  // 4 round 0, 8 the DC pass; outputs are wrong)
+  const int warm_slots = warm_param & 0xFFFF;
+  const int dbg = warm_param >> 16;
   uint32_t* win = &S.win[0][tid];
   if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc dd = desc[img];
@@ -1230,7 +1355,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
     };
 
     // ---- round 0: every run from a guess at its first slot ----
-    {
+    if (!(dbg & 4)) {
       Dec d;
       d.pos = 0;
       d.z = d.bs = 0;
@@ -1267,7 +1392,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
     // ---- sync rounds: re-decode a run from its left neighbour's end state
     // until the trajectory merges with the stored one at a slot boundary ----
     int rounds = 0;
-    for (;;) {
+    for (; !(dbg & 2);) {
       if (tid == 0) S.flag = 0;
       __syncthreads();
       bool redo = false;
@@ -1360,6 +1485,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
         b1 = min(min(run_end_blk, seg_end_blk(slot_seg(r1 - 1))), nblocks);
       }
     }
+    if (dbg & 1) continue;
     // ---- write pass: decode each run once more from its synchronised
     // start, appending its blocks' coefficient lists; the sequential decoder's
     // stop and error rules per segment ----
@@ -1375,8 +1501,12 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       o.bstart = o.cur;
       o.dcv = 0;
       o.open = false;
+#if HJ_STAGE
+      o.stg = &S.stage[0][tid];
+#else
 #pragma unroll
       for (uint32_t i = 0; i < kEntPack; i++) o.pk[i] = 0u;
+#endif
       Dec d;
       for (int k = r0; k < r1 && rc == kOk; k++) {
         if (slot_empty(k)) {
@@ -1405,6 +1535,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
         if (rc == kOk && !done && last && (nb < seb || (nb == seb && d.z != 0)))
           rc = kErrTruncated;
       }
+      flush_tail<NT>(o);
       if (rc != kOk) atomicCAS(&S.err, kOk, rc);
     }
     __syncthreads();
@@ -1413,6 +1544,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       tph[3] += t - tstamp;
       tstamp = t;
     }
+    if (dbg & 8) continue;
     // ---- DC predictors: the write pass stored raw DC differences.  Sum them
     // per component over this run's blocks, segmented-scan the sums over the
     // runs (predictors restart at each restart segment), then replace each
@@ -1473,7 +1605,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
     }
   }
   if (tid == 0) {
-    if (S.err != kOk) infos[img].status = S.err;
+    if (S.err != kOk && !dbg) infos[img].status = S.err;
     infos[img].sync_rounds = rounds_total;
     for (int i = 0; i < 4; i++) infos[img].tphase[i] = tph[i];
     for (int i = 0; i < 4; i++) infos[img].dbg[i] = 0;
@@ -2206,7 +2338,10 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
     }
   }
   int32_t px[64];
-  if (IDCT == 0) {
+  if (IDCT == 2) {
+#pragma unroll
+    for (int i = 0; i < 64; i++) px[i] = blk[i] & 255;
+  } else if (IDCT == 0) {
 #pragma unroll
     for (int i = 0; i < 8; i++) simple_row(blk + 8 * i);
 #pragma unroll
@@ -2786,7 +2921,10 @@ hipError_t launch_idct(const uint32_t* ents, const uint2* bdesc, const ImageDesc
                        const ImageInfo* infos, uint8_t* planes, int idct, int max_blocks, int n,
                        hipStream_t st) {
   dim3 grid((max_blocks + kIdctThreads - 1) / kIdctThreads, n);
-  if (idct == 1)
+  if (idct == 2)  // timing ablation (debug_mask 0x800): no transform, wrong output
+    hipLaunchKernelGGL(idct_kernel<2>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
+                       planes);
+  else if (idct == 1)
     hipLaunchKernelGGL(idct_kernel<1>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
                        planes);
   else
