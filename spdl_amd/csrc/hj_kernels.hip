@@ -1656,6 +1656,15 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
 constexpr int kMsMaxScans = 64;
 constexpr int kMsMaxMarks = 512;
 constexpr int kMsLook = 9;
+// The scan decoder (thread 0) reads only LDS: the scan's raw bytes are staged
+// in a window of kMsWinBytes, restaged by the workgroup whenever the reader
+// gets within kMsMargin bytes of its end at an MCU start (an MCU of <= 10
+// blocks takes < 4.3 KB even with every byte stuffed).  AC refinement scans
+// run in chunks of kMsChunk blocks: the workgroup stages each block's history
+// mask beforehand and applies the decoder's records afterwards.
+constexpr int kMsWinBytes = 16384;
+constexpr int kMsMargin = 4608;
+constexpr int kMsChunk = 192;
 
 struct MsTable {
   uint16_t look[1 << kMsLook];  // (len << 8) | sym for codes <= kMsLook bits, else 0
@@ -1676,68 +1685,53 @@ struct MsShared {
   MsTable tab[8];  // DC 0..3, AC 0..3 (slot 4 + id)
   MsScan scan[kMsMaxScans];
   int32_t marks[kMsMaxMarks];
-  __attribute__((aligned(16))) int32_t blk[64];  // thread 0's block of levels (AC refinement)
+  uint32_t win[kMsWinBytes / 4 + 2];  // raw bytes [wbase, wbase + kMsWinBytes) (+2 words of slack)
+  // AC refinement chunk, per block: coefficients [ss, se] non-zero before the
+  // scan (bit k), correction bits in coefficient order (LSB first), the
+  // coefficients the scan makes non-zero and their signs (1: negative)
+  uint64_t hist[kMsChunk], corr[kMsChunk], nmask[kMsChunk], nsign[kMsChunk];
   int32_t dht[8], comp_id[kMaxComp];  // segment walk state (thread 0)
   int32_t nmarks, nscans, err;
+  int32_t wbase, mcu, fin;  // chunk loop: window base, next MCU, scan finished
 };
 
-// Sequential byte source over the file with a two-chunk (32 B) look-ahead:
-// the next 16-byte chunk is already in flight when the reader reaches it.
-// (Scalar words, not uint4 members: the state must stay in registers.)
-struct MsBytes {
-  const uint8_t* d;
-  int size, base;
-  uint32_t a0, a1, a2, a3, b0, b1, b2, b3;  // chunk at base, chunk at base + 16
-  __device__ __forceinline__ void load(int b, uint32_t& x, uint32_t& y, uint32_t& z,
-                                       uint32_t& w) const {
-    if (b + 16 <= size) {
-      const uint4 q = *reinterpret_cast<const uint4*>(d + b);
-      x = q.x, y = q.y, z = q.z, w = q.w;
-      return;
-    }
-    // the file's last partial chunk, a byte at a time (into locals: a select
-    // between references to the members would put the reader in scratch)
-    uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-#pragma unroll 1
-    for (int i = 0; i < 16 && b + i < size; i++) {
-      const uint32_t v = (uint32_t)d[b + i] << (8 * (i & 3));
-      v0 |= i < 4 ? v : 0u;
-      v1 |= i >= 4 && i < 8 ? v : 0u;
-      v2 |= i >= 8 && i < 12 ? v : 0u;
-      v3 |= i >= 12 ? v : 0u;
-    }
-    x = v0, y = v1, z = v2, w = v3;
-  }
-  __device__ __forceinline__ void seek(int p) {
-    base = p & ~15;
-    load(base, a0, a1, a2, a3);
-    load(base + 16, b0, b1, b2, b3);
-  }
-  __device__ __forceinline__ uint32_t at(int i) {
-    if (i < base) seek(i);  // a step back (a marker found by look-ahead): reload
-    while (i >= base + 16) {
-      base += 16;
-      a0 = b0, a1 = b1, a2 = b2, a3 = b3;
-      load(base + 16, b0, b1, b2, b3);
-    }
+// The scan decoder runs on all of wave 0 with identical values in every lane
+// (wave-uniform: its state lives in SGPRs and its bit twiddling is scalar
+// ALU work; a single active lane would run it on the vector unit at a
+// fraction of the rate).  Every LDS / global read is made uniform with
+// readfirstlane; stores and atomics come from lane 0 only.
+__device__ __forceinline__ uint32_t ms_u(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int ms_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t ms_u64(uint64_t v) {
+  return (uint64_t)ms_u((uint32_t)(v >> 32)) << 32 | ms_u((uint32_t)v);
+}
+__device__ __forceinline__ bool ms_lane0() { return __lane_id() == 0; }
+
+// The staged window of the file's raw bytes (little-endian words).
+struct MsWin {
+  const uint32_t* w;
+  int base, lim;  // bytes [base, lim) are staged
+  __device__ __forceinline__ uint32_t at(int i) const {
     const int k = i - base;
-    // masks, not selects: a select between members becomes a load from a
-    // selected address, which keeps the reader in scratch memory
-    const uint32_t q = (uint32_t)k >> 2;
-    const uint32_t w = (a0 & (0u - (uint32_t)(q == 0))) | (a1 & (0u - (uint32_t)(q == 1))) |
-                       (a2 & (0u - (uint32_t)(q == 2))) | (a3 & (0u - (uint32_t)(q == 3)));
-    return (w >> (8 * (k & 3))) & 0xFFu;
+    return (ms_u(w[k >> 2]) >> (8 * (k & 3))) & 0xFFu;
+  }
+  // bytes i .. i + 3 as a big-endian word
+  __device__ __forceinline__ uint32_t be32(int i) const {
+    const int k = i - base;
+    const uint64_t two = (uint64_t)ms_u(w[k >> 2]) | ((uint64_t)ms_u(w[(k >> 2) + 1]) << 32);
+    return __builtin_bswap32((uint32_t)(two >> (8 * (k & 3))));
   }
 };
 
 // Bit reader over stuffed entropy data: 0xFF00 -> 0xFF; any other marker (or
-// the scan end) stops the data, zeros follow (oracle bitrd_t).
+// the scan end) stops the data, zeros follow (oracle bitrd_t).  Four plain
+// bytes (no 0xFF among them) enter the buffer at once.
 struct MsBits {
-  MsBytes src;
+  MsWin src;
   int pos, end;
   uint64_t buf;
   int cnt;
-  bool marker;
+  bool marker, overrun;
   int64_t real, used;
   __device__ __forceinline__ void start(int p, int e) {
     pos = p;
@@ -1746,14 +1740,26 @@ struct MsBits {
     cnt = 0;
     marker = false;
     real = used = 0;
-    src.seek(p);
   }
   __device__ __forceinline__ void fill() {
     while (cnt <= 56) {
+      if (!marker && cnt <= 32 && pos + 4 <= end && pos + 4 <= src.lim) {
+        const uint32_t v = src.be32(pos);
+        if (((~v - 0x01010101u) & v & 0x80808080u) == 0u) {  // no 0xFF byte
+          buf |= (uint64_t)v << (32 - cnt);
+          cnt += 32;
+          pos += 4;
+          real += 32;
+          continue;
+        }
+      }
       uint32_t byte = 0;
       if (!marker) {
         if (pos >= end) {
           marker = true;
+        } else if (pos + 1 >= src.lim && pos + 1 < end) {
+          marker = true;  // past the staged window (cannot happen within the margin)
+          overrun = true;
         } else {
           const uint32_t c = src.at(pos);
           if (c == 0xFFu) {
@@ -1785,7 +1791,7 @@ struct MsBits {
     cnt -= n;
     used += n;
   }
-  __device__ __forceinline__ uint32_t get(int n) {
+  __device__ __forceinline__ uint32_t get(int n) {  // n <= 32
     if (n == 0) return 0u;
     if (cnt < 32) fill();
     const uint32_t v = (uint32_t)(buf >> (64 - n));
@@ -1795,16 +1801,16 @@ struct MsBits {
   // symbol, or -1 for an invalid code
   __device__ __forceinline__ int decode(const MsTable& t) {
     const uint32_t w = peek16();
-    const uint32_t e = t.look[w >> (16 - kMsLook)];
+    const uint32_t e = ms_u(t.look[w >> (16 - kMsLook)]);
     if (e) {
       skip((int)(e >> 8));
       return (int)(e & 0xFFu);
     }
     for (int l = kMsLook + 1; l <= 16; l++) {
       const int code = (int)(w >> (16 - l));
-      if (code <= t.maxcode[l]) {
+      if (code <= ms_i(t.maxcode[l])) {
         skip(l);
-        return t.vals[t.valoff[l] + code];
+        return ms_i(t.vals[ms_i(t.valoff[l]) + code]);
       }
     }
     return -1;
@@ -1813,6 +1819,50 @@ struct MsBits {
 
 __device__ __forceinline__ int ms_extend(uint32_t v, int s) {
   return v < (1u << (s - 1)) ? (int)v - ((1 << s) - 1) : (int)v;
+}
+
+// bits k .. e (inclusive) of a coefficient mask; 0 when k > e
+__device__ __forceinline__ uint64_t ms_range(int k, int e) {
+  return k > e ? 0ull : ((~0ull) >> (63 - e)) & ((~0ull) << k);
+}
+
+// The image geometry the scan decoder needs (uniform copies).
+// (sampling factors packed 3 bits each: a local array with a dynamic index
+// would live in scratch memory)
+struct MsGeo {
+  int ncomp, mcux, bpm;
+  uint32_t hv;  // comp_h[c] at bit 6c, comp_v[c] at bit 6c + 3
+  __device__ __forceinline__ int h(int c) const { return (int)((hv >> (6 * c)) & 7u); }
+  __device__ __forceinline__ int v(int c) const { return (int)((hv >> (6 * c + 3)) & 7u); }
+};
+
+__device__ __forceinline__ MsGeo ms_geo(const ImageInfo& in) {
+  MsGeo g;
+  g.ncomp = ms_i(in.ncomp);
+  g.mcux = ms_i(in.mcux);
+  g.bpm = ms_i(in.bpm);
+  g.hv = 0;
+  for (int c = 0; c < kMaxComp; c++)
+    g.hv |= (uint32_t)ms_i(in.comp_h[c]) << (6 * c) | (uint32_t)ms_i(in.comp_v[c]) << (6 * c + 3);
+  return g;
+}
+
+// The scalar fields of a scan record, uniform.
+struct MsBand {
+  int ns, ss, se, ah, al, ri, end;
+};
+
+__device__ __forceinline__ MsBand ms_band(const MsScan& sc) {
+  return MsBand{ms_i(sc.ns), ms_i(sc.ss), ms_i(sc.se), ms_i(sc.ah), ms_i(sc.al), ms_i(sc.ri),
+                ms_i(sc.end)};
+}
+
+__device__ __forceinline__ int ms_block(const MsGeo& g, int c, int bx, int by) {
+  if (g.ncomp == 1) return by * g.mcux + bx;
+  int b0 = 0;
+  for (int k = 0; k < c; k++) b0 += g.h(k) * g.v(k);
+  const int hc = g.h(c), vc = g.v(c);
+  return ((by / vc) * g.mcux + bx / hc) * g.bpm + b0 + (by % vc) * hc + (bx % hc);
 }
 
 // MCU-order block index of component c's block (bx, by)
@@ -1825,16 +1875,32 @@ __device__ __forceinline__ int ms_block(const ImageInfo& in, int c, int bx, int 
   return (my * in.mcux + mx) * in.bpm + b;
 }
 
+// One correction bit per set bit of m, appended LSB-first to corr.
+__device__ __forceinline__ void ms_take_corr(MsBits& br, uint64_t m, uint64_t& corr, int& nc) {
+  int c = __popcll(m);
+  while (c > 0) {
+    const int t = c < 32 ? c : 32;
+    const uint32_t v = br.get(t);
+    corr |= (uint64_t)(__builtin_bitreverse32(v) >> (32 - t)) << nc;
+    nc += t;
+    c -= t;
+  }
+}
+
 // One block of one scan (thread 0).  lev: the block's levels in HBM (zig-zag
-// index); AC refinement works on the copy ms_scan staged in S.blk.
-__device__ __forceinline__ int ms_block_decode(MsShared& S, MsBits& br, const MsScan& sc, bool prog,
-                               const MsTable& dh, const MsTable& ah, int32_t& pred,
-                               int32_t* __restrict__ lev, int& eobrun) {
+// index; stores only).  AC refinement (block j of the chunk) decodes against
+// the staged history mask and leaves records for the workgroup to apply:
+// which history coefficients get a correction bit (libjpeg jdphuff
+// decode_mcu_AC_refine reads one per non-zero coefficient it passes, in
+// order) and which zero coefficients become +-(1 << al).
+__device__ __forceinline__ int ms_block_decode(MsShared& S, MsBits& br, const MsBand& sc, bool prog,
+                                               const MsTable& dh, const MsTable& ah, int32_t& pred,
+                                               int32_t* __restrict__ lev, int& eobrun, int j) {
   if (!prog) {  // sequential scan: the whole block
     int s = br.decode(dh);
     if (s < 0 || s > 15) return kErrBadHuffman;
     pred += s ? ms_extend(br.get(s), s) : 0;
-    lev[0] = pred;
+    if (ms_lane0()) lev[0] = pred;
     for (int k = 1; k < 64;) {
       const int rs = br.decode(ah);
       if (rs < 0) return kErrBadHuffman;
@@ -1850,7 +1916,9 @@ __device__ __forceinline__ int ms_block_decode(MsShared& S, MsBits& br, const Ms
       }
       k += r;
       if (k > 63) return kErrBadHuffman;
-      lev[k++] = ms_extend(br.get(s), s);
+      const int v = ms_extend(br.get(s), s);
+      if (ms_lane0()) lev[k] = v;
+      k++;
     }
     return kOk;
   }
@@ -1860,9 +1928,9 @@ __device__ __forceinline__ int ms_block_decode(MsShared& S, MsBits& br, const Ms
       const int s = br.decode(dh);
       if (s < 0 || s > 15) return kErrBadHuffman;
       pred += s ? ms_extend(br.get(s), s) : 0;
-      lev[0] = (int32_t)((uint32_t)pred << al);
+      if (ms_lane0()) lev[0] = (int32_t)((uint32_t)pred << al);
     } else if (br.get(1)) {  // DC refine
-      atomicOr(reinterpret_cast<unsigned int*>(lev), 1u << al);
+      if (ms_lane0()) atomicOr(reinterpret_cast<unsigned int*>(lev), 1u << al);
     }
     return kOk;
   }
@@ -1878,7 +1946,8 @@ __device__ __forceinline__ int ms_block_decode(MsShared& S, MsBits& br, const Ms
       if (s) {
         k += r;
         if (k > sc.se) return kErrBadHuffman;
-        lev[k] = (int32_t)((uint32_t)ms_extend(br.get(s), s) << al);
+        const int32_t v = (int32_t)((uint32_t)ms_extend(br.get(s), s) << al);
+        if (ms_lane0()) lev[k] = v;
       } else if (r == 15) {
         k += 15;
       } else {
@@ -1889,123 +1958,184 @@ __device__ __forceinline__ int ms_block_decode(MsShared& S, MsBits& br, const Ms
     }
     return kOk;
   }
-  // AC refinement (successive approximation) on the LDS copy of the block
-  int32_t* b = S.blk;
-  const int32_t p1 = 1 << al, m1 = -(1 << al);
-  int k = sc.ss;
+  // AC refinement (successive approximation) against the history mask
+  const int se = sc.se;
+  const uint64_t hist = ms_u64(S.hist[j]);
+  uint64_t corr = 0, nm = 0, nsg = 0;
+  int nc = 0, k = sc.ss;
   if (eobrun <= 0) {
-    for (; k <= sc.se; k++) {
+    while (k <= se) {
       const int rs = br.decode(ah);
       if (rs < 0) return kErrBadHuffman;
-      int r = rs >> 4;
-      const int s = rs & 15;
-      int32_t v = 0;
+      const int r = rs >> 4, s = rs & 15;
+      int v = 0;
       if (s) {
         if (s != 1) return kErrBadHuffman;
-        v = br.get(1) ? p1 : m1;
+        v = br.get(1) ? 1 : -1;
       } else if (r != 15) {
         eobrun = 1 << r;
         if (r) eobrun += (int)br.get(r);
         break;
       }
-      for (; k <= sc.se; k++) {
-        const int32_t c = b[k];
-        if (c != 0) {
-          if (br.get(1) && (c & p1) == 0) b[k] = c + (c >= 0 ? p1 : m1);
-        } else {
-          if (r == 0) break;
-          r--;
-        }
-      }
-      if (k > sc.se) {
+      // the (r + 1)-th coefficient from k that was zero before the scan:
+      // the new coefficient's place (ZRL: the 16th zero, left zero); every
+      // non-zero one passed on the way takes a correction bit
+      uint64_t zm = ~hist & ms_range(k, se);
+      for (int i = 0; i < r && zm; i++) zm &= zm - 1;
+      if (zm == 0ull) {  // ran past se
+        ms_take_corr(br, hist & ms_range(k, se), corr, nc);
+        k = se + 1;
         if (v) return kErrBadHuffman;
         break;
       }
-      if (v) b[k] = v;
+      const int p = __builtin_ctzll(zm);
+      ms_take_corr(br, hist & ms_range(k, p - 1), corr, nc);
+      if (v) {
+        nm |= 1ull << p;
+        nsg |= (v < 0 ? 1ull : 0ull) << p;
+      }
+      k = p + 1;
     }
   }
   if (eobrun > 0) {
-    for (; k <= sc.se; k++) {
-      const int32_t c = b[k];
-      if (c != 0 && br.get(1) && (c & p1) == 0) b[k] = c + (c >= 0 ? p1 : m1);
-    }
+    ms_take_corr(br, hist & ms_range(k, se), corr, nc);
     eobrun--;
+  }
+  if (ms_lane0()) {
+    S.corr[j] = corr;
+    S.nmask[j] = nm;
+    S.nsign[j] = nsg;
   }
   return kOk;
 }
 
-// One scan (thread 0): restart intervals, interleaved MCUs or one
+// Thread 0's scan decoder state, carried across chunks in registers.
+struct MsState {
+  MsBits br;
+  int32_t pred0, pred1, pred2;
+  int eobrun, mcu, nmcu, bw1;
+  bool rst_done;  // the restart marker before `mcu` was consumed
+};
+
+// Thread 0: decode MCUs of one scan from st.mcu on, until the scan ends, the
+// chunk ends (AC refinement: MCU chunk_end) or the reader comes within the
+// margin of the staged window's end at an MCU start (wlim; unless the window
+// holds the rest of the scan).  Restart intervals, interleaved MCUs or one
 // component's blocks in raster order over its own (unpadded) block grid.
 // (Everything here is inlined into the kernel: through a call the reader
 // state would live in scratch memory and the LDS tables behind flat loads.)
-__device__ __forceinline__ int ms_scan(MsShared& S, const uint8_t* d, int size, const ImageInfo& in,
-                       const MsScan& sc, bool prog, int32_t* __restrict__ lv) {
-  MsBits br;
-  br.src.d = d;
-  br.src.size = size;
-  br.start(sc.start, sc.end);
-  int32_t pred0 = 0, pred1 = 0, pred2 = 0;  // (scalars: an indexed array would be scratch)
-  int eobrun = 0;
-  int nmcu, bw1 = 1;
-  if (sc.ns > 1) {
-    nmcu = in.mcux * in.mcuy;
-  } else {
-    const int c = sc.comp[0];
-    bw1 = in.ncomp == 1 ? in.mcux : (in.comp_w[c] + 7) / 8;
-    const int bh1 = in.ncomp == 1 ? in.mcuy : (in.comp_hpx[c] + 7) / 8;
-    nmcu = bw1 * bh1;
-  }
-  const bool refine = prog && sc.ss > 0 && sc.ah > 0;  // reads its blocks: staged in S.blk
-  for (int mcu = 0; mcu < nmcu; mcu++) {
-    if (sc.ri && mcu && mcu % sc.ri == 0) {
-      if (br.used > br.real) return kErrTruncated;
+// x / d and x % d for a sampling factor d in 1..4 (no division instruction)
+__device__ __forceinline__ int ms_div(int x, int d) {
+  return d == 1 ? x : (d == 2 ? x >> 1 : (d == 4 ? x >> 2 : (int)(((uint32_t)x * 0xAAABu) >> 17)));
+}
+
+__device__ __forceinline__ int ms_scan_chunk(MsShared& S, const uint8_t* d, int size,
+                                             const MsGeo& in, const MsScan& scl, bool prog,
+                                             int32_t* __restrict__ lv, MsState& st, int wlim,
+                                             int chunk0, int chunk_end) {
+  const MsBand sc = ms_band(scl);
+  const bool refine = prog && sc.ss > 0 && sc.ah > 0;
+  // the state in locals for the loop (a select between members of a
+  // referenced struct becomes a load from a selected scratch address)
+  MsBits br = st.br;
+  int32_t pred0 = st.pred0, pred1 = st.pred1, pred2 = st.pred2;
+  int eobrun = st.eobrun, mcu = st.mcu;
+  bool rst_done = st.rst_done;
+  const int nmcu = st.nmcu, bw1 = st.bw1;
+  // MCU / block coordinates advance incrementally (one division per chunk)
+  const int c1 = ms_i(scl.comp[0]);  // the component of a one-component scan
+  const int hc1 = in.ncomp == 1 ? 1 : in.h(c1), vc1 = in.ncomp == 1 ? 1 : in.v(c1);
+  int b01 = 0;  // blocks of the components before c1 in an MCU
+  for (int k = 0; k < c1; k++) b01 += in.h(k) * in.v(k);
+  int bx = mcu % bw1, by = mcu / bw1;            // one-component scans
+  int rpos = sc.ri ? mcu % sc.ri : 0;            // MCUs since the last restart
+  int rc = kOk;
+  for (; mcu < nmcu; mcu++, rst_done = false) {
+    if (sc.ri && mcu && rpos == 0 && !rst_done) {
+      if (br.used > br.real) {
+        rc = kErrTruncated;
+        break;
+      }
+      // the next marker must be RSTn (found in the file itself: once per interval)
       int p = br.pos;
-      for (;;) {  // the next marker must be RSTn
-        if (p >= sc.end) return kErrBadRestart;
-        const uint32_t c = br.src.at(p);
-        if (c == 0xFFu && p + 1 < size && br.src.at(p + 1) == 0u) {
+      for (;;) {
+        if (p >= sc.end) {
+          rc = kErrBadRestart;
+          break;
+        }
+        const uint32_t c = ms_u(d[p]);
+        if (c == 0xFFu && p + 1 < size && ms_u(d[p + 1]) == 0u) {
           p += 2;
           continue;
         }
         if (c == 0xFFu) break;
         p++;
       }
-      while (p < size && br.src.at(p) == 0xFFu) p++;
-      if (p >= size || br.src.at(p) < 0xD0u || br.src.at(p) > 0xD7u) return kErrBadRestart;
+      if (rc != kOk) break;
+      while (p < size && ms_u(d[p]) == 0xFFu) p++;
+      if (p >= size || ms_u(d[p]) < 0xD0u || ms_u(d[p]) > 0xD7u) {
+        rc = kErrBadRestart;
+        break;
+      }
       br.start(p + 1, sc.end);
       pred0 = pred1 = pred2 = 0;
       eobrun = 0;
+      rst_done = true;
     }
-    const int mx = mcu % in.mcux, my = mcu / in.mcux;
-    for (int i = 0; i < sc.ns; i++) {
-      const int c = sc.comp[i];
-      const MsTable& dh = S.tab[sc.td[i]];
-      const MsTable& ah = S.tab[4 + sc.ta[i]];
-      int32_t pred = c == 0 ? pred0 : (c == 1 ? pred1 : pred2);
-      const int hc = in.comp_h[c], nb = sc.ns > 1 ? hc * in.comp_v[c] : 1;
-      for (int u = 0; u < nb; u++) {
-        const int b = sc.ns > 1 ? ms_block(in, c, mx * hc + u % hc, my * in.comp_v[c] + u / hc)
-                                : ms_block(in, c, mcu % bw1, mcu / bw1);
-        int32_t* lev = lv + (size_t)b * 64;
-        if (refine) {
-          const uint4* src = reinterpret_cast<const uint4*>(lev);
-#pragma unroll
-          for (int q = 0; q < 16; q++) reinterpret_cast<uint4*>(S.blk)[q] = src[q];
+    if (br.pos > wlim || br.pos < br.src.base) break;  // restage the window
+    if (refine && mcu >= chunk_end) break;
+    if (sc.ns > 1) {  // interleaved: the MCU's blocks are consecutive, component by component
+      for (int i = 0; i < sc.ns && rc == kOk; i++) {
+        const int c = ms_i(scl.comp[i]);
+        const MsTable& dh = S.tab[ms_i(scl.td[i])];
+        const MsTable& ah = S.tab[4 + ms_i(scl.ta[i])];
+        int32_t pred = c == 0 ? pred0 : (c == 1 ? pred1 : pred2);
+        const int nb = in.h(c) * in.v(c);
+        int b = mcu * in.bpm;  // + the blocks of the image's components before c
+        for (int k = 0; k < c; k++) b += in.h(k) * in.v(k);
+        for (int u = 0; u < nb; u++, b++) {
+          rc = ms_block_decode(S, br, sc, prog, dh, ah, pred, lv + (size_t)b * 64, eobrun,
+                               mcu - chunk0);
+          if (rc != kOk) break;
         }
-        const int rc = ms_block_decode(S, br, sc, prog, dh, ah, pred, lev, eobrun);
-        if (rc != kOk) return rc;
-        if (refine) {
-          uint4* dst = reinterpret_cast<uint4*>(lev);
-#pragma unroll
-          for (int q = 0; q < 16; q++) dst[q] = reinterpret_cast<const uint4*>(S.blk)[q];
-        }
+        pred0 = c == 0 ? pred : pred0;
+        pred1 = c == 1 ? pred : pred1;
+        pred2 = c == 2 ? pred : pred2;
       }
-      pred0 = c == 0 ? pred : pred0;
-      pred1 = c == 1 ? pred : pred1;
-      pred2 = c == 2 ? pred : pred2;
+    } else {
+      const int b = in.ncomp == 1
+                        ? by * in.mcux + bx
+                        : (ms_div(by, vc1) * in.mcux + ms_div(bx, hc1)) * in.bpm + b01 +
+                              (by - ms_div(by, vc1) * vc1) * hc1 + (bx - ms_div(bx, hc1) * hc1);
+      int32_t pred = c1 == 0 ? pred0 : (c1 == 1 ? pred1 : pred2);
+      rc = ms_block_decode(S, br, sc, prog, S.tab[ms_i(scl.td[0])], S.tab[4 + ms_i(scl.ta[0])],
+                           pred, lv + (size_t)b * 64, eobrun, mcu - chunk0);
+      pred0 = c1 == 0 ? pred : pred0;
+      pred1 = c1 == 1 ? pred : pred1;
+      pred2 = c1 == 2 ? pred : pred2;
     }
+    if (rc != kOk) break;
+    if (++bx == bw1) {
+      bx = 0;
+      by++;
+    }
+    if (sc.ri && ++rpos == sc.ri) rpos = 0;
   }
-  return br.used > br.real ? kErrTruncated : kOk;
+  if (rc == kOk && mcu >= nmcu)
+    rc = br.overrun ? kErrUnsupported : (br.used > br.real ? kErrTruncated : kOk);
+  st.br = br;
+  st.pred0 = pred0;
+  st.pred1 = pred1;
+  st.pred2 = pred2;
+  st.eobrun = eobrun;
+  st.mcu = mcu;
+  st.rst_done = rst_done;
+  return rc;
+}
+
+// block of MCU m of a one-component scan (AC scans)
+__device__ __forceinline__ int ms_scan_block(const ImageInfo& in, const MsScan& sc, int bw1, int m) {
+  return ms_block(in, sc.comp[0], m % bw1, m / bw1);
 }
 
 __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restrict__ bytes,
@@ -2023,7 +2153,11 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   const bool prog = in.progressive != 0;
   int32_t* lv = reinterpret_cast<int32_t*>(ents + (size_t)dd.coef_off * 64);
   const int nblocks = in.nblocks;
-  int64_t t0 = wall_clock64(), tph[4] = {0, 0, 0, 0};
+  int64_t t0 = wall_clock64(), tph[4] = {0, 0, 0, 0}, tdbg[4] = {0, 0, 0, 0};
+  MsState st;  // the scan decoder (wave 0, uniform)
+  // (a uniform condition: readfirstlane of the wave's first thread index)
+  const bool wave0 = __builtin_amdgcn_readfirstlane(tid) < 64;
+  const MsGeo geo = ms_geo(in);
   if (tid == 0) {
     S.nmarks = 0;
     S.nscans = 0;
@@ -2215,9 +2349,110 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
       __syncthreads();
     }
     const int64_t ts = wall_clock64();
-    if (tid == 0 && S.err == kOk) S.err = ms_scan(S, d, size, in, sc, progressive, lv);
+    const bool refine = progressive && sc.ss > 0 && sc.ah > 0;
+    int bw1 = 1, nmcu = in.mcux * in.mcuy;
+    if (sc.ns == 1) {
+      const int c = sc.comp[0];
+      bw1 = in.ncomp == 1 ? in.mcux : (in.comp_w[c] + 7) / 8;
+      nmcu = bw1 * (in.ncomp == 1 ? in.mcuy : (in.comp_hpx[c] + 7) / 8);
+    }
+    if (wave0) {
+      st.br.start(ms_i(sc.start), ms_i(sc.end));
+      st.br.overrun = false;
+      st.pred0 = st.pred1 = st.pred2 = 0;
+      st.eobrun = 0;
+      st.mcu = 0;
+      st.nmcu = ms_i(nmcu);
+      st.bw1 = ms_i(bw1);
+      st.rst_done = false;
+    }
+    if (tid == 0) {
+      S.wbase = sc.start & ~3;
+      S.mcu = 0;
+      S.fin = S.err != kOk;
+    }
     __syncthreads();
-    tph[2] += wall_clock64() - ts;  // decode
+    // chunks: (re)stage the window, stage history masks (AC refinement),
+    // thread 0 decodes, the workgroup applies the refinement records
+    int staged = -1;
+    while (!S.fin) {
+      const int wb = S.wbase, m0 = S.mcu;
+      if (wb != staged) {
+        for (int i = tid; i < kMsWinBytes / 4 + 2; i += nt) {
+          const int o = wb + 4 * i;
+          uint32_t v = 0;
+          if (o + 4 <= size) {
+            v = *reinterpret_cast<const uint32_t*>(d + o);
+          } else {
+            for (int b = 0; b < 4 && o + b < size; b++) v |= (uint32_t)d[o + b] << (8 * b);
+          }
+          S.win[i] = v;
+        }
+        staged = wb;
+      }
+      if (refine) {
+        const uint64_t band = ms_range(sc.ss, sc.se);
+        for (int j = tid; j < kMsChunk && m0 + j < nmcu; j += nt) {
+          const uint4* src =
+              reinterpret_cast<const uint4*>(lv + (size_t)ms_scan_block(in, sc, bw1, m0 + j) * 64);
+          uint64_t h = 0;
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+            const uint4 x = src[q];
+            h |= (uint64_t)((x.x != 0u) | (x.y != 0u) << 1 | (x.z != 0u) << 2 | (x.w != 0u) << 3)
+                 << (4 * q);
+          }
+          S.hist[j] = h & band;
+        }
+      }
+      __syncthreads();
+      if (wave0) {
+        const int wbu = ms_i(wb), m0u = ms_i(m0), send = ms_i(sc.end);
+        st.br.src.w = S.win;
+        st.br.src.base = wbu;
+        const int sizeu = ms_i(size);
+        st.br.src.lim = min(wbu + kMsWinBytes, sizeu);
+        // the window holds the rest of the scan, or the reader stops at an
+        // MCU start within kMsMargin of its end
+        const int wlim =
+            send <= wbu + kMsWinBytes ? 0x7FFFFFFF : wbu + kMsWinBytes - kMsMargin;
+        const int rc = ms_scan_chunk(S, d, sizeu, geo, sc, ms_i(progressive) != 0, lv, st, wlim, m0u,
+                                     m0u + kMsChunk);
+        if (ms_lane0()) {
+          S.err = rc;
+          S.mcu = st.mcu;
+          if (st.br.pos > wlim) S.wbase = st.br.pos & ~3;
+          S.fin = rc != kOk || st.mcu >= nmcu;
+        }
+      }
+      __syncthreads();
+      if (refine && S.err == kOk) {
+        const int32_t p1 = 1 << sc.al, m1 = -p1;
+        for (int j = tid; j < S.mcu - m0; j += nt) {
+          int32_t* lev = lv + (size_t)ms_scan_block(in, sc, bw1, m0 + j) * 64;
+          uint64_t h = S.hist[j], corr = S.corr[j], m = S.nmask[j];
+          const uint64_t sg = S.nsign[j];
+          for (; h; h &= h - 1, corr >>= 1) {
+            if (corr & 1u) {
+              const int k = __builtin_ctzll(h);
+              const int32_t c = lev[k];
+              if ((c & p1) == 0) lev[k] = c + (c >= 0 ? p1 : m1);
+            }
+          }
+          for (; m; m &= m - 1) {
+            const int k = __builtin_ctzll(m);
+            lev[k] = ((sg >> k) & 1u) ? m1 : p1;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    const int64_t dt = wall_clock64() - ts;
+    tph[2] += dt;  // decode
+    // diagnostics by scan kind: DC, AC first, AC refinement, sequential
+    const int kind = !progressive ? 3 : (sc.ss == 0 ? 0 : (sc.ah == 0 ? 1 : 2));
+#pragma unroll
+    for (int i = 0; i < 4; i++) tdbg[i] += i == kind ? dt : 0;  // (static indices: no scratch)
   }
   tph[1] = wall_clock64() - t0 - tph[0] - tph[2];  // table builds
   if (S.err != kOk) {
@@ -2255,6 +2490,7 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   if (tid == 0) {
     tph[3] = wall_clock64() - t0 - tph[0] - tph[1] - tph[2];  // lists
     for (int i = 0; i < 4; i++) in.tphase[i] = tph[i];
+    for (int i = 0; i < 4; i++) in.dbg[i] = tdbg[i];
     in.sync_rounds = S.nscans;
   }
 }
