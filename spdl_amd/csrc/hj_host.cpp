@@ -812,10 +812,14 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         ctx->entropy_threads ? ctx->entropy_threads : (ctx->lanes > 1 ? 256 : 512),
                         ctx->entropy_lds_pad, n, st));
   // progressive / non-interleaved images (the kernels above skipped them)
-  HJ_HIP(launch_multiscan(d_bytes, desc, infos, static_cast<uint32_t*>(W.ents.p),
-                          static_cast<uint2*>(W.bdesc.p), n, st));
+  // (debug_mask 0x10000 / 0x20000 / 0x40000: timing ablations that skip the
+  // multiscan / IDCT / output launch; the output is wrong)
+  if (!(ctx->debug_mask & 0x10000))
+    HJ_HIP(launch_multiscan(d_bytes, desc, infos, static_cast<uint32_t*>(W.ents.p),
+                            static_cast<uint2*>(W.bdesc.p), n, st));
   mark(ctx, slot, 4, st);
-  HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
+  if (!(ctx->debug_mask & 0x20000))
+    HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
                      static_cast<const uint2*>(W.bdesc.p), desc, infos,
                      static_cast<uint8_t*>(W.planes.p), (ctx->debug_mask & 0x800) ? 2 : out->idct,
                      L.max_blocks, n, st));
@@ -849,7 +853,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   // the output kernel writes each image's status into the pinned array itself
   int32_t* hstat = hs && !planes_only ? static_cast<int32_t*>(slot.pin_status.dev) : nullptr;
   mark(ctx, slot, 6, st);
-  if (!planes_only) {
+  if (!planes_only && !(ctx->debug_mask & 0x40000)) {
     if (swscale) {
       HJ_HIP(launch_sws(static_cast<const uint8_t*>(W.planes.p), desc, infos,
                         static_cast<const int32_t*>(W.wts.p), out_dev, bp, L.sws_bands,
