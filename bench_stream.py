@@ -33,6 +33,7 @@ import tarfile
 import tempfile
 import time
 
+import spdl_amd  # noqa: F401  (sets the HW queue count before HIP initialises)
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -59,6 +60,10 @@ def _args():
     p.add_argument("--distinct", type=int, default=32)
     p.add_argument("--d2h", action="store_true")
     p.add_argument("--source", choices=["file", "bytes"], default="file")
+    p.add_argument("--depth", type=int, default=4,
+                   help="batches in flight (= decode pipeline lanes), 1-8")
+    p.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
+                   help="extra decoder parameter (spdl_hj_set_param), for A/B runs")
     return p.parse_args()
 
 
@@ -93,7 +98,10 @@ def main():
             data = f.read()
         src = data if a.source == "bytes" else path
         cfg = sio.cuda_config(device_index=local, stream=torch.cuda.current_stream(device).cuda_stream)
-        st = sio.TarImageStream(src, batch_size=a.batch, device_config=cfg)
+        st = sio.TarImageStream(src, batch_size=a.batch, device_config=cfg, depth=a.depth)
+        for kv in a.param:
+            k, v = kv.split("=", 1)
+            st._dec.set_param(k, int(v))
         d2h = torch.cuda.Stream(device) if a.d2h else None
         host = [torch.empty((a.batch, 224, 224, 3), dtype=torch.uint8).pin_memory()
                 for _ in range(2)] if a.d2h else None
@@ -156,6 +164,7 @@ def main():
                     "tar_bytes_per_rank": tar_bytes,
                     "jpeg_payload_bytes_per_rank": payload,
                     "d2h": bool(a.d2h),
+                    "depth": a.depth,
                     "parallelism": f"{world} independent per-GPU archives, no collective",
                 },
                 "h2d_GBps_per_gpu": round(tar_bytes * a.passes / elapsed / 1e9, 3),

@@ -2508,7 +2508,10 @@ hipError_t launch_multiscan(const uint8_t* bytes, const ImageDesc* desc, ImageIn
 // Per-thread dense block in LDS: 64 int16 in natural order in a 144-byte
 // slot (36 words: the uint4 accesses of 16 consecutive threads fall on
 // disjoint banks).
-constexpr int kIdctThreads = 256;
+#ifndef HJ_IDCT_THREADS
+#define HJ_IDCT_THREADS 256
+#endif
+constexpr int kIdctThreads = HJ_IDCT_THREADS;
 constexpr int kBlkWords = 36;
 
 template <int IDCT>

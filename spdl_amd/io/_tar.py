@@ -87,7 +87,8 @@ class TarImageStream:
         output: :class:`spdl_amd._lib.Output` (default: RGB24 224x224, the
             ``load_image_batch(width=224, height=224)`` filter chain).
         select: predicate on member names (default: JPEG extensions).
-        depth: batches in flight (<= 2; the native ring has 3 slots).
+        depth: batches in flight, each on a decode pipeline lane of its own
+            (1-8; the native ring has 10 staging slots).
 
     Iterating yields ``(names, tensor)`` where ``tensor`` is a device tensor
     ``[B, h, w, 3]`` / ``[B, 3, h, w]`` complete on the stream it was made on
@@ -96,7 +97,7 @@ class TarImageStream:
 
     def __init__(self, src, *, batch_size: int, device_config: CUDAConfig,
                  output: Output | None = None,
-                 select: Callable[[str], bool] | None = None, depth: int = 2):
+                 select: Callable[[str], bool] | None = None, depth: int = 4):
         if device_config is None:
             raise ValueError("device_config must be provided.")
         if batch_size <= 0:
@@ -105,7 +106,7 @@ class TarImageStream:
         self.batch_size = int(batch_size)
         self.output = output or Output(pix_fmt="rgb24", resize=True, fit_w=224, fit_h=224,
                                        aspect="decrease", pad_w=224, pad_h=224)
-        self.depth = max(1, min(int(depth), 2))
+        self.depth = max(1, min(int(depth), 8))
         sel = select or (lambda n: n.lower().endswith(_IMAGE_EXT))
         self._fd = -1
         self._mm = None
@@ -121,9 +122,10 @@ class TarImageStream:
         members, _ = _lib.tar_index(view)
         self.members = [m for m in members if sel(m[0])]
         self._dec = _lib.Decoder(device_config.device_index)
-        # two pipelines: batch k+1's kernels share the CUs with batch k's
-        # latency-bound entropy decode (completion is tracked per ticket)
-        self._dec.set_param("lanes", 2 if self.depth >= 2 else 1)
+        # one pipeline lane per batch in flight: later batches' kernels share
+        # the CUs with earlier batches' latency-bound entropy decode
+        # (completion is tracked per ticket)
+        self._dec.set_param("lanes", self.depth)
         h, w = self._out_hw(view)
         self._shape = (3, h, w) if self.output.planar else (h, w, 3)
         self._dtype = self.output.torch_dtype
