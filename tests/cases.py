@@ -87,6 +87,18 @@ def case(name: str) -> bytes:
                     restart_marker_blocks=5)
     if name == "prog_noise_q100":
         return _enc(_noise(25, 96, 128), quality=100, subsampling=0, progressive=True)
+    # large progressive images: scans past the decoder's 16 KiB LDS byte window
+    # (restaged mid-scan), many refinement chunks, restarts across restages
+    if name == "prog_large_420":
+        return _enc(synthetic_pixels(26, 480, 640), quality=90, subsampling=2, progressive=True)
+    if name == "prog_large_noise":
+        return _enc(_noise(27, 320, 480), quality=95, subsampling=2, progressive=True)
+    if name == "prog_large_restart":
+        return _enc(synthetic_pixels(28, 480, 640), quality=92, progressive=True,
+                    restart_marker_blocks=3)
+    if name == "prog_1080p":
+        return _enc(synthetic_pixels(29, 1080, 1920), quality=90, subsampling=2,
+                    progressive=True)
     # sequential, one non-interleaved scan per component (reverse order);
     # Pillow cannot write these: libjpeg 9 wrote the committed files
     # (tests/gen_golden.py, oracle.lj_encode_multiscan)
@@ -103,6 +115,7 @@ MULTISCAN = {
     "multiscan_444_odd": (31, 101, 67, 85, 1, 1, 0),
     "multiscan_422_rst": (32, 120, 200, 90, 2, 1, 7),
 }
+LARGE_PROGRESSIVE = ["prog_large_420", "prog_large_noise", "prog_large_restart", "prog_1080p"]
 PROGRESSIVE = ["prog_420", "prog_444_odd", "prog_422", "prog_gray", "prog_optimized",
                "prog_restart", "prog_noise_q100"]
 

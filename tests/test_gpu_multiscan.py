@@ -80,6 +80,28 @@ def test_native_planes(oracle, name):
     np.testing.assert_array_equal(hyp.reshape(-1), ref, strict=True)
 
 
+@pytest.mark.parametrize("name", cases.LARGE_PROGRESSIVE)
+def test_large_progressive_planes(oracle, name):
+    """Scans larger than the decoder's LDS byte window (restaged mid-scan,
+    also across restart markers), many AC-refinement chunks: planes
+    bit-exact vs the oracle (whose progressive decode is pinned to libjpeg 9
+    coefficients in test_oracle.py)."""
+    d = cases.case(name)
+    hyp = sio.to_numpy(sio.load_image(d, filter_desc=None))
+    ref = np.concatenate([p.reshape(-1) for p in oracle.decode_planes(d)])
+    np.testing.assert_array_equal(hyp.reshape(-1), ref, strict=True)
+
+
+def test_large_progressive_batch_pad224(oracle):
+    """Large progressive images mixed with baseline ones through the resize chain."""
+    datas = [cases.case(n) for n in ("prog_large_420", "q90_420", "prog_large_restart",
+                                     "prog_large_noise")]
+    hyp = sio.to_numpy(sio.load_image_batch(datas, width=224, height=224))
+    rs = oracle.Resize(**PAD224)
+    for i, d in enumerate(datas):
+        np.testing.assert_array_equal(hyp[i], oracle.decode_resize(d, rs, "rgb24"), strict=True)
+
+
 @pytest.mark.parametrize("bad", ["arithmetic", "cmyk"])
 def test_unsupported_fails_per_image(bad):
     """An unsupported image fails alone: strict=False keeps the others."""
