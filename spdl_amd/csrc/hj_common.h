@@ -59,7 +59,10 @@ constexpr uint32_t kKindCode = 1;  // code resolved, value bits follow
 constexpr uint32_t kKindFull = 2;  // code + value resolved
 constexpr uint32_t kKindSub = 3;   // code longer than kLutBits: look up sub[idx][next 6 bits]
 constexpr int kSubBits = 16 - kLutBits;
-constexpr int kSubPool = 2048;  // entropy LDS entries for the second-level tables of a scan
+#ifndef HJ_SUB_POOL
+#define HJ_SUB_POOL 2048
+#endif
+constexpr int kSubPool = HJ_SUB_POOL;  // entropy LDS entries for the second-level tables of a scan
 constexpr int kMaxSub = 16;        // 64-entry sub-tables per Huffman table
 constexpr int kEntHiShift = 21;    // value / sub-table index field
 

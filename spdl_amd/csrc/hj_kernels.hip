@@ -1618,7 +1618,12 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
 // decode loops; a wide one (parse_kernel's ent_wide) the loops that may read
 // HBM table copies and the canonical fallback.  One launch serves both.
 template <int NT, int NTAB>
-__global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
+#ifdef HJ_ENT_VGPRS  // (occupancy experiments: cap the entropy kernel's VGPRs)
+#define HJ_ENT_ATTR __attribute__((amdgpu_waves_per_eu(HJ_ENT_VGPRS, 8)))
+#else
+#define HJ_ENT_ATTR
+#endif
+__global__ void __launch_bounds__(NT) HJ_ENT_ATTR entropy_kernel(const uint8_t* __restrict__ clean,
                                                      const uint32_t* __restrict__ segs,
                                                      const ImageDesc* __restrict__ desc,
                                                      ImageInfo* __restrict__ infos,
