@@ -117,6 +117,9 @@ def _args():
                    help="extra decoder parameter (spdl_hj_set_param), for A/B runs")
     p.add_argument("--debug-mask", type=int, default=0,
                    help="kernel phase ablations for timing (outputs are wrong; no oracle check)")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="run every rank on device 0 (a one-GPU rehearsal of the N-rank launch; "
+                        "the record says so -- not a multi-GPU measurement)")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU-only rehearsal of the multi-rank launch and timing reduction")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -294,14 +297,14 @@ def main():
     if a.dry_run:
         _dry_run(a, rank, world)
         return
-    device = torch.device("cuda", local)
+    device = torch.device("cuda", 0 if a.rehearse_one_gpu else local)
     torch.cuda.set_device(device)
 
     # this rank's contiguous slice of the global batch (configs[2]: 2048 -> 8 x 256)
     sl = contiguous_shard(world * a.batch, rank, world)
     datas = synthetic_slice(sl, distinct=a.distinct)
     dev, offs, sizes, infos = _pack_device(datas, device)
-    dec = _lib.Decoder(local)
+    dec = _lib.Decoder(device.index)
     if a.sub_bits:
         dec.set_param("sub_bits", a.sub_bits)
     if a.entropy_threads:
@@ -432,6 +435,8 @@ def main():
                 "parallelism": f"{world} ranks (one process per GPU), contiguous slices of the "
                                f"global batch, no collective on the data path",
                 "lanes": a.lanes,
+                **({"rehearsal": f"{world} ranks sharing ONE GPU (launch-path check, not a "
+                                 f"multi-GPU rate)"} if a.rehearse_one_gpu else {}),
             },
             "roofline": {
                 "bound": "hbm",

@@ -60,6 +60,8 @@ def _args():
     p.add_argument("--distinct", type=int, default=32)
     p.add_argument("--d2h", action="store_true")
     p.add_argument("--source", choices=["file", "bytes"], default="file")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="run every rank on device 0 (launch-path rehearsal, not a multi-GPU rate)")
     p.add_argument("--depth", type=int, default=4,
                    help="batches in flight (= decode pipeline lanes), 1-8")
     p.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
@@ -86,6 +88,8 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     init_host_group()  # gloo: barrier + MAX of elapsed seconds only
+    if a.rehearse_one_gpu:
+        local = 0
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -165,6 +169,8 @@ def main():
                     "jpeg_payload_bytes_per_rank": payload,
                     "d2h": bool(a.d2h),
                     "depth": a.depth,
+                    **({"rehearsal": f"{world} ranks sharing ONE GPU"} if a.rehearse_one_gpu
+                       else {}),
                     "parallelism": f"{world} independent per-GPU archives, no collective",
                 },
                 "h2d_GBps_per_gpu": round(tar_bytes * a.passes / elapsed / 1e9, 3),
