@@ -971,7 +971,7 @@ __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32
 // bd.y >> 16 holds the block's raw DC difference until the DC pass replaces
 // it by the final dequantised DC.  Each block is written by the one run its DC
 // symbol lies in, entries appended from that run's region start (first block
-// * 64; a block has at most 63 AC entries, its list starts 16-byte aligned),
+// * 64; a block has at most 63 AC entries; the run's lists follow each other back to back),
 // so no buffer needs clearing and nothing is scattered: HBM sees ~4 bytes per
 // non-zero coefficient.
 #ifndef HJ_ENT_PACK
@@ -1046,7 +1046,18 @@ __device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e) {
 }
 
 template <int NT>
+#ifndef HJ_PACKED_LISTS
+#define HJ_PACKED_LISTS 1  // a run's lists back to back (0: each list 16-byte aligned)
+#endif
+
 __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
+#if HJ_PACKED_LISTS && !HJ_STAGE
+  // the next list continues the current pack: no store at the block end
+  // (the run's last, partial pack leaves in flush_tail)
+  o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
+  o.open = false;
+  return;
+#endif
   const uint32_t nc = (o.cur + 3u) & ~3u;  // the next list starts 16-byte aligned
 #if HJ_STAGE
   constexpr int KS = stage_entries(NT);
@@ -1073,6 +1084,8 @@ __device__ __forceinline__ void flush_tail(BlockOut& o) {
 #if HJ_STAGE
   constexpr int KS = stage_entries(NT);
   if (o.cur & (uint32_t)(KS - 1)) flush_line<NT, KS>(o, o.cur);
+#elif HJ_PACKED_LISTS
+  if (o.cur & (kEntPack - 1u)) store_pack(o);
 #endif
 }
 
@@ -2545,10 +2558,14 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
   }
   // The entropy kernel's list for this block (see BlockOut): DC final, AC
   // dequantised with their natural index; placed in the thread's LDS block.
+  // (a list may start inside a 16-byte group: the run's lists are packed
+  // back to back; entries [lo, lo + count) of the groups from `start`)
   const uint2 bd = bdesc[(size_t)dd.coef_off + j];
   const uint32_t cap = (uint32_t)in.nblocks * 64u;
-  uint32_t start = bd.x & ~3u, count = min(bd.y & 0xFFFFu, 63u);
+  const uint32_t lo = bd.x & 3u, start = bd.x & ~3u;
+  uint32_t count = min(bd.y & 0xFFFFu, 63u);
   if (start > cap - 64u) count = 0;  // only an unwritten list (a failed scan)
+  const uint32_t hi_e = lo + count;
   const uint4* e4 = reinterpret_cast<const uint4*>(ents + (size_t)dd.coef_off * 64 + start);
   uint32_t* my_blk = sblk[threadIdx.x];
   uint4* my4 = reinterpret_cast<uint4*>(my_blk);
@@ -2556,7 +2573,7 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
   for (int i = 0; i < 8; i++) my4[i] = make_uint4(0u, 0u, 0u, 0u);
   int16_t* my16 = reinterpret_cast<int16_t*>(my_blk);
   my16[0] = (int16_t)(bd.y >> 16);
-  const uint32_t n4 = (count + 3u) >> 2;
+  const uint32_t n4 = (hi_e + 3u) >> 2;
   for (uint32_t i = 0; i < n4; i += 4) {
     // unconditional loads (index clamped into the list), then the scatter
     uint4 q[4];
@@ -2566,8 +2583,10 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
     for (int u = 0; u < 4; u++) {
       const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
 #pragma unroll
-      for (int h = 0; h < 4; h++)  // (past the list: into the slot's padding)
-        my16[4u * (i + u) + h < count ? (w[h] & 63u) : 64u] = (int16_t)(w[h] >> 16);
+      for (int h = 0; h < 4; h++) {  // (outside the list: into the slot's padding)
+        const uint32_t k = 4u * (i + u) + h;
+        my16[k >= lo && k < hi_e ? (w[h] & 63u) : 64u] = (int16_t)(w[h] >> 16);
+      }
     }
   }
   int32_t blk[64];
