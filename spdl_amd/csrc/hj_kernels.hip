@@ -1674,15 +1674,17 @@ __global__ void __launch_bounds__(NT) HJ_ENT_ATTR entropy_kernel(const uint8_t* 
 constexpr int kMsMaxScans = 64;
 constexpr int kMsMaxMarks = 512;
 constexpr int kMsLook = 9;
-// The scan decoder (thread 0) reads only LDS: the scan's raw bytes are staged
-// in a window of kMsWinBytes, restaged by the workgroup whenever the reader
-// gets within kMsMargin bytes of its end at an MCU start (an MCU of <= 10
-// blocks takes < 4.3 KB even with every byte stuffed).  AC refinement scans
-// run in chunks of kMsChunk blocks: the workgroup stages each block's history
-// mask beforehand and applies the decoder's records afterwards.
-constexpr int kMsWinBytes = 16384;
-constexpr int kMsMargin = 4608;
-constexpr int kMsChunk = 192;
+// kMsDec decoder waves decode independent scans at once (scans conflict
+// when they share a component and overlapping coefficient bands).  A scan
+// decoder reads only LDS: the scan's raw bytes are staged in its wave's
+// window of kMsWinBytes, restaged by the wave's lanes whenever the reader
+// gets within the scan's margin of its end at an MCU start (an MCU of b
+// blocks takes < 432 b bytes even with every byte stuffed).  AC refinement
+// scans run in chunks of kMsChunk blocks: the wave stages each block's
+// history mask beforehand and applies the decoder's records afterwards.
+constexpr int kMsDec = 2;
+constexpr int kMsWinBytes = 8192;
+constexpr int kMsChunk = 128;
 
 struct MsTable {
   uint16_t look[1 << kMsLook];  // (len << 8) | sym for codes <= kMsLook bits, else 0
@@ -1699,18 +1701,25 @@ struct MsScan {
   int32_t dht[8];      // file offset of the DHT entry in effect per slot (-1: none)
 };
 
-struct MsShared {
-  MsTable tab[8];  // DC 0..3, AC 0..3 (slot 4 + id)
-  MsScan scan[kMsMaxScans];
-  int32_t marks[kMsMaxMarks];
-  uint32_t win[kMsWinBytes / 4 + 2];  // raw bytes [wbase, wbase + kMsWinBytes) (+2 words of slack)
+// One decoder wave's LDS.
+struct MsWave {
+  MsTable tab[8];  // DC 0..3, AC 0..3 (slot 4 + id), as the wave's scan defines them
+  uint32_t win[kMsWinBytes / 4 + 2];  // raw bytes [wb, wb + kMsWinBytes) (+2 words of slack)
   // AC refinement chunk, per block: coefficients [ss, se] non-zero before the
   // scan (bit k), correction bits in coefficient order (LSB first), the
   // coefficients the scan makes non-zero and their signs (1: negative)
   uint64_t hist[kMsChunk], corr[kMsChunk], nmask[kMsChunk], nsign[kMsChunk];
+};
+
+struct MsShared {
+  MsWave wv[kMsDec];
+  MsScan scan[kMsMaxScans];
+  uint64_t deps[kMsMaxScans];  // earlier scans a scan must wait for
+  uint64_t claimed, done;      // scans taken by a decoder wave / finished
+  int64_t tkind[4];            // diagnostics: decode ticks by scan kind
+  int32_t marks[kMsMaxMarks];
   int32_t dht[8], comp_id[kMaxComp];  // segment walk state (thread 0)
   int32_t nmarks, nscans, err;
-  int32_t wbase, mcu, fin;  // chunk loop: window base, next MCU, scan finished
 };
 
 // The scan decoder runs on all of wave 0 with identical values in every lane
@@ -1724,6 +1733,13 @@ __device__ __forceinline__ uint64_t ms_u64(uint64_t v) {
   return (uint64_t)ms_u((uint32_t)(v >> 32)) << 32 | ms_u((uint32_t)v);
 }
 __device__ __forceinline__ bool ms_lane0() { return __lane_id() == 0; }
+// order a wave's own LDS writes before its later reads (the compiler must
+// not move memory operations across; the hardware keeps a wave's LDS
+// operations in order)
+__device__ __forceinline__ void ms_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // The staged window of the file's raw bytes (little-endian words).
 struct MsWin {
@@ -1911,7 +1927,7 @@ __device__ __forceinline__ void ms_take_corr(MsBits& br, uint64_t m, uint64_t& c
 // which history coefficients get a correction bit (libjpeg jdphuff
 // decode_mcu_AC_refine reads one per non-zero coefficient it passes, in
 // order) and which zero coefficients become +-(1 << al).
-__device__ __forceinline__ int ms_block_decode(MsShared& S, MsBits& br, const MsBand& sc, bool prog,
+__device__ __forceinline__ int ms_block_decode(MsWave& S, MsBits& br, const MsBand& sc, bool prog,
                                                const MsTable& dh, const MsTable& ah, int32_t& pred,
                                                int32_t* __restrict__ lev, int& eobrun, int j) {
   if (!prog) {  // sequential scan: the whole block
@@ -2047,7 +2063,7 @@ __device__ __forceinline__ int ms_div(int x, int d) {
   return d == 1 ? x : (d == 2 ? x >> 1 : (d == 4 ? x >> 2 : (int)(((uint32_t)x * 0xAAABu) >> 17)));
 }
 
-__device__ __forceinline__ int ms_scan_chunk(MsShared& S, const uint8_t* d, int size,
+__device__ __forceinline__ int ms_scan_chunk(MsWave& S, const uint8_t* d, int size,
                                              const MsGeo& in, const MsScan& scl, bool prog,
                                              int32_t* __restrict__ lv, MsState& st, int wlim,
                                              int chunk0, int chunk_end) {
@@ -2172,9 +2188,6 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   int32_t* lv = reinterpret_cast<int32_t*>(ents + (size_t)dd.coef_off * 64);
   const int nblocks = in.nblocks;
   int64_t t0 = wall_clock64(), tph[4] = {0, 0, 0, 0}, tdbg[4] = {0, 0, 0, 0};
-  MsState st;  // the scan decoder (wave 0, uniform)
-  // (a uniform condition: readfirstlane of the wave's first thread index)
-  const bool wave0 = __builtin_amdgcn_readfirstlane(tid) < 64;
   const MsGeo geo = ms_geo(in);
   if (tid == 0) {
     S.nmarks = 0;
@@ -2312,167 +2325,225 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   }
   __syncthreads();
   tph[0] = wall_clock64() - t0;  // marker candidates + segment walk
-  // ---- the scans, in order ----
-  const bool progressive = prog;
-  for (int si = 0; si < S.nscans && S.err == kOk; si++) {
-    const MsScan& sc = S.scan[si];
-    // tables this scan reads: DC for DC-first / sequential, AC for AC scans
-    const bool need_dc = !progressive || (sc.ss == 0 && sc.ah == 0);
-    const bool need_ac = !progressive || sc.ss > 0;
-    for (int t = 0; t < 8; t++) {
-      bool used = false;
-      for (int i = 0; i < sc.ns; i++)
-        used |= (t < 4 && need_dc && sc.td[i] == t) || (t >= 4 && need_ac && sc.ta[i] == t - 4);
-      if (!used) continue;  // (uniform: every thread reads the same scan record)
-      const int o = sc.dht[t];
-      if (o < 0) {
-        if (tid == 0) S.err = kErrBadHeader;
-        continue;
+  // ---- scan dependencies: a scan waits for every earlier scan that shares
+  // a component and overlaps its coefficient band ----
+  for (int i = tid; i < S.nscans; i += nt) {
+    const MsScan& x = S.scan[i];
+    int cx = 0;
+    for (int k = 0; k < x.ns; k++) cx |= 1 << x.comp[k];
+    const int lx = prog ? x.ss : 0, hx = prog ? x.se : 63;
+    uint64_t m = 0;
+    for (int j = 0; j < i; j++) {
+      const MsScan& y = S.scan[j];
+      int cy = 0;
+      for (int k = 0; k < y.ns; k++) cy |= 1 << y.comp[k];
+      const int ly = prog ? y.ss : 0, hy = prog ? y.se : 63;
+      if ((cx & cy) && !(hy < lx || hx < ly)) m |= 1ull << j;
+    }
+    S.deps[i] = m;
+  }
+  if (tid == 0) {
+    S.claimed = 0;
+    S.done = 0;
+    for (int k = 0; k < 4; k++) S.tkind[k] = 0;
+  }
+  __syncthreads();
+  const int64_t tdec = wall_clock64();
+  // ---- decoder waves: each takes the first ready scan, decodes it with its
+  // own LDS (tables, byte window, refinement records) and marks it done ----
+  const int wid = __builtin_amdgcn_readfirstlane(tid) >> 6;  // (uniform)
+  const int lane = tid & 63;
+  if (wid < kMsDec) {
+    MsWave& W = S.wv[wid];
+    const bool progu = ms_i(prog) != 0;
+    const int sizeu = ms_i(size);
+    for (;;) {
+      // claim (lane 0 does the LDS atomic; its result is broadcast)
+      int si = -1;
+      for (;;) {
+        const int nsc = ms_i(S.nscans);
+        const uint64_t full = nsc >= 64 ? ~0ull : ((1ull << nsc) - 1ull);
+        const uint64_t done = ms_u64(__hip_atomic_load(&S.done, __ATOMIC_ACQUIRE,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP));
+        const uint64_t claimed = ms_u64(__hip_atomic_load(&S.claimed, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (ms_i(__hip_atomic_load(&S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) !=
+                kOk ||
+            (claimed & full) == full)
+          break;
+        int cand = -1;
+        for (int i = 0; i < nsc && cand < 0; i++)
+          if (!((claimed >> i) & 1ull) && (ms_u64(S.deps[i]) & ~done) == 0ull) cand = i;
+        if (cand < 0) {
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        uint64_t old = 0;
+        if (ms_lane0()) old = atomicOr(reinterpret_cast<unsigned long long*>(&S.claimed),
+                                       1ull << cand);
+        if (!((ms_u64(old) >> cand) & 1ull)) {
+          si = cand;
+          break;
+        }
       }
-      MsTable& T = S.tab[t];
-      if (tid < 17) T.bits[tid] = tid == 0 ? 0 : d[o + tid];
-      __syncthreads();
-      if (tid == 0) {
-        int code = 0, k = 0;
+      if (si < 0) break;
+      __threadfence_block();  // (acquire: the scans it waited for are visible)
+      const int64_t ts = wall_clock64();
+      const MsScan& sc = S.scan[si];
+      const int sns = ms_i(sc.ns), sss = ms_i(sc.ss), sah = ms_i(sc.ah);
+      int rc = kOk;
+      // tables this scan reads: DC for DC-first / sequential, AC for AC scans
+      const bool need_dc = !progu || (sss == 0 && sah == 0);
+      const bool need_ac = !progu || sss > 0;
+      for (int t = 0; t < 8 && rc == kOk; t++) {
+        bool used = false;
+        for (int i = 0; i < sns; i++)
+          used |= (t < 4 && need_dc && ms_i(sc.td[i]) == t) ||
+                  (t >= 4 && need_ac && ms_i(sc.ta[i]) == t - 4);
+        if (!used) continue;
+        const int o = ms_i(sc.dht[t]);
+        if (o < 0) {
+          rc = kErrBadHeader;
+          break;
+        }
+        MsTable& T = W.tab[t];
+        if (lane < 17) T.bits[lane] = lane == 0 ? 0 : d[o + lane];
+        ms_wave_sync();
+        // canonical arrays: every lane computes them, lane 0 stores
+        int code = 0, k = 0, total = 0;
         for (int l = 1; l <= 16; l++) {
-          if (T.bits[l]) {
-            T.valoff[l] = k - code;
-            code += T.bits[l];
-            k += T.bits[l];
-            T.maxcode[l] = code - 1;
-          } else {
-            T.maxcode[l] = -1;
-            T.valoff[l] = 0;
+          const int nb = ms_i(T.bits[l]);
+          if (ms_lane0()) {
+            T.valoff[l] = nb ? k - code : 0;
+            T.maxcode[l] = nb ? code + nb - 1 : -1;
           }
-          if (code > (1 << l)) S.err = kErrBadHeader;
+          code += nb;
+          k += nb;
+          total += nb;
+          if (code > (1 << l)) rc = kErrBadHeader;
           code <<= 1;
         }
-        T.maxcode[17] = 0x7FFFFFFF;
-      }
-      int total = 0;
-      for (int l = 1; l <= 16; l++) total += T.bits[l];
-      for (int i = tid; i < 256; i += nt) T.vals[i] = i < total ? d[o + 17 + i] : 0;
-      __syncthreads();
-      for (int idx = tid; idx < (1 << kMsLook); idx += nt) {
-        uint16_t e = 0;
-        for (int l = 1; l <= kMsLook; l++) {
-          const int code = idx >> (kMsLook - l);
-          if (code <= T.maxcode[l]) {
-            e = (uint16_t)((l << 8) | T.vals[T.valoff[l] + code]);
-            break;
+        if (ms_lane0()) T.maxcode[17] = 0x7FFFFFFF;
+        for (int i = lane; i < 256; i += 64) T.vals[i] = i < total ? d[o + 17 + i] : 0;
+        ms_wave_sync();
+        for (int idx = lane; idx < (1 << kMsLook); idx += 64) {
+          uint16_t e = 0;
+          for (int l = 1; l <= kMsLook; l++) {
+            const int cd = idx >> (kMsLook - l);
+            if (cd <= T.maxcode[l]) {
+              e = (uint16_t)((l << 8) | T.vals[T.valoff[l] + cd]);
+              break;
+            }
           }
+          T.look[idx] = e;
         }
-        T.look[idx] = e;
+        ms_wave_sync();
       }
-      __syncthreads();
-    }
-    const int64_t ts = wall_clock64();
-    const bool refine = progressive && sc.ss > 0 && sc.ah > 0;
-    int bw1 = 1, nmcu = in.mcux * in.mcuy;
-    if (sc.ns == 1) {
-      const int c = sc.comp[0];
-      bw1 = in.ncomp == 1 ? in.mcux : (in.comp_w[c] + 7) / 8;
-      nmcu = bw1 * (in.ncomp == 1 ? in.mcuy : (in.comp_hpx[c] + 7) / 8);
-    }
-    if (wave0) {
-      st.br.start(ms_i(sc.start), ms_i(sc.end));
+      const bool refine = progu && sss > 0 && sah > 0;
+      int bw1 = 1, nmcu = ms_i(in.mcux) * ms_i(in.mcuy), bpmcu = 0;
+      if (sns == 1) {
+        const int c = ms_i(sc.comp[0]);
+        bw1 = geo.ncomp == 1 ? geo.mcux : (ms_i(in.comp_w[c]) + 7) / 8;
+        nmcu = bw1 * (geo.ncomp == 1 ? ms_i(in.mcuy) : (ms_i(in.comp_hpx[c]) + 7) / 8);
+        bpmcu = 1;
+      } else {
+        for (int i = 0; i < sns; i++) bpmcu += geo.h(ms_i(sc.comp[i])) * geo.v(ms_i(sc.comp[i]));
+      }
+      // bytes one MCU can take (every byte stuffed) + the reader's look-ahead
+      const int margin = 96 + 432 * bpmcu;
+      const int sstart = ms_i(sc.start), send = ms_i(sc.end);
+      MsState st;
+      st.br.start(sstart, send);
       st.br.overrun = false;
       st.pred0 = st.pred1 = st.pred2 = 0;
       st.eobrun = 0;
       st.mcu = 0;
-      st.nmcu = ms_i(nmcu);
-      st.bw1 = ms_i(bw1);
+      st.nmcu = nmcu;
+      st.bw1 = bw1;
       st.rst_done = false;
-    }
-    if (tid == 0) {
-      S.wbase = sc.start & ~3;
-      S.mcu = 0;
-      S.fin = S.err != kOk;
-    }
-    __syncthreads();
-    // chunks: (re)stage the window, stage history masks (AC refinement),
-    // thread 0 decodes, the workgroup applies the refinement records
-    int staged = -1;
-    while (!S.fin) {
-      const int wb = S.wbase, m0 = S.mcu;
-      if (wb != staged) {
-        for (int i = tid; i < kMsWinBytes / 4 + 2; i += nt) {
-          const int o = wb + 4 * i;
-          uint32_t v = 0;
-          if (o + 4 <= size) {
-            v = *reinterpret_cast<const uint32_t*>(d + o);
-          } else {
-            for (int b = 0; b < 4 && o + b < size; b++) v |= (uint32_t)d[o + b] << (8 * b);
+      // chunks: (re)stage the window, stage history masks (AC refinement),
+      // decode (uniform), apply the refinement records (the wave's lanes)
+      int wb = sstart & ~3, m0 = 0, staged = -1;
+      bool fin = rc != kOk;
+      while (!fin) {
+        if (wb != staged) {
+          for (int i = lane; i < kMsWinBytes / 4 + 2; i += 64) {
+            const int o = wb + 4 * i;
+            uint32_t v = 0;
+            if (o + 4 <= sizeu) {
+              v = *reinterpret_cast<const uint32_t*>(d + o);
+            } else {
+              for (int bb = 0; bb < 4 && o + bb < sizeu; bb++) v |= (uint32_t)d[o + bb] << (8 * bb);
+            }
+            W.win[i] = v;
           }
-          S.win[i] = v;
+          staged = wb;
         }
-        staged = wb;
-      }
-      if (refine) {
-        const uint64_t band = ms_range(sc.ss, sc.se);
-        for (int j = tid; j < kMsChunk && m0 + j < nmcu; j += nt) {
-          const uint4* src =
-              reinterpret_cast<const uint4*>(lv + (size_t)ms_scan_block(in, sc, bw1, m0 + j) * 64);
-          uint64_t h = 0;
+        if (refine) {
+          const uint64_t band = ms_range(sss, ms_i(sc.se));
+          for (int j = lane; j < kMsChunk && m0 + j < nmcu; j += 64) {
+            const uint4* src =
+                reinterpret_cast<const uint4*>(lv + (size_t)ms_scan_block(in, sc, bw1, m0 + j) * 64);
+            uint64_t h = 0;
 #pragma unroll
-          for (int q = 0; q < 16; q++) {
-            const uint4 x = src[q];
-            h |= (uint64_t)((x.x != 0u) | (x.y != 0u) << 1 | (x.z != 0u) << 2 | (x.w != 0u) << 3)
-                 << (4 * q);
+            for (int q = 0; q < 16; q++) {
+              const uint4 x = src[q];
+              h |= (uint64_t)((x.x != 0u) | (x.y != 0u) << 1 | (x.z != 0u) << 2 | (x.w != 0u) << 3)
+                   << (4 * q);
+            }
+            W.hist[j] = h & band;
           }
-          S.hist[j] = h & band;
         }
-      }
-      __syncthreads();
-      if (wave0) {
-        const int wbu = ms_i(wb), m0u = ms_i(m0), send = ms_i(sc.end);
-        st.br.src.w = S.win;
-        st.br.src.base = wbu;
-        const int sizeu = ms_i(size);
-        st.br.src.lim = min(wbu + kMsWinBytes, sizeu);
+        ms_wave_sync();
+        st.br.src.w = W.win;
+        st.br.src.base = wb;
+        st.br.src.lim = min(wb + kMsWinBytes, sizeu);
         // the window holds the rest of the scan, or the reader stops at an
-        // MCU start within kMsMargin of its end
-        const int wlim =
-            send <= wbu + kMsWinBytes ? 0x7FFFFFFF : wbu + kMsWinBytes - kMsMargin;
-        const int rc = ms_scan_chunk(S, d, sizeu, geo, sc, ms_i(progressive) != 0, lv, st, wlim, m0u,
-                                     m0u + kMsChunk);
-        if (ms_lane0()) {
-          S.err = rc;
-          S.mcu = st.mcu;
-          if (st.br.pos > wlim) S.wbase = st.br.pos & ~3;
-          S.fin = rc != kOk || st.mcu >= nmcu;
-        }
-      }
-      __syncthreads();
-      if (refine && S.err == kOk) {
-        const int32_t p1 = 1 << sc.al, m1 = -p1;
-        for (int j = tid; j < S.mcu - m0; j += nt) {
-          int32_t* lev = lv + (size_t)ms_scan_block(in, sc, bw1, m0 + j) * 64;
-          uint64_t h = S.hist[j], corr = S.corr[j], m = S.nmask[j];
-          const uint64_t sg = S.nsign[j];
-          for (; h; h &= h - 1, corr >>= 1) {
-            if (corr & 1u) {
-              const int k = __builtin_ctzll(h);
-              const int32_t c = lev[k];
-              if ((c & p1) == 0) lev[k] = c + (c >= 0 ? p1 : m1);
+        // MCU start within the margin of its end
+        const int wlim = send <= wb + kMsWinBytes ? 0x7FFFFFFF : wb + kMsWinBytes - margin;
+        rc = ms_scan_chunk(W, d, sizeu, geo, sc, progu, lv, st, wlim, m0, m0 + kMsChunk);
+        const int m1 = st.mcu;
+        ms_wave_sync();
+        if (refine && rc == kOk) {
+          const int32_t p1 = 1 << ms_i(sc.al), m1v = -p1;
+          for (int j = lane; j < m1 - m0; j += 64) {
+            int32_t* lev = lv + (size_t)ms_scan_block(in, sc, bw1, m0 + j) * 64;
+            uint64_t h = W.hist[j], corr = W.corr[j], m = W.nmask[j];
+            const uint64_t sg = W.nsign[j];
+            for (; h; h &= h - 1, corr >>= 1) {
+              if (corr & 1u) {
+                const int kk = __builtin_ctzll(h);
+                const int32_t c = lev[kk];
+                if ((c & p1) == 0) lev[kk] = c + (c >= 0 ? p1 : m1v);
+              }
+            }
+            for (; m; m &= m - 1) {
+              const int kk = __builtin_ctzll(m);
+              lev[kk] = ((sg >> kk) & 1u) ? m1v : p1;
             }
           }
-          for (; m; m &= m - 1) {
-            const int k = __builtin_ctzll(m);
-            lev[k] = ((sg >> k) & 1u) ? m1 : p1;
-          }
         }
+        ms_wave_sync();
+        if (st.br.pos > wlim) wb = st.br.pos & ~3;
+        m0 = m1;
+        fin = rc != kOk || m1 >= nmcu;
       }
-      __syncthreads();
+      // the scan's stores are visible before it counts as done
+      __threadfence_block();
+      if (ms_lane0()) {
+        if (rc != kOk) atomicCAS(&S.err, kOk, rc);
+        const int kind = !progu ? 3 : (sss == 0 ? 0 : (sah == 0 ? 1 : 2));
+        atomicAdd(reinterpret_cast<unsigned long long*>(&S.tkind[kind]),
+                  (unsigned long long)(wall_clock64() - ts));
+        __hip_atomic_fetch_or(&S.done, 1ull << si, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
-    const int64_t dt = wall_clock64() - ts;
-    tph[2] += dt;  // decode
-    // diagnostics by scan kind: DC, AC first, AC refinement, sequential
-    const int kind = !progressive ? 3 : (sc.ss == 0 ? 0 : (sc.ah == 0 ? 1 : 2));
-#pragma unroll
-    for (int i = 0; i < 4; i++) tdbg[i] += i == kind ? dt : 0;  // (static indices: no scratch)
   }
-  tph[1] = wall_clock64() - t0 - tph[0] - tph[2];  // table builds
+  __syncthreads();
+  tph[2] = wall_clock64() - tdec;  // decode (tables included)
+#pragma unroll
+  for (int i = 0; i < 4; i++) tdbg[i] = S.tkind[i];
+  tph[1] = 0;
   if (S.err != kOk) {
     if (tid == 0) in.status = S.err;
     return;
