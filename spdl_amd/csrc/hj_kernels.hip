@@ -1757,6 +1757,9 @@ struct MsWin {
   }
 };
 
+#ifndef HJ_MS_FILL
+#define HJ_MS_FILL 32  // bits the scan reader's buffer is topped up to
+#endif
 // Bit reader over stuffed entropy data: 0xFF00 -> 0xFF; any other marker (or
 // the scan end) stops the data, zeros follow (oracle bitrd_t).  Four plain
 // bytes (no 0xFF among them) enter the buffer at once.
@@ -1775,8 +1778,11 @@ struct MsBits {
     marker = false;
     real = used = 0;
   }
+  // (tops the buffer up to >= 32 bits: every caller needs at most 32, and
+  // one 4-byte step then suffices -- the byte path costs an LDS round trip
+  // per byte)
   __device__ __forceinline__ void fill() {
-    while (cnt <= 56) {
+    while (cnt < HJ_MS_FILL) {
       if (!marker && cnt <= 32 && pos + 4 <= end && pos + 4 <= src.lim) {
         const uint32_t v = src.be32(pos);
         if (((~v - 0x01010101u) & v & 0x80808080u) == 0u) {  // no 0xFF byte

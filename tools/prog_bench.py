@@ -15,8 +15,11 @@ spec = Output(pix_fmt="rgb24", resize=True, fit_w=224, fit_h=224, aspect="decrea
               pad_h=224)
 dec = _lib.Decoder(0)
 out = torch.empty((n, 224, 224, 3), dtype=torch.uint8, device="cuda:0")
-for prog in (False, True):
-    datas = [synthetic_jpeg(2000 + i % 32, progressive=prog) for i in range(n)]
+for prog in (False, True, "one"):
+    # "one": a baseline batch holding a single progressive image (the batch
+    # completes with its slowest image)
+    datas = [synthetic_jpeg(2000 + i % 32, progressive=(prog is True or (prog == "one" and i == 0)))
+             for i in range(n)]
     for _ in range(2):
         dec.decode_batch(datas, spec, out.data_ptr(), out.numel())
     torch.cuda.synchronize()
