@@ -191,3 +191,20 @@ def corrupt_scan(seed: int = 0) -> bytes:
     for p in pos:
         d[p] = int(rng.integers(0, 255))
     return bytes(d)
+
+
+def corrupt_progressive(seed: int = 0) -> bytes:
+    """A progressive image with 1-4 random bytes overwritten past its first scan
+    header (scan data, later DHT/SOS segments; no new 0xFF bytes)."""
+    d = bytearray(case("prog_420"))
+    start = d.index(b"\xff\xda") + 16
+    rng = np.random.default_rng(100 + seed)
+    for p in rng.integers(start, len(d) - 8, size=1 + seed % 4):
+        d[p] = int(rng.integers(0, 255))
+    return bytes(d)
+
+
+def truncated_progressive(frac: float = 0.5) -> bytes:
+    d = case("prog_420")
+    return d[: int(len(d) * frac)]
+

@@ -102,6 +102,43 @@ def test_large_progressive_batch_pad224(oracle):
         np.testing.assert_array_equal(hyp[i], oracle.decode_resize(d, rs, "rgb24"), strict=True)
 
 
+def _agree_or_both_fail(oracle, d):
+    """The GPU decode equals the oracle's, or both reject the image; later
+    calls still work."""
+    try:
+        ref = oracle.decode_rgb(d, 0, "rgb24")
+    except oracle.OracleError:
+        ref = None
+    info = oracle.parse(d)
+    dec = _lib.Decoder(0)
+    t = torch.empty((info.height, info.width, 3), dtype=torch.uint8, device="cuda:0")
+    if ref is None:
+        with pytest.raises(RuntimeError, match="Failed to decode an image"):
+            dec.decode_batch([d], Output(pix_fmt="rgb24"), t.data_ptr(), t.numel())
+    else:
+        dec.decode_batch([d], Output(pix_fmt="rgb24"), t.data_ptr(), t.numel())
+        np.testing.assert_array_equal(t.cpu().numpy(), ref, strict=True)
+    good = cases.case("prog_422")
+    gi = oracle.parse(good)
+    g = torch.empty((gi.height, gi.width, 3), dtype=torch.uint8, device="cuda:0")
+    dec.decode_batch([good], Output(pix_fmt="rgb24"), g.data_ptr(), g.numel())
+    np.testing.assert_array_equal(g.cpu().numpy(), oracle.decode_rgb(good, 0, "rgb24"), strict=True)
+    dec.close()
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_corrupt_progressive_agrees_with_oracle(oracle, seed):
+    """Corrupt scan data / scan headers: the two concurrent scan decoders
+    either reproduce the oracle's pixels or fail the image as it does (no
+    hang waiting for a scan that failed)."""
+    _agree_or_both_fail(oracle, cases.corrupt_progressive(seed))
+
+
+@pytest.mark.parametrize("frac", [0.3, 0.5, 0.8, 0.97])
+def test_truncated_progressive(oracle, frac):
+    _agree_or_both_fail(oracle, cases.truncated_progressive(frac))
+
+
 @pytest.mark.parametrize("bad", ["arithmetic", "cmyk"])
 def test_unsupported_fails_per_image(bad):
     """An unsupported image fails alone: strict=False keeps the others."""
