@@ -651,7 +651,10 @@ struct spdl_hj_ctx {
   // kernel), 256 with two or more (the smaller workgroups leave the other
   // lane's kernels more room: +3 % in the 2-lane bench, r02 A/B)
   int entropy_threads = 0;
-  int warm_slots = 12;  // entropy round 0: slots decoded before a run's first slot
+  // entropy round 0: slots decoded before a run's first slot; -1 = by
+  // workgroup size: 12 with 512+ threads, 6 with 256 (each run then spans
+  // twice the slots; 4-lane A/B: 459-461k vs 450-454k img/s, r02_v5)
+  int warm_slots = -1;
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
   PlanCache plans;          // swscale plans per distinct geometry
 };
@@ -803,13 +806,16 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<uint8_t*>(W.clean.p), static_cast<uint32_t*>(W.segs.p),
                         L.max_chunks, n, st));
   mark(ctx, slot, 3, st);
+  const int ent_threads =
+      ctx->entropy_threads ? ctx->entropy_threads : (ctx->lanes > 1 ? 256 : 512);
+  const int warm = ctx->warm_slots >= 0 ? ctx->warm_slots : (ent_threads <= 256 ? 6 : 12);
   HJ_HIP(launch_entropy(static_cast<const uint8_t*>(W.clean.p),
                         static_cast<const uint32_t*>(W.segs.p), desc, infos,
                         static_cast<const HuffTable*>(W.luts.p),
                         static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
                         static_cast<uint32_t*>(W.recs.p),
-                        ctx->sub_bits, ctx->warm_slots | (((ctx->debug_mask >> 12) & 0xF) << 16),
-                        ctx->entropy_threads ? ctx->entropy_threads : (ctx->lanes > 1 ? 256 : 512),
+                        ctx->sub_bits, warm | (((ctx->debug_mask >> 12) & 0xF) << 16),
+                        ent_threads,
                         ctx->entropy_lds_pad, n, st));
   // progressive / non-interleaved images (the kernels above skipped them)
   // (debug_mask 0x10000 / 0x20000 / 0x40000: timing ablations that skip the
