@@ -132,7 +132,7 @@ def _args():
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="pad224")
     p.add_argument("--norm-dtype", choices=["float16", "bfloat16"], default="float16")
     p.add_argument("--inflight", type=int, default=0, choices=range(0, 11),
-                   help="batches submitted ahead before waiting the oldest (0: one per lane)")
+                   help="batches submitted ahead before waiting the oldest (0: lanes + 2; the ring holds 10)")
     p.add_argument("--lanes", type=int, default=4,
                    help="concurrent decode pipelines in the context (1-8)")
     p.add_argument("--sync-steps", action="store_true",
@@ -285,7 +285,7 @@ def _dry_run(a, rank: int, world: int) -> None:
 def main():
     a = _args()
     if a.inflight == 0:
-        a.inflight = max(2, a.lanes)
+        a.inflight = min(10, max(2, a.lanes + 2))
     rank, world, local = launched_world()
     if a.gpus > 1 and world == 1:
         # one process per GPU, started before anything touches a device
