@@ -54,7 +54,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # Per-launch HBM-side bytes per kernel from the committed rocprofv3 --pmc
 # passes of this same command (tools/pmc_passes.sh + tools/pmc_traffic.py):
 # FETCH_SIZE / WRITE_SIZE cannot be read from inside the timed process.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_v6", "traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_v7", "traffic.json")
 # bench stage -> kernels launched in it
 STAGE_KERNELS = {
     "parse": ["hj::parse_kernel"],
