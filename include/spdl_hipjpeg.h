@@ -252,14 +252,16 @@ int spdl_hj_last_timings(spdl_hj_ctx* ctx, float* us, int32_t cap, int32_t* n_ou
 /* Names of the timed stages in the order spdl_hj_last_timings reports them. */
 const char* spdl_hj_stage_name(int32_t i);
 
-/* Tuning knobs: "sub_bits" (slot size of the parallel Huffman decode),
- * "entropy_threads" (256/512/1024), "warmup_slots" (0-64: slots a Huffman
- * run decodes from a guessed state before its own first slot; default 8),
- * "lanes" (1-3 concurrent pipelines:
- * with 2, successive batches alternate between two device workspaces and run
- * on the context's own two streams, each ordered after the caller's stream at
- * submission; completion is then observed through the ticket --
- * spdl_hj_wait / spdl_hj_stream_wait -- not by the caller's stream). */
+/* Tuning knobs: "sub_bits" (slot size of the parallel Huffman decode,
+ * default 384), "entropy_threads" (256/512/1024; default 512 with one lane,
+ * 256 with more), "warmup_slots" (0-64: slots a Huffman run decodes from a
+ * guessed state before its own first slot; default 6 with 256 threads, 12
+ * with more), "lanes" (1-8 concurrent pipelines: with N > 1, successive
+ * batches rotate over N device workspaces and run on the context's own N
+ * streams, each ordered after the caller's stream at submission; completion
+ * is then observed through the ticket -- spdl_hj_wait / spdl_hj_stream_wait
+ * -- not by the caller's stream; each lane wants a hardware queue of its own,
+ * GPU_MAX_HW_QUEUES >= N + 2). */
 int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value);
 
 #ifdef __cplusplus
