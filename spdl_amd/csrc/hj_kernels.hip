@@ -1662,12 +1662,13 @@ __global__ void __launch_bounds__(NT) HJ_ENT_ATTR entropy_kernel(const uint8_t* 
 // multiscan_kernel: progressive (SOF2) and sequential non-interleaved JPEGs.
 // One workgroup per image.  The whole workgroup finds the marker candidates
 // (one coalesced pass over the file), thread 0 walks the segments and records
-// every scan, the workgroup builds each scan's Huffman tables in LDS, and
-// thread 0 decodes the scan (a progressive scan's meaning depends on every
-// earlier scan of its blocks, so it is one sequential pass per scan; images
-// run in parallel, one per CU).  Levels accumulate as int32 in the image's
-// coefficient-list region, which the final pass turns into the lists
-// idct_kernel reads.  Arithmetic: oracle ms_decode (jpeg_oracle.c), libjpeg
+// every scan with its dependencies, then kMsDec decoder waves each take the
+// next ready scan, build its Huffman tables in their own LDS and decode it
+// wave-uniformly (a progressive scan's meaning depends on every earlier scan
+// of its blocks, so each scan is one sequential pass; independent scans run
+// at once; images run in parallel, one per CU).  Levels accumulate as int32
+// in the image's coefficient-list region, which the final pass turns into
+// the lists idct_kernel reads.  Arithmetic: oracle ms_decode (jpeg_oracle.c), libjpeg
 // jdphuff.c semantics, FFmpeg-style dequantisation.
 // ---------------------------------------------------------------------------
 
@@ -1927,7 +1928,7 @@ __device__ __forceinline__ void ms_take_corr(MsBits& br, uint64_t m, uint64_t& c
   }
 }
 
-// One block of one scan (thread 0).  lev: the block's levels in HBM (zig-zag
+// One block of one scan (a decoder wave, uniform).  lev: the block's levels in HBM (zig-zag
 // index; stores only).  AC refinement (block j of the chunk) decodes against
 // the staged history mask and leaves records for the workgroup to apply:
 // which history coefficients get a correction bit (libjpeg jdphuff
@@ -2049,7 +2050,7 @@ __device__ __forceinline__ int ms_block_decode(MsWave& S, MsBits& br, const MsBa
   return kOk;
 }
 
-// Thread 0's scan decoder state, carried across chunks in registers.
+// A decoder wave's scan state, carried across chunks in (scalar) registers.
 struct MsState {
   MsBits br;
   int32_t pred0, pred1, pred2;
@@ -2057,7 +2058,7 @@ struct MsState {
   bool rst_done;  // the restart marker before `mcu` was consumed
 };
 
-// Thread 0: decode MCUs of one scan from st.mcu on, until the scan ends, the
+// A decoder wave: decode MCUs of one scan from st.mcu on, until the scan ends, the
 // chunk ends (AC refinement: MCU chunk_end) or the reader comes within the
 // margin of the staged window's end at an MCU start (wlim; unless the window
 // holds the rest of the scan).  Restart intervals, interleaved MCUs or one
