@@ -91,7 +91,10 @@ OUT_SPEC = Output(pix_fmt="rgb24", resize=True, fit_w=224, fit_h=224, aspect="de
 # (x/255 - mean)/std in fp32 -> fp16 (or bf16), NCHW.
 IMAGENET_SPEC = Output(pix_fmt="rgb", resize=True, fit_w=256, fit_h=256, aspect="decrease",
                        pad_w=256, pad_h=256, crop_w=224, crop_h=224, normalize=True)
+FULLRES_SPEC = Output(pix_fmt="rgb24", resize=False)
 WORKLOADS = {
+    "fullres": ("configs[1] full resolution: synthetic 480x640 q90 4:2:0 baseline JPEG resident in "
+                "HBM -> RGB 480x640 u8 (rgb24, load_image's format=rgb24 chain)"),
     "pad224": ("configs[1]: synthetic 480x640 q90 4:2:0 baseline JPEG resident in HBM -> RGB "
                "224x224 u8 (scale bicubic decrease + centred pad, rgb24)"),
     "imagenet": ("configs[3]: synthetic 480x640 q90 4:2:0 baseline JPEG resident in HBM -> "
@@ -246,8 +249,11 @@ def _oracle_check(datas, out: torch.Tensor, spec: Output, n_check: int) -> str:
     kw = dict(fit_w=spec.fit_w, fit_h=spec.fit_h, aspect=spec.aspect, pad_w=spec.pad_w,
               pad_h=spec.pad_h, crop_w=spec.crop_w, crop_h=spec.crop_h, filter=spec.filter)
     for i in range(n_check):
-        ref = O.decode_resize(datas[i], O.Resize(**kw), pix_fmt=spec.pix_fmt,
-                              normalize=spec.normalize, norm_dtype=spec.norm_dtype)
+        if not spec.resize:  # full resolution: the format=rgb24 chain
+            ref = O.decode_rgb(datas[i], O.IDCT_SIMPLE, spec.pix_fmt)
+        else:
+            ref = O.decode_resize(datas[i], O.Resize(**kw), pix_fmt=spec.pix_fmt,
+                                  normalize=spec.normalize, norm_dtype=spec.norm_dtype)
         hyp = host[i]
         if spec.normalize:
             hyp = hyp.view(torch.int16).numpy().view(np.uint16)
@@ -322,6 +328,10 @@ def main():
     if a.workload == "imagenet":
         spec = Output(**{**IMAGENET_SPEC.__dict__, "norm_dtype": a.norm_dtype})
         outs = [torch.empty((a.batch, 3, 224, 224), dtype=spec.torch_dtype, device=device)
+                for _ in range(max(3, a.inflight))]
+    elif a.workload == "fullres":
+        spec = FULLRES_SPEC
+        outs = [torch.empty((a.batch, 480, 640, 3), dtype=torch.uint8, device=device)
                 for _ in range(max(3, a.inflight))]
     else:
         spec = OUT_SPEC
@@ -423,7 +433,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8" if a.workload == "pad224" else
+            "dtype": "u8" if a.workload in ("pad224", "fullres") else
                      {"float16": "f16", "bfloat16": "bf16"}[a.norm_dtype] + " out (int decode, f32 normalise)",
             "data": "synthetic",
             "config": {

@@ -48,6 +48,8 @@ hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
 hipError_t launch_nv12(const uint8_t*, uint8_t*, int, int, int, int, int, hipStream_t);
 hipError_t launch_sws(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*, void*,
                       const BatchParams&, int, int, int, int, int32_t*, hipStream_t);
+hipError_t launch_rgb_unscaled(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
+                               const BatchParams&, int64_t, int, int32_t*, hipStream_t);
 }  // namespace hj
 
 using namespace hj;
@@ -356,6 +358,7 @@ struct PackedPlan {
   SwsDesc d{};                  // offsets relative to the blob
   std::vector<int32_t> blob;    // tables, 16-byte aligned sections
   int bands = 0, chunks = 0, lds = 0;
+  bool special = false;         // swscale's unscaled yuv2rgb_c_24_rgb converter
 };
 
 class PlanCache {
@@ -383,6 +386,7 @@ class PlanCache {
     *rc = sws_plan(k.w, k.h, k.hsub, k.vsub, k.gray != 0, k.sw, k.sh, k.filter, &pl);
     if (*rc) return nullptr;
     auto pp = std::make_shared<PackedPlan>();
+    pp->special = pl.special && k.dx == 0 && k.dy == 0 && k.ow == k.sw && k.oh == k.sh;
     SwsDesc& d = pp->d;
     d.sw = k.sw;
     d.sh = k.sh;
@@ -486,6 +490,7 @@ struct Layout {
   int max_chunks = 0;
   int ow = 0, oh = 0;
   int sws_bands = 0, sws_chunks = 0, sws_lds = 0;
+  bool all_special = true;  // every image takes swscale's unscaled converter
 };
 
 int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_image_info* infos,
@@ -587,6 +592,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     }
     d.wt_off = it->second;
     d.sws = plan->d;
+    L.all_special = L.all_special && plan->special;
     L.sws_bands = std::max(L.sws_bands, plan->bands);
     L.sws_chunks = std::max(L.sws_chunks, plan->chunks);
     L.sws_lds = std::max(L.sws_lds, plan->lds);
@@ -860,7 +866,12 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   int32_t* hstat = hs && !planes_only ? static_cast<int32_t*>(slot.pin_status.dev) : nullptr;
   mark(ctx, slot, 6, st);
   if (!planes_only && !(ctx->debug_mask & 0x40000)) {
-    if (swscale) {
+    if (swscale && L.all_special && out->dtype == SPDL_HJ_DTYPE_U8 &&
+        !(ctx->debug_mask & 0x80000)) {
+      // full resolution, u8: swscale's unscaled converter needs no scaling passes
+      HJ_HIP(launch_rgb_unscaled(static_cast<const uint8_t*>(W.planes.p), desc, infos, out_dev,
+                                 bp, L.max_px, n, hstat, st));
+    } else if (swscale) {
       HJ_HIP(launch_sws(static_cast<const uint8_t*>(W.planes.p), desc, infos,
                         static_cast<const int32_t*>(W.wts.p), out_dev, bp, L.sws_bands,
                         L.sws_chunks, L.sws_lds, n, hstat, st));

@@ -232,3 +232,32 @@ def test_subsequence_sizes(oracle, sub_bits, threads):
             dec.decode_batch([d], Output(pix_fmt="rgb24"), t.data_ptr(), t.numel())
             np.testing.assert_array_equal(t.cpu().numpy(), ref)
     dec.close()
+
+
+@pytest.mark.parametrize("pix_fmt", ["rgb", "rgb24", "bgr", "bgr24"])
+@pytest.mark.parametrize("w,h", [(64, 48), (102, 70), (30, 18)])
+def test_fullres_batch_unscaled_converter(decoder, oracle, pix_fmt, w, h):
+    """Full-resolution batches: 420 / 422 images of one size take swscale's
+    unscaled converter (rgb_unscaled_kernel); adding a 444 image sends the
+    batch through the generic sws_kernel.  Both bit-exact vs the oracle."""
+    datas = [cases._enc(cases._noise(s, h, w), quality=85 + s, subsampling=2 if s % 2 else 1)
+             for s in range(5)]
+    shape = (3, h, w) if pix_fmt in ("rgb", "bgr") else (h, w, 3)
+    for batch in (datas, datas + [cases._enc(cases._noise(9, h, w), quality=90, subsampling=0)]):
+        hyp = _decode(decoder, batch, Output(pix_fmt=pix_fmt), shape).numpy()
+        for i, d in enumerate(batch):
+            np.testing.assert_array_equal(hyp[i], oracle.decode_rgb(d, oracle.IDCT_SIMPLE, pix_fmt),
+                                          strict=True)
+
+
+def test_fullres_unscaled_converter_matches_generic(decoder):
+    """The unscaled converter and the generic swscale kernel (debug_mask
+    0x80000 forces it) agree byte for byte on a 480x640 420 batch."""
+    datas = [cases._enc(cases._noise(s, 480, 640), quality=90, subsampling=2) for s in range(4)]
+    fast = _decode(decoder, datas, Output(pix_fmt="rgb24"), (480, 640, 3))
+    decoder.set_param("debug_mask", 0x80000)
+    try:
+        generic = _decode(decoder, datas, Output(pix_fmt="rgb24"), (480, 640, 3))
+    finally:
+        decoder.set_param("debug_mask", 0)
+    assert torch.equal(fast, generic)
