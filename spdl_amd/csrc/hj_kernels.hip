@@ -3202,83 +3202,120 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
 // yuv2rgb_c_24_rgb: yuvj420p with even height / yuvj422p, even width ->
 // rgb24) for full-resolution output: nearest chroma and the same table
 // arithmetic as sws_kernel's one-tap writer with identity filters (Y, U, V
-// are the plane bytes; oracle sws_oracle.c), but one thread per 8 pixels of
-// a row -- no horizontal / vertical passes and no LDS.  u8 only.
+// are the plane bytes; oracle sws_oracle.c), but one thread per
+// kRgbPx pixels of a row -- no horizontal / vertical passes and no LDS.  u8
+// only.  HBM-bound: 1.5 B in + 3 B out per pixel.
+#ifndef HJ_RGBU_PX
+#define HJ_RGBU_PX 8
+#endif
+constexpr int kRgbPx = HJ_RGBU_PX;  // 8 or 16
+
+template <int N>  // N words from a pointer aligned to 4 N bytes
+__device__ __forceinline__ void rgbu_load(const uint8_t* p, uint32_t (&w)[N]) {
+  if constexpr (N == 1) {
+    w[0] = *reinterpret_cast<const uint32_t*>(p);
+  } else if constexpr (N == 2) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    w[0] = v.x, w[1] = v.y;
+  } else {
+    static_assert(N == 4, "rgbu_load: 1, 2 or 4 words");
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+  }
+}
+
+template <int N>  // N words (2 or 4) as one store
+__device__ __forceinline__ void rgbu_store(uint8_t* p, const uint32_t* w) {
+  if constexpr (N == 2) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
+  } else {
+    static_assert(N == 4, "rgbu_store: 2 or 4 words");
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 __global__ void __launch_bounds__(256) rgb_unscaled_kernel(const uint8_t* __restrict__ planes,
                                                            const ImageDesc* __restrict__ desc,
                                                            const ImageInfo* __restrict__ infos,
                                                            uint8_t* __restrict__ out,
                                                            const BatchParams p,
                                                            int32_t* __restrict__ host_status) {
+  constexpr int PX = kRgbPx, YW = PX / 4, CW = PX / 8, SW = PX / 4;  // SW: words per vector store
   const int img = blockIdx.y;
   const ImageInfo& in = infos[img];
   if (host_status && blockIdx.x == 0 && threadIdx.x == 0) host_status[img] = in.status;
   if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
-  const int w = dd.ow, h = dd.oh;  // w is even: a row's last group may hold 2..6 px
-  const int ngr = (w + 7) >> 3;
+  const int w = dd.ow, h = dd.oh;  // w is even: a row's last group may hold 2..PX-2 px
+  const uint32_t ngr = (uint32_t)(w + PX - 1) / PX;
+  const uint32_t total = ngr * (uint32_t)h;  // < 2^27 (nblocks < 2^24)
   const int vsub = in.comp_v[0] > in.comp_v[1] ? 1 : 0;
   const bool planar = p.pix_fmt == 0 || p.pix_fmt == 1;
   const bool swap = p.pix_fmt == 1 || p.pix_fmt == 3;
   const int64_t pl = (int64_t)w * h;
-  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < (int64_t)ngr * h;
-       g += (int64_t)gridDim.x * blockDim.x) {
-    const int y = (int)(g / ngr), x0 = (int)(g - (int64_t)y * ngr) * 8;
-    const int npx = x0 + 8 <= w ? 8 : w - x0;
-    const uint8_t* yr = planes + dd.plane_off[0] + (int64_t)y * dd.plane_stride[0] + x0;
-    const uint8_t* ur = planes + dd.plane_off[1] + (int64_t)(y >> vsub) * dd.plane_stride[1] + (x0 >> 1);
-    const uint8_t* vr = planes + dd.plane_off[2] + (int64_t)(y >> vsub) * dd.plane_stride[2] + (x0 >> 1);
-    // planes are padded to whole blocks: 8 luma / 4 chroma bytes are readable
-    const uint2 yq = *reinterpret_cast<const uint2*>(yr);
-    const uint32_t uq = *reinterpret_cast<const uint32_t*>(ur);
-    const uint32_t vq = *reinterpret_cast<const uint32_t*>(vr);
-    uint8_t px[8][3];
+  const uint8_t* y_pl = planes + dd.plane_off[0];
+  const uint8_t* u_pl = planes + dd.plane_off[1];
+  const uint8_t* v_pl = planes + dd.plane_off[2];
+  uint8_t* base = out + dd.out_off;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
+    const int y = (int)(g / ngr), x0 = (int)(g - (uint32_t)y * ngr) * PX;
+    const int npx = x0 + PX <= w ? PX : w - x0;
+    // planes are padded to whole blocks (luma rows to 16 px for 4:2:x): PX luma
+    // and PX/2 chroma bytes are readable and aligned
+    uint32_t yw[YW], uw[CW], vw[CW];
+    rgbu_load<YW>(y_pl + (int64_t)y * dd.plane_stride[0] + x0, yw);
+    rgbu_load<CW>(u_pl + (int64_t)(y >> vsub) * dd.plane_stride[1] + (x0 >> 1), uw);
+    rgbu_load<CW>(v_pl + (int64_t)(y >> vsub) * dd.plane_stride[2] + (x0 >> 1), vw);
+    uint32_t c0[PX], c1[PX], c2[PX];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int Y = (int)(((i < 4 ? yq.x : yq.y) >> (8 * (i & 3))) & 0xFFu);
-      const int U = (int)((uq >> (8 * (i >> 1))) & 0xFFu);
-      const int V = (int)((vq >> (8 * (i >> 1))) & 0xFFu);
+    for (int i = 0; i < PX; i++) {
+      const int Y = (int)((yw[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+      const int U = (int)((uw[i >> 3] >> (8 * ((i >> 1) & 3))) & 0xFFu);
+      const int V = (int)((vw[i >> 3] >> (8 * ((i >> 1) & 3))) & 0xFFu);
       const int r = clip_i8(Y + tab_off(p.crv, V));
       const int gg = clip_i8(Y + tab_off(p.cgu, U) + tab_off(p.cgv, V));
       const int b = clip_i8(Y + tab_off(p.cbu, U));
-      px[i][0] = (uint8_t)(swap ? b : r);
-      px[i][1] = (uint8_t)gg;
-      px[i][2] = (uint8_t)(swap ? r : b);
+      c0[i] = (uint32_t)(swap ? b : r);
+      c1[i] = (uint32_t)gg;
+      c2[i] = (uint32_t)(swap ? r : b);
     }
-    uint8_t* base = out + dd.out_off;
     if (!planar) {
       uint8_t* o = base + ((int64_t)y * w + x0) * 3;
-      if (npx == 8 && ((uintptr_t)o & 7u) == 0u) {  // 24 bytes: three 8-byte stores
-        uint32_t wv[6];
+      if (npx == PX && ((uintptr_t)o & (4u * SW - 1u)) == 0u) {  // 3 PX bytes: three stores
+        uint32_t wv[3 * PX / 4];
 #pragma unroll
-        for (int k = 0; k < 6; k++)
-          wv[k] = (uint32_t)px[(4 * k) / 3][(4 * k) % 3] |
-                  (uint32_t)px[(4 * k + 1) / 3][(4 * k + 1) % 3] << 8 |
-                  (uint32_t)px[(4 * k + 2) / 3][(4 * k + 2) % 3] << 16 |
-                  (uint32_t)px[(4 * k + 3) / 3][(4 * k + 3) % 3] << 24;
-        uint2* o2 = reinterpret_cast<uint2*>(o);
-        o2[0] = make_uint2(wv[0], wv[1]);
-        o2[1] = make_uint2(wv[2], wv[3]);
-        o2[2] = make_uint2(wv[4], wv[5]);
+        for (int k = 0; k < 3 * PX / 4; k++) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int q = 4 * k + j, i = q / 3, c = q % 3;
+            v |= (c == 0 ? c0[i] : c == 1 ? c1[i] : c2[i]) << (8 * j);
+          }
+          wv[k] = v;
+        }
+#pragma unroll
+        for (int s3 = 0; s3 < 3; s3++) rgbu_store<SW>(o + 4 * SW * s3, wv + SW * s3);
       } else {
-        for (int i = 0; i < npx; i++)
-          for (int c = 0; c < 3; c++) o[3 * i + c] = px[i][c];
+        for (int i = 0; i < npx; i++) {
+          o[3 * i] = (uint8_t)c0[i];
+          o[3 * i + 1] = (uint8_t)c1[i];
+          o[3 * i + 2] = (uint8_t)c2[i];
+        }
       }
     } else {
+#pragma unroll
       for (int c = 0; c < 3; c++) {
+        const uint32_t* cv = c == 0 ? c0 : c == 1 ? c1 : c2;
         uint8_t* o = base + c * pl + (int64_t)y * w + x0;
-        if (npx == 8) {
-          uint2 v;
-          v.x = (uint32_t)px[0][c] | (uint32_t)px[1][c] << 8 | (uint32_t)px[2][c] << 16 |
-                (uint32_t)px[3][c] << 24;
-          v.y = (uint32_t)px[4][c] | (uint32_t)px[5][c] << 8 | (uint32_t)px[6][c] << 16 |
-                (uint32_t)px[7][c] << 24;
-          if (((uintptr_t)o & 7u) == 0u) {
-            *reinterpret_cast<uint2*>(o) = v;
-            continue;
-          }
+        if (npx == PX && ((uintptr_t)o & (4u * SW - 1u)) == 0u) {
+          uint32_t wv[SW];
+#pragma unroll
+          for (int k = 0; k < SW; k++)
+            wv[k] = cv[4 * k] | cv[4 * k + 1] << 8 | cv[4 * k + 2] << 16 | cv[4 * k + 3] << 24;
+          rgbu_store<SW>(o, wv);
+        } else {
+          for (int i = 0; i < npx; i++) o[i] = (uint8_t)cv[i];
         }
-        for (int i = 0; i < npx; i++) o[i] = px[i][c];
       }
     }
   }
@@ -3287,7 +3324,7 @@ __global__ void __launch_bounds__(256) rgb_unscaled_kernel(const uint8_t* __rest
 hipError_t launch_rgb_unscaled(const uint8_t* planes, const ImageDesc* desc,
                                const ImageInfo* infos, void* out, const BatchParams& p,
                                int64_t max_px, int n, int32_t* host_status, hipStream_t st) {
-  const int64_t groups = (max_px + 7) / 8 + 64;
+  const int64_t groups = (max_px + kRgbPx - 1) / kRgbPx + 64;
   const int gx = (int)std::min<int64_t>((groups + 255) / 256, 1024);
   hipLaunchKernelGGL(rgb_unscaled_kernel, dim3(gx, n), dim3(256), 0, st, planes, desc, infos,
                      static_cast<uint8_t*>(out), p, host_status);
