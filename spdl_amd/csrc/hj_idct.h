@@ -40,11 +40,15 @@ HJ_HD inline int32_t clip_u8_opaque(int v) {
 // DC-only row shortcut (row[0] << 3, as int16) is a select.
 HJ_HD inline int32_t sext16(uint32_t v) { return (int32_t)(int16_t)(uint16_t)v; }
 
+// NC = 4: the caller knows r[4..7] are zero (the terms they feed vanish;
+// same results).
+template <int NC = 8>
 HJ_HD inline void simple_row(int32_t* r) {
-  const bool dc_only = !(r[1] | r[2] | r[3] | r[4] | r[5] | r[6] | r[7]);
   const uint32_t u0 = (uint32_t)r[0], u1 = (uint32_t)r[1], u2 = (uint32_t)r[2],
-                 u3 = (uint32_t)r[3], u4 = (uint32_t)r[4], u5 = (uint32_t)r[5],
-                 u6 = (uint32_t)r[6], u7 = (uint32_t)r[7];
+                 u3 = (uint32_t)r[3], u4 = NC > 4 ? (uint32_t)r[4] : 0u,
+                 u5 = NC > 4 ? (uint32_t)r[5] : 0u, u6 = NC > 4 ? (uint32_t)r[6] : 0u,
+                 u7 = NC > 4 ? (uint32_t)r[7] : 0u;
+  const bool dc_only = !(u1 | u2 | u3 | u4 | u5 | u6 | u7);
   uint32_t a0 = (uint32_t)kW4 * u0 + (1u << 10);
   uint32_t a1 = a0, a2 = a0, a3 = a0;
   a0 += (uint32_t)kW2 * u2;
@@ -74,11 +78,13 @@ HJ_HD inline void simple_row(int32_t* r) {
   r[4] = dc_only ? dc : sext16((uint32_t)((int32_t)(a3 - b3) >> 11));
 }
 
-// column k of the row-pass output: c[8*j], j = 0..7; writes 8 pixels o[8*j]
+// column k of the row-pass output: c[8*j], j = 0..7; writes 8 pixels o[8*j].
+// NR = 4: the caller knows rows 4..7 are zero.
+template <int NR = 8>
 HJ_HD inline void simple_col(const int32_t* c, int32_t* o) {
   const uint32_t u1 = (uint32_t)c[8], u2 = (uint32_t)c[16], u3 = (uint32_t)c[24],
-                 u4 = (uint32_t)c[32], u5 = (uint32_t)c[40], u6 = (uint32_t)c[48],
-                 u7 = (uint32_t)c[56];
+                 u4 = NR > 4 ? (uint32_t)c[32] : 0u, u5 = NR > 4 ? (uint32_t)c[40] : 0u,
+                 u6 = NR > 4 ? (uint32_t)c[48] : 0u, u7 = NR > 4 ? (uint32_t)c[56] : 0u;
   uint32_t a0 = (uint32_t)kW4 * (uint32_t)(c[0] + ((1 << 19) / kW4));
   uint32_t a1 = a0, a2 = a0, a3 = a0;
   a0 += (uint32_t)kW2 * u2;

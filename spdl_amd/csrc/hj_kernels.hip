@@ -2608,10 +2608,19 @@ hipError_t launch_multiscan(const uint8_t* bytes, const ImageDesc* desc, ImageIn
 #define HJ_IDCT_THREADS 256
 #endif
 constexpr int kIdctThreads = HJ_IDCT_THREADS;
+// HJ_IDCT_SPARSE 1: wave-uniform sparse transforms (below).  Off: on the
+// bench images 468-470 k vs 474 k img/s (the four variants take 136 VGPRs,
+// or spill under a 4-waves/SIMD cap; r02_v7/ab_idct_sparse/)
+#ifndef HJ_IDCT_SPARSE
+#define HJ_IDCT_SPARSE 0
+#endif
+#ifndef HJ_IDCT_ATTR
+#define HJ_IDCT_ATTR
+#endif
 constexpr int kBlkWords = 36;
 
 template <int IDCT>
-__global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __restrict__ ents,
+__global__ void __launch_bounds__(kIdctThreads) HJ_IDCT_ATTR idct_kernel(const uint32_t* __restrict__ ents,
                                                             const uint2* __restrict__ bdesc,
                                                             const ImageDesc* __restrict__ desc,
                                                             const ImageInfo* __restrict__ infos,
@@ -2668,10 +2677,13 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
     }
   }
   int32_t blk[64];
+  uint32_t rows_hi = 0u, cols_hi = 0u;  // any coefficient in rows 4..7 / columns 4..7
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint4 q = my4[i];
     const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
+    if (i >= 4) rows_hi |= q.x | q.y | q.z | q.w;
+    cols_hi |= q.z | q.w;
 #pragma unroll
     for (int h = 0; h < 4; h++) {
       blk[8 * i + 2 * h] = sext16(wv[h]);
@@ -2683,10 +2695,37 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
 #pragma unroll
     for (int i = 0; i < 64; i++) px[i] = blk[i] & 255;
   } else if (IDCT == 0) {
+    // Sparse blocks, wave-uniform: when no block of the wave has a
+    // coefficient in rows (columns) 4..7, those rows' passes and terms are
+    // additions of zero and are left out -- same results, fewer instructions
+    // (HJ_IDCT_SPARSE 0: always the full transform)
+#if HJ_IDCT_SPARSE
+    const bool r4 = !__any(rows_hi != 0u), c4 = !__any(cols_hi != 0u);
+#else
+    const bool r4 = false, c4 = false;
+    (void)rows_hi, (void)cols_hi;
+#endif
+    if (r4 && c4) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) simple_row(blk + 8 * i);
+      for (int i = 0; i < 4; i++) simple_row<4>(blk + 8 * i);
 #pragma unroll
-    for (int i = 0; i < 8; i++) simple_col(blk + i, px + i);
+      for (int i = 0; i < 8; i++) simple_col<4>(blk + i, px + i);
+    } else if (r4) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) simple_row<8>(blk + 8 * i);
+#pragma unroll
+      for (int i = 0; i < 8; i++) simple_col<4>(blk + i, px + i);
+    } else if (c4) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) simple_row<4>(blk + 8 * i);
+#pragma unroll
+      for (int i = 0; i < 8; i++) simple_col<8>(blk + i, px + i);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) simple_row<8>(blk + 8 * i);
+#pragma unroll
+      for (int i = 0; i < 8; i++) simple_col<8>(blk + i, px + i);
+    }
   } else {
     islow_block(blk, px);
   }
