@@ -50,6 +50,8 @@ hipError_t launch_sws(const uint8_t*, const ImageDesc*, const ImageInfo*, const 
                       const BatchParams&, int, int, int, int, int32_t*, hipStream_t);
 hipError_t launch_rgb_unscaled(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                                const BatchParams&, int64_t, int, int32_t*, hipStream_t);
+hipError_t launch_idct_rgb(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, void*,
+                           const BatchParams&, int, int, int, int32_t*, hipStream_t);
 }  // namespace hj
 
 using namespace hj;
@@ -491,6 +493,8 @@ struct Layout {
   int ow = 0, oh = 0;
   int sws_bands = 0, sws_chunks = 0, sws_lds = 0;
   bool all_special = true;  // every image takes swscale's unscaled converter
+  bool fuse_ok = true;      // ... with standard 4:2:0 / 4:2:2 MCUs (idct_rgb_kernel)
+  int fused_tiles = 0;      // idct_rgb_kernel workgroups per image (max)
 };
 
 int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_image_info* infos,
@@ -593,6 +597,15 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     d.wt_off = it->second;
     d.sws = plan->d;
     L.all_special = L.all_special && plan->special;
+    // idct_rgb_kernel's MCU shapes: Y 2x2 or 2x1, U and V 1x1
+    if (p.ncomp == 3 && p.h_samp[0] == 2 && (p.v_samp[0] == 1 || p.v_samp[0] == 2) &&
+        p.h_samp[1] == 1 && p.v_samp[1] == 1 && p.h_samp[2] == 1 && p.v_samp[2] == 1) {
+      const int bpm = 2 * p.v_samp[0] + 2, tw = 256 / bpm;
+      const int mcux = (p.width + 15) / 16, mcuy = (p.height + 8 * p.v_samp[0] - 1) / (8 * p.v_samp[0]);
+      L.fused_tiles = std::max(L.fused_tiles, (mcux + tw - 1) / tw * mcuy);
+    } else {
+      L.fuse_ok = false;
+    }
     L.sws_bands = std::max(L.sws_bands, plan->bands);
     L.sws_chunks = std::max(L.sws_chunks, plan->chunks);
     L.sws_lds = std::max(L.sws_lds, plan->lds);
@@ -830,11 +843,17 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
     HJ_HIP(launch_multiscan(d_bytes, desc, infos, static_cast<uint32_t*>(W.ents.p),
                             static_cast<uint2*>(W.bdesc.p), n, st));
   mark(ctx, slot, 4, st);
-  if (!(ctx->debug_mask & 0x20000))
+  // full resolution u8 through swscale's unscaled converter: IDCT and
+  // conversion in one kernel (debug_mask 0x80000: the generic sws_kernel,
+  // 0x100000: separate IDCT + rgb_unscaled_kernel)
+  const int idct_kind = (ctx->debug_mask & 0x800) ? 2 : out->idct;
+  const bool fast_rgb = swscale && L.all_special && out->dtype == SPDL_HJ_DTYPE_U8 &&
+                        !(ctx->debug_mask & 0x80000);
+  const bool fused = fast_rgb && L.fuse_ok && L.fused_tiles > 0 && !(ctx->debug_mask & 0x100000);
+  if (!(ctx->debug_mask & 0x20000) && !fused)
     HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
                      static_cast<const uint2*>(W.bdesc.p), desc, infos,
-                     static_cast<uint8_t*>(W.planes.p), (ctx->debug_mask & 0x800) ? 2 : out->idct,
-                     L.max_blocks, n, st));
+                     static_cast<uint8_t*>(W.planes.p), idct_kind, L.max_blocks, n, st));
   mark(ctx, slot, 5, st);
   BatchParams bp{};
   bp.n = n;
@@ -866,8 +885,11 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   int32_t* hstat = hs && !planes_only ? static_cast<int32_t*>(slot.pin_status.dev) : nullptr;
   mark(ctx, slot, 6, st);
   if (!planes_only && !(ctx->debug_mask & 0x40000)) {
-    if (swscale && L.all_special && out->dtype == SPDL_HJ_DTYPE_U8 &&
-        !(ctx->debug_mask & 0x80000)) {
+    if (fused) {
+      HJ_HIP(launch_idct_rgb(static_cast<const uint32_t*>(W.ents.p),
+                             static_cast<const uint2*>(W.bdesc.p), desc, infos, out_dev, bp,
+                             idct_kind, L.fused_tiles, n, hstat, st));
+    } else if (fast_rgb) {
       // full resolution, u8: swscale's unscaled converter needs no scaling passes
       HJ_HIP(launch_rgb_unscaled(static_cast<const uint8_t*>(W.planes.p), desc, infos, out_dev,
                                  bp, L.max_px, n, hstat, st));

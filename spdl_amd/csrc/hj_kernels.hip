@@ -2619,42 +2619,22 @@ constexpr int kIdctThreads = HJ_IDCT_THREADS;
 #endif
 constexpr int kBlkWords = 36;
 
+// One block of the entropy kernel's coefficient lists -> 8x8 pixels (u8
+// values in int32), through the thread's LDS slot `my_blk` (kBlkWords words).
 template <int IDCT>
-__global__ void __launch_bounds__(kIdctThreads) HJ_IDCT_ATTR idct_kernel(const uint32_t* __restrict__ ents,
-                                                            const uint2* __restrict__ bdesc,
-                                                            const ImageDesc* __restrict__ desc,
-                                                            const ImageInfo* __restrict__ infos,
-                                                            uint8_t* __restrict__ planes) {
-  __shared__ __attribute__((aligned(16))) uint32_t sblk[kIdctThreads][kBlkWords];
-  const int img = blockIdx.y;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  const ImageInfo& in = infos[img];
-  if (in.status != kOk || j >= in.nblocks) return;
-  const ImageDesc& dd = desc[img];
-  const int bpm = in.bpm;
-  const int mcu = j / bpm, b = j - mcu * bpm;
-  const int c = in.mcu_comp[b];
-  const int mx = mcu % in.mcux, my = mcu / in.mcux;
-  int bx, by;
-  if (in.ncomp == 1) {
-    bx = mx;
-    by = my;
-  } else {
-    bx = mx * in.comp_h[c] + in.mcu_dx[b];
-    by = my * in.comp_v[c] + in.mcu_dy[b];
-  }
+__device__ __forceinline__ void idct_list_block(const uint32_t* __restrict__ ents, const uint2 bd,
+                                                const int64_t coef_off, const int nblocks,
+                                                uint32_t* my_blk, int32_t (&px)[64]) {
   // The entropy kernel's list for this block (see BlockOut): DC final, AC
   // dequantised with their natural index; placed in the thread's LDS block.
   // (a list may start inside a 16-byte group: the run's lists are packed
   // back to back; entries [lo, lo + count) of the groups from `start`)
-  const uint2 bd = bdesc[(size_t)dd.coef_off + j];
-  const uint32_t cap = (uint32_t)in.nblocks * 64u;
+  const uint32_t cap = (uint32_t)nblocks * 64u;
   const uint32_t lo = bd.x & 3u, start = bd.x & ~3u;
   uint32_t count = min(bd.y & 0xFFFFu, 63u);
   if (start > cap - 64u) count = 0;  // only an unwritten list (a failed scan)
   const uint32_t hi_e = lo + count;
-  const uint4* e4 = reinterpret_cast<const uint4*>(ents + (size_t)dd.coef_off * 64 + start);
-  uint32_t* my_blk = sblk[threadIdx.x];
+  const uint4* e4 = reinterpret_cast<const uint4*>(ents + (size_t)coef_off * 64 + start);
   uint4* my4 = reinterpret_cast<uint4*>(my_blk);
 #pragma unroll
   for (int i = 0; i < 8; i++) my4[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -2690,7 +2670,6 @@ __global__ void __launch_bounds__(kIdctThreads) HJ_IDCT_ATTR idct_kernel(const u
       blk[8 * i + 2 * h + 1] = sext16(wv[h] >> 16);
     }
   }
-  int32_t px[64];
   if (IDCT == 2) {
 #pragma unroll
     for (int i = 0; i < 64; i++) px[i] = blk[i] & 255;
@@ -2729,6 +2708,35 @@ __global__ void __launch_bounds__(kIdctThreads) HJ_IDCT_ATTR idct_kernel(const u
   } else {
     islow_block(blk, px);
   }
+}
+
+template <int IDCT>
+__global__ void __launch_bounds__(kIdctThreads) HJ_IDCT_ATTR idct_kernel(const uint32_t* __restrict__ ents,
+                                                            const uint2* __restrict__ bdesc,
+                                                            const ImageDesc* __restrict__ desc,
+                                                            const ImageInfo* __restrict__ infos,
+                                                            uint8_t* __restrict__ planes) {
+  __shared__ __attribute__((aligned(16))) uint32_t sblk[kIdctThreads][kBlkWords];
+  const int img = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const ImageInfo& in = infos[img];
+  if (in.status != kOk || j >= in.nblocks) return;
+  const ImageDesc& dd = desc[img];
+  const int bpm = in.bpm;
+  const int mcu = j / bpm, b = j - mcu * bpm;
+  const int c = in.mcu_comp[b];
+  const int mx = mcu % in.mcux, my = mcu / in.mcux;
+  int bx, by;
+  if (in.ncomp == 1) {
+    bx = mx;
+    by = my;
+  } else {
+    bx = mx * in.comp_h[c] + in.mcu_dx[b];
+    by = my * in.comp_v[c] + in.mcu_dy[b];
+  }
+  int32_t px[64];
+  idct_list_block<IDCT>(ents, bdesc[(size_t)dd.coef_off + j], dd.coef_off, in.nblocks,
+                        sblk[threadIdx.x], px);
   const int stride = dd.plane_stride[c];
   uint8_t* dst = planes + dd.plane_off[c] + (size_t)by * 8 * stride + bx * 8;
 #pragma unroll
@@ -3273,13 +3281,77 @@ __device__ __forceinline__ void rgbu_store(uint8_t* p, const uint32_t* w) {
   }
 }
 
+// One group of PX pixels of output row y (columns x0 .. x0 + npx) from its
+// luma words yw and chroma words uw / vw (x0 / 2 onwards): the table
+// arithmetic of yuv2rgb_c_24_rgb, then vector stores where aligned.
+template <int PX>
+__device__ __forceinline__ void rgbu_group(const uint32_t (&yw)[PX / 4], const uint32_t (&uw)[PX / 8],
+                                           const uint32_t (&vw)[PX / 8], uint8_t* __restrict__ base,
+                                           const int64_t pl, const int w, const int y, const int x0,
+                                           const int npx, const BatchParams& p, const bool planar,
+                                           const bool swap) {
+  constexpr int SW = PX / 4;  // words per vector store
+  uint32_t c0[PX], c1[PX], c2[PX];
+#pragma unroll
+  for (int i = 0; i < PX; i++) {
+    const int Y = (int)((yw[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+    const int U = (int)((uw[i >> 3] >> (8 * ((i >> 1) & 3))) & 0xFFu);
+    const int V = (int)((vw[i >> 3] >> (8 * ((i >> 1) & 3))) & 0xFFu);
+    const int r = clip_i8(Y + tab_off(p.crv, V));
+    const int gg = clip_i8(Y + tab_off(p.cgu, U) + tab_off(p.cgv, V));
+    const int b = clip_i8(Y + tab_off(p.cbu, U));
+    c0[i] = (uint32_t)(swap ? b : r);
+    c1[i] = (uint32_t)gg;
+    c2[i] = (uint32_t)(swap ? r : b);
+  }
+  if (!planar) {
+    uint8_t* o = base + ((int64_t)y * w + x0) * 3;
+    if (npx == PX && ((uintptr_t)o & (4u * SW - 1u)) == 0u) {  // 3 PX bytes: three stores
+      uint32_t wv[3 * PX / 4];
+#pragma unroll
+      for (int k = 0; k < 3 * PX / 4; k++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int q = 4 * k + j, i = q / 3, c = q % 3;
+          v |= (c == 0 ? c0[i] : c == 1 ? c1[i] : c2[i]) << (8 * j);
+        }
+        wv[k] = v;
+      }
+#pragma unroll
+      for (int s3 = 0; s3 < 3; s3++) rgbu_store<SW>(o + 4 * SW * s3, wv + SW * s3);
+    } else {
+      for (int i = 0; i < npx; i++) {
+        o[3 * i] = (uint8_t)c0[i];
+        o[3 * i + 1] = (uint8_t)c1[i];
+        o[3 * i + 2] = (uint8_t)c2[i];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const uint32_t* cv = c == 0 ? c0 : c == 1 ? c1 : c2;
+      uint8_t* o = base + c * pl + (int64_t)y * w + x0;
+      if (npx == PX && ((uintptr_t)o & (4u * SW - 1u)) == 0u) {
+        uint32_t wv[SW];
+#pragma unroll
+        for (int k = 0; k < SW; k++)
+          wv[k] = cv[4 * k] | cv[4 * k + 1] << 8 | cv[4 * k + 2] << 16 | cv[4 * k + 3] << 24;
+        rgbu_store<SW>(o, wv);
+      } else {
+        for (int i = 0; i < npx; i++) o[i] = (uint8_t)cv[i];
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) rgb_unscaled_kernel(const uint8_t* __restrict__ planes,
                                                            const ImageDesc* __restrict__ desc,
                                                            const ImageInfo* __restrict__ infos,
                                                            uint8_t* __restrict__ out,
                                                            const BatchParams p,
                                                            int32_t* __restrict__ host_status) {
-  constexpr int PX = kRgbPx, YW = PX / 4, CW = PX / 8, SW = PX / 4;  // SW: words per vector store
+  constexpr int PX = kRgbPx, YW = PX / 4, CW = PX / 8;
   const int img = blockIdx.y;
   const ImageInfo& in = infos[img];
   if (host_status && blockIdx.x == 0 && threadIdx.x == 0) host_status[img] = in.status;
@@ -3305,59 +3377,101 @@ __global__ void __launch_bounds__(256) rgb_unscaled_kernel(const uint8_t* __rest
     rgbu_load<YW>(y_pl + (int64_t)y * dd.plane_stride[0] + x0, yw);
     rgbu_load<CW>(u_pl + (int64_t)(y >> vsub) * dd.plane_stride[1] + (x0 >> 1), uw);
     rgbu_load<CW>(v_pl + (int64_t)(y >> vsub) * dd.plane_stride[2] + (x0 >> 1), vw);
-    uint32_t c0[PX], c1[PX], c2[PX];
+    rgbu_group<PX>(yw, uw, vw, base, pl, w, y, x0, npx, p, planar, swap);
+  }
+}
+
+// Full resolution, fused: one workgroup transforms a run of MCUs of one MCU
+// row into LDS (idct_list_block, the IDCT slots then reused as the plane
+// tile) and converts it with swscale's unscaled converter straight from LDS
+// (rgbu_group) -- the planes never go through HBM.  Standard 4:2:0 / 4:2:2
+// MCUs only (Y 2x2 or 2x1 blocks, then U, V 1x1: bpm 6 or 4); the host checks
+// the sampling (Layout::fuse_ok).  u8 output.
+template <int IDCT>
+__global__ void __launch_bounds__(256) idct_rgb_kernel(const uint32_t* __restrict__ ents,
+                                                       const uint2* __restrict__ bdesc,
+                                                       const ImageDesc* __restrict__ desc,
+                                                       const ImageInfo* __restrict__ infos,
+                                                       uint8_t* __restrict__ out,
+                                                       const BatchParams p,
+                                                       int32_t* __restrict__ host_status) {
+  __shared__ __attribute__((aligned(16))) uint32_t sblk[256][kBlkWords];
+  const int img = blockIdx.y, tid = threadIdx.x;
+  const ImageInfo& in = infos[img];
+  if (host_status && blockIdx.x == 0 && tid == 0) host_status[img] = in.status;
+  if (in.status != kOk) return;
+  const ImageDesc& dd = desc[img];
+  const int bpm = in.bpm;   // 6 or 4
+  const int tw = 256 / bpm;  // MCUs per tile
+  const int tiles_x = (in.mcux + tw - 1) / tw;
+  if ((int)blockIdx.x >= tiles_x * in.mcuy) return;
+  const int my = (int)blockIdx.x / tiles_x, mx0 = ((int)blockIdx.x - my * tiles_x) * tw;
+  const int nm = min(tw, in.mcux - mx0);
+  const int hy = 8 * in.comp_v[0];                    // luma rows of the MCU row: 16 or 8
+  const int ys = tw * 16, cs = tw * 8;                 // tile row strides (bytes)
+  const bool act = tid < nm * bpm;
+  const int m = tid / bpm, b = tid - m * bpm;
+  int32_t px[64];
+  if (act) {
+    const int j = (my * in.mcux + mx0 + m) * bpm + b;
+    idct_list_block<IDCT>(ents, bdesc[(size_t)dd.coef_off + j], dd.coef_off, in.nblocks, sblk[tid],
+                          px);
+  }
+  __syncthreads();  // every slot read: the tile takes their place
+  uint8_t* tl = reinterpret_cast<uint8_t*>(&sblk[0][0]);  // hy x ys luma, then 8 x cs U, V
+  uint8_t* tu = tl + hy * ys;
+  uint8_t* tv = tu + 8 * cs;
+  if (act) {
+    const int c = in.mcu_comp[b];
+    uint8_t* dst = c == 0 ? tl + in.mcu_dy[b] * 8 * ys + m * 16 + in.mcu_dx[b] * 8
+                          : (c == 1 ? tu : tv) + m * 8;
+    const int st = c == 0 ? ys : cs;
 #pragma unroll
-    for (int i = 0; i < PX; i++) {
-      const int Y = (int)((yw[i >> 2] >> (8 * (i & 3))) & 0xFFu);
-      const int U = (int)((uw[i >> 3] >> (8 * ((i >> 1) & 3))) & 0xFFu);
-      const int V = (int)((vw[i >> 3] >> (8 * ((i >> 1) & 3))) & 0xFFu);
-      const int r = clip_i8(Y + tab_off(p.crv, V));
-      const int gg = clip_i8(Y + tab_off(p.cgu, U) + tab_off(p.cgv, V));
-      const int b = clip_i8(Y + tab_off(p.cbu, U));
-      c0[i] = (uint32_t)(swap ? b : r);
-      c1[i] = (uint32_t)gg;
-      c2[i] = (uint32_t)(swap ? r : b);
-    }
-    if (!planar) {
-      uint8_t* o = base + ((int64_t)y * w + x0) * 3;
-      if (npx == PX && ((uintptr_t)o & (4u * SW - 1u)) == 0u) {  // 3 PX bytes: three stores
-        uint32_t wv[3 * PX / 4];
-#pragma unroll
-        for (int k = 0; k < 3 * PX / 4; k++) {
-          uint32_t v = 0;
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const int q = 4 * k + j, i = q / 3, c = q % 3;
-            v |= (c == 0 ? c0[i] : c == 1 ? c1[i] : c2[i]) << (8 * j);
-          }
-          wv[k] = v;
-        }
-#pragma unroll
-        for (int s3 = 0; s3 < 3; s3++) rgbu_store<SW>(o + 4 * SW * s3, wv + SW * s3);
-      } else {
-        for (int i = 0; i < npx; i++) {
-          o[3 * i] = (uint8_t)c0[i];
-          o[3 * i + 1] = (uint8_t)c1[i];
-          o[3 * i + 2] = (uint8_t)c2[i];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 3; c++) {
-        const uint32_t* cv = c == 0 ? c0 : c == 1 ? c1 : c2;
-        uint8_t* o = base + c * pl + (int64_t)y * w + x0;
-        if (npx == PX && ((uintptr_t)o & (4u * SW - 1u)) == 0u) {
-          uint32_t wv[SW];
-#pragma unroll
-          for (int k = 0; k < SW; k++)
-            wv[k] = cv[4 * k] | cv[4 * k + 1] << 8 | cv[4 * k + 2] << 16 | cv[4 * k + 3] << 24;
-          rgbu_store<SW>(o, wv);
-        } else {
-          for (int i = 0; i < npx; i++) o[i] = (uint8_t)cv[i];
-        }
-      }
+    for (int r = 0; r < 8; r++) {
+      uint2 v;
+      v.x = (uint32_t)px[8 * r] | ((uint32_t)px[8 * r + 1] << 8) | ((uint32_t)px[8 * r + 2] << 16) |
+            ((uint32_t)px[8 * r + 3] << 24);
+      v.y = (uint32_t)px[8 * r + 4] | ((uint32_t)px[8 * r + 5] << 8) |
+            ((uint32_t)px[8 * r + 6] << 16) | ((uint32_t)px[8 * r + 7] << 24);
+      *reinterpret_cast<uint2*>(dst + r * st) = v;
     }
   }
+  __syncthreads();
+  const int w = dd.ow, h = dd.oh;
+  const int x_base = mx0 * 16, y_base = my * hy;
+  const int cols = min(nm * 16, w - x_base), rows = min(hy, h - y_base);
+  const int ngr = (cols + 7) >> 3;
+  const int vsub = hy == 16 ? 1 : 0;
+  const bool planar = p.pix_fmt == 0 || p.pix_fmt == 1;
+  const bool swap = p.pix_fmt == 1 || p.pix_fmt == 3;
+  const int64_t pl = (int64_t)w * h;
+  uint8_t* base = out + dd.out_off;
+  for (int g = tid; g < ngr * rows; g += 256) {
+    const int r = g / ngr, xl = (g - r * ngr) * 8;
+    const uint2 yq = *reinterpret_cast<const uint2*>(tl + r * ys + xl);
+    const uint32_t yw[2] = {yq.x, yq.y};
+    const uint32_t uw[1] = {*reinterpret_cast<const uint32_t*>(tu + (r >> vsub) * cs + (xl >> 1))};
+    const uint32_t vw[1] = {*reinterpret_cast<const uint32_t*>(tv + (r >> vsub) * cs + (xl >> 1))};
+    rgbu_group<8>(yw, uw, vw, base, pl, w, y_base + r, x_base + xl, min(8, cols - xl), p, planar,
+                  swap);
+  }
+}
+
+hipError_t launch_idct_rgb(const uint32_t* ents, const uint2* bdesc, const ImageDesc* desc,
+                           const ImageInfo* infos, void* out, const BatchParams& p, int idct,
+                           int tiles, int n, int32_t* host_status, hipStream_t st) {
+  const dim3 grid(tiles, n);
+  uint8_t* o = static_cast<uint8_t*>(out);
+  if (idct == 2)  // timing ablation (debug_mask 0x800)
+    hipLaunchKernelGGL(idct_rgb_kernel<2>, grid, dim3(256), 0, st, ents, bdesc, desc, infos, o, p,
+                       host_status);
+  else if (idct == 1)
+    hipLaunchKernelGGL(idct_rgb_kernel<1>, grid, dim3(256), 0, st, ents, bdesc, desc, infos, o, p,
+                       host_status);
+  else
+    hipLaunchKernelGGL(idct_rgb_kernel<0>, grid, dim3(256), 0, st, ents, bdesc, desc, infos, o, p,
+                       host_status);
+  return hipGetLastError();
 }
 
 hipError_t launch_rgb_unscaled(const uint8_t* planes, const ImageDesc* desc,

@@ -238,7 +238,7 @@ def test_subsequence_sizes(oracle, sub_bits, threads):
 @pytest.mark.parametrize("w,h", [(64, 48), (102, 70), (30, 18)])
 def test_fullres_batch_unscaled_converter(decoder, oracle, pix_fmt, w, h):
     """Full-resolution batches: 420 / 422 images of one size take swscale's
-    unscaled converter (rgb_unscaled_kernel); adding a 444 image sends the
+    unscaled converter (idct_rgb_kernel); adding a 444 image sends the
     batch through the generic sws_kernel.  Both bit-exact vs the oracle."""
     datas = [cases._enc(cases._noise(s, h, w), quality=85 + s, subsampling=2 if s % 2 else 1)
              for s in range(5)]
@@ -250,14 +250,19 @@ def test_fullres_batch_unscaled_converter(decoder, oracle, pix_fmt, w, h):
                                           strict=True)
 
 
-def test_fullres_unscaled_converter_matches_generic(decoder):
-    """The unscaled converter and the generic swscale kernel (debug_mask
-    0x80000 forces it) agree byte for byte on a 480x640 420 batch."""
-    datas = [cases._enc(cases._noise(s, 480, 640), quality=90, subsampling=2) for s in range(4)]
-    fast = _decode(decoder, datas, Output(pix_fmt="rgb24"), (480, 640, 3))
-    decoder.set_param("debug_mask", 0x80000)
-    try:
-        generic = _decode(decoder, datas, Output(pix_fmt="rgb24"), (480, 640, 3))
-    finally:
-        decoder.set_param("debug_mask", 0)
-    assert torch.equal(fast, generic)
+@pytest.mark.parametrize("sub,h,w", [(2, 480, 640), (1, 480, 640), (2, 1080, 1920), (1, 46, 1350)])
+def test_fullres_unscaled_paths_agree(decoder, sub, h, w):
+    """Full-resolution u8 output three ways agree byte for byte: the fused
+    IDCT + converter (idct_rgb_kernel, default), IDCT then rgb_unscaled_kernel
+    (debug_mask 0x100000) and the generic sws_kernel (0x80000)."""
+    datas = [cases._enc(cases._noise(s, h, w), quality=90, subsampling=sub) for s in range(3)]
+    fused = _decode(decoder, datas, Output(pix_fmt="rgb24"), (h, w, 3))
+    outs = []
+    for mask in (0x100000, 0x80000):
+        decoder.set_param("debug_mask", mask)
+        try:
+            outs.append(_decode(decoder, datas, Output(pix_fmt="rgb24"), (h, w, 3)))
+        finally:
+            decoder.set_param("debug_mask", 0)
+    assert torch.equal(fused, outs[0])
+    assert torch.equal(fused, outs[1])
