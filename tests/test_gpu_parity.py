@@ -266,3 +266,15 @@ def test_fullres_unscaled_paths_agree(decoder, sub, h, w):
             decoder.set_param("debug_mask", 0)
     assert torch.equal(fused, outs[0])
     assert torch.equal(fused, outs[1])
+
+
+@pytest.mark.parametrize("name", cases.LARGE_PROGRESSIVE)
+def test_fullres_large_progressive(decoder, oracle, name):
+    """Large progressive images at full resolution: the multiscan decoder's
+    lists through the fused IDCT + converter, bit-exact vs the oracle."""
+    d = cases.case(name)
+    info = oracle.parse(d)
+    hyp = _decode(decoder, [d, d], Output(pix_fmt="rgb24"), (info.height, info.width, 3)).numpy()
+    ref = oracle.decode_rgb(d, oracle.IDCT_SIMPLE, "rgb24")
+    for i in range(2):
+        np.testing.assert_array_equal(hyp[i], ref, strict=True)
