@@ -261,7 +261,11 @@ const char* spdl_hj_stage_name(int32_t i);
  * streams, each ordered after the caller's stream at submission; completion
  * is then observed through the ticket -- spdl_hj_wait / spdl_hj_stream_wait
  * -- not by the caller's stream; each lane wants a hardware queue of its own,
- * GPU_MAX_HW_QUEUES >= N + 2). */
+ * GPU_MAX_HW_QUEUES >= N + 2), "debug_mask" (diagnostics only, 0 in
+ * production: bits that skip kernel phases for timing ablations -- outputs
+ * wrong -- or select an equivalent slower path for A/B and tests:
+ * 0x80000 generic swscale kernel at full resolution, 0x100000 separate IDCT
+ * and unscaled converter instead of the fused kernel). */
 int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value);
 
 #ifdef __cplusplus
