@@ -63,6 +63,13 @@ constexpr int kSubBits = 16 - kLutBits;
 #define HJ_SUB_POOL 2048
 #endif
 constexpr int kSubPool = HJ_SUB_POOL;  // entropy LDS entries for the second-level tables of a scan
+
+// idct_rgb_kernel workgroup size: one block per thread, so a tile is
+// kFusedThreads / bpm MCUs of one MCU row (host and kernel agree on it)
+#ifndef HJ_FUSED_THREADS
+#define HJ_FUSED_THREADS 256
+#endif
+constexpr int kFusedThreads = HJ_FUSED_THREADS;
 constexpr int kMaxSub = 16;        // 64-entry sub-tables per Huffman table
 constexpr int kEntHiShift = 21;    // value / sub-table index field
 

@@ -600,7 +600,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     // idct_rgb_kernel's MCU shapes: Y 2x2 or 2x1, U and V 1x1
     if (p.ncomp == 3 && p.h_samp[0] == 2 && (p.v_samp[0] == 1 || p.v_samp[0] == 2) &&
         p.h_samp[1] == 1 && p.v_samp[1] == 1 && p.h_samp[2] == 1 && p.v_samp[2] == 1) {
-      const int bpm = 2 * p.v_samp[0] + 2, tw = 256 / bpm;
+      const int bpm = 2 * p.v_samp[0] + 2, tw = kFusedThreads / bpm;
       const int mcux = (p.width + 15) / 16, mcuy = (p.height + 8 * p.v_samp[0] - 1) / (8 * p.v_samp[0]);
       L.fused_tiles = std::max(L.fused_tiles, (mcux + tw - 1) / tw * mcuy);
     } else {

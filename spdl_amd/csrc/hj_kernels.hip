@@ -3388,21 +3388,21 @@ __global__ void __launch_bounds__(256) rgb_unscaled_kernel(const uint8_t* __rest
 // MCUs only (Y 2x2 or 2x1 blocks, then U, V 1x1: bpm 6 or 4); the host checks
 // the sampling (Layout::fuse_ok).  u8 output.
 template <int IDCT>
-__global__ void __launch_bounds__(256) idct_rgb_kernel(const uint32_t* __restrict__ ents,
+__global__ void __launch_bounds__(kFusedThreads) idct_rgb_kernel(const uint32_t* __restrict__ ents,
                                                        const uint2* __restrict__ bdesc,
                                                        const ImageDesc* __restrict__ desc,
                                                        const ImageInfo* __restrict__ infos,
                                                        uint8_t* __restrict__ out,
                                                        const BatchParams p,
                                                        int32_t* __restrict__ host_status) {
-  __shared__ __attribute__((aligned(16))) uint32_t sblk[256][kBlkWords];
+  __shared__ __attribute__((aligned(16))) uint32_t sblk[kFusedThreads][kBlkWords];
   const int img = blockIdx.y, tid = threadIdx.x;
   const ImageInfo& in = infos[img];
   if (host_status && blockIdx.x == 0 && tid == 0) host_status[img] = in.status;
   if (in.status != kOk) return;
   const ImageDesc& dd = desc[img];
   const int bpm = in.bpm;   // 6 or 4
-  const int tw = 256 / bpm;  // MCUs per tile
+  const int tw = kFusedThreads / bpm;  // MCUs per tile
   const int tiles_x = (in.mcux + tw - 1) / tw;
   if ((int)blockIdx.x >= tiles_x * in.mcuy) return;
   const int my = (int)blockIdx.x / tiles_x, mx0 = ((int)blockIdx.x - my * tiles_x) * tw;
@@ -3446,7 +3446,7 @@ __global__ void __launch_bounds__(256) idct_rgb_kernel(const uint32_t* __restric
   const bool swap = p.pix_fmt == 1 || p.pix_fmt == 3;
   const int64_t pl = (int64_t)w * h;
   uint8_t* base = out + dd.out_off;
-  for (int g = tid; g < ngr * rows; g += 256) {
+  for (int g = tid; g < ngr * rows; g += kFusedThreads) {
     const int r = g / ngr, xl = (g - r * ngr) * 8;
     const uint2 yq = *reinterpret_cast<const uint2*>(tl + r * ys + xl);
     const uint32_t yw[2] = {yq.x, yq.y};
@@ -3463,13 +3463,13 @@ hipError_t launch_idct_rgb(const uint32_t* ents, const uint2* bdesc, const Image
   const dim3 grid(tiles, n);
   uint8_t* o = static_cast<uint8_t*>(out);
   if (idct == 2)  // timing ablation (debug_mask 0x800)
-    hipLaunchKernelGGL(idct_rgb_kernel<2>, grid, dim3(256), 0, st, ents, bdesc, desc, infos, o, p,
+    hipLaunchKernelGGL(idct_rgb_kernel<2>, grid, dim3(kFusedThreads), 0, st, ents, bdesc, desc, infos, o, p,
                        host_status);
   else if (idct == 1)
-    hipLaunchKernelGGL(idct_rgb_kernel<1>, grid, dim3(256), 0, st, ents, bdesc, desc, infos, o, p,
+    hipLaunchKernelGGL(idct_rgb_kernel<1>, grid, dim3(kFusedThreads), 0, st, ents, bdesc, desc, infos, o, p,
                        host_status);
   else
-    hipLaunchKernelGGL(idct_rgb_kernel<0>, grid, dim3(256), 0, st, ents, bdesc, desc, infos, o, p,
+    hipLaunchKernelGGL(idct_rgb_kernel<0>, grid, dim3(kFusedThreads), 0, st, ents, bdesc, desc, infos, o, p,
                        host_status);
   return hipGetLastError();
 }
