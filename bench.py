@@ -25,17 +25,15 @@ import os
 import sys
 import time
 
-# Each pipeline lane is a HIP stream of its own, beside the copy stream and
-# torch's: with HIP's default of 4 hardware queues per process, three or more
-# lanes share queues and serialise (measured: 4 lanes 348k img/s with 4
-# queues, 439k with 16).  Must be set before HIP initialises.
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(16, int(os.environ.get("GPU_MAX_HW_QUEUES") or 0)))
-
-import numpy as np
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+# spdl_amd first: it exports GPU_MAX_HW_QUEUES (one hardware queue per
+# pipeline lane) before torch can initialise HIP
+import spdl_amd  # noqa: E402,F401
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 from spdl_amd import _lib  # noqa: E402
 from spdl_amd._lib import Output  # noqa: E402
@@ -51,10 +49,13 @@ from spdl_amd.synthetic import synthetic_slice  # noqa: E402
 
 METRIC = "images/sec device-resident JPEG→RGB224, 1/2/4/8×MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# Per-launch HBM-side bytes per kernel from the committed rocprofv3 --pmc
-# passes of this same command (tools/pmc_passes.sh + tools/pmc_traffic.py):
-# FETCH_SIZE / WRITE_SIZE cannot be read from inside the timed process.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_v7", "traffic.json")
+# Per-launch HBM-side bytes and SQ issue/wait shares per kernel from the
+# committed rocprofv3 --pmc passes of this same command (tools/pmc_round.sh:
+# tools/pmc_traffic.py, tools/pmc_issue.py): counters cannot be read from
+# inside the timed process.
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
+PMC_TRAFFIC = os.path.join(PROFILE_DIR, "traffic.json")
+PMC_ISSUE = os.path.join(PROFILE_DIR, "issue.json")
 # bench stage -> kernels launched in it
 STAGE_KERNELS = {
     "parse": ["hj::parse_kernel"],
@@ -65,22 +66,29 @@ STAGE_KERNELS = {
 }
 
 
-def _pmc_traffic(stage: str, batch: int):
-    """HBM bytes per launch of `stage`'s kernels from the committed PMC
-    summary (None when absent or recorded for another batch size)."""
+def _pmc(path: str, stage: str, batch: int) -> dict | None:
+    """The committed PMC record of `stage`'s kernel(s) for this batch size
+    (None when absent or recorded for another batch size)."""
     try:
-        with open(PMC_TRAFFIC) as f:
+        with open(path) as f:
             rec = json.load(f)
     except OSError:
         return None
     if rec.get("batch") not in (None, batch):
         return None
-    tot, hit = 0, False
-    for name, v in rec["kernels"].items():
-        if any(name.startswith(k) for k in STAGE_KERNELS.get(stage, [])):
-            tot += v["traffic_bytes"]  # already per dispatch (tools/pmc_traffic.py)
-            hit = True
-    return int(tot) if hit else None
+    hits = [v for name, v in rec["kernels"].items()
+            if any(name.startswith(k) for k in STAGE_KERNELS.get(stage, []))]
+    return hits[0] if len(hits) == 1 else None
+
+
+def _limiter(issue: dict | None) -> str:
+    """What bounds the dominant kernel, from its SQ counters: the share of
+    wave time spent issuing VALU work vs waiting (tools/pmc_issue.py)."""
+    if not issue:
+        return "unmeasured (no PMC record for this configuration)"
+    return (f"latency/issue, not HBM: waves issue VALU {issue['valu_share']:.0%} and wait "
+            f"{issue['wait_share']:.0%} of their cycles ({issue['waves']} waves per launch, "
+            f"{issue['lds_conflict_per_lds_inst']:.1f} LDS bank-conflict cycles per LDS instruction)")
 
 
 BATCH = 256
@@ -119,7 +127,11 @@ def _args():
     p.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
                    help="extra decoder parameter (spdl_hj_set_param), for A/B runs")
     p.add_argument("--debug-mask", type=int, default=0,
-                   help="kernel phase ablations for timing (outputs are wrong; no oracle check)")
+                   help="kernel phase ablations for timing (outputs are wrong; no oracle check); "
+                        "needs a library built with -DHJ_ABLATIONS=1 (SPDL_AMD_LIB)")
+    p.add_argument("--lanes1-steps", type=int, default=20,
+                   help="synchronous one-lane batches timed for the dominant kernel's own "
+                        "duration (0: skip)")
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="run every rank on device 0 (a one-GPU rehearsal of the N-rank launch; "
                         "the record says so -- not a multi-GPU measurement)")
@@ -324,7 +336,12 @@ def main():
         k, v = kv.split("=", 1)
         dec.set_param(k, int(v))
     if a.debug_mask:
-        dec.set_param("debug_mask", a.debug_mask)
+        try:
+            dec.set_param("debug_mask", a.debug_mask)
+        except ValueError:
+            raise SystemExit("--debug-mask needs an HJ_ABLATIONS build of the library "
+                             "(make -C spdl_amd/csrc variant NAME=abl DEFS=-DHJ_ABLATIONS=1; "
+                             "SPDL_AMD_LIB=spdl_amd/lib/variants/libspdl_hipjpeg_abl.so)") from None
     if a.workload == "imagenet":
         spec = Output(**{**IMAGENET_SPEC.__dict__, "norm_dtype": a.norm_dtype})
         outs = [torch.empty((a.batch, 3, 224, 224), dtype=spec.torch_dtype, device=device)
@@ -383,6 +400,7 @@ def main():
     for t in pending:
         collect(t)
     torch.cuda.synchronize(device)
+    own = time.perf_counter() - t0
     barrier()
     torch.cuda.synchronize(device)
     elapsed = reduce_max(time.perf_counter() - t0)
@@ -404,6 +422,43 @@ def main():
     dom_s = kernels[dominant] / 1000.0
     achieved = launch_bytes / dom_s / 1e9
 
+    # The dominant kernel alone: with several lanes its launches share the CUs
+    # with the other lanes' kernels, so the per-launch time above is a shared
+    # wall time.  One lane, synchronous batches, the same HIP-event stages.
+    lanes1 = None
+    if a.lanes1_steps > 0 and not a.debug_mask:
+        dec1 = _lib.Decoder(device.index)
+        dec1.set_param("lanes", 1)
+        dec1.set_profiling(True)
+        acc = {}
+        for i in range(a.lanes1_steps + 2):
+            dec1.decode_batch_device(dev.data_ptr(), dev.numel(), offs, sizes, infos, spec,
+                                     out.data_ptr(), nbytes_out, stream=stream, sync=True)
+            if i >= 2:
+                for k, v in dec1.last_timings().items():
+                    acc[k] = acc.get(k, 0.0) + v
+        th1 = dec1.get_param("entropy_threads")
+        dec1.close()
+        ms1 = acc[dominant] / a.lanes1_steps / 1000.0
+        ach1 = launch_bytes / (ms1 / 1000.0) / 1e9
+        lanes1 = {"kernel_ms": round(ms1, 4), "achieved": round(ach1, 3),
+                  "frac": round(ach1 / HBM_PEAK_GBS, 6), "steps": a.lanes1_steps,
+                  "entropy_threads": th1}
+
+    # per-rank record: each rank's own rate and device (the driver's 8-GPU
+    # run shows N distinct devices working)
+    props = torch.cuda.get_device_properties(device)
+    mine = {"rank": rank, "device": device.index,
+            "pci_bus_id": getattr(props, "pci_bus_id", None),
+            "images_per_sec": round(a.batch * a.steps / own, 1)}
+    if world > 1:
+        import torch.distributed as dist
+
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    else:
+        ranks = [mine]
+
     copies = None
     if a.with_copies and rank == 0:
         host_out = torch.empty_like(out, device="cpu").pin_memory()
@@ -420,6 +475,13 @@ def main():
         threads = a.cpu_threads or _cpu_cores()["usable"]
         cpu = _cpu_baseline(datas, threads, a.cpu_images, a.cpu_images // 2, a.cpu_runs)
 
+    traffic = issue = None
+    if a.workload == "pad224" and a.lanes == 4:  # the configuration the PMC passes ran
+        traffic = _pmc(PMC_TRAFFIC, dominant, a.batch)
+        issue = _pmc(PMC_ISSUE, dominant, a.batch)
+        if traffic:
+            with open(PMC_TRAFFIC) as f:
+                traffic = {**traffic, "correction": json.load(f).get("correction", "")}
     if rank == 0:
         value = world * a.batch * a.steps / elapsed
         rec = {
@@ -444,24 +506,35 @@ def main():
                 "distinct_images": a.distinct,
                 "parallelism": f"{world} ranks (one process per GPU), contiguous slices of the "
                                f"global batch, no collective on the data path",
-                "lanes": a.lanes,
+                "lanes": dec.get_param("lanes"),
+                "hw_queues": dec.get_param("hw_queues"),
+                "entropy_threads": dec.get_param("entropy_threads"),
                 **({"rehearsal": f"{world} ranks sharing ONE GPU (launch-path check, not a "
                                  f"multi-GPU rate)"} if a.rehearse_one_gpu else {}),
             },
             "roofline": {
+                # the roofline the path is priced against (no MFMA work); what
+                # actually limits the kernel is `limiter`
                 "bound": "hbm",
                 "kernel": dominant,
                 "achieved": round(achieved, 3),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": _pmc_traffic(dominant, a.batch) if a.workload == "pad224" else None,
-                "traffic_source": f"{os.path.relpath(PMC_TRAFFIC, ROOT)} (rocprofv3 --pmc "
-                                  "FETCH_SIZE, WRITE_SIZE; separate passes; x1024, FETCH x2 gfx950)",
+                "traffic": traffic["traffic_bytes"] if traffic else None,
+                "traffic_source": (f"{os.path.relpath(PMC_TRAFFIC, ROOT)}: "
+                                   f"{traffic['correction']}") if traffic else None,
                 "algorithmic_bytes_per_image": round(per_image_bytes, 1),
+                "launch_images": a.batch,
+                "formula": "achieved = algorithmic_bytes_per_image x launch_images / mean "
+                           "HIP-event duration of the kernel's launches in the timed steps",
+                "limiter": _limiter(issue),
+                "pipeline_GBps": round(launch_bytes / (elapsed / a.steps) / 1e9, 3),
+                "lanes1": lanes1,
             },
             "stages_ms": {k: round(v, 4) for k, v in stages_ms.items()},
             "oracle_check": checked,
+            "ranks": ranks,
             "cpu_baseline": cpu,
         }
         if copies is not None:

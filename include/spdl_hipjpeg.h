@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SPDL_HJ_ABI_VERSION 2
+#define SPDL_HJ_ABI_VERSION 3
 
 enum spdl_hj_status {
   SPDL_HJ_OK = 0,
@@ -146,15 +146,15 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
                                 size_t errlen);
 
 /* ---- asynchronous submission and the pinned staging ring ----------------
- * A context owns a ring of 3 slots (pinned staging + device copy of the
+ * A context owns a ring of 10 slots (pinned staging + device copy of the
  * JPEG bytes + descriptor/status staging).  Every decode call takes the next
  * slot; a call with sync == 0 returns once the batch is enqueued: the H2D copy
  * runs on the context's own copy stream and `stream` waits for it, so the host
  * can pack batch k+1 and its copy can run while batch k's kernels execute
  * (the reference copies synchronously: transfer_buffer_impl,
  * src/libspdl/cuda/transfer.cpp:37-67; transfer_tensor's pinned cache,
- * src/spdl/io/_transfer.py:82-177).  A slot is reused 3 submissions later, so
- * wait for a ticket before submitting 3 more batches or its statuses are lost. */
+ * src/spdl/io/_transfer.py:82-177).  A slot is reused 10 submissions later, so
+ * wait for a ticket before submitting 10 more batches or its statuses are lost. */
 
 /* Ticket of the most recent submission on `ctx` (0 if none). */
 int64_t spdl_hj_last_ticket(spdl_hj_ctx* ctx);
@@ -261,12 +261,19 @@ const char* spdl_hj_stage_name(int32_t i);
  * streams, each ordered after the caller's stream at submission; completion
  * is then observed through the ticket -- spdl_hj_wait / spdl_hj_stream_wait
  * -- not by the caller's stream; each lane wants a hardware queue of its own,
- * GPU_MAX_HW_QUEUES >= N + 2), "debug_mask" (diagnostics only, 0 in
- * production: bits that skip kernel phases for timing ablations -- outputs
- * wrong -- or select an equivalent slower path for A/B and tests:
- * 0x80000 generic swscale kernel at full resolution, 0x100000 separate IDCT
- * and unscaled converter instead of the fused kernel). */
+ * so the value is clamped to "hw_queues"; a lane's stream is created when
+ * first enabled), "hw_queues" (the hardware queues HIP gave this process:
+ * read from GPU_MAX_HW_QUEUES at spdl_hj_create, default 4; set it when HIP
+ * initialised before that variable was exported), "output_path" (0 = by
+ * batch, 1 = the generic swscale kernel, 2 = separate IDCT + unscaled
+ * converter at full resolution: byte-identical outputs, for A/B and tests).
+ * Builds with -DHJ_ABLATIONS=1 also take "debug_mask" (timing ablations that
+ * skip kernel phases; outputs wrong); release builds reject it. */
 int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value);
+
+/* Value in effect of a knob above (ABI 3), or of "copy_threads" (host
+ * threads packing pinned staging) / "device". */
+int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,7 @@ from dataclasses import dataclass
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPDL_AMD_LIB") or os.path.join(_HERE, "lib", "libspdl_hipjpeg.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # enums (mirror include/spdl_hipjpeg.h)
 PIX_FMTS = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
@@ -39,6 +39,7 @@ EXPORTED = (
     "spdl_hj_last_timings",
     "spdl_hj_stage_name",
     "spdl_hj_set_param",
+    "spdl_hj_get_param",
     "spdl_hj_debug_entropy",
     "spdl_hj_last_ticket",
     "spdl_hj_wait",
@@ -189,6 +190,7 @@ def lib() -> ctypes.CDLL:
         L.spdl_hj_stage_name.argtypes = [i32]
         L.spdl_hj_stage_name.restype = ctypes.c_char_p
         L.spdl_hj_set_param.argtypes = [vp, cp, ctypes.c_int64]
+        L.spdl_hj_get_param.argtypes = [vp, cp, ctypes.POINTER(ctypes.c_int64)]
         L.spdl_hj_debug_entropy.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, cp, sz]
         i64 = ctypes.c_int64
         L.spdl_hj_last_ticket.argtypes = [vp]
@@ -314,6 +316,10 @@ class Decoder:
             raise RuntimeError(f"spdl_amd: cannot create decoder: {err.value.decode()}")
         self._h = h
         self.device_index = int(device_index)
+        from . import HW_QUEUES, HW_QUEUES_LATE
+
+        if HW_QUEUES_LATE:  # HIP initialised before spdl_amd exported the variable
+            self.set_param("hw_queues", HW_QUEUES)
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -330,6 +336,12 @@ class Decoder:
         rc = lib().spdl_hj_set_param(self._h, name.encode(), int(value))
         if rc:
             raise ValueError(f"invalid decoder parameter {name}={value}")
+
+    def get_param(self, name: str) -> int:
+        v = ctypes.c_int64()
+        if lib().spdl_hj_get_param(self._h, name.encode(), ctypes.byref(v)):
+            raise ValueError(f"unknown decoder parameter {name}")
+        return int(v.value)
 
     def set_profiling(self, enable: bool) -> None:
         lib().spdl_hj_set_profiling(self._h, int(bool(enable)))

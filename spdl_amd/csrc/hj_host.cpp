@@ -11,6 +11,7 @@
 #include <sched.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
@@ -501,7 +502,11 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
                  int n, const spdl_hj_output* out, int sub_bits, Layout& L, int32_t* status,
                  char* err, size_t errlen, PlanCache* plans) {
   L.desc.assign(n, ImageDesc{});
-  std::map<const PackedPlan*, int64_t> placed;  // plan -> offset in L.tables
+  // plan -> offset in L.tables.  `alive` holds every placed plan until the
+  // layout is built: the cache may evict (and free) a plan mid-batch, and a
+  // new plan at a recycled address must not match a stale `placed` entry
+  std::map<const PackedPlan*, int64_t> placed;
+  std::vector<std::shared_ptr<const PackedPlan>> alive;
   auto fail = [&](int i, int rc, const char* what) {
     if (status) status[i] = rc;
     set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, what ? what : status_str(rc));
@@ -592,6 +597,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     auto it = placed.find(plan.get());
     if (it == placed.end()) {
       it = placed.emplace(plan.get(), (int64_t)L.tables.size()).first;
+      alive.push_back(plan);
       L.tables.insert(L.tables.end(), plan->blob.begin(), plan->blob.end());
     }
     d.wt_off = it->second;
@@ -656,13 +662,21 @@ struct spdl_hj_ctx {
   Slot slots[kSlots];
   int64_t next_ticket = 1;
   int64_t last_ticket = 0;
+  int lanes_ready = 0;                // workspaces [0, lanes_ready) have their event / stream
   hipStream_t copy = nullptr;         // H2D stream of the staging ring
-  CopyPool* pool = nullptr;
+  CopyPool* pool = nullptr;           // created on the first large host copy
+  // hardware queues HIP gives this process (GPU_MAX_HW_QUEUES when HIP
+  // initialised; 4 is HIP's default): each lane's stream wants one of its own
+  int hw_queues = 4;
+  // output kernels: 0 = by batch (fused IDCT + converter at full resolution
+  // when possible), 1 = the generic swscale kernel, 2 = separate IDCT +
+  // unscaled converter -- byte-identical outputs (tests compare them)
+  int output_path = 0;
   bool profiling = false;
   float timings[kStages] = {};
   int ntimings = 0;
   int sub_bits = 384;
-  int debug_mask = 0;
+  int debug_mask = 0;  // timing ablations, settable only in HJ_ABLATIONS builds
   // the first kernel pulls descriptors + tables from pinned memory and the
   // last writes statuses back (1), or DMA copies do it (0; kept for A/B)
   int host_staging = 1;
@@ -691,6 +705,26 @@ struct DeviceGuard {
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+// The copy pool is only needed by host-side packing of large batches; the
+// device-resident entry points never create it.
+CopyPool* copy_pool(spdl_hj_ctx* c) {
+  if (!c->pool) c->pool = new CopyPool(copy_workers());  // + the calling thread
+  return c->pool;
+}
+
+// Workspaces [0, n) get their completion event and (n > 1) their stream.
+bool ensure_lanes(spdl_hj_ctx* c, int n) {
+  DeviceGuard g(c->device);
+  for (int i = c->lanes_ready; i < n; i++) {
+    Workspace& w = c->ws[i];
+    if (!w.done && hipEventCreateWithFlags(&w.done, hipEventDisableTiming) != hipSuccess) return false;
+    if (!w.stream && hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess)
+      return false;
+    c->lanes_ready = i + 1;
+  }
+  return true;
+}
 
 #define HJ_HIP(expr)                                                                     \
   do {                                                                                   \
@@ -844,12 +878,12 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                             static_cast<uint2*>(W.bdesc.p), n, st));
   mark(ctx, slot, 4, st);
   // full resolution u8 through swscale's unscaled converter: IDCT and
-  // conversion in one kernel (debug_mask 0x80000: the generic sws_kernel,
-  // 0x100000: separate IDCT + rgb_unscaled_kernel)
+  // conversion in one kernel (output_path 1: the generic sws_kernel, 2:
+  // separate IDCT + rgb_unscaled_kernel)
   const int idct_kind = (ctx->debug_mask & 0x800) ? 2 : out->idct;
   const bool fast_rgb = swscale && L.all_special && out->dtype == SPDL_HJ_DTYPE_U8 &&
-                        !(ctx->debug_mask & 0x80000);
-  const bool fused = fast_rgb && L.fuse_ok && L.fused_tiles > 0 && !(ctx->debug_mask & 0x100000);
+                        ctx->output_path != 1;
+  const bool fused = fast_rgb && L.fuse_ok && L.fused_tiles > 0 && ctx->output_path != 2;
   if (!(ctx->debug_mask & 0x20000) && !fused)
     HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
                      static_cast<const uint2*>(W.bdesc.p), desc, infos,
@@ -1029,10 +1063,9 @@ spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen) {
   DeviceGuard g(device);
   auto* c = new spdl_hj_ctx();
   c->device = device;
+  if (const char* q = getenv("GPU_MAX_HW_QUEUES")) c->hw_queues = atoi(q) > 0 ? atoi(q) : 4;
   bool ok = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess;
-  for (int i = 0; ok && i < kMaxLanes; i++)
-    ok = hipEventCreateWithFlags(&c->ws[i].done, hipEventDisableTiming) == hipSuccess &&
-         hipStreamCreateWithFlags(&c->ws[i].stream, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && ensure_lanes(c, 1);
   for (int i = 0; ok && i < kSlots; i++)
     ok = hipEventCreateWithFlags(&c->slots[i].h2d_done, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->slots[i].done, hipEventDisableTiming) == hipSuccess &&
@@ -1044,7 +1077,6 @@ spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen) {
     spdl_hj_destroy(c);
     return nullptr;
   }
-  c->pool = new CopyPool(copy_workers());  // + the calling thread
   return c;
 }
 
@@ -1116,7 +1148,7 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
   rc = acquire_slot(ctx, &s, err, errlen);
   if (rc) return rc;
   HJ_HIP(s->pin_in.ensure((size_t)total));
-  parallel_pack(ctx->pool, static_cast<uint8_t*>(s->pin_in.p), items);
+  parallel_pack(copy_pool(ctx), static_cast<uint8_t*>(s->pin_in.p), items);
   hipStream_t xs;
   rc = exec_stream(ctx, *s, st, &xs, err, errlen);
   if (!rc) rc = stage_h2d(ctx, *s, (size_t)total, xs, err, errlen);
@@ -1209,7 +1241,7 @@ int spdl_hj_staging_fill(spdl_hj_ctx* ctx, int64_t ticket, size_t dst_off, const
     return SPDL_HJ_ERR_INVALID_ARG;
   }
   std::vector<CopyItem> items(1, CopyItem{(int64_t)dst_off, src, (int64_t)len, (int64_t)len});
-  parallel_pack(ctx->pool, static_cast<uint8_t*>(s->pin_in.p), items);
+  parallel_pack(copy_pool(ctx), static_cast<uint8_t*>(s->pin_in.p), items);
   return SPDL_HJ_OK;
 }
 
@@ -1236,8 +1268,8 @@ int spdl_hj_staging_read(spdl_hj_ctx* ctx, int64_t ticket, size_t dst_off, int f
       lo += (size_t)r;
     }
   };
-  if (len < (4u << 20) || ctx->pool->workers() < 2) body(0, 1);
-  else ctx->pool->run(body);
+  if (len < (4u << 20) || copy_pool(ctx)->workers() < 2) body(0, 1);
+  else copy_pool(ctx)->run(body);
   if (bad) {
     set_err(err, errlen, "pread failed or hit end of file (offset %lld, %zu bytes)",
             (long long)file_off, len);
@@ -1590,17 +1622,59 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
   }
   if (!strcmp(name, "lanes")) {  // concurrent pipelines (workspaces + streams)
     if (value < 1 || value > kMaxLanes) return SPDL_HJ_ERR_INVALID_ARG;
-    ctx->lanes = (int)value;
+    // lanes beyond the process's hardware queues would share queues and
+    // serialise: clamp (spdl_hj_get_param reports the lanes in effect)
+    const int lanes = std::min((int)value, std::max(1, ctx->hw_queues));
+    if (!ensure_lanes(ctx, lanes)) return SPDL_HJ_ERR_HIP;
+    ctx->lanes = lanes;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "hw_queues")) {  // the caller knows HIP initialised with another value
+    if (value < 1 || value > 32) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->hw_queues = (int)value;
+    if (ctx->lanes > ctx->hw_queues) ctx->lanes = ctx->hw_queues;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "output_path")) {  // equivalent output kernels (A/B and tests)
+    if (value < 0 || value > 2) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->output_path = (int)value;
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "host_staging")) {  // 1: kernels move descriptors / statuses; 0: DMA copies
     ctx->host_staging = value != 0;
     return SPDL_HJ_OK;
   }
+#if HJ_ABLATIONS
   if (!strcmp(name, "debug_mask")) {  // timing ablations only: output is wrong
     ctx->debug_mask = (int)value;
     return SPDL_HJ_OK;
   }
+#endif
+  return SPDL_HJ_ERR_INVALID_ARG;
+}
+
+int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
+  if (!ctx || !name || !value) return SPDL_HJ_ERR_INVALID_ARG;
+  const int ent = ctx->entropy_threads ? ctx->entropy_threads : (ctx->lanes > 1 ? 256 : 512);
+  const struct {
+    const char* n;
+    int64_t v;
+  } tab[] = {
+      {"sub_bits", ctx->sub_bits},
+      {"entropy_threads", ent},
+      {"warmup_slots", ctx->warm_slots >= 0 ? ctx->warm_slots : (ent <= 256 ? 6 : 12)},
+      {"lanes", ctx->lanes},
+      {"hw_queues", ctx->hw_queues},
+      {"output_path", ctx->output_path},
+      {"host_staging", ctx->host_staging},
+      {"copy_threads", ctx->pool ? ctx->pool->workers() : copy_workers() + 1},
+      {"device", ctx->device},
+  };
+  for (const auto& t : tab)
+    if (!strcmp(name, t.n)) {
+      *value = t.v;
+      return SPDL_HJ_OK;
+    }
   return SPDL_HJ_ERR_INVALID_ARG;
 }
 

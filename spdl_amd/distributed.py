@@ -15,6 +15,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 from collections.abc import Sequence
 from typing import TypeVar
 
@@ -67,9 +68,21 @@ def spawn_ranks(nprocs: int, argv: Sequence[str], master_port: int | None = None
         procs.append(subprocess.Popen([sys.executable, *argv], env=env))
     rc = 0
     try:
-        for p in procs:
-            code = p.wait()
-            rc = code if rc == 0 and code != 0 else rc
+        # poll every rank: the first one to fail ends the job, so a rank
+        # still blocked in a rendezvous or barrier with it does not hang
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0:
+                    rc = rc or code
+            if rc:
+                break
+            if live:
+                time.sleep(0.05)
     finally:
         for p in procs:
             if p.poll() is None:

@@ -11,6 +11,8 @@ All of them decode on the GPU (gfx950 kernels); there is no CPU path.
 from __future__ import annotations
 
 import logging
+import os
+import warnings
 from collections.abc import Sequence
 
 import numpy as np
@@ -42,6 +44,34 @@ def _read(src) -> memoryview:
 
 def _stream(cfg: CUDAConfig) -> int:
     return int(cfg.stream)
+
+
+def _default_config() -> CUDAConfig:
+    """The device a call without ``device_config`` decodes on: the current
+    HIP device once torch has initialised it (a rank that called
+    ``torch.cuda.set_device``), else ``$LOCAL_RANK`` (one process per GPU,
+    torch.distributed.run), else 0 -- never a hard-wired device 0 for every
+    rank of a job."""
+    if torch.cuda.is_initialized():
+        return CUDAConfig(torch.cuda.current_device())
+    rank = int(os.environ.get("LOCAL_RANK", "0") or 0)
+    count = torch.cuda.device_count()
+    return CUDAConfig(rank if 0 <= rank < count else 0)
+
+
+# FFmpeg demux / decoder options of the reference's CPU path.  The GPU
+# decoder has no equivalent knobs (its parser and decoder are fixed), so
+# they are accepted for drop-in compatibility and, when set, reported once.
+_IGNORED_WARNED: set = set()
+
+
+def _ignore_ffmpeg_configs(kwargs: dict) -> None:
+    for k in ("demux_config", "decode_config"):
+        v = kwargs.pop(k, None)
+        if v is not None and k not in _IGNORED_WARNED:
+            _IGNORED_WARNED.add(k)
+            warnings.warn(f"`{k}` configures FFmpeg's demuxer/decoder, which the GPU decode "
+                          f"stage does not use; it is ignored", RuntimeWarning, stacklevel=3)
 
 
 def _alloc_out(cfg: CUDAConfig, shape, dtype) -> CUDABuffer:
@@ -149,13 +179,25 @@ def load_image_batch_nvjpeg(
     )
 
 
-def _to_host(buf: CUDABuffer) -> CPUBuffer:
+def _to_host(buf: CUDABuffer, storage=None) -> CPUBuffer:
+    """Device result -> host buffer.  With ``storage`` (a :class:`CPUStorage`,
+    usually pinned) the bytes land in it, as the reference's convert_frames
+    writes the batch into the caller's storage
+    (src/spdl/io/_composite.py:368,460 -> src/libspdl/core/buffer.cpp:48-69,
+    which raises when the storage is too small)."""
     from ._convert import to_torch
+    from ._transfer import transfer_buffer_cpu
 
-    t = to_torch(buf).cpu()
-    if t.dtype == torch.bfloat16:  # numpy has no bfloat16: keep the bit patterns
-        return CPUBuffer(t.view(torch.int16).numpy().view(np.uint16), dtype=torch.bfloat16)
-    return CPUBuffer(t.numpy())
+    if storage is None:
+        t = to_torch(buf).cpu()
+        if t.dtype == torch.bfloat16:  # numpy has no bfloat16: keep the bit patterns
+            return CPUBuffer(t.view(torch.int16).numpy().view(np.uint16), dtype=torch.bfloat16)
+        return CPUBuffer(t.numpy())
+    nbytes = int(np.prod(buf.shape)) * (1 if buf.dtype == torch.uint8 else 2)
+    if storage.size < nbytes:
+        raise RuntimeError(
+            f"The provided storage does not have enough capacity. ({storage.size} < {nbytes})")
+    return transfer_buffer_cpu(buf, storage=storage)
 
 
 def load_image_batch(
@@ -176,22 +218,23 @@ def load_image_batch(
     """Batch load images into one ``[B,H,W,3]`` buffer with the FFmpeg filter
     semantics of the reference CPU path (scale + centred pad by default).
 
-    Decoding runs on ``device_config``'s GPU (device 0 when absent); without a
-    ``device_config`` the result is copied back to a host ``CPUBuffer``, like
-    the reference's return type.  ``normalize=True`` fuses the ImageNet
+    Decoding runs on ``device_config``'s GPU (when absent: the current HIP
+    device, or ``$LOCAL_RANK``); without a ``device_config`` the result is
+    copied back to a host ``CPUBuffer`` -- into ``storage`` when one is given
+    (a :func:`cpu_storage`), like the reference's return type.  ``normalize=True`` fuses the ImageNet
     epilogue ((x/255 - mean)/std in fp32 -> ``norm_dtype`` float16 or
     bfloat16), an extension for config 4."""
     if not srcs:
         raise ValueError("`srcs` must not be empty.")
-    for k in ("demux_config", "decode_config", "storage"):
-        kwargs.pop(k, None)
+    storage = kwargs.pop("storage", None)
+    _ignore_ffmpeg_configs(kwargs)
     if kwargs:
         raise TypeError(f"unexpected arguments: {sorted(kwargs)}")
     if filter_desc == _FILTER_DESC_DEFAULT:
         filter_desc = get_video_filter_desc(
             scale_width=width, scale_height=height, pix_fmt=pix_fmt
         )
-    cfg = device_config or CUDAConfig(0)
+    cfg = device_config or _default_config()
     if filter_desc is None:
         # no scale and no output format: the decoder's own planes, batched as
         # the reference's convert_frames stacks them ([B, 3, H, W] yuvj444p,
@@ -212,6 +255,10 @@ def load_image_batch(
         arr = np.stack(arrs)
         if device_config is not None:
             return CUDABuffer(torch.from_numpy(arr).to(f"cuda:{cfg.device_index}"))
+        if storage is not None:
+            from ._transfer import convert_array
+
+            return convert_array(arr, storage=storage)
         return CPUBuffer(arr)
     out = parse_image_filter(filter_desc, default_pix_fmt=pix_fmt or "rgb24")
     if normalize:
@@ -253,7 +300,10 @@ def load_image_batch(
 
         buf = CUDABuffer(torch.cat([to_torch(g) for g in good]), stream=cfg.stream)
     if device_config is None:
-        return _to_host(buf)
+        # the reference's CPU result, in the caller's storage when given (with
+        # a device_config the reference only stages through it on the way to
+        # the device; here the batch is decoded on the device directly)
+        return _to_host(buf, storage)
     return buf
 
 
@@ -300,11 +350,11 @@ def load_image(
     back to back: ``[1, 1.5H, W]`` yuvj420p, ``[1, 2H, W]`` yuvj422p,
     ``[3, H, W]`` yuvj444p, ``[H, W, 1]`` gray; see :func:`_native_planes`);
     otherwise RGB per the filter."""
-    for k in ("demux_config", "decode_config", "name"):
-        kwargs.pop(k, None)
+    kwargs.pop("name", None)  # only names the source in FFmpeg demux errors
+    _ignore_ffmpeg_configs(kwargs)
     if kwargs:
         raise TypeError(f"unexpected arguments: {sorted(kwargs)}")
-    cfg = device_config or CUDAConfig(0)
+    cfg = device_config or _default_config()
     data = _read(src)
     if filter_desc is None:
         dec = _lib.thread_decoder(cfg.device_index)

@@ -13,8 +13,12 @@ from __future__ import annotations
 
 from .._lib import Output
 
-_FILTERS = {"bicubic": "bicubic", "bilinear": "bilinear", "fast_bilinear": "bilinear",
-            "lanczos": "lanczos"}
+_FILTERS = {"bicubic": "bicubic", "bilinear": "bilinear", "lanczos": "lanczos"}
+# swscale's SWS_FAST_BILINEAR is its own horizontal scaler (7-bit position
+# fractions), not the bilinear filter: rather than silently return other
+# pixels, it is refused
+_NOT_IMPLEMENTED = {"fast_bilinear": "swscale's fast_bilinear scaler is not implemented; "
+                                     "use flags=bilinear (a different, exact bilinear filter)"}
 
 
 # scale_mode -> scale's force_original_aspect_ratio and the filter that
@@ -86,7 +90,7 @@ def parse_image_filter(filter_desc: str | None, default_pix_fmt: str = "rgb24") 
     spec = dict(pix_fmt=default_pix_fmt, resize=False)
     if not filter_desc:
         return Output(**spec)
-    have_scale = have_pad = False
+    have_scale = False
     for part in filter_desc.split(","):
         part = part.strip()
         if not part:
@@ -99,6 +103,8 @@ def parse_image_filter(filter_desc: str | None, default_pix_fmt: str = "rgb24") 
                 raise ValueError(f"negative scale sizes are not supported: {part}")
             spec.update(resize=True, fit_w=w, fit_h=h)
             flags = kv.get("flags", "bicubic")
+            if flags in _NOT_IMPLEMENTED:
+                raise ValueError(_NOT_IMPLEMENTED[flags])
             if flags not in _FILTERS:
                 raise ValueError(f"unsupported scale flags: {flags}")
             spec["filter"] = _FILTERS[flags]
@@ -120,7 +126,6 @@ def parse_image_filter(filter_desc: str | None, default_pix_fmt: str = "rgb24") 
             if kv.get("color", "black") != "black":
                 raise ValueError("only color=black is supported")
             spec.update(resize=True, pad_w=int(kv["w"]), pad_h=int(kv["h"]))
-            have_pad = True
         elif name == "crop":
             if "x" in kv or "y" in kv:
                 raise ValueError("only centred crop is supported")
@@ -132,5 +137,4 @@ def parse_image_filter(filter_desc: str | None, default_pix_fmt: str = "rgb24") 
             spec["pix_fmt"] = pf
         else:
             raise ValueError(f"filter `{name}` is not supported by the image decode stage")
-    del have_pad
     return Output(**spec)

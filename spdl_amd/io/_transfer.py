@@ -135,9 +135,11 @@ def transfer_buffer(buffer, *, device_config: CUDAConfig) -> CUDABuffer:
     return out
 
 
-def transfer_buffer_cpu(buffer) -> CPUBuffer:
+def transfer_buffer_cpu(buffer, *, storage: CPUStorage | None = None) -> CPUBuffer:
     """Move a C-contiguous device buffer (CUDABuffer, device tensor or any
-    ``__cuda_array_interface__`` object) to host memory."""
+    ``__cuda_array_interface__`` object) to host memory.  ``storage`` (an
+    extension: the reference always allocates) receives the bytes instead of
+    a fresh allocation; it must be large enough."""
     # the copy is issued on the stream the buffer was produced on (its
     # `stream`, or torch's current stream for a tensor) and that stream is
     # synchronised, so pending producers are ordered before it
@@ -160,12 +162,19 @@ def transfer_buffer_cpu(buffer) -> CPUBuffer:
     else:
         raise TypeError(f"expected a device buffer, found {type(buffer)}")
     host_dtype = torch.int16 if dtype == torch.bfloat16 else dtype
-    host = torch.empty(shape, dtype=host_dtype)
+    if storage is None:
+        host = torch.empty(shape, dtype=host_dtype)
+    else:
+        need = int(np.prod(shape)) * _itemsize(dtype)
+        if storage.size < need:
+            raise RuntimeError(f"The provided storage does not have enough capacity. "
+                               f"({storage.size} < {need})")
+        host = storage._tensor[:need].view(host_dtype).view(shape)
     nbytes = host.numel() * _itemsize(dtype)
     _copy(host.data_ptr(), ptr, nbytes, _D2H, dev, stream, True)
     if dtype == torch.bfloat16:
-        return CPUBuffer(host.numpy().view(np.uint16), dtype=torch.bfloat16)
-    return CPUBuffer(host.numpy())
+        return CPUBuffer(host.numpy().view(np.uint16), dtype=torch.bfloat16, storage=storage)
+    return CPUBuffer(host.numpy(), storage=storage)
 
 
 # ---- transfer_tensor: one coalesced pinned H2D per batch -----------------------
@@ -247,7 +256,12 @@ class _BatchMover:
             t = leaves[i].contiguous()
             nb = t.numel() * t.element_size()
             stage[o:o + nb].copy_(t.reshape(-1).view(torch.uint8))
-        dev = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{self.device}")
+        # allocate on the copy stream: the caching allocator then only hands
+        # out a block whose last use was ordered on this stream, never one a
+        # kernel queued on the default stream may still be reading or writing
+        # (the reference allocates under `with torch.cuda.stream(...)` too)
+        with torch.cuda.stream(self.stream):
+            dev = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{self.device}")
         _copy(dev.data_ptr(), stage.data_ptr(), total, _H2D, self.device,
               self.stream.cuda_stream, True)
         self.keep[slot] = dev

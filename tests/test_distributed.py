@@ -111,3 +111,19 @@ def test_bench_rejects_mismatched_world():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--dry-run"], cwd=root,
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
+
+
+def test_spawn_ranks_fails_fast_when_a_later_rank_dies(tmp_path):
+    """A rank > 0 that dies (e.g. in init_process_group) ends the job at once:
+    rank 0, blocked as if in a rendezvous, is killed instead of waited on."""
+    import time
+
+    from spdl_amd.distributed import spawn_ranks
+
+    script = tmp_path / "r.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "time.sleep(600) if r == 0 else sys.exit(3)\n")
+    t0 = time.perf_counter()
+    assert spawn_ranks(2, [str(script)]) == 3
+    assert time.perf_counter() - t0 < 60

@@ -254,16 +254,16 @@ def test_fullres_batch_unscaled_converter(decoder, oracle, pix_fmt, w, h):
 def test_fullres_unscaled_paths_agree(decoder, sub, h, w):
     """Full-resolution u8 output three ways agree byte for byte: the fused
     IDCT + converter (idct_rgb_kernel, default), IDCT then rgb_unscaled_kernel
-    (debug_mask 0x100000) and the generic sws_kernel (0x80000)."""
+    (output_path 2) and the generic sws_kernel (output_path 1)."""
     datas = [cases._enc(cases._noise(s, h, w), quality=90, subsampling=sub) for s in range(3)]
     fused = _decode(decoder, datas, Output(pix_fmt="rgb24"), (h, w, 3))
     outs = []
-    for mask in (0x100000, 0x80000):
-        decoder.set_param("debug_mask", mask)
+    for path in (2, 1):
+        decoder.set_param("output_path", path)
         try:
             outs.append(_decode(decoder, datas, Output(pix_fmt="rgb24"), (h, w, 3)))
         finally:
-            decoder.set_param("debug_mask", 0)
+            decoder.set_param("output_path", 0)
     assert torch.equal(fused, outs[0])
     assert torch.equal(fused, outs[1])
 

@@ -159,3 +159,74 @@ def test_product_never_imports_oracle():
         src = open(p, errors="ignore").read()
         code = re.sub(r"//[^\n]*|/\*.*?\*/", "", src, flags=re.S)  # comments may cite it
         assert "jpeg_oracle" not in code and not re.search(r"\bjo_[a-z_]+\(", code), p
+
+
+def test_fast_bilinear_is_refused_not_aliased():
+    """swscale's SWS_FAST_BILINEAR is a different scaler: refusing it beats
+    returning bilinear pixels under its name."""
+    from spdl_amd.io import parse_image_filter
+
+    with pytest.raises(ValueError, match="fast_bilinear"):
+        parse_image_filter("scale=w=224:h=224:flags=fast_bilinear")
+    assert parse_image_filter("scale=w=224:h=224:flags=bilinear").filter == "bilinear"
+
+
+def test_default_device_follows_local_rank(monkeypatch):
+    """Without device_config the decode device is the current HIP device or
+    $LOCAL_RANK -- never a hard-wired 0 for every rank of a job."""
+    import torch
+
+    from spdl_amd.io import _image
+
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    assert _image._default_config().device_index == 5
+    monkeypatch.setenv("LOCAL_RANK", "9")  # out of range: device 0
+    assert _image._default_config().device_index == 0
+    monkeypatch.delenv("LOCAL_RANK")
+    assert _image._default_config().device_index == 0
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 3)
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    assert _image._default_config().device_index == 3
+
+
+def test_ffmpeg_configs_are_reported_not_silently_dropped():
+    from spdl_amd.io import _image
+
+    _image._IGNORED_WARNED.clear()
+    kw = {"decode_config": object(), "demux_config": None}
+    with pytest.warns(RuntimeWarning, match="decode_config"):
+        _image._ignore_ffmpeg_configs(kw)
+    assert kw == {}
+
+
+def test_storage_too_small_raises_like_reference():
+    """load_image_batch(storage=...) writes the host result into the caller's
+    storage; a short one raises the reference's capacity error
+    (src/libspdl/core/buffer.cpp:56-62)."""
+    import torch
+
+    from spdl_amd.io import _image, cpu_storage
+    from spdl_amd.io._buffer import CUDABuffer
+
+    buf = CUDABuffer(None, ptr=1, shape=(2, 224, 224, 3), dtype=torch.uint8)
+    with pytest.raises(RuntimeError, match="does not have enough capacity"):
+        _image._to_host(buf, cpu_storage(100, pin_memory=False))
+
+
+def test_release_build_rejects_debug_mask():
+    """Timing-ablation knobs that break outputs exist only in HJ_ABLATIONS
+    builds; the shipped library refuses them (no context needed to check:
+    the name is rejected before the context is touched, so a NULL context
+    still returns INVALID_ARG for every name)."""
+    from spdl_amd import _lib
+
+    L = _lib.lib()
+    v = ctypes.c_int64()
+    assert L.spdl_hj_set_param(None, b"debug_mask", 1) == 8
+    assert L.spdl_hj_get_param(None, b"lanes", ctypes.byref(v)) == 8
+    src = open(os.path.join(ROOT, "spdl_amd", "csrc", "hj_host.cpp")).read()
+    i = src.index('"debug_mask"')
+    assert "#if HJ_ABLATIONS" in src[src.rindex("\n#", 0, i) - 40: i]
