@@ -450,7 +450,9 @@ def main():
     props = torch.cuda.get_device_properties(device)
     mine = {"rank": rank, "device": device.index,
             "pci_bus_id": getattr(props, "pci_bus_id", None),
-            "images_per_sec": round(a.batch * a.steps / own, 1)}
+            "slice": [sl.start, sl.stop],
+            "images_per_sec": round(a.batch * a.steps / own, 1),
+            "oracle_check": checked}
     if world > 1:
         import torch.distributed as dist
 

@@ -66,6 +66,10 @@ def _args():
                    help="batches in flight (= decode pipeline lanes), 1-8")
     p.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
                    help="extra decoder parameter (spdl_hj_set_param), for A/B runs")
+    p.add_argument("--sample-out", default="",
+                   help="write the first batch of the last timed pass (member names + "
+                        "--sample-images decoded images) to <sample-out>.r<rank>.npz")
+    p.add_argument("--sample-images", type=int, default=16)
     return p.parse_args()
 
 
@@ -110,10 +114,13 @@ def main():
         host = [torch.empty((a.batch, 224, 224, 3), dtype=torch.uint8).pin_memory()
                 for _ in range(2)] if a.d2h else None
         d2h_ev = [None, None]
+        sample = {}
 
         def one_pass():
             n, k = 0, 0
             for names, t in st:
+                if k == 0 and a.sample_out:  # outside the byte path: a view + names only
+                    sample["names"], sample["t"] = list(names), t
                 if d2h is not None:
                     j = k & 1
                     if d2h_ev[j] is not None:
@@ -143,8 +150,25 @@ def main():
         torch.cuda.synchronize(device)
         barrier()
         torch.cuda.synchronize(device)
-        elapsed = reduce_max(time.perf_counter() - t0)
+        own = time.perf_counter() - t0
+        elapsed = reduce_max(own)
         st.close()
+        mine = {"rank": rank, "device": device.index, "images": total,
+                "pci_bus_id": getattr(torch.cuda.get_device_properties(device), "pci_bus_id", None),
+                "images_per_sec": round(total / own, 1)}
+        if a.sample_out and sample:
+            import numpy as np
+
+            m = min(a.sample_images, sample["t"].shape[0])
+            np.savez(f"{a.sample_out}.r{rank}.npz", names=np.array(sample["names"][:m]),
+                     rgb=sample["t"][:m].cpu().numpy())
+        if world > 1:
+            import torch.distributed as dist
+
+            ranks = [None] * world
+            dist.all_gather_object(ranks, mine)
+        else:
+            ranks = [mine]
         if rank == 0:
             value = world * total / elapsed
             print(json.dumps({
@@ -174,6 +198,7 @@ def main():
                     "parallelism": f"{world} independent per-GPU archives, no collective",
                 },
                 "h2d_GBps_per_gpu": round(tar_bytes * a.passes / elapsed / 1e9, 3),
+                "ranks": ranks,
             }), flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

@@ -31,6 +31,8 @@ import time
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import asdict, dataclass
 
+import numpy as np
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -52,6 +54,9 @@ def _parse_args(argv=None):
     p.add_argument("--num-threads", type=int, default=4)
     p.add_argument("--buffer-size", type=int, default=16)
     p.add_argument("--num-workers", type=int, default=1)
+    p.add_argument("--sample-out", default="",
+                   help="write one decoded image of every batch (with its JPEG bytes) to "
+                        "<sample-out>.w<worker>.npz, for checking pixels after the run")
     p.add_argument("--worker-id", type=int, default=-1, help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
@@ -83,10 +88,19 @@ def worker(args) -> PerfResult:
     cfg = sio.cuda_config(device_index=args.worker_id)
     torch.zeros(1, device=f"cuda:{args.worker_id}")  # warm up the context
 
+    samples = {}
+
     def decode(paths):
         buf = sio.load_image_batch(paths, width=224, height=224, pix_fmt="rgb24",
                                    device_config=cfg, strict=False)
-        return sio.to_torch(buf)
+        t = sio.to_torch(buf)
+        if args.sample_out:  # one image per batch, a different position each time
+            k = len(samples) // 2
+            j = k % t.shape[0]
+            with open(paths[j], "rb") as f:
+                samples[f"jpeg_{k}"] = np.frombuffer(f.read(), np.uint8)
+            samples[f"rgb_{k}"] = t[j].cpu().numpy()
+        return t
 
     src = batches(source(args.input_flist, args.prefix, args.num_workers, args.worker_id),
                   args.batch_size)
@@ -105,7 +119,10 @@ def worker(args) -> PerfResult:
             frames += t.shape[0]
             nb += 1
     torch.cuda.synchronize(args.worker_id)
-    return PerfResult(time.monotonic() - t0, nb, frames)
+    elapsed = time.monotonic() - t0
+    if args.sample_out:
+        np.savez(f"{args.sample_out}.w{args.worker_id}.npz", **samples)
+    return PerfResult(elapsed, nb, frames)
 
 
 def _write_synthetic(n: int, root: str) -> str:
@@ -140,7 +157,7 @@ def main(argv=None) -> None:
         base = [sys.executable, os.path.abspath(__file__), "--input-flist", args.input_flist,
                 "--prefix", args.prefix, "--batch-size", str(args.batch_size),
                 "--num-threads", str(args.num_threads), "--buffer-size", str(args.buffer_size),
-                "--num-workers", str(args.num_workers)]
+                "--num-workers", str(args.num_workers), "--sample-out", args.sample_out]
         procs = [subprocess.Popen(base + ["--worker-id", str(i)], stdout=subprocess.PIPE,
                                   text=True) for i in range(args.num_workers)]
         vals = []

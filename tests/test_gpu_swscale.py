@@ -140,26 +140,32 @@ def bench_batch(oracle):
     return dev, np.asarray(offs, np.int64), np.asarray(sizes, np.int64), infos, refs
 
 
-@pytest.mark.parametrize("lanes", [1, 2])
-@pytest.mark.parametrize("warm", [0, 8, 64])
-def test_bench_path_bit_exact(bench_batch, lanes, warm):
+@pytest.mark.parametrize("lanes,inflight,warm", [
+    (1, 2, 0), (1, 2, 8), (1, 2, 64), (2, 2, 0), (2, 2, 8), (2, 2, 64),
+    (4, 6, -1),  # the driver's bench configuration: 4 lanes, lanes + 2 in flight
+])
+def test_bench_path_bit_exact(bench_batch, lanes, inflight, warm):
     """decode_batch_device exactly as bench.py drives it: async submissions,
-    two in flight on `lanes` pipelines, then every image of every batch
-    against the oracle."""
+    `inflight` batches in flight on `lanes` pipelines, then every image of
+    every batch against the oracle."""
     dev, offs, sizes, infos, refs = bench_batch
     dec = _lib.Decoder(0)
     dec.set_param("lanes", lanes)
-    dec.set_param("warmup_slots", warm)
+    assert dec.get_param("lanes") == lanes  # the box exports 16 hardware queues
+    if warm >= 0:
+        dec.set_param("warmup_slots", warm)
     spec = Output(pix_fmt="rgb24", resize=True, **PAD224)
-    outs = [torch.full((256, 224, 224, 3), 7, dtype=torch.uint8, device="cuda:0") for _ in range(3)]
+    nbatch = inflight + 2
+    outs = [torch.full((256, 224, 224, 3), 7, dtype=torch.uint8, device="cuda:0")
+            for _ in range(nbatch)]
     stream = torch.cuda.current_stream()
     tickets = []
-    for k in range(3):
+    for k in range(nbatch):
         o = outs[k]
         dec.decode_batch_device(dev.data_ptr(), dev.numel(), offs, sizes, infos, spec,
                                 o.data_ptr(), o.numel(), stream=stream, sync=False)
         tickets.append(dec.last_ticket())
-        if len(tickets) > 1:
+        if len(tickets) > inflight - 1:
             assert not any(dec.wait(tickets.pop(0), 256))
     for t in tickets:
         assert not any(dec.wait(t, 256))
