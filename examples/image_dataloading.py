@@ -27,6 +27,7 @@ import json
 import os
 import sys
 import tempfile
+import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import asdict, dataclass
@@ -88,18 +89,22 @@ def worker(args) -> PerfResult:
     cfg = sio.cuda_config(device_index=args.worker_id)
     torch.zeros(1, device=f"cuda:{args.worker_id}")  # warm up the context
 
-    samples = {}
+    samples, lock, nsamp = {}, threading.Lock(), [0]
 
     def decode(paths):
         buf = sio.load_image_batch(paths, width=224, height=224, pix_fmt="rgb24",
                                    device_config=cfg, strict=False)
         t = sio.to_torch(buf)
         if args.sample_out:  # one image per batch, a different position each time
-            k = len(samples) // 2
+            with lock:
+                k = nsamp[0]
+                nsamp[0] += 1
             j = k % t.shape[0]
             with open(paths[j], "rb") as f:
-                samples[f"jpeg_{k}"] = np.frombuffer(f.read(), np.uint8)
-            samples[f"rgb_{k}"] = t[j].cpu().numpy()
+                jpeg = np.frombuffer(f.read(), np.uint8)
+            rgb = t[j].cpu().numpy()
+            with lock:
+                samples[f"jpeg_{k}"], samples[f"rgb_{k}"] = jpeg, rgb
         return t
 
     src = batches(source(args.input_flist, args.prefix, args.num_workers, args.worker_id),
