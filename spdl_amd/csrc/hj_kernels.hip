@@ -675,28 +675,7 @@ __constant__ uint8_t kNatOrder[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32
                                       13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43,
                                       36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45,
                                       38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-#ifndef HJ_WIN_WORDS
-#define HJ_WIN_WORDS 8
-#endif
-#ifndef HJ_REG_READER
-#define HJ_REG_READER 0  // 1: register bit buffer with a read-ahead word (see dec_skip)
-#endif
-constexpr int kWinWords = HJ_WIN_WORDS;  // bit-reader window per thread (words)
-#ifndef HJ_WIN_ALIGN
-#define HJ_WIN_ALIGN 1
-#endif
-// window start: a multiple of HJ_WIN_ALIGN words (1: the word holding the
-// reader's position -- a full window of runway after every restage; the
-// 16-byte loads need only dword alignment)
-constexpr uint32_t kWinAlign = ~(uint32_t)(HJ_WIN_ALIGN - 1);
-
-
-#ifndef HJ_STAGE
-#define HJ_STAGE 0  // write-pass LDS staging line per run, entries (0: register packs; 16/32 measured 3%/15% slower)
-#endif
-__host__ __device__ constexpr int stage_entries(int nt) {
-  return HJ_STAGE == 0 ? 0 : (nt >= 1024 ? 8 : (nt >= 512 && HJ_STAGE > 16 ? 16 : HJ_STAGE));
-}
+constexpr int kWinWords = 8;  // bit-reader window per thread (words)
 
 // NTAB = distinct Huffman tables the workgroup holds in LDS: 4 covers luma +
 // chroma DC/AC (gray: 2) and keeps three entropy workgroups per CU; a scan
@@ -713,7 +692,6 @@ struct EntShared {
   uint32_t run_zb[NT];
   uint32_t qdc[kMaxComp];  // DC quantiser per component
   uint32_t qn[kMaxComp][64];  // per zig-zag index: natural index | quantiser << 16
-  int32_t tdc[kMaxBpm], tac[kMaxBpm], bcomp[kMaxBpm];
   // The bit-reader windows are dead outside round 0 / the sync rounds, so the
   // reduction and scan scratch share their storage (keeps the workgroup at
   // <= 80 KiB of LDS: two entropy workgroups -- e.g. of two concurrent
@@ -726,11 +704,6 @@ struct EntShared {
       int32_t red[NT];
     } sc;
   };
-  // write pass: each run's coefficient entries are staged here and leave as
-  // whole kStage-entry lines (partially written lines cost ~3x their bytes
-  // in HBM writes: many concurrently appending streams)
-  static constexpr int kStage = stage_entries(NT);
-  uint32_t stage[kStage > 0 ? kStage : 1][NT];
   int32_t flag;
   int32_t err;
   // tables past the NTAB LDS slots (5-6 distinct tables, rare): read from
@@ -740,7 +713,7 @@ struct EntShared {
 };
 static_assert(sizeof(EntShared<512, 4>) <= 160 * 1024 / 2,
               "entropy LDS must allow 2 workgroups per CU");
-static_assert(HJ_STAGE > 16 || sizeof(EntShared<256, 4>) <= 160 * 1024 / 3,
+static_assert(sizeof(EntShared<256, 4>) <= 160 * 1024 / 3,
               "entropy LDS must allow 3 workgroups per CU at 256 threads");
 
 // Per-thread bit reader over the destuffed stream (big-endian bytes read as
@@ -760,12 +733,6 @@ struct Dec {
   uint32_t pos;  // absolute bit position of the next symbol
   uint32_t z;    // next coefficient index (0 = DC)
   uint32_t bs;   // 2 * block-in-MCU
-#if HJ_REG_READER
-  uint64_t acc;  // the bits at pos, MSB-aligned (cnt of them valid)
-  uint32_t cnt;  // valid bits in acc (>= 32 between symbols)
-  uint32_t nw;   // absolute index of the next word to shift into acc
-  uint32_t pre;  // that word, read ahead from the LDS window
-#endif
 };
 
 __device__ __forceinline__ constexpr int win_slot(int i) { return kWinWords - 1 - i; }
@@ -788,67 +755,26 @@ __device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, 
   }
 }
 
-template <int NT>
-__device__ __forceinline__ uint32_t win_word(const uint32_t* win, uint32_t i) {  // window word i
-  return win[(kWinWords - 1 - (int)i) * NT];
-}
 
 template <int NT>
 __device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
                                          uint32_t z, uint32_t bs) {
-  d.wb = (p >> 5) & kWinAlign;
+  d.wb = p >> 5;  // the word holding the position: a full window of runway
   win_stage<NT>(win, words, d.wb);
   d.pos = p;
   d.z = z;
   d.bs = bs;
-#if HJ_REG_READER
-  const uint32_t w = (p >> 5) - d.wb;  // 0..3: words w, w + 1, w + 2 are in the window
-  const uint64_t two = ((uint64_t)win_word<NT>(win, w) << 32) | win_word<NT>(win, w + 1);
-  d.acc = two << (p & 31u);
-  d.cnt = 64u - (p & 31u);
-  d.nw = d.wb + w + 2;
-  d.pre = win_word<NT>(win, w + 2);
-#endif
 }
 
 // The 32 bits at d.pos, MSB-first.  Wave-uniform window restage: when any
 // active lane is about to read past its window, every active lane restages
 // from its own position, so the global load and its vmcnt wait happen once
 // per ~25 symbol steps of the wave.
-#if HJ_REG_READER
-// Register bit buffer: the symbol's bits are the top of acc (no LDS read on
-// the symbol chain).  Consuming bits shifts acc; when fewer than 32 remain the
-// read-ahead word is shifted in and the next one is read from the LDS window
-// (its latency overlaps the following symbols: LDS returns in order, so the
-// table lookup's wait covers it).  Wave-uniform window restage as below.
-template <int NT>
-__device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
-  return (uint32_t)(d.acc >> 32);
-}
-
-template <int NT>
-__device__ __forceinline__ void dec_skip(Dec& d, uint32_t* win, const uint32_t* words,
-                                         uint32_t nbits) {
-  d.pos += nbits;
-  d.acc <<= nbits;
-  d.cnt -= nbits;
-  const bool need = d.cnt < 32u;
-  d.acc |= need ? (uint64_t)d.pre << (32u - d.cnt) : 0ull;
-  d.cnt += need ? 32u : 0u;
-  d.nw += need ? 1u : 0u;
-  if (__any(d.nw - d.wb >= (uint32_t)kWinWords)) {
-    d.wb = d.nw & kWinAlign;
-    win_stage<NT>(win, words, d.wb);
-  }
-  d.pre = win_word<NT>(win, d.nw - d.wb);
-}
-#define HJ_DEC_SKIP(d, n) dec_skip<NT>(d, win, words, n)
-#else
 template <int NT>
 __device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
   uint32_t w = (d.pos >> 5) - d.wb;
   if (__any(w >= (uint32_t)(kWinWords - 1))) {
-    d.wb = (d.pos >> 5) & kWinAlign;
+    d.wb = d.pos >> 5;
     win_stage<NT>(win, words, d.wb);
     w = (d.pos >> 5) - d.wb;
   }
@@ -858,8 +784,6 @@ __device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32
 }
 
 __device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) { d.pos += nbits; }
-#define HJ_DEC_SKIP(d, n) dec_skip(d, n)
-#endif
 
 // Canonical decode of a code that is not fully resolved by the LUT (longer
 // than kLutBits, or a DC size > 15): returns a kKindCode entry, 0 if invalid.
@@ -931,7 +855,7 @@ __device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     // entry 0 (invalid) takes one bit, advances nothing and starts no block
     const uint32_t nbits = max(e & 31u, 1u);  // code + value bits, <= 31
     nblk += is_dc ? (int)__builtin_amdgcn_ubfe(e, 19, 1) : 0;  // DC: coef bit = valid
-    HJ_DEC_SKIP(d, nbits);
+    dec_skip(d, nbits);
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool bend = zn >= 64u;
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
@@ -955,7 +879,7 @@ __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32
     const uint32_t t = __builtin_amdgcn_ubfe(tmap, 9u + c * 3u, 3);
     const uint32_t e = lookup<SLOW>(S, t, hi, false);
     const uint32_t nbits = max(e & 31u, 1u);
-    HJ_DEC_SKIP(d, nbits);
+    dec_skip(d, nbits);
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool bend = zn >= 64u;
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
@@ -974,10 +898,6 @@ __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32
 // * 64; a block has at most 63 AC entries; the run's lists follow each other back to back),
 // so no buffer needs clearing and nothing is scattered: HBM sees ~4 bytes per
 // non-zero coefficient.
-#ifndef HJ_ENT_PACK
-#define HJ_ENT_PACK 4  // entries per store (1, 2 or 4; lists start 16-byte aligned)
-#endif
-[[maybe_unused]] constexpr uint32_t kEntPack = HJ_ENT_PACK;
 
 struct BlockOut {
   uint32_t* ents;
@@ -987,106 +907,33 @@ struct BlockOut {
   uint32_t bstart;  // first entry of the open block
   int dcv;          // its DC difference
   bool open;        // a block of this run is being decoded
-#if HJ_STAGE
-  uint32_t* stg;  // this run's LDS staging line (stride NT words)
-#else
-  uint32_t pk[kEntPack];  // entries not yet stored (kEntPack > 1)
-#endif
+  uint32_t pk[4];   // entries of the current 16-byte group not yet stored
 };
 
-#if HJ_STAGE
-// The staged line holding entry c leaves as kStage / 4 16-byte stores
-// (LDS reads strided by NT: conflict-free across the wave).
-template <int NT, int KS>
-__device__ __forceinline__ void flush_line(BlockOut& o, uint32_t c) {
-  static_assert(KS % 4 == 0 && 64 % KS == 0, "lines tile the 64-entry block regions");
-  const uint32_t base = min(c & ~(uint32_t)(KS - 1), o.last & ~(uint32_t)(KS - 1));
-  uint4* dst = reinterpret_cast<uint4*>(o.ents + base);
-#pragma unroll
-  for (int i = 0; i < KS / 4; i++)
-    dst[i] = make_uint4(o.stg[(4 * i) * NT], o.stg[(4 * i + 1) * NT], o.stg[(4 * i + 2) * NT],
-                        o.stg[(4 * i + 3) * NT]);
-}
-#endif
 
-#if !HJ_STAGE
 __device__ __forceinline__ void store_pack(BlockOut& o) {
-  const uint32_t base = min(o.cur & ~(kEntPack - 1u), o.last & ~(kEntPack - 1u));
-  char* a = reinterpret_cast<char*>(o.ents) + (base << 2);
-  if constexpr (kEntPack == 4)
-    *reinterpret_cast<uint4*>(a) = make_uint4(o.pk[0], o.pk[1], o.pk[2], o.pk[3]);
-  else if constexpr (kEntPack == 2)
-    *reinterpret_cast<uint2*>(a) = make_uint2(o.pk[0], o.pk[1]);
-  else
-    *reinterpret_cast<uint32_t*>(a) = o.pk[0];
+  const uint32_t base = min(o.cur & ~3u, o.last & ~3u);
+  *reinterpret_cast<uint4*>(o.ents + base) = make_uint4(o.pk[0], o.pk[1], o.pk[2], o.pk[3]);
 }
 
-#endif
-
-// entry e at o.cur (the caller advances o.cur)
-template <int NT>
+// entry e at o.cur (the caller advances o.cur); four entries per 16-byte store
 __device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e) {
-#if HJ_XP_NOENT
-  if (e == 0x12345u) o.ents[0] = e;
-#elif HJ_STAGE
-  constexpr int KS = stage_entries(NT);
-  const uint32_t k = o.cur & (uint32_t)(KS - 1);
-  o.stg[k * NT] = e;
-  if (k == (uint32_t)(KS - 1)) flush_line<NT, KS>(o, o.cur);
-#else
-  if constexpr (kEntPack == 1) {
-    *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(o.ents) + (min(o.cur, o.last) << 2)) = e;
-  } else {
-    const uint32_t k = o.cur & (kEntPack - 1u);
+  const uint32_t k = o.cur & 3u;
 #pragma unroll
-    for (uint32_t i = 0; i < kEntPack; i++) o.pk[i] = k == i ? e : o.pk[i];
-    if (k == kEntPack - 1u) store_pack(o);
-  }
-#endif
+  for (uint32_t i = 0; i < 4; i++) o.pk[i] = k == i ? e : o.pk[i];
+  if (k == 3u) store_pack(o);
 }
 
-template <int NT>
-#ifndef HJ_PACKED_LISTS
-#define HJ_PACKED_LISTS 1  // a run's lists back to back (0: each list 16-byte aligned)
-#endif
-
+// a run's lists go back to back: the next list continues the current group,
+// so a block end stores nothing but its descriptor (the run's last, partial
+// group leaves in flush_tail)
 __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
-#if HJ_PACKED_LISTS && !HJ_STAGE
-  // the next list continues the current pack: no store at the block end
-  // (the run's last, partial pack leaves in flush_tail)
   o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
-  o.open = false;
-  return;
-#endif
-  const uint32_t nc = (o.cur + 3u) & ~3u;  // the next list starts 16-byte aligned
-#if HJ_STAGE
-  constexpr int KS = stage_entries(NT);
-  // the list's padding completes the staged line: it leaves now
-  if ((o.cur & (uint32_t)(KS - 1)) != 0u && (nc & (uint32_t)(KS - 1)) == 0u)
-    flush_line<NT, KS>(o, o.cur);
-#else
-  if constexpr (kEntPack > 1) {
-    if (o.cur & (kEntPack - 1u)) store_pack(o);  // the partial pack (its tail is unused)
-  }
-#endif
-#if HJ_XP_NOBD
-  if (o.dcv == 0x12345) o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
-#else
-  o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
-#endif
-  o.cur = nc;
   o.open = false;
 }
 
-// the run's last, partial staged line
-template <int NT>
 __device__ __forceinline__ void flush_tail(BlockOut& o) {
-#if HJ_STAGE
-  constexpr int KS = stage_entries(NT);
-  if (o.cur & (uint32_t)(KS - 1)) flush_line<NT, KS>(o, o.cur);
-#elif HJ_PACKED_LISTS
-  if (o.cur & (kEntPack - 1u)) store_pack(o);
-#endif
+  if (o.cur & 3u) store_pack(o);
 }
 
 // Full decode from a synchronised state (z == 0: at a block start) of the
@@ -1124,18 +971,18 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
     const uint32_t msk = (1u << sz) - 1u;
     const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
-    HJ_DEC_SKIP(d, nbits);
+    dec_skip(d, nbits);
     const bool ac = coef & !is_dc;
     if (ac) {
       const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-      put_entry<NT>(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
+      put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
     }
     o.cur += ac ? 1u : 0u;
     o.bstart = is_dc ? o.cur : o.bstart;
     o.dcv = is_dc ? v : o.dcv;
     nb += is_dc ? 1 : 0;
     const bool bend = zn >= 64u;
-    if (bend) close_block<NT>(o, nb - 1);
+    if (bend) close_block(o, nb - 1);
     o.open = !bend;
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
     d.z = bend ? 0u : zn;
@@ -1154,7 +1001,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
     const uint32_t msk = (1u << sz) - 1u;
     const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
-    HJ_DEC_SKIP(d, nbits);
+    dec_skip(d, nbits);
     const uint32_t zinc = __builtin_amdgcn_ubfe(e, 12, 7);
     const bool coef = valid && ((e >> 19) & 1u);
     const bool bad = !valid || (coef && z + zinc > 64u) || ((e >> 20) & 1u);
@@ -1173,7 +1020,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     }
     if (wr && !is_dc) {
       const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-      put_entry<NT>(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
+      put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
       o.cur++;
     }
     nb += (wr && is_dc) ? 1 : 0;
@@ -1183,13 +1030,13 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     done = (bad && past_a) || stop || (trunc && past_b);
     rc = (bad && !past_a) ? kErrBadHuffman : ((trunc && !past_b) ? kErrTruncated : kOk);
     const bool bend = zn >= 64u;
-    if (bend && !stop && o.open) close_block<NT>(o, nb - 1);
+    if (bend && !stop && o.open) close_block(o, nb - 1);
     const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
   // the segment ended (or failed) inside a block: keep what it decoded
-  if (o.open && d.z != 0u) close_block<NT>(o, nb - 1);
+  if (o.open && d.z != 0u) close_block(o, nb - 1);
   return rc;
 }
 
@@ -1514,12 +1361,8 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       o.bstart = o.cur;
       o.dcv = 0;
       o.open = false;
-#if HJ_STAGE
-      o.stg = &S.stage[0][tid];
-#else
 #pragma unroll
-      for (uint32_t i = 0; i < kEntPack; i++) o.pk[i] = 0u;
-#endif
+      for (uint32_t i = 0; i < 4; i++) o.pk[i] = 0u;
       Dec d;
       for (int k = r0; k < r1 && rc == kOk; k++) {
         if (slot_empty(k)) {
@@ -1548,7 +1391,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
         if (rc == kOk && !done && last && (nb < seb || (nb == seb && d.z != 0)))
           rc = kErrTruncated;
       }
-      flush_tail<NT>(o);
+      flush_tail(o);
       if (rc != kOk) atomicCAS(&S.err, kOk, rc);
     }
     __syncthreads();
@@ -1631,12 +1474,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
 // decode loops; a wide one (parse_kernel's ent_wide) the loops that may read
 // HBM table copies and the canonical fallback.  One launch serves both.
 template <int NT, int NTAB>
-#ifdef HJ_ENT_VGPRS  // (occupancy experiments: cap the entropy kernel's VGPRs)
-#define HJ_ENT_ATTR __attribute__((amdgpu_waves_per_eu(HJ_ENT_VGPRS, 8)))
-#else
-#define HJ_ENT_ATTR
-#endif
-__global__ void __launch_bounds__(NT) HJ_ENT_ATTR entropy_kernel(const uint8_t* __restrict__ clean,
+__global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
                                                      const uint32_t* __restrict__ segs,
                                                      const ImageDesc* __restrict__ desc,
                                                      ImageInfo* __restrict__ infos,
@@ -1758,9 +1596,6 @@ struct MsWin {
   }
 };
 
-#ifndef HJ_MS_FILL
-#define HJ_MS_FILL 32  // bits the scan reader's buffer is topped up to
-#endif
 // Bit reader over stuffed entropy data: 0xFF00 -> 0xFF; any other marker (or
 // the scan end) stops the data, zeros follow (oracle bitrd_t).  Four plain
 // bytes (no 0xFF among them) enter the buffer at once.
@@ -1783,7 +1618,7 @@ struct MsBits {
   // one 4-byte step then suffices -- the byte path costs an LDS round trip
   // per byte)
   __device__ __forceinline__ void fill() {
-    while (cnt < HJ_MS_FILL) {
+    while (cnt < 32) {
       if (!marker && cnt <= 32 && pos + 4 <= end && pos + 4 <= src.lim) {
         const uint32_t v = src.be32(pos);
         if (((~v - 0x01010101u) & v & 0x80808080u) == 0u) {  // no 0xFF byte
@@ -2202,8 +2037,10 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
     S.err = kOk;
   }
   __syncthreads();
-  // ---- marker candidates: 0xFF followed by neither 0x00, 0xFF nor RSTn ----
-  for (int g = tid; g * 16 < size; g += nt) {
+  // ---- marker candidates: 0xFF followed by neither 0x00, 0xFF nor RSTn,
+  // from the first scan's data on (APPn payloads before it -- ICC profiles,
+  // EXIF, thumbnails -- are skipped by length and never end a scan) ----
+  for (int g = (in.scan_start >> 4) + tid; g * 16 < size; g += nt) {
     const int b = g * 16;
     uint32_t w[5];
     if (b + 20 <= size) {
@@ -2238,7 +2075,10 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
       }
       S.marks[j + 1] = v;
     }
-    int err = S.nmarks > kMsMaxMarks ? kErrUnsupported : kOk;
+    // more candidates than the list holds: find each scan's end by a forward
+    // search from its start instead
+    const bool overflow = S.nmarks > kMsMaxMarks;
+    int err = kOk;
     int* dht = S.dht;
     int* comp_id = S.comp_id;
     for (int t = 0; t < 8; t++) dht[t] = -1;
@@ -2316,11 +2156,21 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
         for (int t = 0; t < 8; t++) sc.dht[t] = dht[t];
         sc.start = seg_end;
         int e = size;  // the scan's data ends at the first marker past its start
-        for (int i = 0; i < nm; i++)
-          if (S.marks[i] >= seg_end) {
-            e = S.marks[i];
-            break;
+        if (!overflow) {
+          for (int i = 0; i < nm; i++)
+            if (S.marks[i] >= seg_end) {
+              e = S.marks[i];
+              break;
+            }
+        } else {
+          for (int i = seg_end; i + 1 < size; i++) {
+            const int nx = d[i + 1];
+            if (d[i] == 0xFF && nx != 0 && nx != 0xFF && (nx < 0xD0 || nx > 0xD7)) {
+              e = i;
+              break;
+            }
           }
+        }
         sc.end = e;
         pos = e;
         ns++;
@@ -2608,15 +2458,9 @@ hipError_t launch_multiscan(const uint8_t* bytes, const ImageDesc* desc, ImageIn
 #define HJ_IDCT_THREADS 256
 #endif
 constexpr int kIdctThreads = HJ_IDCT_THREADS;
-// HJ_IDCT_SPARSE 1: wave-uniform sparse transforms (below).  Off: on the
+// 0 1: wave-uniform sparse transforms (below).  Off: on the
 // bench images 468-470 k vs 474 k img/s (the four variants take 136 VGPRs,
 // or spill under a 4-waves/SIMD cap; r02_v7/ab_idct_sparse/)
-#ifndef HJ_IDCT_SPARSE
-#define HJ_IDCT_SPARSE 0
-#endif
-#ifndef HJ_IDCT_ATTR
-#define HJ_IDCT_ATTR
-#endif
 constexpr int kBlkWords = 36;
 
 // One block of the entropy kernel's coefficient lists -> 8x8 pixels (u8
@@ -2677,13 +2521,9 @@ __device__ __forceinline__ void idct_list_block(const uint32_t* __restrict__ ent
     // Sparse blocks, wave-uniform: when no block of the wave has a
     // coefficient in rows (columns) 4..7, those rows' passes and terms are
     // additions of zero and are left out -- same results, fewer instructions
-    // (HJ_IDCT_SPARSE 0: always the full transform)
-#if HJ_IDCT_SPARSE
-    const bool r4 = !__any(rows_hi != 0u), c4 = !__any(cols_hi != 0u);
-#else
+    // (0 0: always the full transform)
     const bool r4 = false, c4 = false;
     (void)rows_hi, (void)cols_hi;
-#endif
     if (r4 && c4) {
 #pragma unroll
       for (int i = 0; i < 4; i++) simple_row<4>(blk + 8 * i);
@@ -2711,7 +2551,7 @@ __device__ __forceinline__ void idct_list_block(const uint32_t* __restrict__ ent
 }
 
 template <int IDCT>
-__global__ void __launch_bounds__(kIdctThreads) HJ_IDCT_ATTR idct_kernel(const uint32_t* __restrict__ ents,
+__global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __restrict__ ents,
                                                             const uint2* __restrict__ bdesc,
                                                             const ImageDesc* __restrict__ desc,
                                                             const ImageInfo* __restrict__ infos,
@@ -2843,9 +2683,6 @@ __global__ void __launch_bounds__(256) csc_kernel(const uint8_t* __restrict__ pl
 // ---------------------------------------------------------------------------
 
 typedef short hj_short2 __attribute__((ext_vector_type(2)));
-#ifndef HJ_HG4
-#define HJ_HG4 12  // rows per load group of the short horizontal filters (8: -0.9 %, 16: same, 4-lane A/B)
-#endif
 // 16-byte vector load from a 4-byte aligned address (gfx950 global loads
 // allow it): one global_load_dwordx4 instead of four dword loads
 typedef uint32_t hj_u32x4a __attribute__((ext_vector_type(4), aligned(4)));
@@ -2915,7 +2752,7 @@ __device__ __forceinline__ void hpass_cols(const uint8_t* plane, int stride, int
     int16_t* out = lds + c * cst;
     // rows in groups of G: the G loads are issued back to back, so one
     // memory latency is exposed per group instead of per row
-    constexpr int G = NW <= 4 ? HJ_HG4 : (NW <= 8 ? 4 : 1);
+    constexpr int G = NW <= 4 ? 12 : (NW <= 8 ? 4 : 1);
     for (int r = r0; r < r1; r += G) {
       uint32_t w[G][NW];
 #pragma unroll
@@ -3252,10 +3089,7 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
 // are the plane bytes; oracle sws_oracle.c), but one thread per
 // kRgbPx pixels of a row -- no horizontal / vertical passes and no LDS.  u8
 // only.  HBM-bound: 1.5 B in + 3 B out per pixel.
-#ifndef HJ_RGBU_PX
-#define HJ_RGBU_PX 8
-#endif
-constexpr int kRgbPx = HJ_RGBU_PX;  // 8 or 16
+constexpr int kRgbPx = 8;  // 8 or 16
 
 template <int N>  // N words from a pointer aligned to 4 N bytes
 __device__ __forceinline__ void rgbu_load(const uint8_t* p, uint32_t (&w)[N]) {

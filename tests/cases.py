@@ -99,6 +99,14 @@ def case(name: str) -> bytes:
     if name == "prog_1080p":
         return _enc(synthetic_pixels(29, 1080, 1920), quality=90, subsampling=2,
                     progressive=True)
+    # progressive files with binary metadata full of 0xFF xx pairs: an APP2
+    # blob before the frame (an ICC profile / thumbnail stand-in) and a COM
+    # segment between two scans (more marker candidates than the decoder's
+    # list holds: each scan's end is then found by a forward search)
+    if name == "prog_app2_blob":
+        return _with_segment(case("prog_420"), 0xE2, _ff_blob(40, 30000), before_sos=0)
+    if name == "prog_com_between_scans":
+        return _with_segment(case("prog_420"), 0xFE, _ff_blob(41, 3000), before_sos=1)
     # sequential, one non-interleaved scan per component (reverse order);
     # Pillow cannot write these: libjpeg 9 wrote the committed files
     # (tests/gen_golden.py, oracle.lj_encode_multiscan)
@@ -118,6 +126,7 @@ MULTISCAN = {
 LARGE_PROGRESSIVE = ["prog_large_420", "prog_large_noise", "prog_large_restart", "prog_1080p"]
 PROGRESSIVE = ["prog_420", "prog_444_odd", "prog_422", "prog_gray", "prog_optimized",
                "prog_restart", "prog_noise_q100"]
+METADATA = ["prog_app2_blob", "prog_com_between_scans"]
 
 
 VALID = [
@@ -208,3 +217,26 @@ def truncated_progressive(frac: float = 0.5) -> bytes:
     d = case("prog_420")
     return d[: int(len(d) * frac)]
 
+
+
+def _ff_blob(seed: int, n: int) -> bytes:
+    """n bytes of segment payload, every other one 0xFF followed by a byte that
+    would read as a marker (SOFn, DHT, SOS, EOI ...) outside a segment."""
+    rng = np.random.default_rng(seed)
+    nx = rng.choice(np.array([0xC0, 0xC2, 0xC4, 0xD9, 0xDA, 0xDB, 0xE1], np.uint8), size=n // 2)
+    out = np.empty(2 * (n // 2), np.uint8)
+    out[0::2] = 0xFF
+    out[1::2] = nx
+    return out.tobytes()
+
+
+def _with_segment(data: bytes, marker: int, payload: bytes, before_sos: int) -> bytes:
+    """`data` with one marker segment inserted: right after SOI
+    (before_sos=0) or just before the before_sos-th SOS marker (1 = second)."""
+    seg = bytes([0xFF, marker]) + (len(payload) + 2).to_bytes(2, "big") + payload
+    if before_sos == 0:
+        return data[:2] + seg + data[2:]
+    pos = -1
+    for _ in range(before_sos + 1):
+        pos = data.index(b"\xff\xda", pos + 1)
+    return data[:pos] + seg + data[pos:]

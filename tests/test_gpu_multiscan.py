@@ -148,3 +148,15 @@ def test_unsupported_fails_per_image(bad):
         sio.load_image_batch([d, *good], width=64, height=64, strict=True)
     buf = sio.load_image_batch([d, *good], width=64, height=64, strict=False)
     assert sio.to_numpy(buf).shape == (2, 64, 64, 3)
+
+
+@pytest.mark.parametrize("name", cases.METADATA)
+def test_progressive_with_ff_metadata(oracle, name):
+    """Binary metadata full of 0xFF xx pairs (an APP2 blob before the frame, a
+    COM segment between scans) neither fails the image nor ends a scan
+    early: planes and RGB224 bit-exact vs the oracle."""
+    d = cases.case(name)
+    ref = oracle.decode_planes(d, oracle.IDCT_SIMPLE)
+    hyp = _lib.thread_decoder(0).decode_planes(d)
+    for c in range(len(ref)):
+        np.testing.assert_array_equal(hyp[c], ref[c], strict=True)

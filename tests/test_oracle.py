@@ -363,3 +363,15 @@ def check_edge_values(hyp):
 
 def test_edge_values_oracle(oracle):
     check_edge_values(oracle.decode_rgb(_edge_jpeg()))
+
+
+def test_metadata_segments_do_not_change_pixels(oracle):
+    """The FF-laden APP2 / COM test files decode to the pixels of the file
+    they were made from (their segments are skipped by length)."""
+    from tests import cases
+
+    ref = oracle.decode_planes(cases.case("prog_420"), oracle.IDCT_SIMPLE)
+    for name in cases.METADATA:
+        hyp = oracle.decode_planes(cases.case(name), oracle.IDCT_SIMPLE)
+        for a, b in zip(hyp, ref):
+            np.testing.assert_array_equal(a, b)
