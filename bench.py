@@ -56,6 +56,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
 PMC_TRAFFIC = os.path.join(PROFILE_DIR, "traffic.json")
 PMC_ISSUE = os.path.join(PROFILE_DIR, "issue.json")
+# rocprofv3 --kernel-trace --stats of this command (tools/profile_round.sh)
+KSTATS = {4: os.path.join(PROFILE_DIR, "kernel_stats_lanes4.csv"),
+          1: os.path.join(PROFILE_DIR, "kernel_stats_lanes1.csv")}
 # bench stage -> kernels launched in it
 STAGE_KERNELS = {
     "parse": ["hj::parse_kernel"],
@@ -79,6 +82,23 @@ def _pmc(path: str, stage: str, batch: int) -> dict | None:
     hits = [v for name, v in rec["kernels"].items()
             if any(name.startswith(k) for k in STAGE_KERNELS.get(stage, []))]
     return hits[0] if len(hits) == 1 else None
+
+
+def _rocprof_ms(lanes: int, stage: str) -> float | None:
+    """Average duration (ms) of `stage`'s kernel in the committed rocprofv3
+    kernel-trace summary of the bench at `lanes` lanes (None if absent)."""
+    import csv
+
+    try:
+        with open(KSTATS[lanes]) as f:
+            rows = list(csv.DictReader(f))
+    except (KeyError, OSError):
+        return None
+    for r in rows:
+        name = r["Name"].replace("void ", "")
+        if any(name.startswith(k) for k in STAGE_KERNELS.get(stage, [])):
+            return float(r["AverageNs"]) / 1e6
+    return None
 
 
 def _limiter(issue: dict | None) -> str:
@@ -441,9 +461,10 @@ def main():
         dec1.close()
         ms1 = acc[dominant] / a.lanes1_steps / 1000.0
         ach1 = launch_bytes / (ms1 / 1000.0) / 1e9
+        r1 = _rocprof_ms(1, dominant) if a.workload == "pad224" and a.batch == BATCH else None
         lanes1 = {"kernel_ms": round(ms1, 4), "achieved": round(ach1, 3),
                   "frac": round(ach1 / HBM_PEAK_GBS, 6), "steps": a.lanes1_steps,
-                  "entropy_threads": th1}
+                  "entropy_threads": th1, "kernel_ms_rocprof": r1}
 
     # per-rank record: each rank's own rate and device (the driver's 8-GPU
     # run shows N distinct devices working)
@@ -477,13 +498,12 @@ def main():
         threads = a.cpu_threads or _cpu_cores()["usable"]
         cpu = _cpu_baseline(datas, threads, a.cpu_images, a.cpu_images // 2, a.cpu_runs)
 
-    traffic = issue = None
+    traffic = issue = rocprof_ms = None
+    if a.workload == "pad224" and a.lanes in KSTATS and a.batch == BATCH:
+        rocprof_ms = _rocprof_ms(a.lanes, dominant)
     if a.workload == "pad224" and a.lanes == 4:  # the configuration the PMC passes ran
         traffic = _pmc(PMC_TRAFFIC, dominant, a.batch)
         issue = _pmc(PMC_ISSUE, dominant, a.batch)
-        if traffic:
-            with open(PMC_TRAFFIC) as f:
-                traffic = {**traffic, "correction": json.load(f).get("correction", "")}
     if rank == 0:
         value = world * a.batch * a.steps / elapsed
         rec = {
@@ -525,11 +545,21 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": traffic["traffic_bytes"] if traffic else None,
                 "traffic_source": (f"{os.path.relpath(PMC_TRAFFIC, ROOT)}: "
-                                   f"{traffic['correction']}") if traffic else None,
+                                   f"{traffic['correction']} (tools/fetch_calib.hip)")
+                                  if traffic else None,
                 "algorithmic_bytes_per_image": round(per_image_bytes, 1),
                 "launch_images": a.batch,
                 "formula": "achieved = algorithmic_bytes_per_image x launch_images / mean "
                            "HIP-event duration of the kernel's launches in the timed steps",
+                # the same kernel's average in the committed rocprofv3 summary of
+                # this configuration: the HIP events above also count the time a
+                # launch waits for CUs the other lanes hold
+                "kernel_ms_hip_events": round(kernels[dominant], 4),
+                "kernel_ms_rocprof": rocprof_ms,
+                "frac_rocprof": (round(launch_bytes / (rocprof_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 6)
+                                 if rocprof_ms else None),
+                "rocprof_source": (os.path.relpath(KSTATS[a.lanes], ROOT)
+                                   if rocprof_ms else None),
                 "limiter": _limiter(issue),
                 "pipeline_GBps": round(launch_bytes / (elapsed / a.steps) / 1e9, 3),
                 "lanes1": lanes1,

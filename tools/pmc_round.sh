@@ -11,5 +11,6 @@ bash tools/pmc_passes.sh "$out" \
   "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS" \
   || exit 1
 python3 tools/pmc_traffic.py "$out/traffic.json" "$out/pmc_1" "$out/pmc_2" > "$out/traffic.txt" || exit 1
+python3 tools/pmc_issue.py "$out/issue.json" 256 "$out/pmc_3" "$out/pmc_4" > "$out/issue.txt" || exit 1
 python3 tools/pmc_summary.py "$out"/pmc_* > "$out/counters_summary.txt" || exit 1
 cat "$out/traffic.txt"

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round profile (GPU box): FETCH/WRITE calibration, PMC passes (traffic +
+# SQ issue/wait), and rocprofv3 kernel-trace stats of the bench at 4 lanes
+# and 1 lane.  usage: bash tools/profile_round.sh OUTDIR
+set -o pipefail
+out=${1:-gpurun_out/prof}
+mkdir -p "$out"
+bash tools/fetch_calib.sh "$out/calib" || exit 1
+bash tools/pmc_round.sh "$out/pmc" || exit 1
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+for l in 4 1; do
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/ktrace_l$l" -o run --output-format csv \
+    -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --lanes1-steps 0 --lanes $l \
+    > "$out/ktrace_l$l.log" 2>&1 || { echo "kernel trace lanes $l failed"; exit 1; }
+done
+python3 tools/pmc_traffic.py "$out/traffic.json" "$out/pmc/pmc_1" "$out/pmc/pmc_2" \
+  --calib "$out/calib/calibration.json" > "$out/traffic.txt" || exit 1
+cat "$out/traffic.txt" "$out/pmc/issue.txt" "$out/calib/calibration.txt"
