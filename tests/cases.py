@@ -32,6 +32,10 @@ def _noise(seed, h, w, c=3):
 
 @functools.lru_cache(maxsize=None)
 def case(name: str) -> bytes:
+    if name.startswith("bench_"):  # bench.py's synthetic images (seed 1000 + i)
+        from spdl_amd.synthetic import synthetic_jpeg
+
+        return synthetic_jpeg(int(name[6:]))
     if name == "q90_420":
         return _enc(synthetic_pixels(1), quality=90, subsampling=2)
     if name == "q75_420":

@@ -38,6 +38,9 @@ CASES = [
     "q90_444", "q90_422", "odd_227x333", "odd_444_101x67", "gray", "gray_odd",
     "noise_q100", "restart_rows", "restart_blocks", "restart_every_mcu", "tiny_8x8",
     "tiny_1x1", "optimized", "six_tables",
+    # the bench's own shape: 480x640 q90 4:2:0 (bench.py's first synthetic
+    # image and the q90_420 case)
+    "q90_420", "bench_1000",
     *cases.PROGRESSIVE, *cases.MULTISCAN,
 ]
 
