@@ -30,12 +30,12 @@
 extern "C" {
 #endif
 
-#define SPDL_HJ_ABI_VERSION 3
+#define SPDL_HJ_ABI_VERSION 4
 
 enum spdl_hj_status {
   SPDL_HJ_OK = 0,
   SPDL_HJ_ERR_NOT_JPEG = 1,
-  SPDL_HJ_ERR_UNSUPPORTED = 2,  /* arithmetic, lossless, 12-bit, CMYK */
+  SPDL_HJ_ERR_UNSUPPORTED = 2,  /* arithmetic, lossless, 12-bit, progressive CMYK */
   SPDL_HJ_ERR_BAD_HEADER = 3,
   SPDL_HJ_ERR_BAD_HUFFMAN = 4,
   SPDL_HJ_ERR_TRUNCATED = 5,
@@ -97,9 +97,13 @@ typedef struct spdl_hj_output {
   int32_t csc;          /* enum spdl_hj_csc, since ABI 2 */
 } spdl_hj_output;
 
+/* ncomp 4 (since ABI 4): an Adobe CMYK / YCCK file, every component 1x1, one
+ * interleaved sequential scan; `adobe` is its APP14 transform flag (0 CMYK,
+ * 1 YCbCr + K, 2 YCCK; -1 without the marker, decoded as 0 like FFmpeg). */
 typedef struct spdl_hj_image_info {
   int32_t width, height, ncomp;
-  int32_t h_samp[3], v_samp[3];
+  int32_t h_samp[4], v_samp[4];
+  int32_t adobe;
 } spdl_hj_image_info;
 
 typedef struct spdl_hj_ctx spdl_hj_ctx;

@@ -78,6 +78,7 @@ static int check_huff(const uint8_t* bits) {
 
 int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
   memset(info, 0, sizeof(*info));
+  info->adobe = -1;
   if (size < 4 || d[0] != 0xFF || d[1] != 0xD8) return JO_ERR_NOT_JPEG;
   int have_sof = 0, qt_have[4] = {0}, dc_have[4] = {0}, ac_have[4] = {0};
   int comp_id[JO_MAX_COMP] = {0};
@@ -135,7 +136,7 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
       int nf = s[5];
       if (info->height == 0) return JO_ERR_UNSUPPORTED; /* DNL */
       if (info->width == 0) return JO_ERR_BAD_HEADER;
-      if (nf != 1 && nf != 3) return JO_ERR_UNSUPPORTED;
+      if (nf != 1 && nf != 3 && nf != 4) return JO_ERR_UNSUPPORTED;
       if (n < 6 + 3 * nf) return JO_ERR_BAD_HEADER;
       info->ncomp = nf;
       for (int c = 0; c < nf; c++) {
@@ -146,11 +147,16 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
         if (info->comp_h[c] < 1 || info->comp_h[c] > 4 || info->comp_v[c] < 1 ||
             info->comp_v[c] > 4 || info->comp_tq[c] > 3)
           return JO_ERR_BAD_HEADER;
+        /* 4 components: the Adobe CMYK / YCCK layout, every component 1x1
+         * (FFmpeg's 4-plane pix_fmts GBRAP / YUVA444P) */
+        if (nf == 4 && (info->comp_h[c] != 1 || info->comp_v[c] != 1)) return JO_ERR_UNSUPPORTED;
       }
       have_sof = 1;
     } else if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
                (m >= 0xCD && m <= 0xCF)) {
       return JO_ERR_UNSUPPORTED; /* lossless, hierarchical, arithmetic */
+    } else if (m == 0xEE) { /* APP14: Adobe's transform flag */
+      if (n >= 12 && memcmp(s, "Adobe", 5) == 0) info->adobe = s[11];
     } else if (m == 0xDD) { /* DRI */
       if (n < 2) return JO_ERR_BAD_HEADER;
       info->restart_interval = be16(s);
@@ -161,6 +167,7 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
       /* progressive, or sequential with non-interleaved scans: the first scan
        * fixes nothing beyond the frame; every scan is walked at decode time */
       info->multiscan = info->progressive || ns != info->ncomp;
+      if (info->multiscan && info->ncomp == 4) return JO_ERR_UNSUPPORTED;
       if (n < 1 + 2 * ns + 3) return JO_ERR_BAD_HEADER;
       int order[JO_MAX_COMP];
       for (int i = 0; i < ns; i++) {
@@ -703,7 +710,7 @@ int jo_decode_coefs(const uint8_t* d, size_t size, const jo_info* info, int16_t*
   /* FFmpeg mjpegdec initialises (and resets at each RSTn) the dequantised DC
    * predictor to 4 << bits = 1024: the +128 level shift lives in block[0]. */
   int32_t pred[JO_MAX_COMP] = {0};  /* sum of DC diffs (quantised) */
-  uint32_t last_dc[JO_MAX_COMP] = {JO_DC_BIAS, JO_DC_BIAS, JO_DC_BIAS};
+  uint32_t last_dc[JO_MAX_COMP] = {JO_DC_BIAS, JO_DC_BIAS, JO_DC_BIAS, JO_DC_BIAS};
   int nmcu = info->mcux * info->mcuy;
   int ri = info->restart_interval;
   for (int mcu = 0; mcu < nmcu; mcu++) {
@@ -1090,6 +1097,38 @@ static int decode_planes_info(const uint8_t* d, size_t size, const jo_info* info
   return JO_OK;
 }
 
+/* FFmpeg mjpegdec's in-decoder conversion of 4-component frames (the end of
+ * ff_mjpeg_decode_frame / receive_frame, as recalled; parity UNPINNED):
+ *   Adobe transform 0 (or no marker), pix_fmt GBRAP -- inverted CMYK to RGB:
+ *     R = c k 257 >> 16, G = m k 257 >> 16, B = y k 257 >> 16
+ *   transform 2, YUVA444P -- YCCK to YCbCr:
+ *     Y = (255 - y) k 257 >> 16, Cb = ((128 - cb) k 257 >> 16) + 128, Cr likewise
+ * (c, m, y / y, cb, cr = components 0..2, k = component 3).  Planes 0..2 are
+ * rewritten in place; transform 1 leaves them (YCbCr + K, K dropped). */
+void jo_cmyk_transform(const jo_info* info, uint8_t* planes) {
+  if (info->ncomp != 4 || info->adobe == 1) return;
+  const uint8_t* pc[JO_MAX_COMP];
+  int st[JO_MAX_COMP];
+  plane_ptrs(info, planes, pc, st);
+  for (int y = 0; y < info->height; y++)
+    for (int x = 0; x < info->width; x++) {
+      uint8_t* p0 = (uint8_t*)pc[0] + (size_t)y * st[0] + x;
+      uint8_t* p1 = (uint8_t*)pc[1] + (size_t)y * st[1] + x;
+      uint8_t* p2 = (uint8_t*)pc[2] + (size_t)y * st[2] + x;
+      const int k = pc[3][(size_t)y * st[3] + x];
+      if (info->adobe == 2) {
+        const int r = (255 - *p0) * k, g = (128 - *p1) * k, b = (128 - *p2) * k;
+        *p0 = (uint8_t)((r * 257) >> 16);
+        *p1 = (uint8_t)(((g * 257) >> 16) + 128);
+        *p2 = (uint8_t)(((b * 257) >> 16) + 128);
+      } else {
+        *p0 = (uint8_t)((*p0 * k * 257) >> 16);
+        *p1 = (uint8_t)((*p1 * k * 257) >> 16);
+        *p2 = (uint8_t)((*p2 * k * 257) >> 16);
+      }
+    }
+}
+
 int jo_decode_planes(const uint8_t* d, size_t size, int idct, uint8_t* planes) {
   jo_info info;
   int rc = jo_parse(d, size, &info);
@@ -1138,6 +1177,7 @@ static void store_px(uint8_t* out, int fmt, int ow, int oh, int x, int y, const 
 }
 
 static int planes_to_rgb(const jo_info* info, const uint8_t* planes, int fmt, uint8_t* out) {
+  if (info->ncomp == 4) return JO_ERR_UNSUPPORTED;  /* libjpeg outputs CMYK there */
   const uint8_t* pc[JO_MAX_COMP];
   int st[JO_MAX_COMP];
   plane_ptrs(info, planes, pc, st);
@@ -1188,10 +1228,14 @@ static int sws_planes(const jo_info* info, const uint8_t* planes, int sw, int sh
   int st[JO_MAX_COMP];
   plane_ptrs(info, planes, pc, st);
   jo_sws s;
-  if (jo_sws_init(&s, info->width, info->height, hsub, vsub, info->ncomp == 1, sw, sh, filter)) {
+  /* 4 components: RGB planes (CMYK) through the luma filters, or YCbCr 444 */
+  const int gbr = info->ncomp == 4 && info->adobe != 1 && info->adobe != 2;
+  if (jo_sws_init(&s, info->width, info->height, hsub, vsub, info->ncomp == 1 || gbr, sw, sh,
+                  filter)) {
     jo_sws_free(&s);
     return JO_ERR_BAD_GEOMETRY;
   }
+  s.gbr = gbr;
   uint8_t* rgb = (uint8_t*)scratch(7, (size_t)sw * sh * 3);
   rc = rgb ? jo_sws_scale(&s, pc, st, rgb) : -1;
   jo_sws_free(&s);
@@ -1209,6 +1253,7 @@ int jo_decode_rgb_csc(const uint8_t* d, size_t size, int idct, int csc, int fmt,
   rc = decode_planes_info(d, size, &info, idct, planes);
   if (rc) return rc;
   if (csc == JO_CSC_JFIF) return planes_to_rgb(&info, planes, fmt, out);
+  jo_cmyk_transform(&info, planes);
   uint8_t* rgb;
   rc = sws_planes(&info, planes, info.width, info.height, JO_FILTER_BICUBIC, &rgb);
   if (rc) return rc;
@@ -1374,6 +1419,7 @@ int jo_decode_resize(const uint8_t* d, size_t size, int idct, const jo_resize* r
   uint8_t* planes = (uint8_t*)scratch(1, jo_planes_size(&info));
   if (!planes) return JO_ERR_BAD_HEADER;
   rc = decode_planes_info(d, size, &info, idct, planes);
+  if (!rc) jo_cmyk_transform(&info, planes);
   if (!rc) rc = jo_resize_planes(&info, planes, rs, fmt, dtype, mean, stdv, out, geom_out);
   return rc;
 }

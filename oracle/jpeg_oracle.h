@@ -61,14 +61,14 @@ enum { JO_ASPECT_NONE = 0, JO_ASPECT_DECREASE = 1, JO_ASPECT_INCREASE = 2 };
 enum { JO_FILTER_BICUBIC = 0, JO_FILTER_BILINEAR = 1, JO_FILTER_LANCZOS = 2 };
 enum { JO_DTYPE_U8 = 0, JO_DTYPE_F16 = 1, JO_DTYPE_BF16 = 2 };
 
-#define JO_MAX_COMP 3
+#define JO_MAX_COMP 4
 #define JO_MAX_BPM 10
 /* dequantised DC predictor start value (FFmpeg mjpegdec: 4 << bits) */
 #define JO_DC_BIAS 1024
 
 typedef struct {
   int width, height;
-  int ncomp;                 /* 1 or 3 */
+  int ncomp;                 /* 1, 3 or 4 (Adobe CMYK / YCCK, all components 1x1) */
   int hmax, vmax;
   int mcux, mcuy;            /* MCUs per row / column */
   int bpm;                   /* blocks per MCU */
@@ -87,6 +87,9 @@ typedef struct {
   int multiscan;             /* the image takes more than one scan (progressive,
                                 or sequential with non-interleaved scans):
                                 jo_decode_coefs walks every scan */
+  int adobe;                 /* APP14 "Adobe" transform flag (0 CMYK, 1 YCbCr,
+                                2 YCCK), -1 without the marker (FFmpeg treats
+                                that as 0) */
 } jo_info;
 
 typedef struct {
@@ -162,6 +165,7 @@ typedef struct {
   int chr_src_hsub, chr_src_vsub;
   int full;              /* SWS_FULL_CHR_H_INT in effect */
   int gray;
+  int gbr;               /* three RGB planes through the luma filters */
   int unscaled_special;  /* yuv2rgb_c_24_rgb (nearest chroma) */
   jo_sws_filter hl, hc, vl, vc;
   int32_t crv, cbu, cgu, cgv;                  /* table increments (cy-scaled) */

@@ -201,3 +201,45 @@ long lj_encode_multiscan(const uint8_t* px, int w, int h, int ncomp, int quality
   jpeg_destroy_compress(&c);
   return n;
 }
+
+/* Fixture encoder: a 4-component JPEG from CMYK pixels (libjpeg's Adobe
+ * convention: the values are written as given, Adobe APP14 marker with
+ * transform 0 for JCS_CMYK, 2 for JCS_YCCK), every component 1x1. */
+long lj_encode_cmyk(const uint8_t* px, int w, int h, int quality, int ycck, int restart_blocks,
+                    uint8_t* out, size_t out_cap) {
+  struct jpeg_compress_struct c;
+  err_t e;
+  struct jpeg_destination_mgr dst;
+  c.err = jpeg_std_error(&e.pub);
+  e.pub.error_exit = on_error;
+  e.pub.emit_message = on_message;
+  if (setjmp(e.jb)) {
+    jpeg_destroy_compress(&c);
+    return -1;
+  }
+  jpeg_create_compress(&c);
+  dst.init_destination = dst_init;
+  dst.empty_output_buffer = dst_empty;
+  dst.term_destination = dst_term;
+  dst.next_output_byte = out;
+  dst.free_in_buffer = out_cap;
+  c.dest = &dst;
+  c.image_width = (JDIMENSION)w;
+  c.image_height = (JDIMENSION)h;
+  c.input_components = 4;
+  c.in_color_space = JCS_CMYK;
+  jpeg_set_defaults(&c);
+  jpeg_set_colorspace(&c, ycck ? JCS_YCCK : JCS_CMYK);
+  jpeg_set_quality(&c, quality, TRUE);
+  for (int i = 0; i < 4; i++) c.comp_info[i].h_samp_factor = c.comp_info[i].v_samp_factor = 1;
+  c.restart_interval = (unsigned)restart_blocks;
+  jpeg_start_compress(&c, TRUE);
+  while (c.next_scanline < c.image_height) {
+    JSAMPROW row = (JSAMPROW)(px + (size_t)c.next_scanline * w * 4);
+    jpeg_write_scanlines(&c, &row, 1);
+  }
+  jpeg_finish_compress(&c);
+  long n = (long)(out_cap - dst.free_in_buffer);
+  jpeg_destroy_compress(&c);
+  return n;
+}

@@ -39,15 +39,15 @@ class _Info(ctypes.Structure):
         ("bpm", ctypes.c_int),
         ("nblocks", ctypes.c_int),
         ("restart_interval", ctypes.c_int),
-        ("comp_h", ctypes.c_int * 3),
-        ("comp_v", ctypes.c_int * 3),
-        ("comp_tq", ctypes.c_int * 3),
-        ("comp_td", ctypes.c_int * 3),
-        ("comp_ta", ctypes.c_int * 3),
-        ("comp_bw", ctypes.c_int * 3),
-        ("comp_bh", ctypes.c_int * 3),
-        ("comp_w", ctypes.c_int * 3),
-        ("comp_h_px", ctypes.c_int * 3),
+        ("comp_h", ctypes.c_int * 4),
+        ("comp_v", ctypes.c_int * 4),
+        ("comp_tq", ctypes.c_int * 4),
+        ("comp_td", ctypes.c_int * 4),
+        ("comp_ta", ctypes.c_int * 4),
+        ("comp_bw", ctypes.c_int * 4),
+        ("comp_bh", ctypes.c_int * 4),
+        ("comp_w", ctypes.c_int * 4),
+        ("comp_h_px", ctypes.c_int * 4),
         ("mcu_comp", ctypes.c_int * 10),
         ("mcu_dx", ctypes.c_int * 10),
         ("mcu_dy", ctypes.c_int * 10),
@@ -59,6 +59,7 @@ class _Info(ctypes.Structure):
         ("scan_start", ctypes.c_size_t),
         ("progressive", ctypes.c_int),
         ("multiscan", ctypes.c_int),
+        ("adobe", ctypes.c_int),
     ]
 
 
@@ -420,6 +421,26 @@ def lj_encode_multiscan(px: np.ndarray, quality: int = 90, h0: int = 2, v0: int 
     f.restype = ctypes.c_long
     f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_size_t]
     n = f(px.ctypes.data, w, h, nc, quality, h0, v0, restart_blocks, out.ctypes.data, cap)
+    if n <= 0:
+        raise RuntimeError(f"libjpeg encode failed ({n})")
+    return out[:n].tobytes()
+
+
+def lj_encode_cmyk(cmyk: np.ndarray, quality: int = 90, ycck: bool = False,
+                   restart_blocks: int = 0) -> bytes:
+    """Fixture encoder (libjpeg 9): a 4-component Adobe JPEG (transform 0
+    CMYK, or 2 YCCK) of HxWx4 pixels, every component 1x1."""
+    L = ljpin()
+    if L is None:
+        raise RuntimeError("libjpeg 9 pin helper not available")
+    px = np.ascontiguousarray(cmyk, np.uint8)
+    h, w = px.shape[:2]
+    cap = h * w * 16 + 65536
+    out = np.zeros(cap, np.uint8)
+    f = L.lj_encode_cmyk
+    f.restype = ctypes.c_long
+    f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_size_t]
+    n = f(px.ctypes.data, w, h, quality, int(bool(ycck)), restart_blocks, out.ctypes.data, cap)
     if n <= 0:
         raise RuntimeError(f"libjpeg encode failed ({n})")
     return out[:n].tobytes()

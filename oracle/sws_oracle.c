@@ -405,7 +405,51 @@ static void hscale_row(const uint8_t* src, const jo_sws_filter* f, int16_t* dst)
 
 /* The scaled rgb24 image (dstW x dstH x 3) from the decoded planes.
  * planes[c] / stride[c]: component planes (chroma planes absent for gray). */
+/* Three RGB planes (a CMYK frame after FFmpeg's in-decoder conversion,
+ * GBRAP) each through the luma filters -- hScale8To15, then the vertical
+ * taps with the rounding of swscale's 8-bit planar writers (yuv2planeX:
+ * (sum + 2^18) >> 19; two-tap: blend >> 19; one tap: (x + 64) >> 7), clipped.
+ * swscale itself routes RGB input through its YUV intermediate when it
+ * scales: this per-plane filter is the stated substitute (parity UNPINNED). */
+static int sws_scale_gbr(const jo_sws* s, const uint8_t* const* planes, const int* stride,
+                         uint8_t* rgb) {
+  const int W = s->dstW, H = s->dstH;
+  int16_t* h[3];
+  for (int c = 0; c < 3; c++) {
+    h[c] = (int16_t*)malloc(sizeof(int16_t) * (size_t)s->srcH * W);
+    if (!h[c]) {
+      for (int k = 0; k < c; k++) free(h[k]);
+      return -1;
+    }
+    for (int r = 0; r < s->srcH; r++) hscale_row(planes[c] + (size_t)r * stride[c], &s->hl, h[c] + (size_t)r * W);
+  }
+  const int lfs = s->vl.size;
+  for (int y = 0; y < H; y++) {
+    const int16_t* lf = s->vl.coef + (size_t)y * lfs;
+    const int lp = s->vl.pos[y];
+    const int mode = lfs == 1 ? 1 : lfs == 2 && lf[0] + lf[1] == 4096 && (unsigned)lf[1] <= 4096u ? 2 : 0;
+    for (int x = 0; x < W; x++)
+      for (int c = 0; c < 3; c++) {
+        const int16_t* col = h[c] + x;
+        int v;
+        if (mode == 0) {
+          v = 1 << 18;
+          for (int j = 0; j < lfs; j++) v += col[(size_t)(lp + j) * W] * lf[j];
+          v >>= 19;
+        } else if (mode == 2) {
+          v = (col[(size_t)lp * W] * (4096 - lf[1]) + col[(size_t)(lp + 1) * W] * lf[1]) >> 19;
+        } else {
+          v = (col[(size_t)lp * W] + 64) >> 7;
+        }
+        rgb[((size_t)y * W + x) * 3 + c] = (uint8_t)clip8(v);
+      }
+  }
+  for (int c = 0; c < 3; c++) free(h[c]);
+  return 0;
+}
+
 int jo_sws_scale(const jo_sws* s, const uint8_t* const* planes, const int* stride, uint8_t* rgb) {
+  if (s->gbr) return sws_scale_gbr(s, planes, stride, rgb);
   const int W = s->dstW, H = s->dstH;
   const int cw = s->gray ? 0 : s->chrDstW;
   int16_t* lum = (int16_t*)malloc(sizeof(int16_t) * (size_t)s->srcH * W);

@@ -15,7 +15,7 @@ from dataclasses import dataclass
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPDL_AMD_LIB") or os.path.join(_HERE, "lib", "libspdl_hipjpeg.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # enums (mirror include/spdl_hipjpeg.h)
 PIX_FMTS = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
@@ -59,8 +59,9 @@ class ImageInfo(ctypes.Structure):
         ("width", ctypes.c_int32),
         ("height", ctypes.c_int32),
         ("ncomp", ctypes.c_int32),
-        ("h_samp", ctypes.c_int32 * 3),
-        ("v_samp", ctypes.c_int32 * 3),
+        ("h_samp", ctypes.c_int32 * 4),
+        ("v_samp", ctypes.c_int32 * 4),
+        ("adobe", ctypes.c_int32),  # APP14 transform of a 4-component file, -1 none
     ]
 
 
@@ -506,7 +507,7 @@ class Decoder:
                 w = -(-info.width * info.h_samp[c] // hmax)
                 h = -(-info.height * info.v_samp[c] // vmax)
             planes.append(np.zeros((h, w), np.uint8))
-        ptrs = (ctypes.c_void_p * 3)(*([p.ctypes.data for p in planes] + [None] * (3 - len(planes))))
+        ptrs = (ctypes.c_void_p * 4)(*([p.ctypes.data for p in planes] + [None] * (4 - len(planes))))
         addr, size, keep = buffer_address(data)
         err = ctypes.create_string_buffer(1024)
         rc = lib().spdl_hj_decode_planes(self._h, addr, size, IDCT[idct],

@@ -23,7 +23,7 @@
 
 namespace hj {
 
-constexpr int kMaxComp = 3;
+constexpr int kMaxComp = 4;  // 1 (gray), 3 (YCbCr) or 4 (Adobe CMYK / YCCK, all 1x1)
 constexpr int kMaxBpm = 10;
 constexpr int kLutBits = 10;
 constexpr int kLutSize = 1 << kLutBits;
@@ -111,13 +111,14 @@ enum SwsTable { kHlPos = 0, kHlCoef, kHcPos, kHcCoef, kVlPos, kVlCoef, kVcPos, k
 struct SwsDesc {
   int32_t sw, sh;          // scaled content size (the swscale destination)
   int32_t chr_w;           // chroma intermediate width (chrDstW)
-  int32_t full, gray;      // SWS_FULL_CHR_H_INT; single-component source
+  int32_t full, gray;      // SWS_FULL_CHR_H_INT; luma filters only (gray or gbr)
   int32_t hl_taps, hc_taps, vl_taps, vc_taps;  // taps read per output (trailing zeros cut)
   int32_t hl_size, hc_size, vl_size, vc_size;  // tap row stride (taps, multiple of 4)
   int32_t off[kSwsTables];
   int32_t rb;              // output rows per workgroup band
   int32_t col_chunk;       // output columns per workgroup
-  int32_t pad_;
+  int32_t gbr;             // three RGB planes (CMYK after the K transform), each
+                           // through the luma filters (oracle sws_scale_gbr)
 };
 
 struct ImageDesc {      // host-filled per image
@@ -138,7 +139,7 @@ struct ImageDesc {      // host-filled per image
   SwsDesc sws;
   int64_t ds_off;       // destuff chunk records: offset and count
   int32_t ds_cap;
-  int32_t pad3_;
+  int32_t adobe;        // APP14 Adobe transform (host probe), -1 without the marker
   int64_t rec_off;      // entropy symbol records: offset (u32 units) and capacity
   int64_t rec_cap;
 };
@@ -177,7 +178,7 @@ struct ImageInfo {      // device-filled by the parse kernel
   int32_t multiscan;    // parse: progressive, or sequential with non-interleaved scans
                         // (multiscan_kernel decodes it; destuff / entropy skip it)
   int32_t progressive;  // parse: SOF2
-  int32_t pad_;
+  int32_t adobe;        // parse: APP14 Adobe transform flag, -1 without the marker
   int64_t tphase[4];    // diagnostics: wall_clock64 ticks of the entropy phases
   int64_t dbg[4];       // diagnostics: symbols (round 0), wave iterations, shader clocks, rt ticks
 };

@@ -53,6 +53,7 @@ hipError_t launch_rgb_unscaled(const uint8_t*, const ImageDesc*, const ImageInfo
                                const BatchParams&, int64_t, int, int32_t*, hipStream_t);
 hipError_t launch_idct_rgb(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, void*,
                            const BatchParams&, int, int, int, int32_t*, hipStream_t);
+hipError_t launch_cmyk(const ImageDesc*, const ImageInfo*, uint8_t*, int64_t, int, hipStream_t);
 }  // namespace hj
 
 using namespace hj;
@@ -257,22 +258,36 @@ void parallel_pack(CopyPool* pool, uint8_t* base, const std::vector<CopyItem>& i
 }
 
 // ---- host SOF probe (replaces nvjpegGetImageInfo) --------------------------
+// Stops at the SOF, except for 4 components: the walk then goes on to the
+// first SOS for the APP14 Adobe transform (the parse kernel's rule: the last
+// APP14 before the scan) and the scan shape (one interleaved sequential scan).
 int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
   memset(info, 0, sizeof(*info));
+  info->adobe = -1;
   if (!d || size < 4 || d[0] != 0xFF || d[1] != 0xD8) return SPDL_HJ_ERR_NOT_JPEG;
   size_t pos = 2;
+  bool have_sof = false;
   for (;;) {
     while (pos < size && d[pos] != 0xFF) pos++;
     while (pos < size && d[pos] == 0xFF) pos++;
     if (pos >= size) return SPDL_HJ_ERR_BAD_HEADER;
     int m = d[pos++];
     if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
-    if (m == 0xD9 || m == 0xDA) return SPDL_HJ_ERR_BAD_HEADER;  // no SOF before scan
+    if (m == 0xD9 || (m == 0xDA && !have_sof)) return SPDL_HJ_ERR_BAD_HEADER;  // no SOF before scan
     if (pos + 2 > size) return SPDL_HJ_ERR_BAD_HEADER;
     int len = (d[pos] << 8) | d[pos + 1];
     if (len < 2 || pos + (size_t)len > size) return SPDL_HJ_ERR_BAD_HEADER;
     const uint8_t* s = d + pos + 2;
     pos += (size_t)len;
+    if (m == 0xDA) {  // 4 components: one interleaved scan of all four
+      if (len < 3 || s[0] != 4) return SPDL_HJ_ERR_UNSUPPORTED;
+      return SPDL_HJ_OK;
+    }
+    if (m == 0xEE) {
+      if (len >= 14 && memcmp(s, "Adobe", 5) == 0) info->adobe = s[11];
+      continue;
+    }
+    if (have_sof) continue;
     if (m == 0xC0 || m == 0xC1 || m == 0xC2) {  // sequential or progressive Huffman
       if (len < 8) return SPDL_HJ_ERR_BAD_HEADER;
       if (s[0] != 8) return SPDL_HJ_ERR_UNSUPPORTED;
@@ -281,7 +296,7 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
       info->ncomp = s[5];
       if (info->height == 0) return SPDL_HJ_ERR_UNSUPPORTED;
       if (info->width == 0) return SPDL_HJ_ERR_BAD_HEADER;
-      if (info->ncomp != 1 && info->ncomp != 3) return SPDL_HJ_ERR_UNSUPPORTED;
+      if (info->ncomp != 1 && info->ncomp != 3 && info->ncomp != 4) return SPDL_HJ_ERR_UNSUPPORTED;
       if (len < 8 + 3 * info->ncomp) return SPDL_HJ_ERR_BAD_HEADER;
       for (int c = 0; c < info->ncomp; c++) {
         info->h_samp[c] = s[7 + 3 * c] >> 4;
@@ -289,8 +304,13 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
         if (info->h_samp[c] < 1 || info->h_samp[c] > 4 || info->v_samp[c] < 1 ||
             info->v_samp[c] > 4)
           return SPDL_HJ_ERR_BAD_HEADER;
+        if (info->ncomp == 4 && (info->h_samp[c] != 1 || info->v_samp[c] != 1))
+          return SPDL_HJ_ERR_UNSUPPORTED;
       }
-      return SPDL_HJ_OK;
+      if (info->ncomp != 4) return SPDL_HJ_OK;
+      if (m == 0xC2) return SPDL_HJ_ERR_UNSUPPORTED;  // progressive CMYK
+      have_sof = true;
+      continue;
     }
     if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
         (m >= 0xCD && m <= 0xCF))
@@ -349,11 +369,12 @@ int geometry(int w, int h, const spdl_hj_output* o, Geom* g) {
 // ---- swscale plans (hj_sws.h), packed for the device ----------------------
 // One per distinct (source size, sampling, output placement, filter); cached
 // per context so a stream of same-size images plans once.
+enum { kPlanYuv = 0, kPlanGray = 1, kPlanGbr = 2 };  // source planes of a plan
 struct PlanKey {
-  int w, h, hsub, vsub, gray, filter, sw, sh, dx, dy, ow, oh;
+  int w, h, hsub, vsub, mode, filter, sw, sh, dx, dy, ow, oh;
   bool operator<(const PlanKey& o) const {
-    return std::tie(w, h, hsub, vsub, gray, filter, sw, sh, dx, dy, ow, oh) <
-           std::tie(o.w, o.h, o.hsub, o.vsub, o.gray, o.filter, o.sw, o.sh, o.dx, o.dy, o.ow, o.oh);
+    return std::tie(w, h, hsub, vsub, mode, filter, sw, sh, dx, dy, ow, oh) <
+           std::tie(o.w, o.h, o.hsub, o.vsub, o.mode, o.filter, o.sw, o.sh, o.dx, o.dy, o.ow, o.oh);
   }
 };
 
@@ -386,7 +407,8 @@ class PlanCache {
 
   static std::shared_ptr<const PackedPlan> build(const PlanKey& k, int* rc) {
     SwsPlan pl;
-    *rc = sws_plan(k.w, k.h, k.hsub, k.vsub, k.gray != 0, k.sw, k.sh, k.filter, &pl);
+    // gbr: the luma plan (gray) applied to each of the three RGB planes
+    *rc = sws_plan(k.w, k.h, k.hsub, k.vsub, k.mode != kPlanYuv, k.sw, k.sh, k.filter, &pl);
     if (*rc) return nullptr;
     auto pp = std::make_shared<PackedPlan>();
     pp->special = pl.special && k.dx == 0 && k.dy == 0 && k.ow == k.sw && k.oh == k.sh;
@@ -396,6 +418,7 @@ class PlanCache {
     d.chr_w = pl.chrDstW;
     d.full = pl.full;
     d.gray = pl.gray;
+    d.gbr = k.mode == kPlanGbr;
     const SwsAxis* ax[4] = {&pl.hl, &pl.hc, &pl.vl, &pl.vc};
     int32_t* taps[4] = {&d.hl_taps, &d.hc_taps, &d.vl_taps, &d.vc_taps};
     int32_t* sizes[4] = {&d.hl_size, &d.hc_size, &d.vl_size, &d.vc_size};
@@ -436,7 +459,7 @@ class PlanCache {
             if (xs0 >= xs1) continue;
             const int64_t ncl = xs1 - xs0;
             const int64_t ncc = pl.gray ? 0 : pl.full ? ncl : ((xs1 - 1) >> 1) - (xs0 >> 1) + 1;
-            const int64_t h = 2 * (ncl * sws_col_stride((int)lrows) +
+            const int64_t h = 2 * ((d.gbr ? 3 : 1) * ncl * sws_col_stride((int)lrows) +
                                    (pl.gray ? 0 : 2 * ncc * sws_col_stride((int)crows)));
             lds = std::max(lds, (h + 15) & ~(int64_t)15);
           }
@@ -469,7 +492,7 @@ class PlanCache {
 // a swscale input format here
 int chroma_shifts(const spdl_hj_image_info& p, int* hs, int* vs) {
   *hs = *vs = 0;
-  if (p.ncomp == 1) return SPDL_HJ_OK;
+  if (p.ncomp != 3) return SPDL_HJ_OK;  // gray, or 4 components all 1x1 (probe)
   const int hmax = std::max(p.h_samp[0], std::max(p.h_samp[1], p.h_samp[2]));
   const int vmax = std::max(p.v_samp[0], std::max(p.v_samp[1], p.v_samp[2]));
   if (p.h_samp[0] != hmax || p.v_samp[0] != vmax || p.h_samp[1] != p.h_samp[2] ||
@@ -495,6 +518,7 @@ struct Layout {
   int sws_bands = 0, sws_chunks = 0, sws_lds = 0;
   bool all_special = true;  // every image takes swscale's unscaled converter
   bool fuse_ok = true;      // ... with standard 4:2:0 / 4:2:2 MCUs (idct_rgb_kernel)
+  int64_t cmyk_px = 0;      // 4-component images needing cmyk_kernel's K transform: max pixels
   int fused_tiles = 0;      // idct_rgb_kernel workgroups per image (max)
 };
 
@@ -520,6 +544,13 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     d.width = p.width;
     d.height = p.height;
     d.ncomp = p.ncomp;
+    d.adobe = p.adobe;
+    if (p.ncomp == 4) {
+      // libjpeg's JFIF conversion has no CMYK -> RGB; the K transform
+      // (FFmpeg's, cmyk_kernel) runs unless the planes are YCbCr + K
+      if (out->csc == SPDL_HJ_CSC_JFIF) return fail(i, SPDL_HJ_ERR_UNSUPPORTED, "CMYK with csc=jfif");
+      if (p.adobe != 1) L.cmyk_px = std::max(L.cmyk_px, (int64_t)p.width * p.height);
+    }
     int hmax = 1, vmax = 1;
     for (int c = 0; c < p.ncomp; c++) {
       d.h_samp[c] = p.h_samp[c];
@@ -527,7 +558,7 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
       hmax = p.h_samp[c] > hmax ? p.h_samp[c] : hmax;
       vmax = p.v_samp[c] > vmax ? p.v_samp[c] : vmax;
     }
-    int bw[3] = {0, 0, 0}, bh[3] = {0, 0, 0};
+    int bw[kMaxComp] = {}, bh[kMaxComp] = {};
     int64_t nblocks;
     if (p.ncomp == 1) {
       bw[0] = (p.width + 7) / 8;
@@ -590,7 +621,10 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     if (!plans || out->csc == SPDL_HJ_CSC_JFIF) continue;
     int hs, vs;
     if ((rc = chroma_shifts(p, &hs, &vs))) return fail(i, rc, nullptr);
-    const PlanKey key{p.width, p.height, hs, vs, p.ncomp == 1, out->resize ? out->filter : 0,
+    // 4 components: RGB planes after the K transform (Adobe 0 / no marker), or
+    // YCbCr 4:4:4 (Adobe 1, 2): FFmpeg's GBRAP / YUVA444P frames
+    const int mode = p.ncomp == 1 ? kPlanGray : p.ncomp == 4 && p.adobe != 1 && p.adobe != 2 ? kPlanGbr : kPlanYuv;
+    const PlanKey key{p.width, p.height, hs, vs, mode, out->resize ? out->filter : 0,
                       g.sw, g.sh, g.dx, g.dy, g.ow, g.oh};
     auto plan = plans->get(key, &rc);
     if (!plan) return fail(i, rc, rc == SPDL_HJ_ERR_BAD_GEOMETRY ? "scale filter too long" : nullptr);
@@ -888,6 +922,10 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
     HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
                      static_cast<const uint2*>(W.bdesc.p), desc, infos,
                      static_cast<uint8_t*>(W.planes.p), idct_kind, L.max_blocks, n, st));
+  // 4-component frames: FFmpeg's K transform on the planes (not on the raw
+  // planes surface, which returns the IDCT output as the oracle does)
+  if (!planes_only && L.cmyk_px > 0)
+    HJ_HIP(launch_cmyk(desc, infos, static_cast<uint8_t*>(W.planes.p), L.cmyk_px, n, st));
   mark(ctx, slot, 5, st);
   BatchParams bp{};
   bp.n = n;

@@ -318,7 +318,11 @@ def _native_planes(planes: list) -> np.ndarray:
       yuvj422p  [1, 2H, W]       (convert_yuv422p)
     A frame whose planes do not fit that shape (odd 4:2:0 / 4:2:2 sizes)
     fails the copy there ("Failed to copy image data."); other samplings
-    (yuvj440p, yuvj411p) are "Unsupported pixel format"."""
+    (yuvj440p, yuvj411p) are "Unsupported pixel format", and so are the
+    4-plane frames FFmpeg makes of Adobe CMYK / YCCK files (gbrap,
+    yuva444p: not in convert_frames' list, conversion.cpp:420-444)."""
+    if len(planes) == 4:
+        raise RuntimeError("Unsupported pixel format: gbrap / yuva444p (4-component JPEG)")
     if len(planes) == 1:
         return np.ascontiguousarray(planes[0])[:, :, None]
     (H, W), (ch, cw) = planes[0].shape, planes[1].shape

@@ -111,10 +111,15 @@ def case(name: str) -> bytes:
         return _with_segment(case("prog_420"), 0xE2, _ff_blob(40, 30000), before_sos=0)
     if name == "prog_com_between_scans":
         return _with_segment(case("prog_420"), 0xFE, _ff_blob(41, 3000), before_sos=1)
+    # Adobe 4-component files written by Pillow (inverted CMYK, transform 0)
+    if name == "cmyk_pillow":
+        return _cmyk_pillow(synthetic_pixels(26, 64, 64))
+    if name == "cmyk_pillow_odd":
+        return _cmyk_pillow(synthetic_pixels(27, 75, 111), quality=80)
     # sequential, one non-interleaved scan per component (reverse order);
     # Pillow cannot write these: libjpeg 9 wrote the committed files
     # (tests/gen_golden.py, oracle.lj_encode_multiscan)
-    if name in MULTISCAN:
+    if name in MULTISCAN or name in CMYK:
         with open(os.path.join(GOLD_JPEG, name + ".jpg"), "rb") as f:
             return f.read()
     raise KeyError(name)
@@ -127,6 +132,15 @@ MULTISCAN = {
     "multiscan_444_odd": (31, 101, 67, 85, 1, 1, 0),
     "multiscan_422_rst": (32, 120, 200, 90, 2, 1, 7),
 }
+# Adobe CMYK (transform 0) / YCCK (transform 2), libjpeg 9 from inverted CMYK
+# pixels (tests/gen_golden.py, cmyk_pixels + oracle.lj_encode_cmyk):
+# name -> (pixels seed, h, w, quality, ycck, restart blocks)
+CMYK = {
+    "cmyk_adobe": (33, 120, 160, 90, False, 0),
+    "ycck_adobe": (34, 120, 160, 90, True, 0),
+    "ycck_odd_rst": (35, 77, 131, 85, True, 5),
+}
+FOUR_COMPONENT = [*CMYK, "cmyk_pillow", "cmyk_pillow_odd"]
 LARGE_PROGRESSIVE = ["prog_large_420", "prog_large_noise", "prog_large_restart", "prog_1080p"]
 PROGRESSIVE = ["prog_420", "prog_444_odd", "prog_422", "prog_gray", "prog_optimized",
                "prog_restart", "prog_noise_q100"]
@@ -137,7 +151,7 @@ VALID = [
     "q90_420", "q75_420", "q95_420", "q90_444", "q90_422", "odd_227x333", "odd_444_101x67",
     "gray", "gray_odd", "noise_420", "noise_q100", "restart_rows", "restart_blocks",
     "restart_every_mcu", "tiny_8x8", "tiny_1x1", "optimized", "six_tables", "large_1080p",
-    *PROGRESSIVE, *MULTISCAN,
+    *PROGRESSIVE, *MULTISCAN, *FOUR_COMPONENT,
 ]
 
 
@@ -184,11 +198,25 @@ def arithmetic() -> bytes:
     return bytes(d)
 
 
-def cmyk() -> bytes:
-    """A 4-component (Adobe CMYK) JPEG: unsupported."""
+def _cmyk_pillow(px, quality=90, **kw) -> bytes:
     b = io.BytesIO()
-    Image.fromarray(synthetic_pixels(26, 64, 64)).convert("CMYK").save(b, "JPEG", quality=90)
+    Image.fromarray(px).convert("CMYK").save(b, "JPEG", quality=quality, **kw)
     return b.getvalue()
+
+
+def cmyk_pixels(seed: int, h: int, w: int) -> np.ndarray:
+    """HxWx4 Adobe-inverted CMYK whose product decode is ~ synthetic_pixels:
+    K = max(R, G, B), C = R * 255 / K (and M, Y likewise), so R ~ C * K / 255."""
+    px = synthetic_pixels(seed, h, w).astype(np.int32)
+    k = px.max(axis=2, keepdims=True)
+    cmy = np.where(k > 0, (px * 255 + k // 2) // np.maximum(k, 1), 255)
+    return np.concatenate([cmy, k], axis=2).astype(np.uint8)
+
+
+def cmyk() -> bytes:
+    """A progressive 4-component (Adobe CMYK) JPEG: unsupported (the decoder
+    takes 4-component files only as sequential interleaved 1x1 scans)."""
+    return _cmyk_pillow(synthetic_pixels(26, 64, 64), progressive=True)
 
 
 def truncated() -> bytes:

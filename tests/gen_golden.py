@@ -8,7 +8,9 @@ Fixtures (data only -- inputs and expected outputs):
   <case>.libjpeg.npz            IJG libjpeg 9d (/opt/conda/lib/libjpeg.so.9):
                                   quantised coefficients per component
                                   (jpeg_read_coefficients) and the islow /
-                                  no-fancy-upsampling RGB decode
+                                  no-fancy-upsampling RGB decode (not for
+                                  4-component CMYK/YCCK: libjpeg has no such
+                                  conversion)
   <case>.oracle.npz             oracle outputs (regression pin of the restatement):
                                   simple-IDCT planes, rgb24, pad224 resize,
                                   normalised fp16
@@ -41,7 +43,7 @@ CASES = [
     # the bench's own shape: 480x640 q90 4:2:0 (bench.py's first synthetic
     # image and the q90_420 case)
     "q90_420", "bench_1000",
-    *cases.PROGRESSIVE, *cases.MULTISCAN,
+    *cases.PROGRESSIVE, *cases.MULTISCAN, *cases.FOUR_COMPONENT,
 ]
 
 PAD224 = O.Resize(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224)
@@ -69,15 +71,19 @@ def main() -> None:
             from spdl_amd.synthetic import synthetic_pixels
 
             data = O.lj_encode_multiscan(synthetic_pixels(seed, h, w), q, h0, v0, rst)
+        elif name in cases.CMYK:  # libjpeg 9 writes these too (Adobe marker)
+            seed, h, w, q, ycck, rst = cases.CMYK[name]
+            data = O.lj_encode_cmyk(cases.cmyk_pixels(seed, h, w), q, ycck, rst)
         else:
             data = cases.case(name)
         with open(os.path.join(GOLD, "jpeg", f"{name}.jpg"), "wb") as f:
             f.write(data)
         comps = O.lj_read_coefs(data)
-        rgb = O.lj_decode_rgb(data)
+        # libjpeg converts no 4-component colour space to RGB: coefficients only
+        rgb = {} if len(comps) == 4 else dict(rgb_islow=O.lj_decode_rgb(data))
         np.savez_compressed(
             os.path.join(GOLD, f"{name}.libjpeg.npz"),
-            rgb_islow=rgb,
+            **rgb,
             **{f"coef{c}": comps[c] for c in range(len(comps))},
         )
         planes = O.decode_planes(data, O.IDCT_SIMPLE)

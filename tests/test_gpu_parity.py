@@ -70,7 +70,7 @@ RESIZES = {
 
 
 @pytest.mark.parametrize("name", ["q90_420", "odd_227x333", "gray", "q90_444", "restart_rows",
-                                  "large_1080p", "tiny_8x8"])
+                                  "large_1080p", "tiny_8x8", "cmyk_pillow_odd", "ycck_adobe"])
 @pytest.mark.parametrize("rk", list(RESIZES))
 @pytest.mark.parametrize("filt", ["bicubic", "bilinear", "lanczos"])
 def test_resize_bit_exact(decoder, oracle, name, rk, filt):
@@ -128,6 +128,32 @@ def test_batch_mixed_sizes_resize(decoder, oracle):
     for i, d in enumerate(datas):
         ref = oracle.decode_resize(d, oracle.Resize(**kw), pix_fmt="rgb24")
         np.testing.assert_array_equal(hyp[i], ref, strict=True)
+
+
+@pytest.mark.parametrize("fmt", ["rgb24", "bf16"])
+def test_batch_mixed_cmyk(decoder, oracle, fmt):
+    """4-component Adobe files (CMYK transform 0 / no marker -> three RGB
+    planes through the luma filters; YCCK transform 2 -> YCbCr 4:4:4) in one
+    batch with YCbCr and gray images: per-image plans and the K transform
+    (FFmpeg's, restated by the oracle; parity unpinned against FFmpeg itself)."""
+    names = ["cmyk_adobe", "q90_420", "ycck_adobe", "gray", "cmyk_pillow", "ycck_odd_rst",
+             "cmyk_pillow_odd", "q90_444"]
+    datas = [cases.case(n) for n in names]
+    kw = RESIZES["imagenet"]
+    if fmt == "rgb24":
+        out, shape, dt = Output(pix_fmt="rgb24", resize=True, **kw), (224, 224, 3), torch.uint8
+    else:
+        out = Output(pix_fmt="rgb", resize=True, normalize=True, norm_dtype="bfloat16", **kw)
+        shape, dt = (3, 224, 224), torch.bfloat16
+    hyp = _decode(decoder, datas, out, shape, dtype=dt)
+    for i, d in enumerate(datas):
+        if fmt == "rgb24":
+            ref = oracle.decode_resize(d, oracle.Resize(**kw), pix_fmt="rgb24")
+            np.testing.assert_array_equal(hyp[i].numpy(), ref, strict=True)
+        else:
+            ref = oracle.decode_resize(d, oracle.Resize(**kw), pix_fmt="rgb", normalize=True,
+                                       norm_dtype="bfloat16")
+            np.testing.assert_array_equal(hyp[i].view(torch.int16).numpy().view(np.uint16), ref)
 
 
 def test_batch_256_fullres(decoder, oracle):

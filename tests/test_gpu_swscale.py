@@ -72,6 +72,18 @@ def test_native_planes_odd_420_fails_like_the_reference():
         sio.load_image(cases.case("odd_227x333"), filter_desc=None)
 
 
+def test_cmyk_through_the_io_surface(oracle):
+    """load_image of Adobe CMYK / YCCK files: RGB through the default filter
+    (FFmpeg's K transform, oracle-restated), and the unfiltered 4-plane frame
+    refused as the reference's convert_frames refuses gbrap / yuva444p."""
+    for name in ("cmyk_adobe", "ycck_odd_rst"):
+        d = cases.case(name)
+        hyp = sio.to_numpy(sio.load_image(d))
+        np.testing.assert_array_equal(hyp, oracle.decode_rgb(d), strict=True)
+        with pytest.raises(RuntimeError, match="Unsupported pixel format"):
+            sio.load_image(d, filter_desc=None)
+
+
 def test_native_planes_batch(oracle):
     datas = [cases.case("q90_444"), cases.case("q90_444")]
     hyp = sio.to_numpy(sio.load_image_batch(datas, width=None, height=None, pix_fmt=None))
@@ -104,6 +116,12 @@ def test_jfif_option_matches_oracle(decoder, oracle, name):
     d = cases.case(name)
     info = oracle.parse(d)
     t = torch.empty((info.height, info.width, 3), dtype=torch.uint8, device="cuda:0")
+    if info.ncomp == 4:  # libjpeg's JFIF tables have no CMYK conversion
+        with pytest.raises(oracle.OracleError):
+            oracle.decode_rgb(d, 0, "rgb24", csc="jfif")
+        with pytest.raises(RuntimeError, match="jfif"):
+            decoder.decode_batch([d], Output(pix_fmt="rgb24", csc="jfif"), t.data_ptr(), t.numel())
+        return
     decoder.decode_batch([d], Output(pix_fmt="rgb24", csc="jfif"), t.data_ptr(), t.numel())
     np.testing.assert_array_equal(t.cpu().numpy(), oracle.decode_rgb(d, 0, "rgb24", csc="jfif"))
 

@@ -54,6 +54,8 @@ def test_host_probe_matches_oracle(oracle):
         assert (info.width, info.height, info.ncomp) == (ref.width, ref.height, ref.ncomp), name
         for c in range(ref.ncomp):
             assert (info.h_samp[c], info.v_samp[c]) == (ref.comp_h[c], ref.comp_v[c])
+        if ref.ncomp == 4:  # the Adobe transform decides the planes' meaning
+            assert info.adobe == ref.adobe, name
 
 
 def test_host_probe_rejects_garbage():
@@ -65,7 +67,13 @@ def test_host_probe_rejects_garbage():
     with pytest.raises(RuntimeError, match="Failed to decode"):
         _lib.get_image_info(cases.arithmetic())  # unsupported SOF9
     with pytest.raises(RuntimeError, match="Failed to decode"):
-        _lib.get_image_info(cases.cmyk())  # unsupported 4 components
+        _lib.get_image_info(cases.cmyk())  # unsupported progressive 4 components
+    # 4 components in non-interleaved scans (one component per scan)
+    d = bytearray(cases.case("cmyk_adobe"))
+    sos = d.index(b"\xff\xda")
+    d[sos + 4] = 1
+    with pytest.raises(RuntimeError, match="Failed to decode"):
+        _lib.get_image_info(bytes(d))
 
 
 @pytest.mark.parametrize("w,h", [(640, 480), (480, 640), (333, 227), (1, 1), (1920, 1080)])
