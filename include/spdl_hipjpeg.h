@@ -97,13 +97,30 @@ typedef struct spdl_hj_output {
   int32_t csc;          /* enum spdl_hj_csc, since ABI 2 */
 } spdl_hj_output;
 
-/* ncomp 4 (since ABI 4): an Adobe CMYK / YCCK file, every component 1x1, one
- * interleaved sequential scan; `adobe` is its APP14 transform flag (0 CMYK,
- * 1 YCbCr + K, 2 YCCK; -1 without the marker, decoded as 0 like FFmpeg). */
+/* The frame's colour model (since ABI 4), decided at the SOF as FFmpeg's
+ * mjpeg decoder picks its pix_fmt: from the Adobe APP14 transform flag seen
+ * before the SOF and the component ids.
+ *   GRAY    1 component                                        (gray8)
+ *   YCBCR   3 components                                       (yuvj4xxp)
+ *   RGB     3, Adobe transform 0 or ids 'R' 'G' 'B'; all 1x1   (gbrp)
+ *   CMYK    4, all 1x1, Adobe transform 0: inverted CMYK, converted to RGB
+ *           in the decoder (R = C K 257 >> 16 ...)              (gbrap)
+ *   YCCK    4, Adobe transform 2: converted to YCbCr            (yuva444p)
+ *   YCBCRK  4, other or no marker: YCbCr, K dropped             (yuva444p)
+ * 4-component files must be one interleaved sequential scan. */
+enum spdl_hj_color {
+  SPDL_HJ_COLOR_GRAY = 0,
+  SPDL_HJ_COLOR_YCBCR = 1,
+  SPDL_HJ_COLOR_RGB = 2,
+  SPDL_HJ_COLOR_CMYK = 3,
+  SPDL_HJ_COLOR_YCCK = 4,
+  SPDL_HJ_COLOR_YCBCRK = 5,
+};
+
 typedef struct spdl_hj_image_info {
   int32_t width, height, ncomp;
   int32_t h_samp[4], v_samp[4];
-  int32_t adobe;
+  int32_t color;  /* enum spdl_hj_color, since ABI 4 */
 } spdl_hj_image_info;
 
 typedef struct spdl_hj_ctx spdl_hj_ctx;

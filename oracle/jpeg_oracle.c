@@ -76,6 +76,35 @@ static int check_huff(const uint8_t* bits) {
   return 1;
 }
 
+/* The frame's colour model, decided at the SOF as FFmpeg's mjpeg decoder
+ * picks the frame's pix_fmt (ff_mjpeg_decode_sof, as recalled; parity
+ * UNPINNED for everything but YCbCr / gray): from the Adobe APP14 transform
+ * seen so far and the component ids.
+ *   1 component                                   gray8        JO_COLOR_GRAY
+ *   3, Adobe transform 0 or ids 'R' 'G' 'B'       gbrp         JO_COLOR_RGB
+ *      (all components 1x1; FFmpeg upsamples other samplings of it itself:
+ *      unsupported here)
+ *   3, otherwise                                  yuvj4xxp     JO_COLOR_YCBCR
+ *   4 (all components 1x1), Adobe transform 0     gbrap        JO_COLOR_CMYK
+ *   4, Adobe transform 2                          yuva444p     JO_COLOR_YCCK
+ *   4, other / no marker                          yuva444p     JO_COLOR_YCBCRK
+ * (CMYK and YCCK are converted in the decoder: jo_cmyk_transform.) */
+int jo_frame_color(const jo_info* info, const int* comp_id, int* color) {
+  int all11 = 1;
+  for (int c = 0; c < info->ncomp; c++) all11 &= info->comp_h[c] == 1 && info->comp_v[c] == 1;
+  if (info->ncomp == 1) {
+    *color = JO_COLOR_GRAY;
+  } else if (info->ncomp == 3) {
+    const int rgb = info->adobe == 0 || (comp_id[0] == 'R' && comp_id[1] == 'G' && comp_id[2] == 'B');
+    if (rgb && !all11) return JO_ERR_UNSUPPORTED;
+    *color = rgb ? JO_COLOR_RGB : JO_COLOR_YCBCR;
+  } else {
+    if (!all11) return JO_ERR_UNSUPPORTED;
+    *color = info->adobe == 0 ? JO_COLOR_CMYK : info->adobe == 2 ? JO_COLOR_YCCK : JO_COLOR_YCBCRK;
+  }
+  return JO_OK;
+}
+
 int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
   memset(info, 0, sizeof(*info));
   info->adobe = -1;
@@ -147,15 +176,14 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
         if (info->comp_h[c] < 1 || info->comp_h[c] > 4 || info->comp_v[c] < 1 ||
             info->comp_v[c] > 4 || info->comp_tq[c] > 3)
           return JO_ERR_BAD_HEADER;
-        /* 4 components: the Adobe CMYK / YCCK layout, every component 1x1
-         * (FFmpeg's 4-plane pix_fmts GBRAP / YUVA444P) */
-        if (nf == 4 && (info->comp_h[c] != 1 || info->comp_v[c] != 1)) return JO_ERR_UNSUPPORTED;
       }
+      int rc = jo_frame_color(info, comp_id, &info->color);
+      if (rc) return rc;
       have_sof = 1;
     } else if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
                (m >= 0xCD && m <= 0xCF)) {
       return JO_ERR_UNSUPPORTED; /* lossless, hierarchical, arithmetic */
-    } else if (m == 0xEE) { /* APP14: Adobe's transform flag */
+    } else if (m == 0xEE) { /* APP14: Adobe's transform flag (in effect from the next SOF) */
       if (n >= 12 && memcmp(s, "Adobe", 5) == 0) info->adobe = s[11];
     } else if (m == 0xDD) { /* DRI */
       if (n < 2) return JO_ERR_BAD_HEADER;
@@ -1106,7 +1134,7 @@ static int decode_planes_info(const uint8_t* d, size_t size, const jo_info* info
  * (c, m, y / y, cb, cr = components 0..2, k = component 3).  Planes 0..2 are
  * rewritten in place; transform 1 leaves them (YCbCr + K, K dropped). */
 void jo_cmyk_transform(const jo_info* info, uint8_t* planes) {
-  if (info->ncomp != 4 || info->adobe == 1) return;
+  if (info->color != JO_COLOR_CMYK && info->color != JO_COLOR_YCCK) return;
   const uint8_t* pc[JO_MAX_COMP];
   int st[JO_MAX_COMP];
   plane_ptrs(info, planes, pc, st);
@@ -1116,7 +1144,7 @@ void jo_cmyk_transform(const jo_info* info, uint8_t* planes) {
       uint8_t* p1 = (uint8_t*)pc[1] + (size_t)y * st[1] + x;
       uint8_t* p2 = (uint8_t*)pc[2] + (size_t)y * st[2] + x;
       const int k = pc[3][(size_t)y * st[3] + x];
-      if (info->adobe == 2) {
+      if (info->color == JO_COLOR_YCCK) {
         const int r = (255 - *p0) * k, g = (128 - *p1) * k, b = (128 - *p2) * k;
         *p0 = (uint8_t)((r * 257) >> 16);
         *p1 = (uint8_t)(((g * 257) >> 16) + 128);
@@ -1177,7 +1205,10 @@ static void store_px(uint8_t* out, int fmt, int ow, int oh, int x, int y, const 
 }
 
 static int planes_to_rgb(const jo_info* info, const uint8_t* planes, int fmt, uint8_t* out) {
-  if (info->ncomp == 4) return JO_ERR_UNSUPPORTED;  /* libjpeg outputs CMYK there */
+  /* libjpeg's conversion to RGB (jdcolor.c): YCbCr, gray, and RGB-coded
+   * frames (a copy); it has none for CMYK / YCCK */
+  if (info->color != JO_COLOR_YCBCR && info->color != JO_COLOR_GRAY && info->color != JO_COLOR_RGB)
+    return JO_ERR_UNSUPPORTED;
   const uint8_t* pc[JO_MAX_COMP];
   int st[JO_MAX_COMP];
   plane_ptrs(info, planes, pc, st);
@@ -1190,6 +1221,10 @@ static int planes_to_rgb(const jo_info* info, const uint8_t* planes, int fmt, ui
       int yv = pc[0][(size_t)y * st[0] + x];
       if (info->ncomp == 1) {
         rgb[0] = rgb[1] = rgb[2] = (uint8_t)yv;
+      } else if (info->color == JO_COLOR_RGB) { /* all components 1x1 */
+        rgb[0] = (uint8_t)yv;
+        rgb[1] = pc[1][(size_t)y * st[1] + x];
+        rgb[2] = pc[2][(size_t)y * st[2] + x];
       } else {
         int cx1 = x * info->comp_h[1] / info->hmax, cy1 = y * info->comp_v[1] / info->vmax;
         int cx2 = x * info->comp_h[2] / info->hmax, cy2 = y * info->comp_v[2] / info->vmax;
@@ -1228,8 +1263,9 @@ static int sws_planes(const jo_info* info, const uint8_t* planes, int sw, int sh
   int st[JO_MAX_COMP];
   plane_ptrs(info, planes, pc, st);
   jo_sws s;
-  /* 4 components: RGB planes (CMYK) through the luma filters, or YCbCr 444 */
-  const int gbr = info->ncomp == 4 && info->adobe != 1 && info->adobe != 2;
+  /* RGB planes (an RGB frame, or CMYK after the K transform) through the
+   * luma filters; YCCK (after the transform) and YCbCr + K are YCbCr 4:4:4 */
+  const int gbr = info->color == JO_COLOR_RGB || info->color == JO_COLOR_CMYK;
   if (jo_sws_init(&s, info->width, info->height, hsub, vsub, info->ncomp == 1 || gbr, sw, sh,
                   filter)) {
     jo_sws_free(&s);

@@ -87,10 +87,14 @@ typedef struct {
   int multiscan;             /* the image takes more than one scan (progressive,
                                 or sequential with non-interleaved scans):
                                 jo_decode_coefs walks every scan */
-  int adobe;                 /* APP14 "Adobe" transform flag (0 CMYK, 1 YCbCr,
-                                2 YCCK), -1 without the marker (FFmpeg treats
-                                that as 0) */
+  int adobe;                 /* APP14 "Adobe" transform flag (0 RGB / CMYK,
+                                1 YCbCr, 2 YCCK), -1 without the marker */
+  int color;                 /* JO_COLOR_*: the frame's colour model (jo_frame_color) */
 } jo_info;
+
+enum { JO_COLOR_GRAY = 0, JO_COLOR_YCBCR = 1, JO_COLOR_RGB = 2, JO_COLOR_CMYK = 3,
+       JO_COLOR_YCCK = 4, JO_COLOR_YCBCRK = 5 };
+int jo_frame_color(const jo_info* info, const int* comp_id, int* color);
 
 typedef struct {
   int fit_w, fit_h;          /* scale box; <=0 means "input size" */

@@ -202,11 +202,14 @@ long lj_encode_multiscan(const uint8_t* px, int w, int h, int ncomp, int quality
   return n;
 }
 
-/* Fixture encoder: a 4-component JPEG from CMYK pixels (libjpeg's Adobe
- * convention: the values are written as given, Adobe APP14 marker with
- * transform 0 for JCS_CMYK, 2 for JCS_YCCK), every component 1x1. */
-long lj_encode_cmyk(const uint8_t* px, int w, int h, int quality, int ycck, int restart_blocks,
-                    uint8_t* out, size_t out_cap) {
+/* Fixture encoder for the non-YCbCr colour spaces, every component 1x1:
+ *   mode 0: 4-component CMYK from CMYK pixels (libjpeg's Adobe convention:
+ *           the values are written as given, APP14 transform 0)
+ *   mode 1: 4-component YCCK from CMYK pixels (APP14 transform 2)
+ *   mode 2: 3-component RGB from RGB pixels (component ids 'R', 'G', 'B',
+ *           APP14 transform 0, no colour transform) */
+long lj_encode_cs(const uint8_t* px, int w, int h, int quality, int mode, int restart_blocks,
+                  uint8_t* out, size_t out_cap) {
   struct jpeg_compress_struct c;
   err_t e;
   struct jpeg_destination_mgr dst;
@@ -226,16 +229,17 @@ long lj_encode_cmyk(const uint8_t* px, int w, int h, int quality, int ycck, int 
   c.dest = &dst;
   c.image_width = (JDIMENSION)w;
   c.image_height = (JDIMENSION)h;
-  c.input_components = 4;
-  c.in_color_space = JCS_CMYK;
+  const int nc = mode == 2 ? 3 : 4;
+  c.input_components = nc;
+  c.in_color_space = mode == 2 ? JCS_RGB : JCS_CMYK;
   jpeg_set_defaults(&c);
-  jpeg_set_colorspace(&c, ycck ? JCS_YCCK : JCS_CMYK);
+  jpeg_set_colorspace(&c, mode == 2 ? JCS_RGB : mode == 1 ? JCS_YCCK : JCS_CMYK);
   jpeg_set_quality(&c, quality, TRUE);
-  for (int i = 0; i < 4; i++) c.comp_info[i].h_samp_factor = c.comp_info[i].v_samp_factor = 1;
+  for (int i = 0; i < nc; i++) c.comp_info[i].h_samp_factor = c.comp_info[i].v_samp_factor = 1;
   c.restart_interval = (unsigned)restart_blocks;
   jpeg_start_compress(&c, TRUE);
   while (c.next_scanline < c.image_height) {
-    JSAMPROW row = (JSAMPROW)(px + (size_t)c.next_scanline * w * 4);
+    JSAMPROW row = (JSAMPROW)(px + (size_t)c.next_scanline * w * nc);
     jpeg_write_scanlines(&c, &row, 1);
   }
   jpeg_finish_compress(&c);

@@ -60,6 +60,7 @@ class _Info(ctypes.Structure):
         ("progressive", ctypes.c_int),
         ("multiscan", ctypes.c_int),
         ("adobe", ctypes.c_int),
+        ("color", ctypes.c_int),
     ]
 
 
@@ -426,21 +427,31 @@ def lj_encode_multiscan(px: np.ndarray, quality: int = 90, h0: int = 2, v0: int 
     return out[:n].tobytes()
 
 
+def _lj_encode_cs(px: np.ndarray, quality: int, mode: int, restart_blocks: int) -> bytes:
+    L = ljpin()
+    if L is None:
+        raise RuntimeError("libjpeg 9 pin helper not available")
+    px = np.ascontiguousarray(px, np.uint8)
+    h, w = px.shape[:2]
+    cap = h * w * 16 + 65536
+    out = np.zeros(cap, np.uint8)
+    f = L.lj_encode_cs
+    f.restype = ctypes.c_long
+    f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_size_t]
+    n = f(px.ctypes.data, w, h, quality, mode, restart_blocks, out.ctypes.data, cap)
+    if n <= 0:
+        raise RuntimeError(f"libjpeg encode failed ({n})")
+    return out[:n].tobytes()
+
+
 def lj_encode_cmyk(cmyk: np.ndarray, quality: int = 90, ycck: bool = False,
                    restart_blocks: int = 0) -> bytes:
     """Fixture encoder (libjpeg 9): a 4-component Adobe JPEG (transform 0
     CMYK, or 2 YCCK) of HxWx4 pixels, every component 1x1."""
-    L = ljpin()
-    if L is None:
-        raise RuntimeError("libjpeg 9 pin helper not available")
-    px = np.ascontiguousarray(cmyk, np.uint8)
-    h, w = px.shape[:2]
-    cap = h * w * 16 + 65536
-    out = np.zeros(cap, np.uint8)
-    f = L.lj_encode_cmyk
-    f.restype = ctypes.c_long
-    f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_size_t]
-    n = f(px.ctypes.data, w, h, quality, int(bool(ycck)), restart_blocks, out.ctypes.data, cap)
-    if n <= 0:
-        raise RuntimeError(f"libjpeg encode failed ({n})")
-    return out[:n].tobytes()
+    return _lj_encode_cs(cmyk, quality, 1 if ycck else 0, restart_blocks)
+
+
+def lj_encode_rgb_colorspace(rgb: np.ndarray, quality: int = 90, restart_blocks: int = 0) -> bytes:
+    """Fixture encoder (libjpeg 9): a 3-component JPEG coded in RGB (no
+    YCbCr transform; component ids 'R' 'G' 'B', Adobe transform 0)."""
+    return _lj_encode_cs(rgb, quality, 2, restart_blocks)

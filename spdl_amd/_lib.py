@@ -61,7 +61,7 @@ class ImageInfo(ctypes.Structure):
         ("ncomp", ctypes.c_int32),
         ("h_samp", ctypes.c_int32 * 4),
         ("v_samp", ctypes.c_int32 * 4),
-        ("adobe", ctypes.c_int32),  # APP14 transform of a 4-component file, -1 none
+        ("color", ctypes.c_int32),  # spdl_hj_color: GRAY YCBCR RGB CMYK YCCK YCBCRK
     ]
 
 
@@ -221,7 +221,7 @@ def lib() -> ctypes.CDLL:
 
 
 def get_image_info(data) -> ImageInfo:
-    """Host SOF probe (width, height, components, sampling factors)."""
+    """Host SOF probe (width, height, components, sampling factors, colour model)."""
     addr, size, keep = buffer_address(data)
     info = ImageInfo()
     rc = lib().spdl_hj_get_image_info(addr, size, ctypes.byref(info))

@@ -23,7 +23,30 @@
 
 namespace hj {
 
-constexpr int kMaxComp = 4;  // 1 (gray), 3 (YCbCr) or 4 (Adobe CMYK / YCCK, all 1x1)
+constexpr int kMaxComp = 4;  // 1 (gray), 3 (YCbCr / RGB) or 4 (Adobe CMYK / YCCK, all 1x1)
+
+// The frame's colour model (spdl_hj_color), decided at the SOF as FFmpeg's
+// mjpeg decoder picks the pix_fmt (oracle jo_frame_color): from the Adobe
+// APP14 transform seen before the SOF (-1: none) and the component ids.
+// false: a colour model this decoder does not take (RGB or 4-component
+// frames with subsampled components).
+enum { kColorGray = 0, kColorYcbcr, kColorRgb, kColorCmyk, kColorYcck, kColorYcbcrk };
+inline HJ_HD bool frame_color(int ncomp, const int32_t* h, const int32_t* v, const int* ids,
+                              int adobe, int32_t* color) {
+  bool all11 = true;
+  for (int c = 0; c < ncomp; c++) all11 = all11 && h[c] == 1 && v[c] == 1;
+  if (ncomp == 1) {
+    *color = kColorGray;
+  } else if (ncomp == 3) {
+    const bool rgb = adobe == 0 || (ids[0] == 'R' && ids[1] == 'G' && ids[2] == 'B');
+    if (rgb && !all11) return false;
+    *color = rgb ? kColorRgb : kColorYcbcr;
+  } else {
+    if (!all11) return false;
+    *color = adobe == 0 ? kColorCmyk : adobe == 2 ? kColorYcck : kColorYcbcrk;
+  }
+  return true;
+}
 constexpr int kMaxBpm = 10;
 constexpr int kLutBits = 10;
 constexpr int kLutSize = 1 << kLutBits;
@@ -139,7 +162,7 @@ struct ImageDesc {      // host-filled per image
   SwsDesc sws;
   int64_t ds_off;       // destuff chunk records: offset and count
   int32_t ds_cap;
-  int32_t adobe;        // APP14 Adobe transform (host probe), -1 without the marker
+  int32_t color;        // spdl_hj_color (host probe)
   int64_t rec_off;      // entropy symbol records: offset (u32 units) and capacity
   int64_t rec_cap;
 };
@@ -178,7 +201,7 @@ struct ImageInfo {      // device-filled by the parse kernel
   int32_t multiscan;    // parse: progressive, or sequential with non-interleaved scans
                         // (multiscan_kernel decodes it; destuff / entropy skip it)
   int32_t progressive;  // parse: SOF2
-  int32_t adobe;        // parse: APP14 Adobe transform flag, -1 without the marker
+  int32_t color;        // parse: spdl_hj_color, decided at the SOF (frame_color)
   int64_t tphase[4];    // diagnostics: wall_clock64 ticks of the entropy phases
   int64_t dbg[4];       // diagnostics: symbols (round 0), wave iterations, shader clocks, rt ticks
 };

@@ -258,15 +258,15 @@ void parallel_pack(CopyPool* pool, uint8_t* base, const std::vector<CopyItem>& i
 }
 
 // ---- host SOF probe (replaces nvjpegGetImageInfo) --------------------------
-// Stops at the SOF, except for 4 components: the walk then goes on to the
-// first SOS for the APP14 Adobe transform (the parse kernel's rule: the last
-// APP14 before the scan) and the scan shape (one interleaved sequential scan).
+// The SOF fields and the frame's colour model (frame_color: the APP14 Adobe
+// flag seen before the SOF, the component ids).  A 4-component frame is
+// walked on to its first SOS: it must be one interleaved scan.
 int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
   memset(info, 0, sizeof(*info));
-  info->adobe = -1;
   if (!d || size < 4 || d[0] != 0xFF || d[1] != 0xD8) return SPDL_HJ_ERR_NOT_JPEG;
   size_t pos = 2;
   bool have_sof = false;
+  int adobe = -1;
   for (;;) {
     while (pos < size && d[pos] != 0xFF) pos++;
     while (pos < size && d[pos] == 0xFF) pos++;
@@ -279,15 +279,13 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
     if (len < 2 || pos + (size_t)len > size) return SPDL_HJ_ERR_BAD_HEADER;
     const uint8_t* s = d + pos + 2;
     pos += (size_t)len;
-    if (m == 0xDA) {  // 4 components: one interleaved scan of all four
-      if (len < 3 || s[0] != 4) return SPDL_HJ_ERR_UNSUPPORTED;
-      return SPDL_HJ_OK;
-    }
+    if (m == 0xDA)  // 4 components: one interleaved scan of all four
+      return len >= 3 && s[0] == 4 ? SPDL_HJ_OK : SPDL_HJ_ERR_UNSUPPORTED;
+    if (have_sof) continue;
     if (m == 0xEE) {
-      if (len >= 14 && memcmp(s, "Adobe", 5) == 0) info->adobe = s[11];
+      if (len >= 14 && memcmp(s, "Adobe", 5) == 0) adobe = s[11];
       continue;
     }
-    if (have_sof) continue;
     if (m == 0xC0 || m == 0xC1 || m == 0xC2) {  // sequential or progressive Huffman
       if (len < 8) return SPDL_HJ_ERR_BAD_HEADER;
       if (s[0] != 8) return SPDL_HJ_ERR_UNSUPPORTED;
@@ -298,15 +296,17 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
       if (info->width == 0) return SPDL_HJ_ERR_BAD_HEADER;
       if (info->ncomp != 1 && info->ncomp != 3 && info->ncomp != 4) return SPDL_HJ_ERR_UNSUPPORTED;
       if (len < 8 + 3 * info->ncomp) return SPDL_HJ_ERR_BAD_HEADER;
+      int ids[kMaxComp] = {};
       for (int c = 0; c < info->ncomp; c++) {
+        ids[c] = s[6 + 3 * c];
         info->h_samp[c] = s[7 + 3 * c] >> 4;
         info->v_samp[c] = s[7 + 3 * c] & 15;
         if (info->h_samp[c] < 1 || info->h_samp[c] > 4 || info->v_samp[c] < 1 ||
             info->v_samp[c] > 4)
           return SPDL_HJ_ERR_BAD_HEADER;
-        if (info->ncomp == 4 && (info->h_samp[c] != 1 || info->v_samp[c] != 1))
-          return SPDL_HJ_ERR_UNSUPPORTED;
       }
+      if (!frame_color(info->ncomp, info->h_samp, info->v_samp, ids, adobe, &info->color))
+        return SPDL_HJ_ERR_UNSUPPORTED;
       if (info->ncomp != 4) return SPDL_HJ_OK;
       if (m == 0xC2) return SPDL_HJ_ERR_UNSUPPORTED;  // progressive CMYK
       have_sof = true;
@@ -544,12 +544,12 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     d.width = p.width;
     d.height = p.height;
     d.ncomp = p.ncomp;
-    d.adobe = p.adobe;
+    d.color = p.color;
     if (p.ncomp == 4) {
       // libjpeg's JFIF conversion has no CMYK -> RGB; the K transform
       // (FFmpeg's, cmyk_kernel) runs unless the planes are YCbCr + K
       if (out->csc == SPDL_HJ_CSC_JFIF) return fail(i, SPDL_HJ_ERR_UNSUPPORTED, "CMYK with csc=jfif");
-      if (p.adobe != 1) L.cmyk_px = std::max(L.cmyk_px, (int64_t)p.width * p.height);
+      if (p.color != kColorYcbcrk) L.cmyk_px = std::max(L.cmyk_px, (int64_t)p.width * p.height);
     }
     int hmax = 1, vmax = 1;
     for (int c = 0; c < p.ncomp; c++) {
@@ -621,9 +621,11 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     if (!plans || out->csc == SPDL_HJ_CSC_JFIF) continue;
     int hs, vs;
     if ((rc = chroma_shifts(p, &hs, &vs))) return fail(i, rc, nullptr);
-    // 4 components: RGB planes after the K transform (Adobe 0 / no marker), or
-    // YCbCr 4:4:4 (Adobe 1, 2): FFmpeg's GBRAP / YUVA444P frames
-    const int mode = p.ncomp == 1 ? kPlanGray : p.ncomp == 4 && p.adobe != 1 && p.adobe != 2 ? kPlanGbr : kPlanYuv;
+    // RGB planes (gbrp; CMYK after the K transform, gbrap) through the luma
+    // filters; YCCK after the transform and YCbCr + K are YCbCr 4:4:4
+    const int mode = p.ncomp == 1                                        ? kPlanGray
+                     : p.color == kColorRgb || p.color == kColorCmyk ? kPlanGbr
+                                                                      : kPlanYuv;
     const PlanKey key{p.width, p.height, hs, vs, mode, out->resize ? out->filter : 0,
                       g.sw, g.sh, g.dx, g.dy, g.ow, g.oh};
     auto plan = plans->get(key, &rc);

@@ -91,7 +91,7 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
   int have_sof = 0, prog = 0;
   int comp_id[kMaxComp] = {};
   int comp_tq[kMaxComp] = {};
-  in.adobe = -1;
+  int adobe = -1;
   int pos = 2;
   for (;;) {
     while (pos < size && d[pos] != 0xFF) pos++;
@@ -159,16 +159,15 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
         if (in.comp_h[c] < 1 || in.comp_h[c] > 4 || in.comp_v[c] < 1 || in.comp_v[c] > 4 ||
             comp_tq[c] > 3)
           return kErrBadHeader;
-        // 4 components: Adobe CMYK / YCCK, every component 1x1 (oracle jo_parse)
-        if (nf == 4 && (in.comp_h[c] != 1 || in.comp_v[c] != 1)) return kErrUnsupported;
       }
+      if (!frame_color(nf, in.comp_h, in.comp_v, comp_id, adobe, &in.color)) return kErrUnsupported;
       have_sof = 1;
     } else if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
                (m >= 0xCD && m <= 0xCF)) {
       return kErrUnsupported;
-    } else if (m == 0xEE) {  // APP14 "Adobe": the transform flag of a 4-component file
+    } else if (m == 0xEE) {  // APP14 "Adobe": the transform flag, for the next SOF
       if (n >= 12 && p[0] == 'A' && p[1] == 'd' && p[2] == 'o' && p[3] == 'b' && p[4] == 'e')
-        in.adobe = p[11];
+        adobe = p[11];
     } else if (m == 0xDD) {
       if (n < 2) return kErrBadHeader;
       in.ri = be16(p);
@@ -286,7 +285,7 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     if (rc == kOk) {
       // the host probe sized every buffer; it must agree with the device parse
       if (s.info.width != dd.width || s.info.height != dd.height || s.info.ncomp != dd.ncomp ||
-          s.info.nblocks != dd.nblocks || (s.info.ncomp == 4 && s.info.adobe != dd.adobe))
+          s.info.nblocks != dd.nblocks || s.info.color != dd.color)
         rc = kErrBadHeader;
       for (int c = 0; c < s.info.ncomp && rc == kOk; c++)
         if (s.info.comp_h[c] != dd.h_samp[c] || s.info.comp_v[c] != dd.v_samp[c])
@@ -2674,7 +2673,13 @@ __global__ void __launch_bounds__(256) csc_kernel(const uint8_t* __restrict__ pl
       const int cx2 = x * in.comp_h[2] / in.hmax, cy2 = y * in.comp_v[2] / in.vmax;
       const int cb = planes[dd.plane_off[1] + (int64_t)cy1 * dd.plane_stride[1] + cx1];
       const int cr = planes[dd.plane_off[2] + (int64_t)cy2 * dd.plane_stride[2] + cx2];
-      ycc_rgb(yv, cb, cr, rgb);
+      if (in.color == kColorRgb) {  // libjpeg's RGB-coded frame: a copy (1x1)
+        rgb[0] = yv;
+        rgb[1] = cb;
+        rgb[2] = cr;
+      } else {
+        ycc_rgb(yv, cb, cr, rgb);
+      }
     }
     store_rgb(out, dd.out_off, p.pix_fmt, p.dtype, W, H, x, y, rgb, p);
   }
@@ -3366,10 +3371,10 @@ __global__ void __launch_bounds__(256) cmyk_kernel(const ImageDesc* __restrict__
                                                    uint8_t* __restrict__ planes) {
   const int img = blockIdx.y;
   const ImageInfo& in = infos[img];
-  if (in.status != kOk || in.ncomp != 4 || in.adobe == 1) return;
+  if (in.status != kOk || (in.color != kColorCmyk && in.color != kColorYcck)) return;
   const ImageDesc& dd = desc[img];
   const int wq = (in.width + 3) >> 2, stride = dd.plane_stride[0];
-  const bool ycck = in.adobe == 2;
+  const bool ycck = in.color == kColorYcck;
   const int64_t nq = (int64_t)wq * in.height;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq;
        i += (int64_t)gridDim.x * blockDim.x) {

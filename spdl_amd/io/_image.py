@@ -243,7 +243,8 @@ def load_image_batch(
         arrs = []
         for i, s in enumerate(srcs):
             try:
-                arrs.append(_native_planes(dec.decode_planes(_read(s), stream=_stream(cfg))))
+                data = _read(s)
+                arrs.append(_native_planes(dec.decode_planes(data, stream=_stream(cfg)), data))
             except Exception as err:  # reference: log, skip, raise later if strict
                 _LG.error("Failed to load image %d: %s", i, err)
         if strict and len(arrs) != len(srcs):
@@ -307,7 +308,10 @@ def load_image_batch(
     return buf
 
 
-def _native_planes(planes: list) -> np.ndarray:
+_UNSUPPORTED_FRAMES = {2: "gbrp", 3: "gbrap", 4: "yuva444p", 5: "yuva444p"}  # by spdl_hj_color
+
+
+def _native_planes(planes: list, data) -> np.ndarray:
     """The buffer the reference's convert_frames makes of an unfiltered
     frame (src/libspdl/core/detail/ffmpeg/conversion.cpp:172-303,411-454,
     single-frame form conversion.h:45-53): av_image_copy_to_buffer packs Y,
@@ -319,10 +323,11 @@ def _native_planes(planes: list) -> np.ndarray:
     A frame whose planes do not fit that shape (odd 4:2:0 / 4:2:2 sizes)
     fails the copy there ("Failed to copy image data."); other samplings
     (yuvj440p, yuvj411p) are "Unsupported pixel format", and so are the
-    4-plane frames FFmpeg makes of Adobe CMYK / YCCK files (gbrap,
-    yuva444p: not in convert_frames' list, conversion.cpp:420-444)."""
-    if len(planes) == 4:
-        raise RuntimeError("Unsupported pixel format: gbrap / yuva444p (4-component JPEG)")
+    frames FFmpeg makes of RGB-coded and Adobe CMYK / YCCK files (gbrp,
+    gbrap, yuva444p: not in convert_frames' list, conversion.cpp:420-444)."""
+    fmt = _UNSUPPORTED_FRAMES.get(_lib.get_image_info(data).color)
+    if fmt is not None:
+        raise RuntimeError(f"Unsupported pixel format: {fmt}")
     if len(planes) == 1:
         return np.ascontiguousarray(planes[0])[:, :, None]
     (H, W), (ch, cw) = planes[0].shape, planes[1].shape
@@ -362,7 +367,7 @@ def load_image(
     data = _read(src)
     if filter_desc is None:
         dec = _lib.thread_decoder(cfg.device_index)
-        arr = _native_planes(dec.decode_planes(data, stream=_stream(cfg)))
+        arr = _native_planes(dec.decode_planes(data, stream=_stream(cfg)), data)
         if device_config is not None:
             return CUDABuffer(torch.from_numpy(arr).to(f"cuda:{cfg.device_index}"))
         return CPUBuffer(arr)

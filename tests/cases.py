@@ -119,7 +119,15 @@ def case(name: str) -> bytes:
     # sequential, one non-interleaved scan per component (reverse order);
     # Pillow cannot write these: libjpeg 9 wrote the committed files
     # (tests/gen_golden.py, oracle.lj_encode_multiscan)
-    if name in MULTISCAN or name in CMYK:
+    # one colour cue removed: the APP14 marker (ids 'R' 'G' 'B' left; a CMYK
+    # file without it is YCbCr + K), or the ids (renumbered 1 2 3)
+    if name == "rgb_ids_only":
+        return _strip_app14(case("rgb_coded"))
+    if name == "cmyk_no_marker":
+        return _strip_app14(case("cmyk_adobe"))
+    if name == "rgb_adobe_only":
+        return _renumber_ids(case("rgb_coded"))
+    if name in MULTISCAN or name in CMYK or name in RGB_CODED:
         with open(os.path.join(GOLD_JPEG, name + ".jpg"), "rb") as f:
             return f.read()
     raise KeyError(name)
@@ -140,7 +148,12 @@ CMYK = {
     "ycck_adobe": (34, 120, 160, 90, True, 0),
     "ycck_odd_rst": (35, 77, 131, 85, True, 5),
 }
-FOUR_COMPONENT = [*CMYK, "cmyk_pillow", "cmyk_pillow_odd"]
+FOUR_COMPONENT = [*CMYK, "cmyk_pillow", "cmyk_pillow_odd", "cmyk_no_marker"]
+# 3 components coded in RGB (FFmpeg's gbrp frames): libjpeg 9 JCS_RGB writes
+# ids 'R' 'G' 'B' and an Adobe transform-0 marker; the variants keep one cue
+# each. name -> (pixels seed, h, w, quality, restart blocks)
+RGB_CODED = {"rgb_coded": (36, 100, 150, 90, 0), "rgb_coded_odd_rst": (37, 77, 131, 85, 4)}
+RGB_VARIANTS = ["rgb_ids_only", "rgb_adobe_only"]
 LARGE_PROGRESSIVE = ["prog_large_420", "prog_large_noise", "prog_large_restart", "prog_1080p"]
 PROGRESSIVE = ["prog_420", "prog_444_odd", "prog_422", "prog_gray", "prog_optimized",
                "prog_restart", "prog_noise_q100"]
@@ -151,7 +164,7 @@ VALID = [
     "q90_420", "q75_420", "q95_420", "q90_444", "q90_422", "odd_227x333", "odd_444_101x67",
     "gray", "gray_odd", "noise_420", "noise_q100", "restart_rows", "restart_blocks",
     "restart_every_mcu", "tiny_8x8", "tiny_1x1", "optimized", "six_tables", "large_1080p",
-    *PROGRESSIVE, *MULTISCAN, *FOUR_COMPONENT,
+    *PROGRESSIVE, *MULTISCAN, *FOUR_COMPONENT, *RGB_CODED, *RGB_VARIANTS,
 ]
 
 
@@ -202,6 +215,22 @@ def _cmyk_pillow(px, quality=90, **kw) -> bytes:
     b = io.BytesIO()
     Image.fromarray(px).convert("CMYK").save(b, "JPEG", quality=quality, **kw)
     return b.getvalue()
+
+
+def _strip_app14(data: bytes) -> bytes:
+    i = data.index(b"\xff\xee")
+    n = int.from_bytes(data[i + 2 : i + 4], "big")
+    return data[:i] + data[i + 2 + n :]
+
+
+def _renumber_ids(data: bytes) -> bytes:
+    """Component ids 'R' 'G' 'B' -> 1 2 3 in the SOF and the SOS."""
+    d = bytearray(data)
+    sof, sos = d.index(b"\xff\xc0"), d.index(b"\xff\xda")
+    for c in range(3):
+        assert d[sof + 10 + 3 * c] == b"RGB"[c] and d[sos + 5 + 2 * c] == b"RGB"[c]
+        d[sof + 10 + 3 * c] = d[sos + 5 + 2 * c] = c + 1
+    return bytes(d)
 
 
 def cmyk_pixels(seed: int, h: int, w: int) -> np.ndarray:

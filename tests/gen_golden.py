@@ -43,7 +43,8 @@ CASES = [
     # the bench's own shape: 480x640 q90 4:2:0 (bench.py's first synthetic
     # image and the q90_420 case)
     "q90_420", "bench_1000",
-    *cases.PROGRESSIVE, *cases.MULTISCAN, *cases.FOUR_COMPONENT,
+    *cases.PROGRESSIVE, *cases.MULTISCAN, *cases.FOUR_COMPONENT, *cases.RGB_CODED,
+    *cases.RGB_VARIANTS,
 ]
 
 PAD224 = O.Resize(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224)
@@ -74,13 +75,22 @@ def main() -> None:
         elif name in cases.CMYK:  # libjpeg 9 writes these too (Adobe marker)
             seed, h, w, q, ycck, rst = cases.CMYK[name]
             data = O.lj_encode_cmyk(cases.cmyk_pixels(seed, h, w), q, ycck, rst)
+        elif name in cases.RGB_CODED:
+            from spdl_amd.synthetic import synthetic_pixels
+
+            seed, h, w, q, rst = cases.RGB_CODED[name]
+            data = O.lj_encode_rgb_colorspace(synthetic_pixels(seed, h, w), q, rst)
         else:
             data = cases.case(name)
         with open(os.path.join(GOLD, "jpeg", f"{name}.jpg"), "wb") as f:
             f.write(data)
         comps = O.lj_read_coefs(data)
-        # libjpeg converts no 4-component colour space to RGB: coefficients only
-        rgb = {} if len(comps) == 4 else dict(rgb_islow=O.lj_decode_rgb(data))
+        # libjpeg converts YCbCr / gray / RGB-coded frames to RGB, no CMYK / YCCK:
+        # coefficients only for those
+        # (and rgb_adobe_only: libjpeg 9 takes ids 1 2 3 for YCbCr ahead of the
+        # Adobe transform-0 flag, FFmpeg -- the reference -- the flag for RGB)
+        skip = O.parse(data).color > 2 or name == "rgb_adobe_only"
+        rgb = {} if skip else dict(rgb_islow=O.lj_decode_rgb(data))
         np.savez_compressed(
             os.path.join(GOLD, f"{name}.libjpeg.npz"),
             **rgb,

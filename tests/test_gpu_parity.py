@@ -46,7 +46,8 @@ def test_fullres_rgb_bit_exact(decoder, oracle, name, pix_fmt):
     np.testing.assert_array_equal(hyp, ref, strict=True)
 
 
-@pytest.mark.parametrize("name", ["q90_420", "odd_227x333", "gray", "restart_blocks", "noise_420"])
+@pytest.mark.parametrize("name", ["q90_420", "odd_227x333", "gray", "restart_blocks", "noise_420",
+                                  "rgb_coded", "rgb_ids_only"])
 def test_islow_matches_libjpeg_fixture(decoder, oracle, name):
     """islow mode end-to-end vs libjpeg 9d when the pin helper is present."""
     d = cases.case(name)
@@ -70,7 +71,8 @@ RESIZES = {
 
 
 @pytest.mark.parametrize("name", ["q90_420", "odd_227x333", "gray", "q90_444", "restart_rows",
-                                  "large_1080p", "tiny_8x8", "cmyk_pillow_odd", "ycck_adobe"])
+                                  "large_1080p", "tiny_8x8", "cmyk_pillow_odd", "ycck_adobe",
+                                  "rgb_coded_odd_rst"])
 @pytest.mark.parametrize("rk", list(RESIZES))
 @pytest.mark.parametrize("filt", ["bicubic", "bilinear", "lanczos"])
 def test_resize_bit_exact(decoder, oracle, name, rk, filt):
@@ -132,12 +134,13 @@ def test_batch_mixed_sizes_resize(decoder, oracle):
 
 @pytest.mark.parametrize("fmt", ["rgb24", "bf16"])
 def test_batch_mixed_cmyk(decoder, oracle, fmt):
-    """4-component Adobe files (CMYK transform 0 / no marker -> three RGB
-    planes through the luma filters; YCCK transform 2 -> YCbCr 4:4:4) in one
-    batch with YCbCr and gray images: per-image plans and the K transform
-    (FFmpeg's, restated by the oracle; parity unpinned against FFmpeg itself)."""
+    """Colour models in one batch: Adobe CMYK (K transform -> three RGB
+    planes through the luma filters), YCCK (-> YCbCr 4:4:4), YCbCr + K (no
+    marker: K dropped), RGB-coded 3-component frames (gbrp), YCbCr and gray:
+    per-image plans and the K transform (FFmpeg's, restated by the oracle;
+    parity unpinned against FFmpeg itself)."""
     names = ["cmyk_adobe", "q90_420", "ycck_adobe", "gray", "cmyk_pillow", "ycck_odd_rst",
-             "cmyk_pillow_odd", "q90_444"]
+             "cmyk_pillow_odd", "q90_444", "rgb_coded", "cmyk_no_marker", "rgb_adobe_only"]
     datas = [cases.case(n) for n in names]
     kw = RESIZES["imagenet"]
     if fmt == "rgb24":

@@ -76,7 +76,7 @@ def test_cmyk_through_the_io_surface(oracle):
     """load_image of Adobe CMYK / YCCK files: RGB through the default filter
     (FFmpeg's K transform, oracle-restated), and the unfiltered 4-plane frame
     refused as the reference's convert_frames refuses gbrap / yuva444p."""
-    for name in ("cmyk_adobe", "ycck_odd_rst"):
+    for name in ("cmyk_adobe", "ycck_odd_rst", "rgb_coded", "cmyk_no_marker"):
         d = cases.case(name)
         hyp = sio.to_numpy(sio.load_image(d))
         np.testing.assert_array_equal(hyp, oracle.decode_rgb(d), strict=True)

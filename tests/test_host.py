@@ -54,8 +54,7 @@ def test_host_probe_matches_oracle(oracle):
         assert (info.width, info.height, info.ncomp) == (ref.width, ref.height, ref.ncomp), name
         for c in range(ref.ncomp):
             assert (info.h_samp[c], info.v_samp[c]) == (ref.comp_h[c], ref.comp_v[c])
-        if ref.ncomp == 4:  # the Adobe transform decides the planes' meaning
-            assert info.adobe == ref.adobe, name
+        assert info.color == ref.color, name  # the frame's colour model
 
 
 def test_host_probe_rejects_garbage():

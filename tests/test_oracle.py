@@ -37,7 +37,8 @@ def test_islow_pipeline_matches_libjpeg(oracle, name):
     (dct_method=JDCT_ISLOW, do_fancy_upsampling=FALSE)."""
     ref = np.load(os.path.join(GOLD, name + ".libjpeg.npz"))
     if "rgb_islow" not in ref.files:
-        pytest.skip("libjpeg has no CMYK/YCCK -> RGB conversion (coefficients pinned only)")
+        pytest.skip("libjpeg has no CMYK/YCCK -> RGB conversion, or reads the colour cues "
+                    "differently from FFmpeg (coefficients pinned only)")
     ref = ref["rgb_islow"]
     hyp = oracle.decode_rgb(_jpeg(name), oracle.IDCT_ISLOW, "rgb24", csc="jfif")
     np.testing.assert_array_equal(hyp, ref, strict=True)
@@ -382,11 +383,12 @@ def test_metadata_segments_do_not_change_pixels(oracle):
 
 def test_cmyk_ycck_decode(oracle):
     """4-component Adobe files (FFmpeg mjpeg, parity unpinned: libjpeg has no
-    CMYK/YCCK -> RGB conversion to pin against): transform 0 / no marker is
-    inverted CMYK -> RGB = C * K * 257 >> 16 per channel (restated here from
-    the raw planes); transform 2 YCCK inverts Y, Cb, Cr against K first and
-    then takes the YCbCr path.  Both decode the fixtures' source pixels to
-    within JPEG error (the fixtures were made from cases.cmyk_pixels)."""
+    CMYK/YCCK -> RGB conversion to pin against): transform 0 is inverted
+    CMYK -> RGB = C * K * 257 >> 16 per channel (restated here from the raw
+    planes); transform 2 YCCK inverts Y, Cb, Cr against K first and then takes
+    the YCbCr path.  Both decode the fixtures' source pixels to within JPEG
+    error (the fixtures were made from cases.cmyk_pixels).  Without the
+    marker the frame is YCbCr + K: same planes, no transform."""
     from spdl_amd.synthetic import synthetic_pixels
     from tests import cases
 
@@ -395,6 +397,13 @@ def test_cmyk_ycck_decode(oracle):
         info = oracle.parse(data)
         assert info.ncomp == 4
         rgb = oracle.decode_rgb(data).astype(np.int64)
+        if name == "cmyk_no_marker":
+            assert (info.adobe, info.color) == (-1, 5)
+            ref = cases.case("cmyk_adobe")
+            for a, b in zip(oracle.decode_planes(data), oracle.decode_planes(ref)):
+                np.testing.assert_array_equal(a, b)
+            assert np.abs(rgb - oracle.decode_rgb(ref)).mean() > 30
+            continue
         if info.adobe != 2:
             p = [x.astype(np.int64) for x in oracle.decode_planes(data)]
             exp = np.stack([(p[c] * p[3] * 257) >> 16 for c in range(3)], axis=-1)
@@ -406,3 +415,21 @@ def test_cmyk_ycck_decode(oracle):
             seed, h, w = {"cmyk_pillow": (26, 64, 64), "cmyk_pillow_odd": (27, 75, 111)}[name]
         src = synthetic_pixels(seed, h, w).astype(np.int64)
         assert np.abs(rgb - src).mean() < 6.0, name  # a wrong sign or bias is > 30
+
+
+def test_rgb_coded_decode(oracle):
+    """3-component RGB-coded files (FFmpeg gbrp: Adobe transform 0 or ids
+    'R' 'G' 'B'): full-resolution rgb24 is the planes themselves, and it is
+    the source pixels to within JPEG error."""
+    from spdl_amd.synthetic import synthetic_pixels
+    from tests import cases
+
+    for name in [*cases.RGB_CODED, *cases.RGB_VARIANTS]:
+        data = cases.case(name)
+        assert oracle.parse(data).color == 2, name
+        p = oracle.decode_planes(data)
+        rgb = oracle.decode_rgb(data)
+        np.testing.assert_array_equal(rgb, np.stack(p, axis=-1))
+        seed, h, w = cases.RGB_CODED.get(name, cases.RGB_CODED["rgb_coded"])[:3]
+        src = synthetic_pixels(seed, h, w).astype(np.int64)
+        assert np.abs(rgb - src).mean() < 4.0, name
