@@ -239,8 +239,10 @@ int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
  * bytes, and diagnostics diag[0..3] = {status, clean_len, nseg, sync_rounds},
  * diag[4..7] = entropy phase durations (wall_clock64 ticks, 100 MHz) for
  * round 0, sync rounds, prefix scan, write pass; diag[8..11] debug counters
- * (round-0 symbols, wave iterations, shader clocks, realtime ticks); diag
- * must hold 12 ints. */
+ * (round-0 symbols, wave iterations, shader clocks, realtime ticks);
+ * diag[12 + 3 s .. 14 + 3 s] multi-scan images, scan s < 16: start and end
+ * (realtime ticks from the decode start) and Huffman symbols; diag must hold
+ * 60 ints. */
 int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, int16_t* coefs,
                           size_t coef_cap, uint8_t* clean, size_t clean_cap, int32_t* diag,
                           char* err, size_t errlen);

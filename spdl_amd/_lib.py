@@ -480,7 +480,7 @@ class Decoder:
         addr, size, keep = buffer_address(data)
         coefs = np.zeros((nblocks, 64), np.int16)
         clean = np.zeros(size, np.uint8)
-        diag = np.zeros(12, np.int32)
+        diag = np.zeros(60, np.int32)
         err = ctypes.create_string_buffer(1024)
         rc = lib().spdl_hj_debug_entropy(self._h, addr, size, coefs.ctypes.data,
                                          coefs.size, clean.ctypes.data, clean.size,
@@ -491,7 +491,8 @@ class Decoder:
             "status": int(diag[0]), "clean_len": int(diag[1]), "nseg": int(diag[2]),
             "sync_rounds": int(diag[3]),
             "phase_us": [round(int(x) / 100.0, 1) for x in diag[4:8]],
-            "dbg": [int(x) for x in diag[8:12]]}
+            "dbg": [int(x) for x in diag[8:12]],
+            "scans": [tuple(int(x) for x in diag[12 + 3 * s:15 + 3 * s]) for s in range(16)]}
 
     def decode_planes(self, data, idct: str = "simple", stream=None):
         import numpy as np

@@ -204,6 +204,8 @@ struct ImageInfo {      // device-filled by the parse kernel
   int32_t color;        // parse: spdl_hj_color, decided at the SOF (frame_color)
   int64_t tphase[4];    // diagnostics: wall_clock64 ticks of the entropy phases
   int64_t dbg[4];       // diagnostics: symbols (round 0), wave iterations, shader clocks, rt ticks
+  int32_t sdiag[48];    // diagnostics, multiscan: per scan (16) start / end (wall_clock64
+                        // ticks from the decode start) and Huffman symbols decoded
 };
 
 // destuff: chunk-parallel over kDsChunk-byte chunks; per-chunk counts and prefixes

@@ -1545,6 +1545,7 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   diag[3] = hi.sync_rounds;
   for (int i = 0; i < 4; i++) diag[4 + i] = (int32_t)hi.tphase[i];
   for (int i = 0; i < 4; i++) diag[8 + i] = (int32_t)hi.dbg[i];
+  for (int i = 0; i < 48; i++) diag[12 + i] = hi.sdiag[i];
   // expand the coefficient lists (see BlockOut in hj_kernels.hip) to the dense
   // natural-order blocks the IDCT consumes
   const size_t nbk = (size_t)L.desc[0].nblocks;

@@ -1511,38 +1511,33 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
 // multiscan_kernel: progressive (SOF2) and sequential non-interleaved JPEGs.
 // One workgroup per image.  The whole workgroup finds the marker candidates
 // (one coalesced pass over the file), thread 0 walks the segments and records
-// every scan with its dependencies, then kMsDec decoder waves each take the
-// next ready scan, build its Huffman tables in their own LDS and decode it
-// wave-uniformly (a progressive scan's meaning depends on every earlier scan
-// of its blocks, so each scan is one sequential pass; independent scans run
-// at once; images run in parallel, one per CU).  Levels accumulate as int32
-// in the image's coefficient-list region, which the final pass turns into
-// the lists idct_kernel reads.  Arithmetic: oracle ms_decode (jpeg_oracle.c), libjpeg
+// every scan with its dependencies, then every wave of the workgroup is a
+// scan decoder: it takes the next ready scan and decodes it wave-uniformly (a
+// progressive scan's meaning depends on every earlier scan of its blocks, so
+// each scan is one sequential pass; independent scans run at once; images
+// run in parallel, one per CU).  Levels accumulate as int32 in the image's
+// coefficient-list region, which the final pass turns into the lists
+// idct_kernel reads.  Arithmetic: oracle ms_decode (jpeg_oracle.c), libjpeg
 // jdphuff.c semantics, FFmpeg-style dequantisation.
+//
+// The decoder keeps its whole working set in registers, so that the serial
+// bit chain never waits on LDS:
+//   - state (bit buffer, positions, predictors, EOB run) in SGPRs;
+//   - the file's bytes through scalar loads (constant address space), the
+//     next dword prefetched one refill ahead;
+//   - Huffman tables as VGPRs read with v_readlane at a uniform lane
+//     (RTab: a 6-bit first level, the canonical limits for the rest);
+//   - a block's coefficients gathered in the lanes of one VGPR (v_writelane)
+//     and stored as one coalesced band store;
+//   - AC refinement: 64-block chunks, the blocks' non-zero masks in VGPR
+//     lanes (prefetched a chunk ahead), the correction / new-coefficient
+//     records written to the lanes of the decoding block, and applied by
+//     the lanes (one block each) at the chunk end to levels loaded at the
+//     chunk start.
 // ---------------------------------------------------------------------------
 
 constexpr int kMsMaxScans = 64;
 constexpr int kMsMaxMarks = 512;
-constexpr int kMsLook = 9;
-// kMsDec decoder waves decode independent scans at once (scans conflict
-// when they share a component and overlapping coefficient bands).  A scan
-// decoder reads only LDS: the scan's raw bytes are staged in its wave's
-// window of kMsWinBytes, restaged by the wave's lanes whenever the reader
-// gets within the scan's margin of its end at an MCU start (an MCU of b
-// blocks takes < 432 b bytes even with every byte stuffed).  AC refinement
-// scans run in chunks of kMsChunk blocks: the wave stages each block's
-// history mask beforehand and applies the decoder's records afterwards.
-constexpr int kMsDec = 2;
-constexpr int kMsWinBytes = 8192;
-constexpr int kMsChunk = 128;
-
-struct MsTable {
-  uint16_t look[1 << kMsLook];  // (len << 8) | sym for codes <= kMsLook bits, else 0
-  int32_t maxcode[18];
-  int32_t valoff[17];
-  uint8_t vals[256];
-  uint8_t bits[17];
-};
 
 struct MsScan {
   int32_t ns, comp[kMaxComp], td[kMaxComp], ta[kMaxComp];
@@ -1551,161 +1546,228 @@ struct MsScan {
   int32_t dht[8];      // file offset of the DHT entry in effect per slot (-1: none)
 };
 
-// One decoder wave's LDS.
-struct MsWave {
-  MsTable tab[8];  // DC 0..3, AC 0..3 (slot 4 + id), as the wave's scan defines them
-  uint32_t win[kMsWinBytes / 4 + 2];  // raw bytes [wb, wb + kMsWinBytes) (+2 words of slack)
-  // AC refinement chunk, per block: coefficients [ss, se] non-zero before the
-  // scan (bit k), correction bits in coefficient order (LSB first), the
-  // coefficients the scan makes non-zero and their signs (1: negative)
-  uint64_t hist[kMsChunk], corr[kMsChunk], nmask[kMsChunk], nsign[kMsChunk];
-};
-
 struct MsShared {
-  MsWave wv[kMsDec];
   MsScan scan[kMsMaxScans];
-  uint64_t deps[kMsMaxScans];  // earlier scans a scan must wait for
+  uint64_t deps[kMsMaxScans];  // earlier scans a scan must wait for (to finish)
+  uint64_t soft[kMsMaxScans];  // ... or only to run ahead of it (trailing, below)
+  int32_t prog[kMsMaxScans];   // blocks a scan has finished, in scan order
   uint64_t claimed, done;      // scans taken by a decoder wave / finished
   int64_t tkind[4];            // diagnostics: decode ticks by scan kind
   int32_t marks[kMsMaxMarks];
+  int32_t sdiag[48];                  // diagnostics (ImageInfo::sdiag)
   int32_t dht[8], comp_id[kMaxComp];  // segment walk state (thread 0)
   int32_t nmarks, nscans, err;
 };
 
-// The scan decoder runs on all of wave 0 with identical values in every lane
-// (wave-uniform: its state lives in SGPRs and its bit twiddling is scalar
-// ALU work; a single active lane would run it on the vector unit at a
-// fraction of the rate).  Every LDS / global read is made uniform with
-// readfirstlane; stores and atomics come from lane 0 only.
+// Wave-uniform values: every LDS / global read of the decoder's inputs goes
+// through readfirstlane; stores and atomics of one value come from lane 0.
 __device__ __forceinline__ uint32_t ms_u(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int ms_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t ms_u64(uint64_t v) {
   return (uint64_t)ms_u((uint32_t)(v >> 32)) << 32 | ms_u((uint32_t)v);
 }
 __device__ __forceinline__ bool ms_lane0() { return __lane_id() == 0; }
-// order a wave's own LDS writes before its later reads (the compiler must
-// not move memory operations across; the hardware keeps a wave's LDS
-// operations in order)
-__device__ __forceinline__ void ms_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+// lane i of v (i uniform): v_readlane; v with lane i set to x
+__device__ __forceinline__ uint32_t ms_rl(uint32_t v, int i) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+}
+__device__ __forceinline__ uint32_t ms_wl(uint32_t v, uint32_t x, int i) {
+  return (int)__lane_id() == i ? x : v;  // v_cmp + v_cndmask
 }
 
-// The staged window of the file's raw bytes (little-endian words).
-struct MsWin {
-  const uint32_t* w;
-  int base, lim;  // bytes [base, lim) are staged
-  __device__ __forceinline__ uint32_t at(int i) const {
-    const int k = i - base;
-    return (ms_u(w[k >> 2]) >> (8 * (k & 3))) & 0xFFu;
-  }
-  // bytes i .. i + 3 as a big-endian word
-  __device__ __forceinline__ uint32_t be32(int i) const {
-    const int k = i - base;
-    const uint64_t two = (uint64_t)ms_u(w[k >> 2]) | ((uint64_t)ms_u(w[(k >> 2) + 1]) << 32);
-    return __builtin_bswap32((uint32_t)(two >> (8 * (k & 3))));
-  }
-};
+// An SGPR value the compiler may not re-derive (it would turn a sign test of
+// the bit buffer's top word back into a 64-bit compare, which only the VALU
+// has).  No instruction.
+__device__ __forceinline__ void ms_opaque(uint32_t& v) { asm("" : "+s"(v)); }
+__device__ __forceinline__ void ms_opaque(int& v) { asm("" : "+s"(v)); }
+
+// The file's bytes as dwords in the constant address space: uniform loads of
+// them are scalar loads (the bytes are never written while the kernel runs).
+typedef const uint32_t __attribute__((address_space(4)))* MsWords;
 
 // Bit reader over stuffed entropy data: 0xFF00 -> 0xFF; any other marker (or
 // the scan end) stops the data, zeros follow (oracle bitrd_t).  Four plain
-// bytes (no 0xFF among them) enter the buffer at once.
+// bytes (no 0xFF among them) enter the buffer at once from two prefetched
+// dwords; `fake` counts the zero bits appended past the data (the
+// truncation test: more bits used than the data held).
 struct MsBits {
-  MsWin src;
-  int pos, end;
-  uint64_t buf;
-  int cnt;
-  bool marker, overrun;
-  int64_t real, used;
+  MsWords w;
+  int size, pos, end;
+  uint64_t buf;  // left-justified
+  int cnt, fake;
+  uint32_t n0, n1;  // dwords pos >> 2 and (pos >> 2) + 1
+  bool marker;
+  int lastw;  // last dword holding a byte of the file
+  // dword i (clamped: never a byte past the file is used)
+  __device__ __forceinline__ uint32_t word(int i) const { return w[i < lastw ? i : lastw]; }
+  __device__ __forceinline__ uint32_t byte(int i) const {
+    return (word(i >> 2) >> (8 * (i & 3))) & 0xFFu;
+  }
+  // dwords i, i + 1: two scalar loads, each clamped as above (and so not
+  // merged into one 8-byte load, which would need 8-byte alignment to be
+  // a scalar load)
+  __device__ __forceinline__ void pair(int i) {
+    n0 = word(i);
+    n1 = word(i + 1);
+  }
   __device__ __forceinline__ void start(int p, int e) {
     pos = p;
     end = e;
     buf = 0;
     cnt = 0;
+    fake = 0;
     marker = false;
-    real = used = 0;
+    pair(p >> 2);
   }
-  // (tops the buffer up to >= 32 bits: every caller needs at most 32, and
-  // one 4-byte step then suffices -- the byte path costs an LDS round trip
-  // per byte)
+  // tops the buffer up to >= 32 bits (every step needs at most 32).  The
+  // next refill's 8 bytes are loaded right after each 4-byte step, so the
+  // scalar load has a few symbols' time to land.
   __device__ __forceinline__ void fill() {
     while (cnt < 32) {
-      if (!marker && cnt <= 32 && pos + 4 <= end && pos + 4 <= src.lim) {
-        const uint32_t v = src.be32(pos);
-        if (((~v - 0x01010101u) & v & 0x80808080u) == 0u) {  // no 0xFF byte
-          buf |= (uint64_t)v << (32 - cnt);
+      if (!marker && pos + 4 <= end) {
+        const uint32_t x = (uint32_t)((((uint64_t)n1 << 32) | n0) >> (8 * (pos & 3)));
+        if (((~x - 0x01010101u) & x & 0x80808080u) == 0u) {  // no 0xFF byte
+          // (bswap is a VALU v_perm: back to an SGPR at once, or the whole bit
+          // buffer would follow it onto the vector unit)
+          buf |= (uint64_t)ms_u(__builtin_bswap32(x)) << (32 - cnt);
           cnt += 32;
           pos += 4;
-          real += 32;
+          pair(pos >> 2);
           continue;
         }
       }
-      uint32_t byte = 0;
+      uint32_t b = 0;
       if (!marker) {
         if (pos >= end) {
           marker = true;
-        } else if (pos + 1 >= src.lim && pos + 1 < end) {
-          marker = true;  // past the staged window (cannot happen within the margin)
-          overrun = true;
         } else {
-          const uint32_t c = src.at(pos);
+          const uint32_t c = byte(pos);
           if (c == 0xFFu) {
-            const uint32_t nx = pos + 1 < end ? src.at(pos + 1) : 0xD9u;
-            if (nx == 0u) {
+            const uint32_t nb = pos + 1 < end ? byte(pos + 1) : 0xD9u;
+            if (nb == 0u) {
               pos += 2;
-              byte = 0xFFu;
-              real += 8;
+              b = 0xFFu;
             } else {
               marker = true;
             }
           } else {
             pos++;
-            byte = c;
-            real += 8;
+            b = c;
           }
         }
+        pair(pos >> 2);
       }
-      buf |= (uint64_t)byte << (56 - cnt);
+      if (marker) fake += 8;
+      buf |= (uint64_t)b << (56 - cnt);
       cnt += 8;
     }
   }
-  __device__ __forceinline__ uint32_t peek16() {
+  __device__ __forceinline__ void need() {
     if (cnt < 32) fill();
-    return (uint32_t)(buf >> 48);
+  }
+  __device__ __forceinline__ uint32_t hi32() const { return (uint32_t)(buf >> 32); }
+  __device__ __forceinline__ uint32_t peek16() const { return hi32() >> 16; }
+  // the next s bits (1..16) as a JPEG signed value (F.2.2.1 EXTEND), taken;
+  // the sign test on the 32-bit top word (SALU has no 64-bit signed
+  // compare: a 64-bit one is a VALU v_cmp, ~40 cycles back to the scalar unit)
+  __device__ __forceinline__ int take_ext(int s) {
+    uint32_t h = hi32();
+    ms_opaque(h);
+    const int v = (int)(h >> (32 - s));
+    skip(s);
+    return (int32_t)h < 0 ? v : v + 1 - (1 << s);
+  }
+  // one bit, taken
+  __device__ __forceinline__ uint32_t take_bit() {
+    uint32_t h = hi32();
+    ms_opaque(h);
+    skip(1);
+    return h >> 31;
   }
   __device__ __forceinline__ void skip(int n) {
     buf <<= n;
     cnt -= n;
-    used += n;
   }
-  __device__ __forceinline__ uint32_t get(int n) {  // n <= 32
-    if (n == 0) return 0u;
-    if (cnt < 32) fill();
-    const uint32_t v = (uint32_t)(buf >> (64 - n));
+  // n in 1..32 bits already in the buffer
+  __device__ __forceinline__ uint32_t take(int n) {
+    const uint32_t v = hi32() >> (32 - n);
     skip(n);
     return v;
   }
-  // symbol, or -1 for an invalid code
-  __device__ __forceinline__ int decode(const MsTable& t) {
-    const uint32_t w = peek16();
-    const uint32_t e = ms_u(t.look[w >> (16 - kMsLook)]);
-    if (e) {
-      skip((int)(e >> 8));
-      return (int)(e & 0xFFu);
-    }
-    for (int l = kMsLook + 1; l <= 16; l++) {
-      const int code = (int)(w >> (16 - l));
-      if (code <= ms_i(t.maxcode[l])) {
-        skip(l);
-        return ms_i(t.vals[ms_i(t.valoff[l]) + code]);
-      }
-    }
-    return -1;
+  __device__ __forceinline__ uint32_t get(int n) {  // n in 0..32
+    if (n == 0) return 0u;
+    need();
+    return take(n);
   }
+  __device__ __forceinline__ bool truncated() const { return fake > cnt; }
 };
 
-__device__ __forceinline__ int ms_extend(uint32_t v, int s) {
-  return v < (1u << (s - 1)) ? (int)v - ((1 << s) - 1) : (int)v;
+// A Huffman table held in four VGPRs (one entry per lane):
+//   l1   lane p: the code starting with the 6-bit prefix p, len | symbol << 8
+//        (0: the code is longer than 6 bits)
+//   lim  lane l in 1..16: sum over i <= l of bits[i] << (16 - i), i.e. the
+//        first left-justified 16-bit word past the codes of length <= l
+//        (monotone; ~0 on the other lanes): a word w has the code length
+//        1 + #{l : lim[l] <= w} (17: invalid)
+//   voff lane l: (symbols of length < l) - (first code of length l)
+//   vals lane i: symbols 4i .. 4i + 3
+struct RTab {
+  uint32_t l1, lim, voff, vals;
+};
+
+// Builds the table of the DHT entry at file offset o (uniform); all lanes.
+// Sets bad for an over-subscribed code (oracle: code > 1 << l).
+__device__ __noinline__ RTab rt_build(const uint8_t* __restrict__ d, int o, int lane, bool& bad) {
+  RTab t;
+  const bool len_lane = lane >= 1 && lane <= 16;
+  const int nb = len_lane ? d[o + lane] : 0;
+  const uint32_t lim = (uint32_t)wave_incl_scan(len_lane ? nb << (16 - lane) : 0);
+  const int kc = wave_incl_scan(nb);
+  const int total = (int)ms_rl((uint32_t)kc, 16);
+  bad = ms_rl(lim, 16) > 65536u;
+  const uint32_t limp = (uint32_t)__shfl_up((int)lim, 1, 64);
+  const int kp = __shfl_up(kc, 1, 64);
+  t.lim = len_lane ? lim : ~0u;
+  t.voff = len_lane ? (uint32_t)kp - (lane == 1 ? 0u : (limp >> (16 - lane))) : 0u;
+  uint32_t v = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const int i = 4 * lane + b;
+    if (i < total) v |= (uint32_t)d[o + 17 + i] << (8 * b);
+  }
+  t.vals = v;
+  // first level: lane p decodes the word p << 10
+  const uint32_t w = (uint32_t)lane << 10;
+  int L = 1;
+#pragma unroll
+  for (int l = 1; l <= 6; l++) L += ms_rl(lim, l) <= w ? 1 : 0;
+  uint32_t e = 0;
+  const uint32_t vo = (uint32_t)__shfl((int)t.voff, L, 64);
+  if (L <= 6) {
+    const uint32_t idx = vo + (w >> (16 - L));
+    e = (uint32_t)L | ((uint32_t)d[o + 17 + idx] << 8);
+  }
+  t.l1 = e;
+  return t;
+}
+
+// symbol of the code at the top of w16 (uniform), or -1; len: its length
+__device__ __forceinline__ int rt_decode(const RTab& t, uint32_t w16, int& len) {
+  const uint32_t e = ms_rl(t.l1, (int)(w16 >> 10));
+  if (e) {
+    len = (int)(e & 31u);
+    return (int)(e >> 8);
+  }
+  int L = __popcll(__builtin_amdgcn_ballot_w64(t.lim <= w16));
+  ms_opaque(L);  // (a 32-bit count, not a 64-bit compare)
+  L += 1;
+  if (L > 16) {
+    len = 0;
+    return -1;
+  }
+  len = L;
+  const uint32_t idx = ms_rl(t.voff, L) + (w16 >> (16 - L));
+  return (int)((ms_rl(t.vals, (int)(idx >> 2)) >> (8 * (idx & 3u))) & 0xFFu);
 }
 
 // bits k .. e (inclusive) of a coefficient mask; 0 when k > e
@@ -1736,14 +1798,15 @@ __device__ __forceinline__ MsGeo ms_geo(const ImageInfo& in) {
 
 // The scalar fields of a scan record, uniform.
 struct MsBand {
-  int ns, ss, se, ah, al, ri, end;
+  int ns, ss, se, ah, al, ri, start, end;
 };
 
 __device__ __forceinline__ MsBand ms_band(const MsScan& sc) {
   return MsBand{ms_i(sc.ns), ms_i(sc.ss), ms_i(sc.se), ms_i(sc.ah), ms_i(sc.al), ms_i(sc.ri),
-                ms_i(sc.end)};
+                ms_i(sc.start), ms_i(sc.end)};
 }
 
+// MCU-order block index of component c's block (bx, by)
 __device__ __forceinline__ int ms_block(const MsGeo& g, int c, int bx, int by) {
   if (g.ncomp == 1) return by * g.mcux + bx;
   int b0 = 0;
@@ -1752,14 +1815,9 @@ __device__ __forceinline__ int ms_block(const MsGeo& g, int c, int bx, int by) {
   return ((by / vc) * g.mcux + bx / hc) * g.bpm + b0 + (by % vc) * hc + (bx % hc);
 }
 
-// MCU-order block index of component c's block (bx, by)
-__device__ __forceinline__ int ms_block(const ImageInfo& in, int c, int bx, int by) {
-  if (in.ncomp == 1) return by * in.mcux + bx;
-  int b0 = 0;
-  for (int k = 0; k < c; k++) b0 += in.comp_h[k] * in.comp_v[k];
-  const int mx = bx / in.comp_h[c], my = by / in.comp_v[c];
-  const int b = b0 + (by % in.comp_v[c]) * in.comp_h[c] + (bx % in.comp_h[c]);
-  return (my * in.mcux + mx) * in.bpm + b;
+// x / d for a sampling factor d in 1..4 (no division instruction)
+__device__ __forceinline__ int ms_div(int x, int d) {
+  return d == 1 ? x : (d == 2 ? x >> 1 : (d == 4 ? x >> 2 : (int)(((uint32_t)x * 0xAAABu) >> 17)));
 }
 
 // One correction bit per set bit of m, appended LSB-first to corr.
@@ -1774,172 +1832,229 @@ __device__ __forceinline__ void ms_take_corr(MsBits& br, uint64_t m, uint64_t& c
   }
 }
 
-// One block of one scan (a decoder wave, uniform).  lev: the block's levels in HBM (zig-zag
-// index; stores only).  AC refinement (block j of the chunk) decodes against
-// the staged history mask and leaves records for the workgroup to apply:
-// which history coefficients get a correction bit (libjpeg jdphuff
-// decode_mcu_AC_refine reads one per non-zero coefficient it passes, in
-// order) and which zero coefficients become +-(1 << al).
-__device__ __forceinline__ int ms_block_decode(MsWave& S, MsBits& br, const MsBand& sc, bool prog,
-                                               const MsTable& dh, const MsTable& ah, int32_t& pred,
-                                               int32_t* __restrict__ lev, int& eobrun, int j) {
-  if (!prog) {  // sequential scan: the whole block
-    int s = br.decode(dh);
-    if (s < 0 || s > 15) return kErrBadHuffman;
-    pred += s ? ms_extend(br.get(s), s) : 0;
-    if (ms_lane0()) lev[0] = pred;
-    for (int k = 1; k < 64;) {
-      const int rs = br.decode(ah);
-      if (rs < 0) return kErrBadHuffman;
-      const int r = rs >> 4;
-      s = rs & 15;
-      if (s == 0) {
-        if (r == 15) {
-          k += 16;
-          continue;
-        }
-        if (r != 0) return kErrBadHuffman;
-        break;
-      }
-      k += r;
-      if (k > 63) return kErrBadHuffman;
-      const int v = ms_extend(br.get(s), s);
-      if (ms_lane0()) lev[k] = v;
-      k++;
-    }
-    return kOk;
-  }
-  const int al = sc.al;
-  if (sc.ss == 0) {
-    if (sc.ah == 0) {  // DC first
-      const int s = br.decode(dh);
-      if (s < 0 || s > 15) return kErrBadHuffman;
-      pred += s ? ms_extend(br.get(s), s) : 0;
-      if (ms_lane0()) lev[0] = (int32_t)((uint32_t)pred << al);
-    } else if (br.get(1)) {  // DC refine
-      if (ms_lane0()) atomicOr(reinterpret_cast<unsigned int*>(lev), 1u << al);
-    }
-    return kOk;
-  }
-  if (sc.ah == 0) {  // AC first (spectral selection)
-    if (eobrun > 0) {
-      eobrun--;
-      return kOk;
-    }
-    for (int k = sc.ss; k <= sc.se; k++) {
-      const int rs = br.decode(ah);
-      if (rs < 0) return kErrBadHuffman;
-      const int r = rs >> 4, s = rs & 15;
-      if (s) {
-        k += r;
-        if (k > sc.se) return kErrBadHuffman;
-        const int32_t v = (int32_t)((uint32_t)ms_extend(br.get(s), s) << al);
-        if (ms_lane0()) lev[k] = v;
-      } else if (r == 15) {
-        k += 15;
-      } else {
-        eobrun = (1 << r) - 1;
-        if (r) eobrun += (int)br.get(r);
-        break;
-      }
-    }
-    return kOk;
-  }
-  // AC refinement (successive approximation) against the history mask
-  const int se = sc.se;
-  const uint64_t hist = ms_u64(S.hist[j]);
-  uint64_t corr = 0, nm = 0, nsg = 0;
-  int nc = 0, k = sc.ss;
-  if (eobrun <= 0) {
-    while (k <= se) {
-      const int rs = br.decode(ah);
-      if (rs < 0) return kErrBadHuffman;
-      const int r = rs >> 4, s = rs & 15;
-      int v = 0;
-      if (s) {
-        if (s != 1) return kErrBadHuffman;
-        v = br.get(1) ? 1 : -1;
-      } else if (r != 15) {
-        eobrun = 1 << r;
-        if (r) eobrun += (int)br.get(r);
-        break;
-      }
-      // the (r + 1)-th coefficient from k that was zero before the scan:
-      // the new coefficient's place (ZRL: the 16th zero, left zero); every
-      // non-zero one passed on the way takes a correction bit
-      uint64_t zm = ~hist & ms_range(k, se);
-      for (int i = 0; i < r && zm; i++) zm &= zm - 1;
-      if (zm == 0ull) {  // ran past se
-        ms_take_corr(br, hist & ms_range(k, se), corr, nc);
-        k = se + 1;
-        if (v) return kErrBadHuffman;
-        break;
-      }
-      const int p = __builtin_ctzll(zm);
-      ms_take_corr(br, hist & ms_range(k, p - 1), corr, nc);
-      if (v) {
-        nm |= 1ull << p;
-        nsg |= (v < 0 ? 1ull : 0ull) << p;
-      }
-      k = p + 1;
-    }
-  }
-  if (eobrun > 0) {
-    ms_take_corr(br, hist & ms_range(k, se), corr, nc);
-    eobrun--;
-  }
-  if (ms_lane0()) {
-    S.corr[j] = corr;
-    S.nmask[j] = nm;
-    S.nsign[j] = nsg;
-  }
-  return kOk;
-}
+enum { kScanSeq = 0, kScanDcFirst, kScanDcRefine, kScanAcFirst, kScanAcRefine };
+constexpr int kMsChunk = 64;  // AC refinement blocks per chunk (one per lane)
 
-// A decoder wave's scan state, carried across chunks in (scalar) registers.
-struct MsState {
-  MsBits br;
-  int32_t pred0, pred1, pred2;
-  int eobrun, mcu, nmcu, bw1;
-  bool rst_done;  // the restart marker before `mcu` was consumed
+// AC refinement chunk: the lanes' blocks (lane j = block m0 + j of the scan)
+struct MsChunk {
+  int32_t lv[64];          // the lane's block levels (zig-zag), loaded at the chunk start
+  uint32_t mlo, mhi;       // the lane's block non-zero mask (all bands)
+  uint32_t nlo, nhi;       // the same for the next chunk (prefetched)
+  uint32_t clo, chi, wlo, whi, slo, shi;  // records: correction bits, new coefficients, signs
+  int blk, nblk;           // the lane's block index (-1: none) / the next chunk's
 };
 
-// A decoder wave: decode MCUs of one scan from st.mcu on, until the scan ends, the
-// chunk ends (AC refinement: MCU chunk_end) or the reader comes within the
-// margin of the staged window's end at an MCU start (wlim; unless the window
-// holds the rest of the scan).  Restart intervals, interleaved MCUs or one
-// component's blocks in raster order over its own (unpadded) block grid.
-// (Everything here is inlined into the kernel: through a call the reader
-// state would live in scratch memory and the LDS tables behind flat loads.)
-// x / d and x % d for a sampling factor d in 1..4 (no division instruction)
-__device__ __forceinline__ int ms_div(int x, int d) {
-  return d == 1 ? x : (d == 2 ? x >> 1 : (d == 4 ? x >> 2 : (int)(((uint32_t)x * 0xAAABu) >> 17)));
+// block index of scan position m of a one-component scan (per lane; -1 past the end)
+__device__ __forceinline__ int ms_lane_block(const MsGeo& g, int c1, int bw1, int nmcu, int m) {
+  return m < nmcu ? ms_block(g, c1, m % bw1, m / bw1) : -1;
 }
 
-__device__ __forceinline__ int ms_scan_chunk(MsWave& S, const uint8_t* d, int size,
-                                             const MsGeo& in, const MsScan& scl, bool prog,
-                                             int32_t* __restrict__ lv, MsState& st, int wlim,
-                                             int chunk0, int chunk_end) {
+__device__ __forceinline__ void ms_chunk_load(MsChunk& ch, const int32_t* __restrict__ lv,
+                                              int blk) {
+  ch.blk = blk;
+  if (blk >= 0) {
+    const uint4* src = reinterpret_cast<const uint4*>(lv + (size_t)blk * 64);
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const uint4 x = src[q];
+      ch.lv[4 * q] = (int32_t)x.x;
+      ch.lv[4 * q + 1] = (int32_t)x.y;
+      ch.lv[4 * q + 2] = (int32_t)x.z;
+      ch.lv[4 * q + 3] = (int32_t)x.w;
+    }
+  }
+}
+
+// Apply the chunk's records (libjpeg decode_mcu_AC_refine: a correction bit
+// adds +-p1 to a coefficient whose bit al is clear; a new coefficient is
+// +-p1), store the band's levels and the updated non-zero mask.
+__device__ __forceinline__ void ms_chunk_apply(MsChunk& ch, int32_t* __restrict__ lv,
+                                               uint64_t* __restrict__ masks, int ss, int se,
+                                               int al) {
+  if (ch.blk < 0) return;
+  const uint64_t band = ms_range(ss, se);
+  const uint64_t m = (uint64_t)ch.mhi << 32 | ch.mlo;
+  uint64_t h = m & band;
+  uint64_t corr = (uint64_t)ch.chi << 32 | ch.clo;
+  const uint64_t nm = (uint64_t)ch.whi << 32 | ch.wlo;
+  const uint64_t sg = (uint64_t)ch.shi << 32 | ch.slo;
+  const int32_t p1 = 1 << al, m1 = -p1;
+#pragma unroll
+  for (int k = 1; k < 64; k++) {
+    if ((h >> k) & 1u) {
+      if (corr & 1u) {
+        const int32_t c = ch.lv[k];
+        if ((c & p1) == 0) ch.lv[k] = c + (c >= 0 ? p1 : m1);
+      }
+      corr >>= 1;
+    }
+    if ((nm >> k) & 1u) ch.lv[k] = ((sg >> k) & 1u) ? m1 : p1;
+  }
+  int32_t* dst = lv + (size_t)ch.blk * 64;
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    if (4 * q >= ss && 4 * q + 3 <= se) {
+      reinterpret_cast<uint4*>(dst)[q] = make_uint4((uint32_t)ch.lv[4 * q], (uint32_t)ch.lv[4 * q + 1],
+                                                    (uint32_t)ch.lv[4 * q + 2],
+                                                    (uint32_t)ch.lv[4 * q + 3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (4 * q + e >= ss && 4 * q + e <= se) dst[4 * q + e] = ch.lv[4 * q + e];
+    }
+  }
+  // (atomic: a first scan of another band of the component may run at once)
+  if (nm) atomicOr(reinterpret_cast<unsigned long long*>(masks + ch.blk), nm);
+}
+
+// Trailing scans: a one-component AC scan may run while the earlier AC scans
+// of its component that it depends on are still decoding, one chunk of
+// kMsChunk blocks behind them (all of them visit the component's blocks in
+// the same raster order).  Every AC scan publishes how many blocks it has
+// finished (S.prog, after its level and mask stores for them); a trailing
+// scan waits at each chunk start until its producers are past the chunk.
+// The scans of a progressive image's component then overlap instead of
+// running one after another (the default script's luma chain: two AC-first
+// bands, then two refinement scans).
+__device__ __forceinline__ void ms_publish(MsShared& S, int si, int n) {
+  __threadfence_block();  // (the blocks' level / mask stores before the count)
+  if (ms_lane0()) __hip_atomic_store(&S.prog[si], n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// every scan in `soft` has finished `need` blocks (false: a scan failed)
+__device__ __forceinline__ bool ms_reached(MsShared& S, uint64_t soft, int need) {
+  for (; soft; soft &= soft - 1) {
+    const int t = __builtin_ctzll(soft);
+    if (ms_i(__hip_atomic_load(&S.prog[t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
+      return false;
+  }
+  return true;
+}
+__device__ __forceinline__ bool ms_wait(MsShared& S, uint64_t soft, int need) {
+  while (!ms_reached(S, soft, need)) {
+    if (ms_i(__hip_atomic_load(&S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != kOk)
+      return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+// t[i] for a uniform i (selects, not a dynamically indexed register array)
+__device__ __forceinline__ RTab rt_pick(int i, const RTab (&t)[kMaxComp]) {
+  RTab r = t[0];
+  if (i == 1) r = t[1];
+  if (i == 2) r = t[2];
+  if (i == 3) r = t[3];
+  return r;
+}
+__device__ __forceinline__ int32_t ms_pick(int i, const int32_t (&v)[kMaxComp]) {
+  return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
+}
+__device__ __forceinline__ void ms_put(int i, int32_t (&v)[kMaxComp], int32_t x) {
+  v[0] = i == 0 ? x : v[0];
+  v[1] = i == 1 ? x : v[1];
+  v[2] = i == 2 ? x : v[2];
+  v[3] = i == 3 ? x : v[3];
+}
+
+// Decode one scan (a whole decoder wave, uniform control flow).
+// lv: the image's levels (64 int32 per block, zig-zag); masks: per block the
+// coefficients non-zero so far (AC bands of progressive images); soft: the
+// running scans this one trails (AC scans).
+template <int kind>
+__device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft, const MsGeo& g,
+                                              const ImageInfo& in, const uint8_t* __restrict__ d,
+                                              int size, int32_t* __restrict__ lv,
+                                              uint64_t* __restrict__ masks, int lane, int& nsym) {
+  const MsScan& scl = S.scan[si];
   const MsBand sc = ms_band(scl);
-  const bool refine = prog && sc.ss > 0 && sc.ah > 0;
-  // the state in locals for the loop (a select between members of a
-  // referenced struct becomes a load from a selected scratch address)
-  MsBits br = st.br;
-  int32_t pred0 = st.pred0, pred1 = st.pred1, pred2 = st.pred2;
-  int eobrun = st.eobrun, mcu = st.mcu;
-  bool rst_done = st.rst_done;
-  const int nmcu = st.nmcu, bw1 = st.bw1;
-  // MCU / block coordinates advance incrementally (one division per chunk)
-  const int c1 = ms_i(scl.comp[0]);  // the component of a one-component scan
-  const int hc1 = in.ncomp == 1 ? 1 : in.h(c1), vc1 = in.ncomp == 1 ? 1 : in.v(c1);
-  int b01 = 0;  // blocks of the components before c1 in an MCU
-  for (int k = 0; k < c1; k++) b01 += in.h(k) * in.v(k);
-  int bx = mcu % bw1, by = mcu / bw1;            // one-component scans
-  int rpos = sc.ri ? mcu % sc.ri : 0;            // MCUs since the last restart
+  // AC scans of a progressive image have one component
+  constexpr bool kAc = kind == kScanAcFirst || kind == kScanAcRefine;
+  constexpr int kComp = kAc ? 1 : kMaxComp;
+  constexpr bool need_dc = kind == kScanSeq || kind == kScanDcFirst;
+  constexpr bool need_ac = kind == kScanSeq || kAc;
   int rc = kOk;
-  for (; mcu < nmcu; mcu++, rst_done = false) {
-    if (sc.ri && mcu && rpos == 0 && !rst_done) {
-      if (br.used > br.real) {
+  // tables per scan component, as the scan reads them
+  RTab tdc[kMaxComp], tac[kMaxComp];
+#pragma unroll
+  for (int i = 0; i < kComp; i++) {
+    if (i < sc.ns) {
+      bool bad = false, bad2 = false;
+      if (need_dc) {
+        const int o = ms_i(scl.dht[ms_i(scl.td[i])]);
+        if (o < 0) rc = kErrBadHeader;
+        else tdc[i] = rt_build(d, o, lane, bad);
+      }
+      if (need_ac) {
+        const int o = ms_i(scl.dht[4 + ms_i(scl.ta[i])]);
+        if (o < 0) rc = kErrBadHeader;
+        else tac[i] = rt_build(d, o, lane, bad2);
+      }
+      if (bad || bad2) rc = kErrBadHeader;
+    }
+  }
+  if (rc != kOk) return rc;
+  int nmcu = ms_i(in.mcux) * ms_i(in.mcuy), bw1 = 1;
+  const int c1 = ms_i(scl.comp[0]);  // the component of a one-component scan
+  if (sc.ns == 1) {
+    bw1 = g.ncomp == 1 ? g.mcux : (ms_i(in.comp_w[c1]) + 7) / 8;
+    nmcu = bw1 * (g.ncomp == 1 ? ms_i(in.mcuy) : (ms_i(in.comp_hpx[c1]) + 7) / 8);
+  }
+  const int hc1 = g.ncomp == 1 ? 1 : g.h(c1), vc1 = g.ncomp == 1 ? 1 : g.v(c1);
+  int b01 = 0;  // blocks of the components before c1 in an MCU
+  for (int k = 0; k < c1; k++) b01 += g.h(k) * g.v(k);
+  MsBits br;
+  br.w = (MsWords)(const void*)d;
+  br.size = size;
+  br.lastw = (size - 1) >> 2;
+  br.start(sc.start, sc.end);
+  int32_t pred[kMaxComp] = {0, 0, 0, 0};
+  int eobrun = 0;
+  const int al = sc.al, ss = sc.ss, se = sc.se;
+  const bool inband = lane >= ss && lane <= se;
+  const uint64_t band = ms_range(ss, se);
+  uint32_t vblk = 0;  // the block being decoded, lane k = coefficient k
+  MsChunk ch;
+  bool have_next = false;
+  if constexpr (kind == kScanAcRefine) ch.blk = -1;
+  int bx = 0, by = 0, rpos = 0;
+  for (int mcu = 0;; mcu++) {
+    if constexpr (kind == kScanAcRefine) {
+      if ((mcu & (kMsChunk - 1)) == 0 || mcu >= nmcu) {
+        // chunk boundary: apply the finished chunk, load the next one's
+        // levels and masks once the scans this one trails are past it
+        ms_chunk_apply(ch, lv, masks, ss, se, al);
+        if (mcu) ms_publish(S, si, mcu);
+        if (mcu >= nmcu) break;
+        const int nxt = min(mcu + kMsChunk, nmcu);
+        if (!have_next) {
+          if (!ms_wait(S, soft, nxt)) {
+            rc = kErrBadHuffman;  // (another scan failed; its status is the image's)
+            break;
+          }
+          ch.nblk = ms_lane_block(g, c1, bw1, nmcu, mcu + lane);
+          const uint64_t m = ch.nblk >= 0 ? masks[ch.nblk] : 0ull;
+          ch.nlo = (uint32_t)m;
+          ch.nhi = (uint32_t)(m >> 32);
+        }
+        ch.mlo = ch.nlo;
+        ch.mhi = ch.nhi;
+        ms_chunk_load(ch, lv, ch.nblk);
+        ch.clo = ch.chi = ch.wlo = ch.whi = ch.slo = ch.shi = 0;
+        // the next chunk's masks now, if its producers are already past it
+        have_next = nxt < nmcu && ms_reached(S, soft, min(nxt + kMsChunk, nmcu));
+        if (have_next) {
+          ch.nblk = ms_lane_block(g, c1, bw1, nmcu, nxt + lane);
+          const uint64_t m = ch.nblk >= 0 ? masks[ch.nblk] : 0ull;
+          ch.nlo = (uint32_t)m;
+          ch.nhi = (uint32_t)(m >> 32);
+        }
+      }
+    } else {
+      if (mcu >= nmcu) break;
+    }
+    if (sc.ri && mcu && rpos == 0) {
+      if (br.truncated()) {
         rc = kErrTruncated;
         break;
       }
@@ -1950,8 +2065,8 @@ __device__ __forceinline__ int ms_scan_chunk(MsWave& S, const uint8_t* d, int si
           rc = kErrBadRestart;
           break;
         }
-        const uint32_t c = ms_u(d[p]);
-        if (c == 0xFFu && p + 1 < size && ms_u(d[p + 1]) == 0u) {
+        const uint32_t c = br.byte(p);
+        if (c == 0xFFu && p + 1 < size && br.byte(p + 1) == 0u) {
           p += 2;
           continue;
         }
@@ -1959,47 +2074,195 @@ __device__ __forceinline__ int ms_scan_chunk(MsWave& S, const uint8_t* d, int si
         p++;
       }
       if (rc != kOk) break;
-      while (p < size && ms_u(d[p]) == 0xFFu) p++;
-      if (p >= size || ms_u(d[p]) < 0xD0u || ms_u(d[p]) > 0xD7u) {
+      while (p < size && br.byte(p) == 0xFFu) p++;
+      if (p >= size || br.byte(p) < 0xD0u || br.byte(p) > 0xD7u) {
         rc = kErrBadRestart;
         break;
       }
       br.start(p + 1, sc.end);
-      pred0 = pred1 = pred2 = 0;
+      pred[0] = pred[1] = pred[2] = pred[3] = 0;
       eobrun = 0;
-      rst_done = true;
     }
-    if (br.pos > wlim || br.pos < br.src.base) break;  // restage the window
-    if (refine && mcu >= chunk_end) break;
-    if (sc.ns > 1) {  // interleaved: the MCU's blocks are consecutive, component by component
-      for (int i = 0; i < sc.ns && rc == kOk; i++) {
+#pragma unroll 1
+    for (int i = 0; i < sc.ns && rc == kOk; i++) {
+      // the MCU's blocks of scan component i (one block for a one-component scan)
+      int b, nb = 1;
+      if (sc.ns > 1) {
         const int c = ms_i(scl.comp[i]);
-        const MsTable& dh = S.tab[ms_i(scl.td[i])];
-        const MsTable& ah = S.tab[4 + ms_i(scl.ta[i])];
-        int32_t pred = c == 0 ? pred0 : (c == 1 ? pred1 : pred2);
-        const int nb = in.h(c) * in.v(c);
-        int b = mcu * in.bpm;  // + the blocks of the image's components before c
-        for (int k = 0; k < c; k++) b += in.h(k) * in.v(k);
-        for (int u = 0; u < nb; u++, b++) {
-          rc = ms_block_decode(S, br, sc, prog, dh, ah, pred, lv + (size_t)b * 64, eobrun,
-                               mcu - chunk0);
-          if (rc != kOk) break;
-        }
-        pred0 = c == 0 ? pred : pred0;
-        pred1 = c == 1 ? pred : pred1;
-        pred2 = c == 2 ? pred : pred2;
+        nb = g.h(c) * g.v(c);
+        b = mcu * g.bpm;
+        for (int k = 0; k < c; k++) b += g.h(k) * g.v(k);
+      } else {
+        b = g.ncomp == 1 ? by * g.mcux + bx
+                         : (ms_div(by, vc1) * g.mcux + ms_div(bx, hc1)) * g.bpm + b01 +
+                               (by - ms_div(by, vc1) * vc1) * hc1 + (bx - ms_div(bx, hc1) * hc1);
       }
-    } else {
-      const int b = in.ncomp == 1
-                        ? by * in.mcux + bx
-                        : (ms_div(by, vc1) * in.mcux + ms_div(bx, hc1)) * in.bpm + b01 +
-                              (by - ms_div(by, vc1) * vc1) * hc1 + (bx - ms_div(bx, hc1) * hc1);
-      int32_t pred = c1 == 0 ? pred0 : (c1 == 1 ? pred1 : pred2);
-      rc = ms_block_decode(S, br, sc, prog, S.tab[ms_i(scl.td[0])], S.tab[4 + ms_i(scl.ta[0])],
-                           pred, lv + (size_t)b * 64, eobrun, mcu - chunk0);
-      pred0 = c1 == 0 ? pred : pred0;
-      pred1 = c1 == 1 ? pred : pred1;
-      pred2 = c1 == 2 ? pred : pred2;
+      RTab dt, at;
+      if constexpr (need_dc) dt = kComp == 1 ? tdc[0] : rt_pick(i, tdc);
+      if constexpr (need_ac) at = kComp == 1 ? tac[0] : rt_pick(i, tac);
+      int32_t pr = ms_pick(i, pred);
+      for (int u = 0; u < nb; u++, b++) {
+        int32_t* blev = lv + (size_t)b * 64;
+        if constexpr (kind == kScanDcFirst) {
+          br.need();
+          int len;
+          const int s = rt_decode(dt, br.peek16(), len);
+          nsym++;
+          if (s < 0 || s > 15) {
+            rc = kErrBadHuffman;
+            break;
+          }
+          br.skip(len);
+          pr += s ? br.take_ext(s) : 0;
+          if (ms_lane0()) blev[0] = (int32_t)((uint32_t)pr << al);
+        } else if constexpr (kind == kScanDcRefine) {
+          br.need();
+          if (br.take_bit() && ms_lane0()) atomicOr(reinterpret_cast<unsigned int*>(blev), 1u << al);
+        } else if constexpr (kind == kScanAcFirst) {
+          if (eobrun > 0) {
+            eobrun--;
+          } else {
+            uint64_t nz = 0;
+            for (int k = ss; k <= se; k++) {
+              br.need();
+              int len;
+              const int rs = rt_decode(at, br.peek16(), len);
+              nsym++;
+              if (rs < 0) {
+                rc = kErrBadHuffman;
+                break;
+              }
+              br.skip(len);
+              const int r = rs >> 4, s = rs & 15;
+              if (s) {
+                k += r;
+                if (k > se) {
+                  rc = kErrBadHuffman;
+                  break;
+                }
+                vblk = ms_wl(vblk, (uint32_t)br.take_ext(s) << al, k);
+                nz |= 1ull << k;
+              } else if (r == 15) {
+                k += 15;
+              } else {
+                eobrun = (1 << r) - 1;
+                if (r) eobrun += (int)br.take(r);
+                break;
+              }
+            }
+            if (nz) {
+              if (inband) blev[lane] = (int32_t)vblk;
+              vblk = 0;
+              if (ms_lane0()) atomicOr(reinterpret_cast<unsigned long long*>(masks + b), nz);
+            }
+          }
+          if ((mcu & (kMsChunk - 1)) == kMsChunk - 1) ms_publish(S, si, mcu + 1);
+        } else if constexpr (kind == kScanAcRefine) {
+          // against the block's non-zero mask (lane j of the chunk)
+          const int j = mcu & (kMsChunk - 1);
+          const uint64_t hist = ((uint64_t)ms_rl(ch.mhi, j) << 32 | ms_rl(ch.mlo, j)) & band;
+          uint64_t corr = 0, nm = 0, nsg = 0;
+          int nc = 0, k = ss;
+          if (eobrun <= 0) {
+            while (k <= se) {
+              br.need();
+              int len;
+              const int rs = rt_decode(at, br.peek16(), len);
+              nsym++;
+              if (rs < 0) {
+                rc = kErrBadHuffman;
+                break;
+              }
+              br.skip(len);
+              const int r = rs >> 4, s = rs & 15;
+              int v = 0;
+              if (s) {
+                if (s != 1) {
+                  rc = kErrBadHuffman;
+                  break;
+                }
+                v = br.take_bit() ? 1 : -1;  // (a flag: the compiler keeps it scalar)
+              } else if (r != 15) {
+                eobrun = 1 << r;
+                if (r) eobrun += (int)br.take(r);
+                break;
+              }
+              // the (r + 1)-th coefficient from k that was zero before the
+              // scan: the new coefficient's place (ZRL: the 16th zero, left
+              // zero); every non-zero one passed on the way takes a
+              // correction bit
+              uint64_t zm = ~hist & ms_range(k, se);
+              for (int q = 0; q < r && zm; q++) zm &= zm - 1;
+              if (zm == 0ull) {  // ran past se
+                ms_take_corr(br, hist & ms_range(k, se), corr, nc);
+                k = se + 1;
+                if (v) rc = kErrBadHuffman;
+                break;
+              }
+              const int p = __builtin_ctzll(zm);
+              ms_take_corr(br, hist & ms_range(k, p - 1), corr, nc);
+              if (v) {
+                nm |= 1ull << p;
+                nsg |= (v < 0 ? 1ull : 0ull) << p;
+              }
+              k = p + 1;
+            }
+          }
+          if (rc != kOk) break;
+          if (eobrun > 0) {
+            ms_take_corr(br, hist & ms_range(k, se), corr, nc);
+            eobrun--;
+          }
+          ch.clo = ms_wl(ch.clo, (uint32_t)corr, j);
+          ch.chi = ms_wl(ch.chi, (uint32_t)(corr >> 32), j);
+          ch.wlo = ms_wl(ch.wlo, (uint32_t)nm, j);
+          ch.whi = ms_wl(ch.whi, (uint32_t)(nm >> 32), j);
+          ch.slo = ms_wl(ch.slo, (uint32_t)nsg, j);
+          ch.shi = ms_wl(ch.shi, (uint32_t)(nsg >> 32), j);
+        } else {  // sequential: the whole block
+          br.need();
+          int len;
+          int s = rt_decode(dt, br.peek16(), len);
+          nsym++;
+          if (s < 0 || s > 15) {
+            rc = kErrBadHuffman;
+            break;
+          }
+          br.skip(len);
+          pr += s ? br.take_ext(s) : 0;
+          vblk = ms_wl(vblk, (uint32_t)pr, 0);
+          for (int k = 1; k < 64;) {
+            br.need();
+            const int rs = rt_decode(at, br.peek16(), len);
+            nsym++;
+            if (rs < 0) {
+              rc = kErrBadHuffman;
+              break;
+            }
+            br.skip(len);
+            const int r = rs >> 4;
+            s = rs & 15;
+            if (s == 0) {
+              if (r == 15) {
+                k += 16;
+                continue;
+              }
+              if (r != 0) rc = kErrBadHuffman;
+              break;
+            }
+            k += r;
+            if (k > 63) {
+              rc = kErrBadHuffman;
+              break;
+            }
+            vblk = ms_wl(vblk, (uint32_t)br.take_ext(s), k);
+            k++;
+          }
+          blev[lane] = (int32_t)vblk;
+          vblk = 0;
+        }
+      }
+      ms_put(i, pred, pr);
     }
     if (rc != kOk) break;
     if (++bx == bw1) {
@@ -2008,21 +2271,8 @@ __device__ __forceinline__ int ms_scan_chunk(MsWave& S, const uint8_t* d, int si
     }
     if (sc.ri && ++rpos == sc.ri) rpos = 0;
   }
-  if (rc == kOk && mcu >= nmcu)
-    rc = br.overrun ? kErrUnsupported : (br.used > br.real ? kErrTruncated : kOk);
-  st.br = br;
-  st.pred0 = pred0;
-  st.pred1 = pred1;
-  st.pred2 = pred2;
-  st.eobrun = eobrun;
-  st.mcu = mcu;
-  st.rst_done = rst_done;
+  if (rc == kOk) rc = br.truncated() ? kErrTruncated : kOk;
   return rc;
-}
-
-// block of MCU m of a one-component scan (AC scans)
-__device__ __forceinline__ int ms_scan_block(const ImageInfo& in, const MsScan& sc, int bw1, int m) {
-  return ms_block(in, sc.comp[0], m % bw1, m / bw1);
 }
 
 __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restrict__ bytes,
@@ -2039,6 +2289,9 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   const int size = (int)dd.in_size;
   const bool prog = in.progressive != 0;
   int32_t* lv = reinterpret_cast<int32_t*>(ents + (size_t)dd.coef_off * 64);
+  // per block non-zero coefficient masks while the scans decode (bdesc is
+  // written only by the final pass)
+  uint64_t* masks = reinterpret_cast<uint64_t*>(bdesc + dd.coef_off);
   const int nblocks = in.nblocks;
   int64_t t0 = wall_clock64(), tph[4] = {0, 0, 0, 0}, tdbg[4] = {0, 0, 0, 0};
   const MsGeo geo = ms_geo(in);
@@ -2073,6 +2326,7 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   }
   for (int i = tid; i < nblocks * 16; i += nt)
     reinterpret_cast<uint4*>(lv)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < nblocks; i += nt) masks[i] = 0ull;
   __syncthreads();
   // ---- thread 0: sort the candidates, walk the segments, record the scans ----
   if (tid == 0) {
@@ -2194,22 +2448,31 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   __syncthreads();
   tph[0] = wall_clock64() - t0;  // marker candidates + segment walk
   // ---- scan dependencies: a scan waits for every earlier scan that shares
-  // a component and overlaps its coefficient band ----
+  // a component and overlaps its coefficient band -- to finish, or, when
+  // both are one-component AC scans of a progressive image, only to stay
+  // ahead of it (soft: the later scan trails it chunk by chunk) ----
   for (int i = tid; i < S.nscans; i += nt) {
     const MsScan& x = S.scan[i];
     int cx = 0;
     for (int k = 0; k < x.ns; k++) cx |= 1 << x.comp[k];
     const int lx = prog ? x.ss : 0, hx = prog ? x.se : 63;
-    uint64_t m = 0;
+    const bool xac = prog && x.ss > 0;
+    uint64_t m = 0, sm = 0;
     for (int j = 0; j < i; j++) {
       const MsScan& y = S.scan[j];
       int cy = 0;
       for (int k = 0; k < y.ns; k++) cy |= 1 << y.comp[k];
       const int ly = prog ? y.ss : 0, hy = prog ? y.se : 63;
-      if ((cx & cy) && !(hy < lx || hx < ly)) m |= 1ull << j;
+      if ((cx & cy) && !(hy < lx || hx < ly)) {
+        if (xac && y.ss > 0) sm |= 1ull << j;  // (AC scans have one component)
+        else m |= 1ull << j;
+      }
     }
     S.deps[i] = m;
+    S.soft[i] = sm;
+    S.prog[i] = 0;
   }
+  if (tid < 48) S.sdiag[tid] = 0;
   if (tid == 0) {
     S.claimed = 0;
     S.done = 0;
@@ -2217,12 +2480,15 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   }
   __syncthreads();
   const int64_t tdec = wall_clock64();
-  // ---- decoder waves: each takes the first ready scan, decodes it with its
-  // own LDS (tables, byte window, refinement records) and marks it done ----
-  const int wid = __builtin_amdgcn_readfirstlane(tid) >> 6;  // (uniform)
+  const int64_t cdec = (int64_t)__builtin_amdgcn_s_memtime();
+  // ---- decoder waves: each takes the first ready scan, decodes it and marks
+  // it done ----
   const int lane = tid & 63;
-  if (wid < kMsDec) {
-    MsWave& W = S.wv[wid];
+#ifndef HJ_MS_WAVES
+#define HJ_MS_WAVES 4
+#endif
+  if ((__builtin_amdgcn_readfirstlane(tid) >> 6) < HJ_MS_WAVES) {
+    __builtin_amdgcn_s_setprio(2);  // the serial bit chains: first in issue
     const bool progu = ms_i(prog) != 0;
     const int sizeu = ms_i(size);
     for (;;) {
@@ -2241,7 +2507,9 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
           break;
         int cand = -1;
         for (int i = 0; i < nsc && cand < 0; i++)
-          if (!((claimed >> i) & 1ull) && (ms_u64(S.deps[i]) & ~done) == 0ull) cand = i;
+          if (!((claimed >> i) & 1ull) && (ms_u64(S.deps[i]) & ~done) == 0ull &&
+              (ms_u64(S.soft[i]) & ~(done | claimed)) == 0ull)
+            cand = i;
         if (cand < 0) {
           __builtin_amdgcn_s_sleep(2);
           continue;
@@ -2255,162 +2523,45 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
         }
       }
       if (si < 0) break;
-      __threadfence_block();  // (acquire: the scans it waited for are visible)
+      __threadfence_block();  // (acquire: the stores of the scans it waited for are visible)
       const int64_t ts = wall_clock64();
       const MsScan& sc = S.scan[si];
-      const int sns = ms_i(sc.ns), sss = ms_i(sc.ss), sah = ms_i(sc.ah);
-      int rc = kOk;
-      // tables this scan reads: DC for DC-first / sequential, AC for AC scans
-      const bool need_dc = !progu || (sss == 0 && sah == 0);
-      const bool need_ac = !progu || sss > 0;
-      for (int t = 0; t < 8 && rc == kOk; t++) {
-        bool used = false;
-        for (int i = 0; i < sns; i++)
-          used |= (t < 4 && need_dc && ms_i(sc.td[i]) == t) ||
-                  (t >= 4 && need_ac && ms_i(sc.ta[i]) == t - 4);
-        if (!used) continue;
-        const int o = ms_i(sc.dht[t]);
-        if (o < 0) {
-          rc = kErrBadHeader;
-          break;
-        }
-        MsTable& T = W.tab[t];
-        if (lane < 17) T.bits[lane] = lane == 0 ? 0 : d[o + lane];
-        ms_wave_sync();
-        // canonical arrays: every lane computes them, lane 0 stores
-        int code = 0, k = 0, total = 0;
-        for (int l = 1; l <= 16; l++) {
-          const int nb = ms_i(T.bits[l]);
-          if (ms_lane0()) {
-            T.valoff[l] = nb ? k - code : 0;
-            T.maxcode[l] = nb ? code + nb - 1 : -1;
-          }
-          code += nb;
-          k += nb;
-          total += nb;
-          if (code > (1 << l)) rc = kErrBadHeader;
-          code <<= 1;
-        }
-        if (ms_lane0()) T.maxcode[17] = 0x7FFFFFFF;
-        for (int i = lane; i < 256; i += 64) T.vals[i] = i < total ? d[o + 17 + i] : 0;
-        ms_wave_sync();
-        for (int idx = lane; idx < (1 << kMsLook); idx += 64) {
-          uint16_t e = 0;
-          for (int l = 1; l <= kMsLook; l++) {
-            const int cd = idx >> (kMsLook - l);
-            if (cd <= T.maxcode[l]) {
-              e = (uint16_t)((l << 8) | T.vals[T.valoff[l] + cd]);
-              break;
-            }
-          }
-          T.look[idx] = e;
-        }
-        ms_wave_sync();
-      }
-      const bool refine = progu && sss > 0 && sah > 0;
-      int bw1 = 1, nmcu = ms_i(in.mcux) * ms_i(in.mcuy), bpmcu = 0;
-      if (sns == 1) {
-        const int c = ms_i(sc.comp[0]);
-        bw1 = geo.ncomp == 1 ? geo.mcux : (ms_i(in.comp_w[c]) + 7) / 8;
-        nmcu = bw1 * (geo.ncomp == 1 ? ms_i(in.mcuy) : (ms_i(in.comp_hpx[c]) + 7) / 8);
-        bpmcu = 1;
-      } else {
-        for (int i = 0; i < sns; i++) bpmcu += geo.h(ms_i(sc.comp[i])) * geo.v(ms_i(sc.comp[i]));
-      }
-      // bytes one MCU can take (every byte stuffed) + the reader's look-ahead
-      const int margin = 96 + 432 * bpmcu;
-      const int sstart = ms_i(sc.start), send = ms_i(sc.end);
-      MsState st;
-      st.br.start(sstart, send);
-      st.br.overrun = false;
-      st.pred0 = st.pred1 = st.pred2 = 0;
-      st.eobrun = 0;
-      st.mcu = 0;
-      st.nmcu = nmcu;
-      st.bw1 = bw1;
-      st.rst_done = false;
-      // chunks: (re)stage the window, stage history masks (AC refinement),
-      // decode (uniform), apply the refinement records (the wave's lanes)
-      int wb = sstart & ~3, m0 = 0, staged = -1;
-      bool fin = rc != kOk;
-      while (!fin) {
-        if (wb != staged) {
-          for (int i = lane; i < kMsWinBytes / 4 + 2; i += 64) {
-            const int o = wb + 4 * i;
-            uint32_t v = 0;
-            if (o + 4 <= sizeu) {
-              v = *reinterpret_cast<const uint32_t*>(d + o);
-            } else {
-              for (int bb = 0; bb < 4 && o + bb < sizeu; bb++) v |= (uint32_t)d[o + bb] << (8 * bb);
-            }
-            W.win[i] = v;
-          }
-          staged = wb;
-        }
-        if (refine) {
-          const uint64_t band = ms_range(sss, ms_i(sc.se));
-          for (int j = lane; j < kMsChunk && m0 + j < nmcu; j += 64) {
-            const uint4* src =
-                reinterpret_cast<const uint4*>(lv + (size_t)ms_scan_block(in, sc, bw1, m0 + j) * 64);
-            uint64_t h = 0;
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-              const uint4 x = src[q];
-              h |= (uint64_t)((x.x != 0u) | (x.y != 0u) << 1 | (x.z != 0u) << 2 | (x.w != 0u) << 3)
-                   << (4 * q);
-            }
-            W.hist[j] = h & band;
-          }
-        }
-        ms_wave_sync();
-        st.br.src.w = W.win;
-        st.br.src.base = wb;
-        st.br.src.lim = min(wb + kMsWinBytes, sizeu);
-        // the window holds the rest of the scan, or the reader stops at an
-        // MCU start within the margin of its end
-        const int wlim = send <= wb + kMsWinBytes ? 0x7FFFFFFF : wb + kMsWinBytes - margin;
-        rc = ms_scan_chunk(W, d, sizeu, geo, sc, progu, lv, st, wlim, m0, m0 + kMsChunk);
-        const int m1 = st.mcu;
-        ms_wave_sync();
-        if (refine && rc == kOk) {
-          const int32_t p1 = 1 << ms_i(sc.al), m1v = -p1;
-          for (int j = lane; j < m1 - m0; j += 64) {
-            int32_t* lev = lv + (size_t)ms_scan_block(in, sc, bw1, m0 + j) * 64;
-            uint64_t h = W.hist[j], corr = W.corr[j], m = W.nmask[j];
-            const uint64_t sg = W.nsign[j];
-            for (; h; h &= h - 1, corr >>= 1) {
-              if (corr & 1u) {
-                const int kk = __builtin_ctzll(h);
-                const int32_t c = lev[kk];
-                if ((c & p1) == 0) lev[kk] = c + (c >= 0 ? p1 : m1v);
-              }
-            }
-            for (; m; m &= m - 1) {
-              const int kk = __builtin_ctzll(m);
-              lev[kk] = ((sg >> kk) & 1u) ? m1v : p1;
-            }
-          }
-        }
-        ms_wave_sync();
-        if (st.br.pos > wlim) wb = st.br.pos & ~3;
-        m0 = m1;
-        fin = rc != kOk || m1 >= nmcu;
-      }
+      const MsBand bd = ms_band(sc);
+      const uint64_t soft = ms_u64(S.soft[si]);
+      int rc, nsym = 0;
+      if (!progu)
+        rc = ms_decode_scan<kScanSeq>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
+      else if (bd.ss == 0 && bd.ah == 0)
+        rc = ms_decode_scan<kScanDcFirst>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
+      else if (bd.ss == 0)
+        rc = ms_decode_scan<kScanDcRefine>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
+      else if (bd.ah == 0)
+        rc = ms_decode_scan<kScanAcFirst>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
+      else
+        rc = ms_decode_scan<kScanAcRefine>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
       // the scan's stores are visible before it counts as done
-      __threadfence_block();
+      ms_publish(S, si, 1 << 30);
+      if (ms_lane0() && si < 16) {
+        S.sdiag[3 * si] = (int32_t)(ts - tdec);
+        S.sdiag[3 * si + 1] = (int32_t)(wall_clock64() - tdec);
+        S.sdiag[3 * si + 2] = nsym;
+      }
       if (ms_lane0()) {
         if (rc != kOk) atomicCAS(&S.err, kOk, rc);
+        const int sss = ms_i(sc.ss), sah = ms_i(sc.ah);
         const int kind = !progu ? 3 : (sss == 0 ? 0 : (sah == 0 ? 1 : 2));
         atomicAdd(reinterpret_cast<unsigned long long*>(&S.tkind[kind]),
                   (unsigned long long)(wall_clock64() - ts));
         __hip_atomic_fetch_or(&S.done, 1ull << si, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
+    __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
   tph[2] = wall_clock64() - tdec;  // decode (tables included)
 #pragma unroll
   for (int i = 0; i < 4; i++) tdbg[i] = S.tkind[i];
+  tdbg[3] = (int64_t)__builtin_amdgcn_s_memtime() - cdec;  // shader clocks of the decode
   tph[1] = 0;
   if (S.err != kOk) {
     if (tid == 0) in.status = S.err;
@@ -2448,6 +2599,7 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
     tph[3] = wall_clock64() - t0 - tph[0] - tph[1] - tph[2];  // lists
     for (int i = 0; i < 4; i++) in.tphase[i] = tph[i];
     for (int i = 0; i < 4; i++) in.dbg[i] = tdbg[i];
+    for (int i = 0; i < 48; i++) in.sdiag[i] = S.sdiag[i];
     in.sync_rounds = S.nscans;
   }
 }
