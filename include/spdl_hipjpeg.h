@@ -35,7 +35,7 @@ extern "C" {
 enum spdl_hj_status {
   SPDL_HJ_OK = 0,
   SPDL_HJ_ERR_NOT_JPEG = 1,
-  SPDL_HJ_ERR_UNSUPPORTED = 2,  /* arithmetic, lossless, 12-bit, progressive CMYK */
+  SPDL_HJ_ERR_UNSUPPORTED = 2,  /* arithmetic, lossless, hierarchical, 12-bit */
   SPDL_HJ_ERR_BAD_HEADER = 3,
   SPDL_HJ_ERR_BAD_HUFFMAN = 4,
   SPDL_HJ_ERR_TRUNCATED = 5,
@@ -107,7 +107,7 @@ typedef struct spdl_hj_output {
  *           in the decoder (R = C K 257 >> 16 ...)              (gbrap)
  *   YCCK    4, Adobe transform 2: converted to YCbCr            (yuva444p)
  *   YCBCRK  4, other or no marker: YCbCr, K dropped             (yuva444p)
- * 4-component files must be one interleaved sequential scan. */
+ * 4-component files may be sequential (interleaved or not) or progressive. */
 enum spdl_hj_color {
   SPDL_HJ_COLOR_GRAY = 0,
   SPDL_HJ_COLOR_YCBCR = 1,

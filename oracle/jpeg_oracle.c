@@ -195,7 +195,6 @@ int jo_parse(const uint8_t* d, size_t size, jo_info* info) {
       /* progressive, or sequential with non-interleaved scans: the first scan
        * fixes nothing beyond the frame; every scan is walked at decode time */
       info->multiscan = info->progressive || ns != info->ncomp;
-      if (info->multiscan && info->ncomp == 4) return JO_ERR_UNSUPPORTED;
       if (n < 1 + 2 * ns + 3) return JO_ERR_BAD_HEADER;
       int order[JO_MAX_COMP];
       for (int i = 0; i < ns; i++) {

@@ -207,7 +207,9 @@ long lj_encode_multiscan(const uint8_t* px, int w, int h, int ncomp, int quality
  *           the values are written as given, APP14 transform 0)
  *   mode 1: 4-component YCCK from CMYK pixels (APP14 transform 2)
  *   mode 2: 3-component RGB from RGB pixels (component ids 'R', 'G', 'B',
- *           APP14 transform 0, no colour transform) */
+ *           APP14 transform 0, no colour transform)
+ * plus the scan script: mode | 4 progressive (jpeg_simple_progression),
+ * mode | 8 sequential with one component per scan (non-interleaved). */
 long lj_encode_cs(const uint8_t* px, int w, int h, int quality, int mode, int restart_blocks,
                   uint8_t* out, size_t out_cap) {
   struct jpeg_compress_struct c;
@@ -229,14 +231,30 @@ long lj_encode_cs(const uint8_t* px, int w, int h, int quality, int mode, int re
   c.dest = &dst;
   c.image_width = (JDIMENSION)w;
   c.image_height = (JDIMENSION)h;
-  const int nc = mode == 2 ? 3 : 4;
+  const int cs = mode & 3;
+  const int nc = cs == 2 ? 3 : 4;
   c.input_components = nc;
-  c.in_color_space = mode == 2 ? JCS_RGB : JCS_CMYK;
+  c.in_color_space = cs == 2 ? JCS_RGB : JCS_CMYK;
   jpeg_set_defaults(&c);
-  jpeg_set_colorspace(&c, mode == 2 ? JCS_RGB : mode == 1 ? JCS_YCCK : JCS_CMYK);
+  jpeg_set_colorspace(&c, cs == 2 ? JCS_RGB : cs == 1 ? JCS_YCCK : JCS_CMYK);
   jpeg_set_quality(&c, quality, TRUE);
   for (int i = 0; i < nc; i++) c.comp_info[i].h_samp_factor = c.comp_info[i].v_samp_factor = 1;
   c.restart_interval = (unsigned)restart_blocks;
+  static jpeg_scan_info seq[4];
+  if (mode & 4) {
+    jpeg_simple_progression(&c);
+  } else if (mode & 8) {
+    for (int i = 0; i < nc; i++) {
+      seq[i].comps_in_scan = 1;
+      seq[i].component_index[0] = i;
+      seq[i].Ss = 0;
+      seq[i].Se = 63;
+      seq[i].Ah = 0;
+      seq[i].Al = 0;
+    }
+    c.scan_info = seq;
+    c.num_scans = nc;
+  }
   jpeg_start_compress(&c, TRUE);
   while (c.next_scanline < c.image_height) {
     JSAMPROW row = (JSAMPROW)(px + (size_t)c.next_scanline * w * nc);

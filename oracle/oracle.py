@@ -445,10 +445,13 @@ def _lj_encode_cs(px: np.ndarray, quality: int, mode: int, restart_blocks: int) 
 
 
 def lj_encode_cmyk(cmyk: np.ndarray, quality: int = 90, ycck: bool = False,
-                   restart_blocks: int = 0) -> bytes:
+                   restart_blocks: int = 0, script: str = "sequential") -> bytes:
     """Fixture encoder (libjpeg 9): a 4-component Adobe JPEG (transform 0
-    CMYK, or 2 YCCK) of HxWx4 pixels, every component 1x1."""
-    return _lj_encode_cs(cmyk, quality, 1 if ycck else 0, restart_blocks)
+    CMYK, or 2 YCCK) of HxWx4 pixels, every component 1x1.  script:
+    "sequential" (one interleaved scan), "progressive" (libjpeg's
+    jpeg_simple_progression) or "multiscan" (one component per scan)."""
+    bits = {"sequential": 0, "progressive": 4, "multiscan": 8}[script]
+    return _lj_encode_cs(cmyk, quality, (1 if ycck else 0) | bits, restart_blocks)
 
 
 def lj_encode_rgb_colorspace(rgb: np.ndarray, quality: int = 90, restart_blocks: int = 0) -> bytes:

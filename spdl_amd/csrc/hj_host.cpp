@@ -259,13 +259,11 @@ void parallel_pack(CopyPool* pool, uint8_t* base, const std::vector<CopyItem>& i
 
 // ---- host SOF probe (replaces nvjpegGetImageInfo) --------------------------
 // The SOF fields and the frame's colour model (frame_color: the APP14 Adobe
-// flag seen before the SOF, the component ids).  A 4-component frame is
-// walked on to its first SOS: it must be one interleaved scan.
+// flag seen before the SOF, the component ids).
 int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
   memset(info, 0, sizeof(*info));
   if (!d || size < 4 || d[0] != 0xFF || d[1] != 0xD8) return SPDL_HJ_ERR_NOT_JPEG;
   size_t pos = 2;
-  bool have_sof = false;
   int adobe = -1;
   for (;;) {
     while (pos < size && d[pos] != 0xFF) pos++;
@@ -273,15 +271,12 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
     if (pos >= size) return SPDL_HJ_ERR_BAD_HEADER;
     int m = d[pos++];
     if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
-    if (m == 0xD9 || (m == 0xDA && !have_sof)) return SPDL_HJ_ERR_BAD_HEADER;  // no SOF before scan
+    if (m == 0xD9 || m == 0xDA) return SPDL_HJ_ERR_BAD_HEADER;  // no SOF before the scan
     if (pos + 2 > size) return SPDL_HJ_ERR_BAD_HEADER;
     int len = (d[pos] << 8) | d[pos + 1];
     if (len < 2 || pos + (size_t)len > size) return SPDL_HJ_ERR_BAD_HEADER;
     const uint8_t* s = d + pos + 2;
     pos += (size_t)len;
-    if (m == 0xDA)  // 4 components: one interleaved scan of all four
-      return len >= 3 && s[0] == 4 ? SPDL_HJ_OK : SPDL_HJ_ERR_UNSUPPORTED;
-    if (have_sof) continue;
     if (m == 0xEE) {
       if (len >= 14 && memcmp(s, "Adobe", 5) == 0) adobe = s[11];
       continue;
@@ -307,10 +302,7 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
       }
       if (!frame_color(info->ncomp, info->h_samp, info->v_samp, ids, adobe, &info->color))
         return SPDL_HJ_ERR_UNSUPPORTED;
-      if (info->ncomp != 4) return SPDL_HJ_OK;
-      if (m == 0xC2) return SPDL_HJ_ERR_UNSUPPORTED;  // progressive CMYK
-      have_sof = true;
-      continue;
+      return SPDL_HJ_OK;
     }
     if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
         (m >= 0xCD && m <= 0xCF))

@@ -179,7 +179,6 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
       // walks every scan; the MCU holds the components in frame order
       in.multiscan = prog || ns != in.ncomp;
       in.progressive = prog;
-      if (in.multiscan && in.ncomp == 4) return kErrUnsupported;
       if (n < 1 + 2 * ns + 3) return kErrBadHeader;
       int order[kMaxComp] = {};
       for (int i = 0; i < ns; i++) {
@@ -1820,14 +1819,12 @@ __device__ __forceinline__ int ms_div(int x, int d) {
   return d == 1 ? x : (d == 2 ? x >> 1 : (d == 4 ? x >> 2 : (int)(((uint32_t)x * 0xAAABu) >> 17)));
 }
 
-// One correction bit per set bit of m, appended LSB-first to corr.
-__device__ __forceinline__ void ms_take_corr(MsBits& br, uint64_t m, uint64_t& corr, int& nc) {
-  int c = __popcll(m);
+// c correction bits appended MSB-first to corr (bit order of the stream:
+// the block's i-th non-zero history coefficient of n takes bit n - 1 - i)
+__device__ __forceinline__ void ms_take_corr(MsBits& br, int c, uint64_t& corr) {
   while (c > 0) {
     const int t = c < 32 ? c : 32;
-    const uint32_t v = br.get(t);
-    corr |= (uint64_t)(__builtin_bitreverse32(v) >> (32 - t)) << nc;
-    nc += t;
+    corr = (corr << t) | br.get(t);
     c -= t;
   }
 }
@@ -1874,19 +1871,20 @@ __device__ __forceinline__ void ms_chunk_apply(MsChunk& ch, int32_t* __restrict_
   if (ch.blk < 0) return;
   const uint64_t band = ms_range(ss, se);
   const uint64_t m = (uint64_t)ch.mhi << 32 | ch.mlo;
-  uint64_t h = m & band;
-  uint64_t corr = (uint64_t)ch.chi << 32 | ch.clo;
+  const uint64_t h = m & band;
+  const uint64_t corr = (uint64_t)ch.chi << 32 | ch.clo;
   const uint64_t nm = (uint64_t)ch.whi << 32 | ch.wlo;
   const uint64_t sg = (uint64_t)ch.shi << 32 | ch.slo;
   const int32_t p1 = 1 << al, m1 = -p1;
+  int rem = __popcll(h);  // one correction bit per non-zero history coefficient, MSB-first
 #pragma unroll
   for (int k = 1; k < 64; k++) {
     if ((h >> k) & 1u) {
-      if (corr & 1u) {
+      rem--;
+      if ((corr >> rem) & 1u) {
         const int32_t c = ch.lv[k];
         if ((c & p1) == 0) ch.lv[k] = c + (c >= 0 ? p1 : m1);
       }
-      corr >>= 1;
     }
     if ((nm >> k) & 1u) ch.lv[k] = ((sg >> k) & 1u) ? m1 : p1;
   }
@@ -2161,8 +2159,11 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
           // against the block's non-zero mask (lane j of the chunk)
           const int j = mcu & (kMsChunk - 1);
           const uint64_t hist = ((uint64_t)ms_rl(ch.mhi, j) << 32 | ms_rl(ch.mlo, j)) & band;
+          const uint64_t hz = ~hist & band;  // zero before the scan
+          const int htot = __popcll(hist);
           uint64_t corr = 0, nm = 0, nsg = 0;
-          int nc = 0, k = ss;
+          int cb = 0;  // correction bits taken (non-zero history coefficients below k)
+          int k = ss;
           if (eobrun <= 0) {
             while (k <= se) {
               br.need();
@@ -2175,13 +2176,13 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
               }
               br.skip(len);
               const int r = rs >> 4, s = rs & 15;
-              int v = 0;
+              uint32_t neg = 0;
               if (s) {
                 if (s != 1) {
                   rc = kErrBadHuffman;
                   break;
                 }
-                v = br.take_bit() ? 1 : -1;  // (a flag: the compiler keeps it scalar)
+                neg = br.take_bit() ^ 1u;
               } else if (r != 15) {
                 eobrun = 1 << r;
                 if (r) eobrun += (int)br.take(r);
@@ -2191,26 +2192,29 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
               // scan: the new coefficient's place (ZRL: the 16th zero, left
               // zero); every non-zero one passed on the way takes a
               // correction bit
-              uint64_t zm = ~hist & ms_range(k, se);
+              uint64_t zm = hz & (~0ull << k);
               for (int q = 0; q < r && zm; q++) zm &= zm - 1;
               if (zm == 0ull) {  // ran past se
-                ms_take_corr(br, hist & ms_range(k, se), corr, nc);
+                ms_take_corr(br, htot - cb, corr);
+                cb = htot;
                 k = se + 1;
-                if (v) rc = kErrBadHuffman;
+                if (s) rc = kErrBadHuffman;
                 break;
               }
               const int p = __builtin_ctzll(zm);
-              ms_take_corr(br, hist & ms_range(k, p - 1), corr, nc);
-              if (v) {
+              const int c = __popcll(hist & ((1ull << p) - 1ull)) - cb;
+              ms_take_corr(br, c, corr);
+              cb += c;
+              if (s) {
                 nm |= 1ull << p;
-                nsg |= (v < 0 ? 1ull : 0ull) << p;
+                nsg |= (uint64_t)neg << p;
               }
               k = p + 1;
             }
           }
           if (rc != kOk) break;
           if (eobrun > 0) {
-            ms_take_corr(br, hist & ms_range(k, se), corr, nc);
+            ms_take_corr(br, htot - cb, corr);
             eobrun--;
           }
           ch.clo = ms_wl(ch.clo, (uint32_t)corr, j);

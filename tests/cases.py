@@ -123,6 +123,8 @@ def case(name: str) -> bytes:
     # file without it is YCbCr + K), or the ids (renumbered 1 2 3)
     if name == "rgb_ids_only":
         return _strip_app14(case("rgb_coded"))
+    if name == "cmyk_pillow_prog":  # Pillow's progressive CMYK (libjpeg-turbo script)
+        return _cmyk_pillow(synthetic_pixels(26, 64, 64), progressive=True)
     if name == "cmyk_no_marker":
         return _strip_app14(case("cmyk_adobe"))
     if name == "rgb_adobe_only":
@@ -142,13 +144,19 @@ MULTISCAN = {
 }
 # Adobe CMYK (transform 0) / YCCK (transform 2), libjpeg 9 from inverted CMYK
 # pixels (tests/gen_golden.py, cmyk_pixels + oracle.lj_encode_cmyk):
-# name -> (pixels seed, h, w, quality, ycck, restart blocks)
+# name -> (pixels seed, h, w, quality, ycck, restart blocks[, scan script])
 CMYK = {
     "cmyk_adobe": (33, 120, 160, 90, False, 0),
     "ycck_adobe": (34, 120, 160, 90, True, 0),
     "ycck_odd_rst": (35, 77, 131, 85, True, 5),
+    # progressive (libjpeg's jpeg_simple_progression for 4 components: DC
+    # first, AC 1-5 / 6-63 first, AC refine, DC refine, AC refine per
+    # component) and one component per sequential scan
+    "prog_cmyk": (38, 120, 160, 90, False, 0, "progressive"),
+    "prog_ycck_odd_rst": (39, 77, 131, 85, True, 5, "progressive"),
+    "multiscan_cmyk": (40, 96, 128, 90, False, 0, "multiscan"),
 }
-FOUR_COMPONENT = [*CMYK, "cmyk_pillow", "cmyk_pillow_odd", "cmyk_no_marker"]
+FOUR_COMPONENT = [*CMYK, "cmyk_pillow", "cmyk_pillow_odd", "cmyk_no_marker", "cmyk_pillow_prog"]
 # 3 components coded in RGB (FFmpeg's gbrp frames): libjpeg 9 JCS_RGB writes
 # ids 'R' 'G' 'B' and an Adobe transform-0 marker; the variants keep one cue
 # each. name -> (pixels seed, h, w, quality, restart blocks)
@@ -242,10 +250,14 @@ def cmyk_pixels(seed: int, h: int, w: int) -> np.ndarray:
     return np.concatenate([cmy, k], axis=2).astype(np.uint8)
 
 
-def cmyk() -> bytes:
-    """A progressive 4-component (Adobe CMYK) JPEG: unsupported (the decoder
-    takes 4-component files only as sequential interleaved 1x1 scans)."""
-    return _cmyk_pillow(synthetic_pixels(26, 64, 64), progressive=True)
+def twelve_bit() -> bytes:
+    """A baseline file re-labelled 12-bit extended sequential (SOF1, P = 12):
+    unsupported (FFmpeg decodes it to a 16-bit pix_fmt)."""
+    d = bytearray(case("q90_420"))
+    i = d.index(b"\xff\xc0")
+    d[i + 1] = 0xC1
+    d[i + 4] = 12
+    return bytes(d)
 
 
 def truncated() -> bytes:

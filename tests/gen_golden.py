@@ -73,8 +73,9 @@ def main() -> None:
 
             data = O.lj_encode_multiscan(synthetic_pixels(seed, h, w), q, h0, v0, rst)
         elif name in cases.CMYK:  # libjpeg 9 writes these too (Adobe marker)
-            seed, h, w, q, ycck, rst = cases.CMYK[name]
-            data = O.lj_encode_cmyk(cases.cmyk_pixels(seed, h, w), q, ycck, rst)
+            seed, h, w, q, ycck, rst, *script = cases.CMYK[name]
+            data = O.lj_encode_cmyk(cases.cmyk_pixels(seed, h, w), q, ycck, rst,
+                                    script[0] if script else "sequential")
         elif name in cases.RGB_CODED:
             from spdl_amd.synthetic import synthetic_pixels
 

@@ -139,7 +139,7 @@ def test_truncated_progressive(oracle, frac):
     _agree_or_both_fail(oracle, cases.truncated_progressive(frac))
 
 
-@pytest.mark.parametrize("bad", ["arithmetic", "cmyk"])
+@pytest.mark.parametrize("bad", ["arithmetic", "twelve_bit"])
 def test_unsupported_fails_per_image(bad):
     """An unsupported image fails alone: strict=False keeps the others."""
     d = getattr(cases, bad)()

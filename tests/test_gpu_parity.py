@@ -171,14 +171,14 @@ def test_batch_256_fullres(decoder, oracle):
         np.testing.assert_array_equal(hyp[i], refs[d], strict=True)
 
 
-@pytest.mark.parametrize("bad", ["arithmetic", "cmyk", "truncated", "not_jpeg", "corrupt"])
+@pytest.mark.parametrize("bad", ["arithmetic", "twelve_bit", "truncated", "not_jpeg", "corrupt"])
 def test_errors_then_recover(decoder, oracle, bad):
     """Rubbish raises RuntimeError and later calls still work
     (reference tests/cuda/nvjpeg_decode_test.py:51-78)."""
     if bad == "arithmetic":
         d = cases.arithmetic()
-    elif bad == "cmyk":
-        d = cases.cmyk()
+    elif bad == "twelve_bit":
+        d = cases.twelve_bit()
     elif bad == "truncated":
         d = cases.truncated()
     elif bad == "not_jpeg":

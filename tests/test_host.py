@@ -66,13 +66,11 @@ def test_host_probe_rejects_garbage():
     with pytest.raises(RuntimeError, match="Failed to decode"):
         _lib.get_image_info(cases.arithmetic())  # unsupported SOF9
     with pytest.raises(RuntimeError, match="Failed to decode"):
-        _lib.get_image_info(cases.cmyk())  # unsupported progressive 4 components
-    # 4 components in non-interleaved scans (one component per scan)
-    d = bytearray(cases.case("cmyk_adobe"))
-    sos = d.index(b"\xff\xda")
-    d[sos + 4] = 1
-    with pytest.raises(RuntimeError, match="Failed to decode"):
-        _lib.get_image_info(bytes(d))
+        _lib.get_image_info(cases.twelve_bit())  # unsupported 12-bit precision
+    # 4 components, progressive or one component per scan: the probe takes them
+    # (the scans are walked on the device)
+    for name in ("prog_cmyk", "multiscan_cmyk", "cmyk_pillow_prog"):
+        assert _lib.get_image_info(cases.case(name)).ncomp == 4
 
 
 @pytest.mark.parametrize("w,h", [(640, 480), (480, 640), (333, 227), (1, 1), (1920, 1080)])

@@ -185,7 +185,7 @@ def test_oracle_errors(oracle):
     with pytest.raises(oracle.OracleError):
         oracle.decode_rgb(cases.arithmetic())
     with pytest.raises(oracle.OracleError):
-        oracle.decode_rgb(cases.cmyk())  # progressive 4-component
+        oracle.decode_rgb(cases.twelve_bit())  # 12-bit precision
     with pytest.raises(oracle.OracleError):
         oracle.decode_rgb(cases.truncated())
     with pytest.raises(oracle.OracleError):
@@ -412,7 +412,8 @@ def test_cmyk_ycck_decode(oracle):
             seed, h, w = cases.CMYK[name][:3]
             assert info.adobe == (2 if cases.CMYK[name][4] else 0)
         else:
-            seed, h, w = {"cmyk_pillow": (26, 64, 64), "cmyk_pillow_odd": (27, 75, 111)}[name]
+            seed, h, w = {"cmyk_pillow": (26, 64, 64), "cmyk_pillow_odd": (27, 75, 111),
+                          "cmyk_pillow_prog": (26, 64, 64)}[name]
         src = synthetic_pixels(seed, h, w).astype(np.int64)
         assert np.abs(rgb - src).mean() < 6.0, name  # a wrong sign or bias is > 30
 
