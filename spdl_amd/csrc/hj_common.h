@@ -202,6 +202,13 @@ struct ImageInfo {      // device-filled by the parse kernel
                         // (multiscan_kernel decodes it; destuff / entropy skip it)
   int32_t progressive;  // parse: SOF2
   int32_t color;        // parse: spdl_hj_color, decided at the SOF (frame_color)
+  // Huffman tables by slot (DC 0..3, AC 4..7): file offset of the DHT entry's 16
+  // length bytes, number of symbols (0: absent), a hash of lengths + symbols
+  // (parse), and the table (image * 8 + slot in the LUT pool) that lut_kernel
+  // built for it -- the first image of the batch whose table has these bytes
+  int32_t tab_off[8], tab_n[8];
+  uint32_t tab_hash[8];
+  int32_t lut_ref[8];
   int64_t tphase[4];    // diagnostics: wall_clock64 ticks of the entropy phases
   int64_t dbg[4];       // diagnostics: symbols (round 0), wave iterations, shader clocks, rt ticks
   int32_t sdiag[48];    // diagnostics, multiscan: per scan (16) start / end (wall_clock64

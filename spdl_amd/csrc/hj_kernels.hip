@@ -347,68 +347,46 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     if (tid == 0) infos[img] = s.info;
     return;
   }
-  HuffTable* tabs = luts + (size_t)img * 8;
-  int tab_nsub[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tab_slow = 0;  // per table slot (thread 0 uses)
-  for (int t = 0; t < 8; t++) {
-    if (!s.have[t]) continue;
-    const bool is_dc = t < 4;
-    // canonical codes are consecutive: the 10-bit prefixes of all codes longer
-    // than kLutBits form one contiguous range [p_lo, p_hi]
-    int p_lo = kLutSize, p_hi = -1;
-    for (int l = kLutBits + 1; l <= 16; l++) {
-      if (s.bits[t][l] == 0) continue;
-      const int first = s.maxcode[t][l] - s.bits[t][l] + 1;
-      p_lo = min(p_lo, first >> (l - kLutBits));
-      p_hi = max(p_hi, s.maxcode[t][l] >> (l - kLutBits));
-    }
-    const int nsub = p_hi >= p_lo ? p_hi - p_lo + 1 : 0;
-    const bool sub_ok = nsub <= kMaxSub;
-    // one 16-bit window -> entry (levels share this): codes up to max_len
-    // bits; the value is folded in (Full) when code + value fit full_max bits
-    // (level 1: |v| < 2^9; sub-tables: codes >= 11 bits, |v| < 2^5 -- both
-    // fit the entry's int11 field)
-    auto entry16 = [&](uint32_t w16, int max_len, int full_max) -> uint32_t {
-      for (int l = 1; l <= max_len; l++) {
-        const int code = (int)(w16 >> (16 - l));
-        if (code <= s.maxcode[t][l]) {
-          const int sym = s.vals[t][s.valoff[t][l] + code];
-          const int sz = is_dc ? sym : (sym & 15);
-          if (is_dc && sym > 15) return 0u;  // invalid size -> slow path reports it
-          if (l + sz <= full_max) {
-            int v = 0;
-            if (sz) {
-              const int raw = (int)((w16 >> (16 - l - sz)) & ((1u << sz) - 1));
-              v = raw < (1 << (sz - 1)) ? raw - ((1 << sz) - 1) : raw;
-            }
-            return hj_entry(kKindFull, l + sz, sym, is_dc, v);
-          }
-          return hj_entry(kKindCode, l, sym, is_dc, 0);
-        }
+  // The tables themselves are built by lut_kernel, once per distinct table of
+  // the batch; here: their identity (offset, size, FNV-1a hash of the 16
+  // lengths + symbols) and the sub-table count the entropy instance choice
+  // needs.  One thread per table slot.
+  __shared__ int tab_nsub[8], tab_slow;
+  if (tid == 0) tab_slow = 0;
+  __syncthreads();
+  if (tid < 8) {
+    const int t = tid;
+    int nsub = 0;
+    if (s.have[t]) {
+      uint32_t h = 2166136261u;
+      for (int l = 1; l <= 16; l++) h = (h ^ s.bits[t][l]) * 16777619u;
+      for (int k = 0; k < s.dht_n[t]; k++) h = (h ^ s.vals[t][k]) * 16777619u;
+      s.info.tab_off[t] = s.dht_off[t] - 16;
+      s.info.tab_n[t] = s.dht_n[t];
+      s.info.tab_hash[t] = h;
+      // canonical codes are consecutive: the 10-bit prefixes of all codes
+      // longer than kLutBits form one contiguous range
+      int p_lo = kLutSize, p_hi = -1;
+      for (int l = kLutBits + 1; l <= 16; l++) {
+        if (s.bits[t][l] == 0) continue;
+        const int first = s.maxcode[t][l] - s.bits[t][l] + 1;
+        p_lo = min(p_lo, first >> (l - kLutBits));
+        p_hi = max(p_hi, s.maxcode[t][l] >> (l - kLutBits));
       }
-      return 0u;
-    };
-    for (int idx = tid; idx < kLutSize; idx += blockDim.x) {
-      // level 1 resolves codes (and code+value) that fit in kLutBits
-      uint32_t e = entry16((uint32_t)idx << kSubBits, kLutBits, kLutBits);
-      if (e == 0u && idx >= p_lo && idx <= p_hi)
-        e = sub_ok ? ((kKindSub << 5) | ((uint32_t)(idx - p_lo) << kEntHiShift)) : 0u;
-      tabs[t].lut[idx] = e;
+      nsub = p_hi >= p_lo ? p_hi - p_lo + 1 : 0;
+      if (nsub > kMaxSub) {
+        atomicOr(&tab_slow, 1 << t);
+        nsub = 0;
+      }
+    } else {
+      s.info.tab_off[t] = 0;
+      s.info.tab_n[t] = 0;
+      s.info.tab_hash[t] = 0;
     }
-    if (sub_ok)
-      for (int i = tid; i < nsub << kSubBits; i += blockDim.x)
-        tabs[t].sub[i] = entry16(((uint32_t)(p_lo + (i >> kSubBits)) << kSubBits) |
-                                     (uint32_t)(i & ((1 << kSubBits) - 1)),
-                                 16, 16);
-    tab_nsub[t] = sub_ok ? nsub : 0;
-    tab_slow |= sub_ok ? 0 : 1 << t;
-    if (tid == 0) {
-      tabs[t].nsub = sub_ok ? nsub : 0;
-      tabs[t].long_slow = sub_ok ? 0 : 1;  // long codes left to the canonical path
-    }
-    for (int i = tid; i < 18; i += blockDim.x) tabs[t].maxcode[i] = s.maxcode[t][i];
-    for (int i = tid; i < 17; i += blockDim.x) tabs[t].valoff[i] = s.valoff[t][i];
-    for (int i = tid; i < 256; i += blockDim.x) tabs[t].vals[i] = s.vals[t][i];
+    s.info.lut_ref[t] = img * 8 + t;
+    tab_nsub[t] = nsub;
   }
+  __syncthreads();
   if (tid == 0) {
     // Which entropy instance decodes this scan: NTAB = 4 takes <= 4 distinct
     // tables whose long codes all fit the LDS sub-table pool (no canonical
@@ -434,6 +412,126 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     uint32_t* dst = reinterpret_cast<uint32_t*>(infos + img);
     for (int i = tid; i < (int)(sizeof(ImageInfo) / 4); i += blockDim.x) dst[i] = src[i];
   }
+}
+
+// ---------------------------------------------------------------------------
+// lut_kernel: the Huffman LUTs, once per distinct table of the batch.  One
+// workgroup per (table slot, image): the table is looked for among the
+// earlier images' tables of the same slot (hash, then the bytes); the first
+// image holding these bytes builds it into its own LUT slot, the others only
+// point there (ImageInfo::lut_ref).  A batch of one encoder's files (shared
+// standard or per-quality tables) builds a handful of tables instead of
+// eight per image.
+// ---------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(256) lut_kernel(const uint8_t* __restrict__ bytes,
+                                                  const ImageDesc* __restrict__ desc,
+                                                  ImageInfo* __restrict__ infos,
+                                                  HuffTable* __restrict__ luts) {
+  __shared__ int first, same, maxcode[18], valoff[17];
+  __shared__ uint8_t bits[17], vals[256];
+  const int t = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+  const ImageInfo& in = infos[img];
+  if (in.status != kOk || in.multiscan || in.tab_n[t] == 0) return;
+  const uint32_t h = in.tab_hash[t];
+  const int n = in.tab_n[t];
+  const uint8_t* d = bytes + desc[img].in_off + in.tab_off[t];
+  if (tid == 0) first = img;
+  __syncthreads();
+  for (int j = tid; j < img; j += blockDim.x) {
+    const ImageInfo& o = infos[j];
+    if (o.status == kOk && !o.multiscan && o.tab_n[t] == n && o.tab_hash[t] == h)
+      atomicMin(&first, j);
+  }
+  __syncthreads();
+  const int j = first;
+  if (j < img) {  // the same bytes? (a hash match is only a candidate)
+    if (tid == 0) same = 1;
+    __syncthreads();
+    const uint8_t* e = bytes + desc[j].in_off + infos[j].tab_off[t];
+    for (int k = tid; k < 16 + n; k += blockDim.x)
+      if (d[k] != e[k]) same = 0;
+    __syncthreads();
+    if (same) {
+      if (tid == 0) infos[img].lut_ref[t] = j * 8 + t;
+      return;
+    }
+  }
+  // build: canonical arrays (T.81 F.2.2.3 / libjpeg jdhuff.c), then the LUT
+  if (tid < 16) bits[tid + 1] = d[tid];
+  for (int k = tid; k < 256; k += blockDim.x) vals[k] = k < n ? d[16 + k] : 0;
+  __syncthreads();
+  if (tid == 0) {
+    int code = 0, k = 0;
+    for (int l = 1; l <= 16; l++) {
+      if (bits[l]) {
+        valoff[l] = k - code;
+        code += bits[l];
+        k += bits[l];
+        maxcode[l] = code - 1;
+      } else {
+        maxcode[l] = -1;
+        valoff[l] = 0;
+      }
+      code <<= 1;
+    }
+    maxcode[17] = 0x7FFFFFFF;
+  }
+  __syncthreads();
+  HuffTable& T = luts[(size_t)img * 8 + t];
+  const bool is_dc = t < 4;
+  int p_lo = kLutSize, p_hi = -1;
+  for (int l = kLutBits + 1; l <= 16; l++) {
+    if (bits[l] == 0) continue;
+    const int fc = maxcode[l] - bits[l] + 1;
+    p_lo = min(p_lo, fc >> (l - kLutBits));
+    p_hi = max(p_hi, maxcode[l] >> (l - kLutBits));
+  }
+  const int nsub = p_hi >= p_lo ? p_hi - p_lo + 1 : 0;
+  const bool sub_ok = nsub <= kMaxSub;
+  // one 16-bit window -> entry (levels share this): codes up to max_len
+  // bits; the value is folded in (Full) when code + value fit full_max bits
+  // (level 1: |v| < 2^9; sub-tables: codes >= 11 bits, |v| < 2^5 -- both
+  // fit the entry's int11 field)
+  auto entry16 = [&](uint32_t w16, int max_len, int full_max) -> uint32_t {
+    for (int l = 1; l <= max_len; l++) {
+      const int code = (int)(w16 >> (16 - l));
+      if (code <= maxcode[l]) {
+        const int sym = vals[valoff[l] + code];
+        const int sz = is_dc ? sym : (sym & 15);
+        if (is_dc && sym > 15) return 0u;  // invalid size -> slow path reports it
+        if (l + sz <= full_max) {
+          int v = 0;
+          if (sz) {
+            const int raw = (int)((w16 >> (16 - l - sz)) & ((1u << sz) - 1));
+            v = raw < (1 << (sz - 1)) ? raw - ((1 << sz) - 1) : raw;
+          }
+          return hj_entry(kKindFull, l + sz, sym, is_dc, v);
+        }
+        return hj_entry(kKindCode, l, sym, is_dc, 0);
+      }
+    }
+    return 0u;
+  };
+  for (int idx = tid; idx < kLutSize; idx += blockDim.x) {
+    // level 1 resolves codes (and code+value) that fit in kLutBits
+    uint32_t e = entry16((uint32_t)idx << kSubBits, kLutBits, kLutBits);
+    if (e == 0u && idx >= p_lo && idx <= p_hi)
+      e = sub_ok ? ((kKindSub << 5) | ((uint32_t)(idx - p_lo) << kEntHiShift)) : 0u;
+    T.lut[idx] = e;
+  }
+  if (sub_ok)
+    for (int i = tid; i < nsub << kSubBits; i += blockDim.x)
+      T.sub[i] = entry16(((uint32_t)(p_lo + (i >> kSubBits)) << kSubBits) |
+                             (uint32_t)(i & ((1 << kSubBits) - 1)),
+                         16, 16);
+  if (tid == 0) {
+    T.nsub = sub_ok ? nsub : 0;
+    T.long_slow = sub_ok ? 0 : 1;  // long codes left to the canonical path
+  }
+  if (tid < 18) T.maxcode[tid] = maxcode[tid];
+  if (tid < 17) T.valoff[tid] = valoff[tid];
+  for (int i = tid; i < 256; i += blockDim.x) T.vals[i] = vals[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -500,8 +598,8 @@ __device__ __forceinline__ void wg_scan2(int a, int b, int& ea, int& eb, int& ta
 // (fill 0xFF allowed before it); *term = first 0xFF starting any other marker
 // (bytes past the file read as 0xD9, EOI).  Bytes before `start` are ignored.
 __device__ __forceinline__ void ds_classify(const uint8_t* __restrict__ d, int size, int start,
-                                            int j0, uint32_t& keep, uint32_t& rst, int& term) {
-  uint8_t b[18];
+                                            int j0, uint32_t& keep, uint32_t& rst, int& term,
+                                            uint8_t (&b)[18]) {
   b[0] = j0 > 0 && j0 - 1 < size ? d[j0 - 1] : 0;
   if (j0 + 16 <= size) {
     const uint4 q = *reinterpret_cast<const uint4*>(d + j0);
@@ -554,7 +652,8 @@ __global__ void __launch_bounds__(kDsThreads) destuff_count_kernel(
   if (tid == 0) shterm = 0x7FFFFFFF;
   uint32_t keep, rst;
   int term;
-  ds_classify(bytes + dd.in_off, size, start, cbase + tid * kDsPer, keep, rst, term);
+  uint8_t b[18];
+  ds_classify(bytes + dd.in_off, size, start, cbase + tid * kDsPer, keep, rst, term, b);
   int ek, er, tk, tr;
   wg_scan2(__popc(keep), __popc(rst), ek, er, tk, tr, sh);
   if (term != 0x7FFFFFFF) atomicMin(&shterm, term);
@@ -621,7 +720,8 @@ __global__ void __launch_bounds__(kDsThreads) destuff_write_kernel(
   const int j0 = cbase + tid * kDsPer;
   uint32_t keep, rst;
   int term;
-  ds_classify(bytes + dd.in_off, size, start, j0, keep, rst, term);
+  uint8_t b[18];  // b[1 + i] = byte j0 + i (classified and compacted from registers)
+  ds_classify(bytes + dd.in_off, size, start, j0, keep, rst, term, b);
   const int lim = end - j0;  // bytes at or past the scan end are not part of it
   const uint32_t m = lim >= 16 ? 0xFFFFu : (lim <= 0 ? 0u : ((1u << lim) - 1u));
   keep &= m;
@@ -630,15 +730,14 @@ __global__ void __launch_bounds__(kDsThreads) destuff_write_kernel(
   wg_scan2(__popc(keep), __popc(rst), ek, er, tk, tr, sh);
   const DsChunk& c = chunks[dd.ds_off + k];
   uint32_t* sg = segs + dd.seg_off;
-  const uint8_t* d = bytes + dd.in_off;
   // compact this thread's kept bytes; RSTn markers record segment starts
   {
     int o = ek, r = c.rst_pre + er;
     bool overflow = false;
+#pragma unroll
     for (int i = 0; i < 16; i++) {
       if (keep >> i & 1u) {
-        const uint8_t v = d[j0 + i];
-        ob[o++] = v;
+        ob[o++] = b[1 + i];
       } else if (rst >> i & 1u) {
         r++;
         if (r < dd.seg_cap) sg[r] = (uint32_t)(c.keep_pre + o);
@@ -1121,15 +1220,15 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
         (k == 0 ? ldc : lac)[c] = f;
       }
     }
-    const HuffTable* tabs = luts + (size_t)img * 8;
-    if (tid == 0) S.gtab = tabs;
+    if (tid == 0) S.gtab = luts;
     int pool = 0;  // in units of 64-entry sub-tables
     for (int i = 0; i < ns; i++) {
+      const int ref = in.lut_ref[slots[i]];  // the batch's build of this table (lut_kernel)
       if (i >= NTAB) {  // kept in HBM (kSlow images only)
-        if (tid == 0) S.gslot[i] = slots[i];
+        if (tid == 0) S.gslot[i] = ref;
         continue;
       }
-      const HuffTable& T = tabs[slots[i]];
+      const HuffTable& T = luts[ref];
       const int nsub = T.nsub;
       const bool fits = (pool + nsub) << kSubBits <= kSubPool;
       const int base = pool;
@@ -3577,6 +3676,7 @@ hipError_t launch_parse(const uint8_t* bytes, const ImageDesc* host_desc, ImageD
   hipLaunchKernelGGL(parse_kernel, dim3(n), dim3(256), 0, st, bytes, host_desc, desc, infos, luts,
                      static_cast<const uint4*>(host_tables), static_cast<uint4*>(tables),
                      (table_bytes + 15) / 16);
+  hipLaunchKernelGGL(lut_kernel, dim3(8, n), dim3(256), 0, st, bytes, desc, infos, luts);
   return hipGetLastError();
 }
 hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
