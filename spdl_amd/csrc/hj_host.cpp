@@ -1552,7 +1552,10 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
       const uint32_t cnt = bd[j].y & 0xFFFFu;
       for (uint32_t i = 0; i < cnt && bd[j].x + i < nbk * 64; i++) {
         const uint32_t e = ents[bd[j].x + i];
-        dense[j * 64 + (e & 63u)] = (int16_t)(e >> 16);  // natural index, dequantised
+        // the entry's IDCT slot (kSlotOrder in hj_kernels.hip) -> natural index
+        const uint32_t sl = e & 63u, q = sl & 7u;
+        const uint32_t nat = (sl & 56u) | (q < 4u ? 2u * q : 2u * (q - 4u) + 1u);
+        dense[j * 64 + nat] = (int16_t)(e >> 16);  // dequantised
       }
     }
     memcpy(coefs, dense.data(), 2 * (dense.size() < coef_cap ? dense.size() : coef_cap));

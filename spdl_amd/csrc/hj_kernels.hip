@@ -32,12 +32,6 @@
 
 namespace hj {
 
-__constant__ uint8_t kNat[80] = {
-    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33,
-    40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36,
-    29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
-    47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
-
 // ---------------------------------------------------------------------------
 // parse_kernel
 // ---------------------------------------------------------------------------
@@ -773,12 +767,16 @@ __device__ __forceinline__ uint32_t pk_mul_lo16(uint32_t a, uint32_t b) {
 }
 
 constexpr int kMaxTabs = 2 * kMaxComp;  // distinct (DC, AC) tables of a scan
-// natural (row-major) index of each zig-zag position
-__constant__ uint8_t kNatOrder[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
-                                      11, 4,  5,  12, 19, 26, 33, 40, 48, 41, 34, 27, 20,
-                                      13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43,
-                                      36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45,
-                                      38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+// The coefficient lists' index field: a coefficient's slot in the IDCT's
+// LDS block, not its natural index: each row stored as the pairs (x0, x2),
+// (x4, x6), (x1, x3), (x5, x7), so the row pass reads its even and odd
+// halves as ready-packed int16 pairs for v_dot2 (slot = row * 8 +
+// ((c >> 1) | (c & 1) << 2) for natural index row * 8 + c).  Per zig-zag
+// position:
+__constant__ uint8_t kSlotOrder[64] = {
+    0,  4,  8,  16, 12, 1,  5,  9,  20, 24, 32, 28, 17, 13, 2,  6,  10, 21, 25, 36, 40, 48,
+    44, 33, 29, 18, 14, 3,  7,  11, 22, 26, 37, 41, 52, 56, 60, 49, 45, 34, 30, 19, 15, 23,
+    27, 38, 42, 53, 57, 61, 50, 46, 35, 31, 39, 43, 54, 58, 62, 51, 47, 55, 59, 63};
 constexpr int kWinWords = 8;  // bit-reader window per thread (words)
 
 // NTAB = distinct Huffman tables the workgroup holds in LDS: 4 covers luma +
@@ -795,7 +793,7 @@ struct EntShared {
   uint32_t run_pos[NT];
   uint32_t run_zb[NT];
   uint32_t qdc[kMaxComp];  // DC quantiser per component
-  uint32_t qn[kMaxComp][64];  // per zig-zag index: natural index | quantiser << 16
+  uint32_t qn[kMaxComp][64];  // per zig-zag index: IDCT slot (kSlotOrder) | quantiser << 16
   // The bit-reader windows are dead outside round 0 / the sync rounds, so the
   // reduction and scan scratch share their storage (keeps the workgroup at
   // <= 80 KiB of LDS: two entropy workgroups -- e.g. of two concurrent
@@ -995,7 +993,7 @@ __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32
 // Coefficient lists, the write pass's output (read by idct_kernel): block j
 // of an image keeps its non-zero AC coefficients, dequantised (the int16
 // product the sequential decoder stores), as u32 entries (value << 16 |
-// natural index) in ents[bd.x, bd.x + (bd.y & 0xFFFF)), bd = bdesc[j];
+// IDCT slot, kSlotOrder) in ents[bd.x, bd.x + (bd.y & 0xFFFF)), bd = bdesc[j];
 // bd.y >> 16 holds the block's raw DC difference until the DC pass replaces
 // it by the final dequantised DC.  Each block is written by the one run its DC
 // symbol lies in, entries appended from that run's region start (first block
@@ -1247,7 +1245,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
     }
     for (int k = tid; k < kMaxComp * 64; k += NT) {
       if (k % 64 == 0) S.qdc[k / 64] = in.qt[k / 64][0];
-      S.qn[k / 64][k % 64] = kNatOrder[k % 64] | ((uint32_t)in.qt[k / 64][k % 64] << 16);
+      S.qn[k / 64][k % 64] = kSlotOrder[k % 64] | ((uint32_t)in.qt[k / 64][k % 64] << 16);
     }
     for (int b = 0; b < bpm; b++) bcomp |= (uint32_t)in.mcu_comp[b] << (2 * b);
     for (int c = 0; c < kMaxComp; c++)
@@ -2691,7 +2689,7 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
     for (int k = 1; k < 64; k++) {
       if (l[k] != 0) {
         const uint32_t v = (uint32_t)l[k] * (uint32_t)in.qt[c][k];
-        out[n++] = (v << 16) | kNatOrder[k];
+        out[n++] = (v << 16) | kSlotOrder[k];
       }
     }
     const int32_t dc = (int32_t)(int16_t)(uint16_t)((uint32_t)kDcBias + (uint32_t)l[0] * in.qt[c][0]);
@@ -2731,12 +2729,79 @@ constexpr int kBlkWords = 36;
 
 // One block of the entropy kernel's coefficient lists -> 8x8 pixels (u8
 // values in int32), through the thread's LDS slot `my_blk` (kBlkWords words).
+// FFmpeg simple_idct (8-bit) on packed int16 pairs with v_dot2_i32_i16: a
+// row of the slot block is (x0, x2), (x4, x6), (x1, x3), (x5, x7), so each
+// even / odd partial sum of a pass is two dot2 steps.  The products and
+// 32-bit sums are the C code's exactly (oracle simple_row / simple_col_put;
+// the C code's unsigned wrap-around equals the dot2's modular int32 sum).
+typedef short hj_s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int32_t dot2(uint32_t a, uint32_t w, int32_t c) {
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(hj_s16x2, a), __builtin_bit_cast(hj_s16x2, w),
+                                c, false);
+}
+constexpr uint32_t pk16(int lo, int hi) {
+  return (uint32_t)(uint16_t)(int16_t)lo | ((uint32_t)(uint16_t)(int16_t)hi << 16);
+}
+// low halves of lo and hi as one pair (v_perm)
+__device__ __forceinline__ uint32_t pack_lo16(uint32_t lo, uint32_t hi) {
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+// an 8-point pass: a[k] even sums (+ bias), b[k] odd sums
+__device__ __forceinline__ void sidct8(uint32_t e0, uint32_t e1, uint32_t o0, uint32_t o1,
+                                       int32_t bias, int32_t (&a)[4], int32_t (&b)[4]) {
+  a[0] = dot2(e1, pk16(kW4, kW6), dot2(e0, pk16(kW4, kW2), bias));
+  a[1] = dot2(e1, pk16(-kW4, -kW2), dot2(e0, pk16(kW4, kW6), bias));
+  a[2] = dot2(e1, pk16(-kW4, kW2), dot2(e0, pk16(kW4, -kW6), bias));
+  a[3] = dot2(e1, pk16(kW4, -kW6), dot2(e0, pk16(kW4, -kW2), bias));
+  b[0] = dot2(o1, pk16(kW5, kW7), dot2(o0, pk16(kW1, kW3), 0));
+  b[1] = dot2(o1, pk16(-kW1, -kW5), dot2(o0, pk16(kW3, -kW7), 0));
+  b[2] = dot2(o1, pk16(kW7, kW3), dot2(o0, pk16(kW5, -kW1), 0));
+  b[3] = dot2(o1, pk16(kW3, -kW1), dot2(o0, pk16(kW7, -kW5), 0));
+}
+// blk: the slot block (8 rows of 4 words); px: 64 pixels, row-major
+__device__ __forceinline__ void simple_idct_slots(const uint4* blk, int32_t (&px)[64]) {
+  // rows: results truncated to int16 (FFmpeg keeps them in the int16 block);
+  // only their low halves are used, packed below.  DC-only rows: x0 << 3.
+  uint32_t r[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint4 q = blk[i];
+    int32_t a[4], b[4];
+    sidct8(q.x, q.y, q.z, q.w, 1 << 10, a, b);
+    const bool dc_only = ((q.x >> 16) | q.y | q.z | q.w) == 0u;
+    const uint32_t dc = q.x << 3;
+    r[i][0] = dc_only ? dc : (uint32_t)((int32_t)((uint32_t)a[0] + (uint32_t)b[0]) >> 11);
+    r[i][7] = dc_only ? dc : (uint32_t)((int32_t)((uint32_t)a[0] - (uint32_t)b[0]) >> 11);
+    r[i][1] = dc_only ? dc : (uint32_t)((int32_t)((uint32_t)a[1] + (uint32_t)b[1]) >> 11);
+    r[i][6] = dc_only ? dc : (uint32_t)((int32_t)((uint32_t)a[1] - (uint32_t)b[1]) >> 11);
+    r[i][2] = dc_only ? dc : (uint32_t)((int32_t)((uint32_t)a[2] + (uint32_t)b[2]) >> 11);
+    r[i][5] = dc_only ? dc : (uint32_t)((int32_t)((uint32_t)a[2] - (uint32_t)b[2]) >> 11);
+    r[i][3] = dc_only ? dc : (uint32_t)((int32_t)((uint32_t)a[3] + (uint32_t)b[3]) >> 11);
+    r[i][4] = dc_only ? dc : (uint32_t)((int32_t)((uint32_t)a[3] - (uint32_t)b[3]) >> 11);
+  }
+  // columns: (c0 + 32) W4 = c0 W4 + 32 W4
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    int32_t a[4], b[4];
+    sidct8(pack_lo16(r[0][k], r[2][k]), pack_lo16(r[4][k], r[6][k]), pack_lo16(r[1][k], r[3][k]),
+           pack_lo16(r[5][k], r[7][k]), kW4 * ((1 << 19) / kW4), a, b);
+    px[k] = clip_u8_opaque((int32_t)((uint32_t)a[0] + (uint32_t)b[0]) >> 20);
+    px[8 + k] = clip_u8_opaque((int32_t)((uint32_t)a[1] + (uint32_t)b[1]) >> 20);
+    px[16 + k] = clip_u8_opaque((int32_t)((uint32_t)a[2] + (uint32_t)b[2]) >> 20);
+    px[24 + k] = clip_u8_opaque((int32_t)((uint32_t)a[3] + (uint32_t)b[3]) >> 20);
+    px[32 + k] = clip_u8_opaque((int32_t)((uint32_t)a[3] - (uint32_t)b[3]) >> 20);
+    px[40 + k] = clip_u8_opaque((int32_t)((uint32_t)a[2] - (uint32_t)b[2]) >> 20);
+    px[48 + k] = clip_u8_opaque((int32_t)((uint32_t)a[1] - (uint32_t)b[1]) >> 20);
+    px[56 + k] = clip_u8_opaque((int32_t)((uint32_t)a[0] - (uint32_t)b[0]) >> 20);
+  }
+}
+
 template <int IDCT>
 __device__ __forceinline__ void idct_list_block(const uint32_t* __restrict__ ents, const uint2 bd,
                                                 const int64_t coef_off, const int nblocks,
                                                 uint32_t* my_blk, int32_t (&px)[64]) {
   // The entropy kernel's list for this block (see BlockOut): DC final, AC
-  // dequantised with their natural index; placed in the thread's LDS block.
+  // dequantised with their IDCT slot (kSlotOrder); placed in the thread's LDS block.
   // (a list may start inside a 16-byte group: the run's lists are packed
   // back to back; entries [lo, lo + count) of the groups from `start`)
   const uint32_t cap = (uint32_t)nblocks * 64u;
@@ -2766,51 +2831,27 @@ __device__ __forceinline__ void idct_list_block(const uint32_t* __restrict__ ent
       }
     }
   }
+  if (IDCT == 0) {
+    simple_idct_slots(my4, px);
+    return;
+  }
+  // natural order from the slot layout (a compile-time permutation)
   int32_t blk[64];
-  uint32_t rows_hi = 0u, cols_hi = 0u;  // any coefficient in rows 4..7 / columns 4..7
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint4 q = my4[i];
-    const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
-    if (i >= 4) rows_hi |= q.x | q.y | q.z | q.w;
-    cols_hi |= q.z | q.w;
-#pragma unroll
-    for (int h = 0; h < 4; h++) {
-      blk[8 * i + 2 * h] = sext16(wv[h]);
-      blk[8 * i + 2 * h + 1] = sext16(wv[h] >> 16);
-    }
+    blk[8 * i + 0] = sext16(q.x);
+    blk[8 * i + 2] = sext16(q.x >> 16);
+    blk[8 * i + 4] = sext16(q.y);
+    blk[8 * i + 6] = sext16(q.y >> 16);
+    blk[8 * i + 1] = sext16(q.z);
+    blk[8 * i + 3] = sext16(q.z >> 16);
+    blk[8 * i + 5] = sext16(q.w);
+    blk[8 * i + 7] = sext16(q.w >> 16);
   }
   if (IDCT == 2) {
 #pragma unroll
     for (int i = 0; i < 64; i++) px[i] = blk[i] & 255;
-  } else if (IDCT == 0) {
-    // Sparse blocks, wave-uniform: when no block of the wave has a
-    // coefficient in rows (columns) 4..7, those rows' passes and terms are
-    // additions of zero and are left out -- same results, fewer instructions
-    // (0 0: always the full transform)
-    const bool r4 = false, c4 = false;
-    (void)rows_hi, (void)cols_hi;
-    if (r4 && c4) {
-#pragma unroll
-      for (int i = 0; i < 4; i++) simple_row<4>(blk + 8 * i);
-#pragma unroll
-      for (int i = 0; i < 8; i++) simple_col<4>(blk + i, px + i);
-    } else if (r4) {
-#pragma unroll
-      for (int i = 0; i < 4; i++) simple_row<8>(blk + 8 * i);
-#pragma unroll
-      for (int i = 0; i < 8; i++) simple_col<4>(blk + i, px + i);
-    } else if (c4) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) simple_row<4>(blk + 8 * i);
-#pragma unroll
-      for (int i = 0; i < 8; i++) simple_col<8>(blk + i, px + i);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; i++) simple_row<8>(blk + 8 * i);
-#pragma unroll
-      for (int i = 0; i < 8; i++) simple_col<8>(blk + i, px + i);
-    }
   } else {
     islow_block(blk, px);
   }
