@@ -132,6 +132,23 @@ def test_batch_mixed_sizes_resize(decoder, oracle):
         np.testing.assert_array_equal(hyp[i], ref, strict=True)
 
 
+def test_batch_shared_and_distinct_huffman_tables(decoder, oracle):
+    """lut_kernel builds a Huffman table once per distinct table of the batch
+    (the first image holding the bytes) and the others read that build:
+    repeated files, files sharing the standard tables (gray's luma slots
+    among them), files with their own optimised tables (the same slots, other
+    bytes) and six-table files -- every image bit-exact vs the oracle."""
+    names = ["optimized", "q90_420", "optimized", "six_tables", "q90_444", "q75_420", "q90_420",
+             "six_tables", "gray", "optimized", "restart_rows", "q75_420"]
+    datas = [cases.case(n) for n in names]
+    kw = RESIZES["pad224"]
+    out = Output(pix_fmt="rgb24", resize=True, **kw)
+    hyp = _decode(decoder, datas, out, (224, 224, 3)).numpy()
+    for i, d in enumerate(datas):
+        ref = oracle.decode_resize(d, oracle.Resize(**kw), pix_fmt="rgb24")
+        np.testing.assert_array_equal(hyp[i], ref, strict=True)
+
+
 @pytest.mark.parametrize("fmt", ["rgb24", "bf16"])
 def test_batch_mixed_cmyk(decoder, oracle, fmt):
     """Colour models in one batch: Adobe CMYK (K transform -> three RGB
