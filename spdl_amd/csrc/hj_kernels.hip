@@ -1647,6 +1647,7 @@ struct MsShared {
   uint64_t deps[kMsMaxScans];  // earlier scans a scan must wait for (to finish)
   uint64_t soft[kMsMaxScans];  // ... or only to run ahead of it (trailing, below)
   int32_t prog[kMsMaxScans];   // blocks a scan has finished, in scan order
+  int32_t prio[kMsMaxScans];   // claim priority (bytes of its heaviest dependent chain)
   uint64_t claimed, done;      // scans taken by a decoder wave / finished
   int64_t tkind[4];            // diagnostics: decode ticks by scan kind
   int32_t marks[kMsMaxMarks];
@@ -2574,7 +2575,18 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
     S.prog[i] = 0;
   }
   if (tid < 48) S.sdiag[tid] = 0;
+  __syncthreads();
   if (tid == 0) {
+    // claim priority: a scan's bytes plus the heaviest chain of scans that
+    // wait for it (hard or trailing), so the chain that bounds the image --
+    // for the libjpeg script the luma AC bands and the two refinement scans
+    // trailing them -- takes the waves first
+    for (int i = S.nscans - 1; i >= 0; i--) {
+      int down = 0;
+      for (int j = i + 1; j < S.nscans; j++)
+        if (((S.deps[j] | S.soft[j]) >> i) & 1ull) down = max(down, S.prio[j]);
+      S.prio[i] = S.scan[i].end - S.scan[i].start + down;
+    }
     S.claimed = 0;
     S.done = 0;
     for (int k = 0; k < 4; k++) S.tkind[k] = 0;
@@ -2606,11 +2618,17 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
                 kOk ||
             (claimed & full) == full)
           break;
-        int cand = -1;
-        for (int i = 0; i < nsc && cand < 0; i++)
+        // the claimable scan of the heaviest chain first (S.prio)
+        int cand = -1, cprio = -1;
+        for (int i = 0; i < nsc; i++)
           if (!((claimed >> i) & 1ull) && (ms_u64(S.deps[i]) & ~done) == 0ull &&
-              (ms_u64(S.soft[i]) & ~(done | claimed)) == 0ull)
-            cand = i;
+              (ms_u64(S.soft[i]) & ~(done | claimed)) == 0ull) {
+            const int pr = ms_i(S.prio[i]);
+            if (pr > cprio) {
+              cand = i;
+              cprio = pr;
+            }
+          }
         if (cand < 0) {
           __builtin_amdgcn_s_sleep(2);
           continue;
