@@ -1696,7 +1696,10 @@ struct MsBits {
   bool marker;
   int lastw;  // last dword holding a byte of the file
   // dword i (clamped: never a byte past the file is used)
-  __device__ __forceinline__ uint32_t word(int i) const { return w[i < lastw ? i : lastw]; }
+  __device__ __forceinline__ uint32_t word(int i) const {
+    // (an unsigned 32-bit index: no 64-bit sign extension in the address)
+    return w[(uint32_t)(i < lastw ? i : lastw)];
+  }
   __device__ __forceinline__ uint32_t byte(int i) const {
     return (word(i >> 2) >> (8 * (i & 3))) & 0xFFu;
   }
@@ -1759,9 +1762,7 @@ struct MsBits {
       cnt += 8;
     }
   }
-  __device__ __forceinline__ void need() {
-    if (cnt < 32) fill();
-  }
+  __device__ __forceinline__ void need();
   __device__ __forceinline__ uint32_t hi32() const { return (uint32_t)(buf >> 32); }
   __device__ __forceinline__ uint32_t peek16() const { return hi32() >> 16; }
   // the next s bits (1..16) as a JPEG signed value (F.2.2.1 EXTEND), taken;
@@ -1798,6 +1799,57 @@ struct MsBits {
   }
   __device__ __forceinline__ bool truncated() const { return fake > cnt; }
 };
+
+// The bit reader's slow refill (an 0xFF byte, a marker, the scan's last
+// bytes: ~2 % of refills), out of line so that the decode loops keep only
+// the 4-byte step: fewer branches and register copies on the symbol path.
+// (Arguments of a non-kernel function live in VGPRs: the fields come back
+// through readfirstlane.)
+struct MsFillState {
+  uint64_t buf;
+  int cnt, pos, fake, marker;
+  uint32_t n0, n1;
+};
+__device__ __noinline__ MsFillState ms_fill_slow(MsWords w, int size, int end, int lastw,
+                                                 MsFillState f) {
+  MsBits b;
+  b.w = w;
+  b.size = size;
+  b.end = end;
+  b.lastw = lastw;
+  b.buf = f.buf;
+  b.cnt = f.cnt;
+  b.pos = f.pos;
+  b.fake = f.fake;
+  b.marker = f.marker != 0;
+  b.n0 = f.n0;
+  b.n1 = f.n1;
+  b.fill();
+  return MsFillState{b.buf, b.cnt, b.pos, b.fake, b.marker ? 1 : 0, b.n0, b.n1};
+}
+
+__device__ __forceinline__ void MsBits::need() {
+  if (cnt < 32) {
+    // the common step inline (one 4-byte step always tops the buffer up)
+    const uint32_t x = (uint32_t)((((uint64_t)n1 << 32) | n0) >> (8 * (pos & 3)));
+    if (!marker && pos + 4 <= end && ((~x - 0x01010101u) & x & 0x80808080u) == 0u) {
+      buf |= (uint64_t)ms_u(__builtin_bswap32(x)) << (32 - cnt);
+      cnt += 32;
+      pos += 4;
+      pair(pos >> 2);
+    } else {
+      const MsFillState f =
+          ms_fill_slow(w, size, end, lastw, MsFillState{buf, cnt, pos, fake, marker ? 1 : 0, n0, n1});
+      buf = ms_u64(f.buf);
+      cnt = ms_i(f.cnt);
+      pos = ms_i(f.pos);
+      fake = ms_i(f.fake);
+      marker = ms_i(f.marker) != 0;
+      n0 = ms_u(f.n0);
+      n1 = ms_u(f.n1);
+    }
+  }
+}
 
 // A Huffman table held in four VGPRs (one entry per lane):
 //   l1   lane p: the code starting with the 6-bit prefix p, len | symbol << 8
@@ -1865,6 +1917,22 @@ __device__ __forceinline__ int rt_decode(const RTab& t, uint32_t w16, int& len) 
   len = L;
   const uint32_t idx = ms_rl(t.voff, L) + (w16 >> (16 - L));
   return (int)((ms_rl(t.vals, (int)(idx >> 2)) >> (8 * (idx & 3u))) & 0xFFu);
+}
+
+// The same as one packed entry, len | symbol << 8 (0xFFFFFF00: a bad code,
+// len 0, symbol -1), with a single branch for the codes longer than 6 bits.
+__device__ __forceinline__ uint32_t rt_entry(const RTab& t, uint32_t w16) {
+  uint32_t e = ms_rl(t.l1, (int)(w16 >> 10));
+  if (e == 0u) {
+    int L = __popcll(__builtin_amdgcn_ballot_w64(t.lim <= w16));
+    ms_opaque(L);
+    L += 1;
+    const int Lc = L > 16 ? 16 : L;
+    const uint32_t idx = ms_rl(t.voff, Lc) + (w16 >> (16 - Lc));
+    const uint32_t sym = (ms_rl(t.vals, (int)((idx >> 2) & 63u)) >> (8 * (idx & 3u))) & 0xFFu;
+    e = L > 16 ? 0xFFFFFF00u : ((uint32_t)L | sym << 8);
+  }
+  return e;
 }
 
 // bits k .. e (inclusive) of a coefficient mask; 0 when k > e
@@ -2061,7 +2129,8 @@ template <int kind>
 __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft, const MsGeo& g,
                                               const ImageInfo& in, const uint8_t* __restrict__ d,
                                               int size, int32_t* __restrict__ lv,
-                                              uint64_t* __restrict__ masks, int lane, int& nsym) {
+                                              uint64_t* __restrict__ masks, int lane, int& nsym,
+                                              int64_t (&prof)[3]) {
   const MsScan& scl = S.scan[si];
   const MsBand sc = ms_band(scl);
   // AC scans of a progressive image have one component
@@ -2114,6 +2183,15 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
   bool have_next = false;
   if constexpr (kind == kScanAcRefine) ch.blk = -1;
   int bx = 0, by = 0, rpos = 0;
+  // a one-component scan's block index, kept incrementally: rowb (the row's
+  // first block) + colq (whole MCUs along the row) + colr (the block within
+  // the MCU's width)
+  const int bpm1 = g.ncomp == 1 ? 1 : g.bpm;
+  const auto row_base = [&](int y) {
+    return g.ncomp == 1 ? y * g.mcux
+                        : ms_div(y, vc1) * g.mcux * g.bpm + b01 + (y - ms_div(y, vc1) * vc1) * hc1;
+  };
+  int rowb = row_base(0), colq = 0, colr = 0;
   for (int mcu = 0;; mcu++) {
     if constexpr (kind == kScanAcRefine) {
       if ((mcu & (kMsChunk - 1)) == 0 || mcu >= nmcu) {
@@ -2180,18 +2258,16 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
       eobrun = 0;
     }
 #pragma unroll 1
-    for (int i = 0; i < sc.ns && rc == kOk; i++) {
+    for (int i = 0; i < (kAc ? 1 : sc.ns) && rc == kOk; i++) {
       // the MCU's blocks of scan component i (one block for a one-component scan)
       int b, nb = 1;
-      if (sc.ns > 1) {
+      if (!kAc && sc.ns > 1) {
         const int c = ms_i(scl.comp[i]);
         nb = g.h(c) * g.v(c);
         b = mcu * g.bpm;
         for (int k = 0; k < c; k++) b += g.h(k) * g.v(k);
       } else {
-        b = g.ncomp == 1 ? by * g.mcux + bx
-                         : (ms_div(by, vc1) * g.mcux + ms_div(bx, hc1)) * g.bpm + b01 +
-                               (by - ms_div(by, vc1) * vc1) * hc1 + (bx - ms_div(bx, hc1) * hc1);
+        b = rowb + colq + colr;
       }
       RTab dt, at;
       if constexpr (need_dc) dt = kComp == 1 ? tdc[0] : rt_pick(i, tdc);
@@ -2218,34 +2294,41 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
           if (eobrun > 0) {
             eobrun--;
           } else {
+            // one exit, at the bottom (as the refinement loop below)
             uint64_t nz = 0;
-            for (int k = ss; k <= se; k++) {
-              br.need();
-              int len;
-              const int rs = rt_decode(at, br.peek16(), len);
+            int k = ss, rs, r, s;
+            bool eob, bad, cont;
+            br.need();
+            do {
+              const uint32_t e = rt_entry(at, br.peek16());  // (len 0, -1: bad code)
               nsym++;
-              if (rs < 0) {
-                rc = kErrBadHuffman;
-                break;
-              }
-              br.skip(len);
-              const int r = rs >> 4, s = rs & 15;
-              if (s) {
-                k += r;
-                if (k > se) {
-                  rc = kErrBadHuffman;
-                  break;
-                }
-                vblk = ms_wl(vblk, (uint32_t)br.take_ext(s) << al, k);
-                nz |= 1ull << k;
-              } else if (r == 15) {
-                k += 15;
-              } else {
-                eobrun = (1 << r) - 1;
-                if (r) eobrun += (int)br.take(r);
-                break;
-              }
+              br.skip((int)(e & 31u));
+              rs = (int)e >> 8;
+              r = rs >> 4;
+              s = rs & 15;
+              eob = s == 0 && r != 15;
+              k += r;  // (ZRL: 15)
+              bad = rs < 0 || (s != 0 && k > se);
+              // the value (F.2.2.1 EXTEND; 0 for s = 0), branch-free
+              uint32_t h = br.hi32();
+              ms_opaque(h);
+              const int v = (int)((h >> 1) >> (31 - s));
+              const int x = (int32_t)h < 0 ? v : v + 1 - (1 << s);
+              br.skip(s);
+              const bool put = s != 0 && !bad;
+              vblk = ms_wl(vblk, (uint32_t)x << al, put ? k : 64);
+              nz |= put ? 1ull << k : 0ull;
+              k++;
+              cont = !eob && !bad && k <= se;
+              br.need();
+            } while (cont);
+            if (bad) {
+              rc = kErrBadHuffman;
+            } else if (eob) {
+              eobrun = (1 << r) - 1;
+              if (r) eobrun += (int)br.take(r);
             }
+            if (rc != kOk) break;
             if (nz) {
               if (inband) blev[lane] = (int32_t)vblk;
               vblk = 0;
@@ -2255,72 +2338,104 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
           if ((mcu & (kMsChunk - 1)) == kMsChunk - 1) ms_publish(S, si, mcu + 1);
         } else if constexpr (kind == kScanAcRefine) {
           // against the block's non-zero mask (lane j of the chunk)
+#ifdef HJ_MS_PROF
+          const int64_t pt0 = (int64_t)__builtin_amdgcn_s_memtime();
+          int64_t pt1 = pt0;
+#endif
           const int j = mcu & (kMsChunk - 1);
           const uint64_t hist = ((uint64_t)ms_rl(ch.mhi, j) << 32 | ms_rl(ch.mlo, j)) & band;
-          const uint64_t hz = ~hist & band;  // zero before the scan
           const int htot = __popcll(hist);
           uint64_t corr = 0, nm = 0, nsg = 0;
-          int cb = 0;  // correction bits taken (non-zero history coefficients below k)
-          int k = ss;
+          int cb = 0;  // correction bits taken (non-zero history coefficients passed)
           if (eobrun <= 0) {
-            while (k <= se) {
-              br.need();
-              int len;
-              const int rs = rt_decode(at, br.peek16(), len);
+            // zpos lane i: the place of the band's i-th coefficient that was
+            // zero before the scan (a lane permutation: the others go after)
+            const uint64_t hz = ~hist & band;
+            const int nzero = __popcll(hz);
+            const int below = (int)__builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(hz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hz, 0u));
+            const bool isz = (hz >> lane) & 1ull;
+            const uint32_t zpos = (uint32_t)__builtin_amdgcn_ds_permute(
+                (isz ? below : nzero + lane - below) << 2, lane);
+            // One exit, at the bottom: the rare ends (EOBr, a run past se, a
+            // bad code) only clear `live` and are sorted out after the loop,
+            // so the symbol step is straight-line scalar code.
+            int k = ss, zi = 0;  // next coefficient; zeros before it
+            int r, s, t;
+            bool cont;
+#ifdef HJ_MS_PROF
+            (void)ms_rl(zpos, 0);
+            pt1 = (int64_t)__builtin_amdgcn_s_memtime();
+#endif
+            // (the refill at the bottom: the common path falls through)
+            br.need();
+            do {
+              const uint32_t e = rt_entry(at, br.peek16());  // (len 0, -1: bad code)
               nsym++;
-              if (rs < 0) {
-                rc = kErrBadHuffman;
-                break;
-              }
-              br.skip(len);
-              const int r = rs >> 4, s = rs & 15;
-              uint32_t neg = 0;
-              if (s) {
-                if (s != 1) {
-                  rc = kErrBadHuffman;
-                  break;
-                }
-                neg = br.take_bit() ^ 1u;
-              } else if (r != 15) {
-                eobrun = 1 << r;
-                if (r) eobrun += (int)br.take(r);
-                break;
-              }
+              br.skip((int)(e & 31u));
+              const int rs = (int)e >> 8;
+              r = rs >> 4;
+              s = rs & 15;
+              const bool eob = s == 0 && r != 15;
+              const int s1 = s & 1;  // (s > 1 ends the loop as an error: its state is moot)
+              // the new coefficient's sign (bit 1: positive)
+              uint32_t h = br.hi32();
+              ms_opaque(h);
+              const uint32_t neg = (~h >> 31) & (uint32_t)s1;
+              br.skip(s1);
               // the (r + 1)-th coefficient from k that was zero before the
-              // scan: the new coefficient's place (ZRL: the 16th zero, left
-              // zero); every non-zero one passed on the way takes a
+              // scan is the new coefficient's place (ZRL: the 16th, left
+              // zero); each non-zero one passed on the way takes a
               // correction bit
-              uint64_t zm = hz & (~0ull << k);
-              for (int q = 0; q < r && zm; q++) zm &= zm - 1;
-              if (zm == 0ull) {  // ran past se
-                ms_take_corr(br, htot - cb, corr);
-                cb = htot;
-                k = se + 1;
-                if (s) rc = kErrBadHuffman;
-                break;
+              t = zi + r;
+              const bool live = !eob && s <= 1 && t < nzero;
+              const int p = (int)ms_rl(zpos, live ? t : 0);
+              int c = p - k - r;
+              c = live ? c : 0;
+              if (c <= 15) {  // (>= 15 bits are left after a code and a sign)
+                uint32_t hc = br.hi32();
+                ms_opaque(hc);
+                corr = (corr << c) | ((hc >> 1) >> (31 - c));
+                br.skip(c);
+              } else {
+                ms_take_corr(br, c, corr);
               }
-              const int p = __builtin_ctzll(zm);
-              const int c = __popcll(hist & ((1ull << p) - 1ull)) - cb;
-              ms_take_corr(br, c, corr);
               cb += c;
-              if (s) {
-                nm |= 1ull << p;
-                nsg |= (uint64_t)neg << p;
-              }
+              const uint32_t m1 = live ? (uint32_t)s1 : 0u;
+              nm |= (uint64_t)m1 << p;
+              nsg |= (uint64_t)(m1 & neg) << p;
               k = p + 1;
+              zi = t + 1;
+              cont = live && k <= se;
+              br.need();
+            } while (cont);
+            if (s > 1 || (s == 1 && t >= nzero)) {
+              rc = kErrBadHuffman;  // (a bad code, a value other than +-1, a new coefficient past se)
+            } else if (s == 0 && r != 15) {  // EOBr
+              eobrun = 1 << r;
+              if (r) eobrun += (int)br.take(r);
             }
           }
+#ifdef HJ_MS_PROF
+          const int64_t pt2 = (int64_t)__builtin_amdgcn_s_memtime();
+#endif
           if (rc != kOk) break;
-          if (eobrun > 0) {
-            ms_take_corr(br, htot - cb, corr);
-            eobrun--;
-          }
+          // the history coefficients after the last symbol (an EOB run, or a
+          // run past se) take their correction bits
+          ms_take_corr(br, htot - cb, corr);
+          if (eobrun > 0) eobrun--;
           ch.clo = ms_wl(ch.clo, (uint32_t)corr, j);
           ch.chi = ms_wl(ch.chi, (uint32_t)(corr >> 32), j);
           ch.wlo = ms_wl(ch.wlo, (uint32_t)nm, j);
           ch.whi = ms_wl(ch.whi, (uint32_t)(nm >> 32), j);
           ch.slo = ms_wl(ch.slo, (uint32_t)nsg, j);
           ch.shi = ms_wl(ch.shi, (uint32_t)(nsg >> 32), j);
+#ifdef HJ_MS_PROF
+          const int64_t pt3 = (int64_t)__builtin_amdgcn_s_memtime();
+          prof[0] += pt1 - pt0;
+          prof[1] += pt2 - pt1;
+          prof[2] += pt3 - pt2;
+#endif
         } else {  // sequential: the whole block
           br.need();
           int len;
@@ -2370,6 +2485,12 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
     if (++bx == bw1) {
       bx = 0;
       by++;
+      rowb = row_base(by);
+      colq = colr = 0;
+    } else {
+      const bool wrap = colr + 1 == hc1;
+      colr = wrap ? 0 : colr + 1;
+      colq += wrap ? bpm1 : 0;
     }
     if (sc.ri && ++rpos == sc.ri) rpos = 0;
   }
@@ -2648,22 +2769,32 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
       const MsBand bd = ms_band(sc);
       const uint64_t soft = ms_u64(S.soft[si]);
       int rc, nsym = 0;
+      int64_t prof[3] = {0, 0, 0};
       if (!progu)
-        rc = ms_decode_scan<kScanSeq>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
+        rc = ms_decode_scan<kScanSeq>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
       else if (bd.ss == 0 && bd.ah == 0)
-        rc = ms_decode_scan<kScanDcFirst>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
+        rc = ms_decode_scan<kScanDcFirst>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
       else if (bd.ss == 0)
-        rc = ms_decode_scan<kScanDcRefine>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
+        rc = ms_decode_scan<kScanDcRefine>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
       else if (bd.ah == 0)
-        rc = ms_decode_scan<kScanAcFirst>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
+        rc = ms_decode_scan<kScanAcFirst>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
       else
-        rc = ms_decode_scan<kScanAcRefine>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym);
+        rc = ms_decode_scan<kScanAcRefine>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
       // the scan's stores are visible before it counts as done
       ms_publish(S, si, 1 << 30);
       if (ms_lane0() && si < 16) {
         S.sdiag[3 * si] = (int32_t)(ts - tdec);
         S.sdiag[3 * si + 1] = (int32_t)(wall_clock64() - tdec);
         S.sdiag[3 * si + 2] = nsym;
+#ifdef HJ_MS_PROF
+        // (profile build: cycles / 256 of the refinement blocks' setup, symbol
+        // loops and ends in place of the start / end times)
+        if (prof[1]) {
+          S.sdiag[3 * si] = (int32_t)(prof[0] >> 8);
+          S.sdiag[3 * si + 1] = (int32_t)(prof[1] >> 8);
+          S.sdiag[3 * si + 2] = (int32_t)(prof[2] >> 8);
+        }
+#endif
       }
       if (ms_lane0()) {
         if (rc != kOk) atomicCAS(&S.err, kOk, rc);

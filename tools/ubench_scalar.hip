@@ -70,6 +70,35 @@ __global__ void __launch_bounds__(64) ub(const uint32_t* __restrict__ data, int 
       acc += bit;
       if (mode == 5 && bit && lane == 0) atomicOr(out + 64 + ((i & 1023) * 64), 1u);
     }
+  } else if (mode == 8) {
+    // four independent chains of the mode-0 ops (issue rate, not latency)
+    uint32_t a2 = acc + 1u, a3 = acc + 2u, a4 = acc + 3u;
+    for (int i = 0; i < iters; i++) {
+      acc ^= acc << 7;
+      a2 ^= a2 << 7;
+      a3 ^= a3 << 7;
+      a4 ^= a4 << 7;
+      acc += (acc >> 3) ^ 0x9e37u;
+      a2 += (a2 >> 3) ^ 0x9e37u;
+      a3 += (a3 >> 3) ^ 0x9e37u;
+      a4 += (a4 >> 3) ^ 0x9e37u;
+    }
+    acc ^= a2 ^ a3 ^ a4;
+  } else if (mode == 9) {
+    // 64-bit shifts and selects, one chain (the bit buffer's ops)
+    uint64_t b = ((uint64_t)acc << 32) | 0x12345u;
+    for (int i = 0; i < iters; i++) {
+      const uint32_t s = (uint32_t)(b >> 59);
+      b = (b << s) | (uint64_t)(s + 1u);
+      b = (s & 1u) ? b ^ 0x5555ull : b;
+    }
+    acc += (uint32_t)b;
+  } else if (mode == 10) {
+    // branch taken every iteration (structurizer-style flow)
+    for (int i = 0; i < iters; i++) {
+      if (acc & 1u) acc = acc * 3u + 1u; else acc >>= 1;
+      asm volatile("" : "+s"(acc));
+    }
   } else if (mode == 7) {
     for (int i = 0; i < iters; i++)
       if (lane == 0) atomicOr(out + 64 + ((i & 1023) * 64), 1u);
@@ -92,8 +121,9 @@ int main() {
   const char* names[] = {"salu chain (2 dep ops)", "s_load used at once", "s_load one ahead",
                          "v_readlane chain", "ds_read+readfirstlane chain",
                          "bit reader get(1) + lane0 atomic", "bit reader get(1)",
-                         "lane0 atomicOr only"};
-  for (int m = 0; m < 8; m++) {
+                         "lane0 atomicOr only", "4 independent salu chains", "64-bit shift/select chain",
+                         "data-dependent branch"};
+  for (int m = 0; m < 11; m++) {
     for (int rep = 0; rep < 2; rep++) {
       hipLaunchKernelGGL(ub, dim3(1), dim3(64), 0, 0, d, nwords, iters, m, o, c);
       hipDeviceSynchronize();
