@@ -1829,10 +1829,10 @@ __device__ __noinline__ MsFillState ms_fill_slow(MsWords w, int size, int end, i
 }
 
 __device__ __forceinline__ void MsBits::need() {
-  if (cnt < 32) {
+  if (__builtin_expect(cnt < 32, 0)) {
     // the common step inline (one 4-byte step always tops the buffer up)
     const uint32_t x = (uint32_t)((((uint64_t)n1 << 32) | n0) >> (8 * (pos & 3)));
-    if (!marker && pos + 4 <= end && ((~x - 0x01010101u) & x & 0x80808080u) == 0u) {
+    if (__builtin_expect(!marker && pos + 4 <= end && ((~x - 0x01010101u) & x & 0x80808080u) == 0u, 1)) {
       buf |= (uint64_t)ms_u(__builtin_bswap32(x)) << (32 - cnt);
       cnt += 32;
       pos += 4;
@@ -1923,7 +1923,7 @@ __device__ __forceinline__ int rt_decode(const RTab& t, uint32_t w16, int& len) 
 // len 0, symbol -1), with a single branch for the codes longer than 6 bits.
 __device__ __forceinline__ uint32_t rt_entry(const RTab& t, uint32_t w16) {
   uint32_t e = ms_rl(t.l1, (int)(w16 >> 10));
-  if (e == 0u) {
+  if (__builtin_expect(e == 0u, 0)) {
     int L = __popcll(__builtin_amdgcn_ballot_w64(t.lim <= w16));
     ms_opaque(L);
     L += 1;
@@ -1931,6 +1931,34 @@ __device__ __forceinline__ uint32_t rt_entry(const RTab& t, uint32_t w16) {
     const uint32_t idx = ms_rl(t.voff, Lc) + (w16 >> (16 - Lc));
     const uint32_t sym = (ms_rl(t.vals, (int)((idx >> 2) & 63u)) >> (8 * (idx & 3u))) & 0xFFu;
     e = L > 16 ? 0xFFFFFF00u : ((uint32_t)L | sym << 8);
+  }
+  return e;
+}
+
+// AC refinement entries: the symbol's fields the symbol loop needs, unpacked
+// once per table instead of once per symbol:
+//   bits 0-4 code length (0: bad code), bit 5 s == 1 (a new coefficient),
+//   bit 6 stop (EOBr, or s > 1: an error), bits 8-11 r, bits 16-31 the
+//   symbol (-1: bad code)
+__device__ __forceinline__ uint32_t ms_ref_pack(uint32_t L, int sym) {
+  const int s = sym & 15, r = sym >> 4;
+  const uint32_t stop = ((s == 0 && r != 15) || s > 1) ? 1u : 0u;
+  return L | (s == 1 ? 32u : 0u) | stop << 6 | (uint32_t)(r & 15) << 8 | (uint32_t)sym << 16;
+}
+// (per lane, on a built table's first level)
+__device__ __forceinline__ uint32_t ms_ref_l1(uint32_t e) {
+  return e ? ms_ref_pack(e & 31u, (int)(e >> 8)) : 0u;
+}
+__device__ __forceinline__ uint32_t rt_entry_ref(const RTab& t, uint32_t w16) {
+  uint32_t e = ms_rl(t.l1, (int)(w16 >> 10));
+  if (__builtin_expect(e == 0u, 0)) {
+    int L = __popcll(__builtin_amdgcn_ballot_w64(t.lim <= w16));
+    ms_opaque(L);
+    L += 1;
+    const int Lc = L > 16 ? 16 : L;
+    const uint32_t idx = ms_rl(t.voff, Lc) + (w16 >> (16 - Lc));
+    const uint32_t sym = (ms_rl(t.vals, (int)((idx >> 2) & 63u)) >> (8 * (idx & 3u))) & 0xFFu;
+    e = L > 16 ? 0xFFFF0040u : ms_ref_pack((uint32_t)L, (int)sym);
   }
   return e;
 }
@@ -1993,6 +2021,45 @@ __device__ __forceinline__ void ms_take_corr(MsBits& br, int c, uint64_t& corr) 
     corr = (corr << t) | br.get(t);
     c -= t;
   }
+}
+
+// The same for a long run of correction bits (> 15), out of line: the
+// symbol loop's registers stay put on its common path.
+struct MsCorrState {
+  MsFillState f;
+  uint64_t corr;
+};
+__device__ __noinline__ MsCorrState ms_take_corr_slow(MsWords w, int size, int end, int lastw,
+                                                      MsCorrState st, int c) {
+  MsBits b;
+  b.w = w;
+  b.size = size;
+  b.end = end;
+  b.lastw = lastw;
+  b.buf = st.f.buf;
+  b.cnt = st.f.cnt;
+  b.pos = st.f.pos;
+  b.fake = st.f.fake;
+  b.marker = st.f.marker != 0;
+  b.n0 = st.f.n0;
+  b.n1 = st.f.n1;
+  ms_take_corr(b, c, st.corr);
+  st.f = MsFillState{b.buf, b.cnt, b.pos, b.fake, b.marker ? 1 : 0, b.n0, b.n1};
+  return st;
+}
+__device__ __forceinline__ void ms_take_corr_long(MsBits& br, int c, uint64_t& corr) {
+  const MsCorrState st = ms_take_corr_slow(
+      br.w, br.size, br.end, br.lastw,
+      MsCorrState{MsFillState{br.buf, br.cnt, br.pos, br.fake, br.marker ? 1 : 0, br.n0, br.n1}, corr},
+      c);
+  br.buf = ms_u64(st.f.buf);
+  br.cnt = ms_i(st.f.cnt);
+  br.pos = ms_i(st.f.pos);
+  br.fake = ms_i(st.f.fake);
+  br.marker = ms_i(st.f.marker) != 0;
+  br.n0 = ms_u(st.f.n0);
+  br.n1 = ms_u(st.f.n1);
+  corr = ms_u64(st.corr);
 }
 
 enum { kScanSeq = 0, kScanDcFirst, kScanDcRefine, kScanAcFirst, kScanAcRefine };
@@ -2179,6 +2246,11 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
   const bool inband = lane >= ss && lane <= se;
   const uint64_t band = ms_range(ss, se);
   uint32_t vblk = 0;  // the block being decoded, lane k = coefficient k
+  RTab atr;  // AC refinement: the table with packed first-level entries
+  if constexpr (kind == kScanAcRefine) {
+    atr = tac[0];
+    atr.l1 = ms_ref_l1(atr.l1);
+  }
   MsChunk ch;
   bool have_next = false;
   if constexpr (kind == kScanAcRefine) ch.blk = -1;
@@ -2359,25 +2431,26 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
                 (isz ? below : nzero + lane - below) << 2, lane);
             // One exit, at the bottom: the rare ends (EOBr, a run past se, a
             // bad code) only clear `live` and are sorted out after the loop,
-            // so the symbol step is straight-line scalar code.
+            // so the symbol step is straight-line scalar code (flags as 0/1
+            // integers, not compare results).
             int k = ss, zi = 0;  // next coefficient; zeros before it
-            int r, s, t;
-            bool cont;
+            uint32_t e;
+            int t, cont;
+            // zpos is waited for here, once: in the loop the LDS and scalar
+            // load counters are one, and a wait for it there would also wait
+            // for the bit reader's prefetch
+            asm volatile("" ::"s"(ms_rl(zpos, 0)));
 #ifdef HJ_MS_PROF
-            (void)ms_rl(zpos, 0);
             pt1 = (int64_t)__builtin_amdgcn_s_memtime();
 #endif
             // (the refill at the bottom: the common path falls through)
             br.need();
             do {
-              const uint32_t e = rt_entry(at, br.peek16());  // (len 0, -1: bad code)
+              e = rt_entry_ref(atr, br.peek16());
               nsym++;
               br.skip((int)(e & 31u));
-              const int rs = (int)e >> 8;
-              r = rs >> 4;
-              s = rs & 15;
-              const bool eob = s == 0 && r != 15;
-              const int s1 = s & 1;  // (s > 1 ends the loop as an error: its state is moot)
+              const int s1 = (int)((e >> 5) & 1u), stop = (int)((e >> 6) & 1u);
+              const int r = (int)((e >> 8) & 15u);
               // the new coefficient's sign (bit 1: positive)
               uint32_t h = br.hi32();
               ms_opaque(h);
@@ -2388,27 +2461,34 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
               // zero); each non-zero one passed on the way takes a
               // correction bit
               t = zi + r;
-              const bool live = !eob && s <= 1 && t < nzero;
-              const int p = (int)ms_rl(zpos, live ? t : 0);
-              int c = p - k - r;
-              c = live ? c : 0;
-              if (c <= 15) {  // (>= 15 bits are left after a code and a sign)
+              // (sign bits, not compares: a compare result the loop keeps
+              // would become a lane mask and go through the VALU)
+              uint32_t dz = (uint32_t)(t - nzero);
+              ms_opaque(dz);
+              const int live = (int)(dz >> 31) & (stop ^ 1);
+              const int lm = -live;
+              const int p = (int)ms_rl(zpos, t & lm);
+              const int c = (p - k - r) & lm;
+              if (__builtin_expect(c <= 15, 1)) {  // (>= 15 bits are left after a code and a sign)
                 uint32_t hc = br.hi32();
                 ms_opaque(hc);
                 corr = (corr << c) | ((hc >> 1) >> (31 - c));
                 br.skip(c);
               } else {
-                ms_take_corr(br, c, corr);
+                ms_take_corr_long(br, c, corr);
               }
               cb += c;
-              const uint32_t m1 = live ? (uint32_t)s1 : 0u;
+              const uint32_t m1 = (uint32_t)(s1 & live);
               nm |= (uint64_t)m1 << p;
               nsg |= (uint64_t)(m1 & neg) << p;
               k = p + 1;
               zi = t + 1;
-              cont = live && k <= se;
+              uint32_t dk = (uint32_t)(se - k);
+              ms_opaque(dk);
+              cont = live & (int)((dk >> 31) ^ 1u);
               br.need();
-            } while (cont);
+            } while (__builtin_expect(cont, 1));
+            const int rs = (int)e >> 16, r = rs >> 4, s = rs & 15;
             if (s > 1 || (s == 1 && t >= nzero)) {
               rc = kErrBadHuffman;  // (a bad code, a value other than +-1, a new coefficient past se)
             } else if (s == 0 && r != 15) {  // EOBr
