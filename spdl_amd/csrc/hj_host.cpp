@@ -42,7 +42,7 @@ hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, Ima
                           hipStream_t);
 hipError_t launch_idct(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, uint8_t*,
                        int, int, int, hipStream_t);
-hipError_t launch_multiscan(const uint8_t*, const ImageDesc*, ImageInfo*, uint32_t*, uint2*, int,
+hipError_t launch_multiscan(const uint8_t*, uint8_t*, const ImageDesc*, ImageInfo*, uint32_t*, uint2*, int,
                             hipStream_t);
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                       const BatchParams&, int64_t, int, int32_t*, hipStream_t);
@@ -902,7 +902,8 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   // (debug_mask 0x10000 / 0x20000 / 0x40000: timing ablations that skip the
   // multiscan / IDCT / output launch; the output is wrong)
   if (!(ctx->debug_mask & 0x10000))
-    HJ_HIP(launch_multiscan(d_bytes, desc, infos, static_cast<uint32_t*>(W.ents.p),
+    HJ_HIP(launch_multiscan(d_bytes, static_cast<uint8_t*>(W.clean.p), desc, infos,
+                            static_cast<uint32_t*>(W.ents.p),
                             static_cast<uint2*>(W.bdesc.p), n, st));
   mark(ctx, slot, 4, st);
   // full resolution u8 through swscale's unscaled converter: IDCT and

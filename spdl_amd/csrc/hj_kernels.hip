@@ -1648,6 +1648,8 @@ struct MsShared {
   uint64_t soft[kMsMaxScans];  // ... or only to run ahead of it (trailing, below)
   int32_t prog[kMsMaxScans];   // blocks a scan has finished, in scan order
   int32_t prio[kMsMaxScans];   // claim priority (bytes of its heaviest dependent chain)
+  int32_t dlen[kMsMaxScans];   // destuffed bytes in `clean` (-1: the stuffed reader)
+  int32_t wtot[4], dodd;       // destuff scratch
   uint64_t claimed, done;      // scans taken by a decoder wave / finished
   int64_t tkind[4];            // diagnostics: decode ticks by scan kind
   int32_t marks[kMsMaxMarks];
@@ -1851,6 +1853,85 @@ __device__ __forceinline__ void MsBits::need() {
   }
 }
 
+// Bit reader over a scan's pre-destuffed data (multiscan_kernel writes it to
+// `clean` as big-endian dwords before any decoder wave starts): a refill is
+// one aligned dword, loaded one refill ahead by a scalar load, with no 0xFF
+// test, marker or byte swap.  Past the data it reads zeros, as the stuffed
+// reader feeds zeros after a marker.  (The copy is read through the scalar
+// cache, which starts each dispatch empty, only after the kernel wrote it
+// and fenced: the stuffed reader's file bytes take the same path.)
+struct MsWBits {
+  MsWords w;
+  uint64_t buf;  // left-justified
+  int cnt;
+  int wi, lastw;  // next dword to enter the buffer; last dword holding data
+  uint32_t nxm;   // ~0 while wi <= lastw
+  uint32_t nx;    // dword wi (prefetched)
+  int nbits;      // bits of data
+  __device__ __forceinline__ void init(const uint8_t* p, int len) {
+    // (readfirstlane: the pointer is uniform, but the compiler cannot see
+    // it through the destuff pass's stores and would load through VGPRs)
+    w = (MsWords)(const void*)(uintptr_t)ms_u64((uint64_t)(uintptr_t)p);
+    nbits = 8 * len;
+    lastw = len > 0 ? (len - 1) >> 2 : 0;
+    wi = 0;
+    nxm = len > 0 ? ~0u : 0u;
+    nx = w[0];
+    buf = 0;
+    cnt = 0;
+  }
+  __device__ __forceinline__ void need() {
+    if (__builtin_expect(cnt < 32, 0)) {
+      buf |= (uint64_t)(nx & nxm) << (32 - cnt);
+      cnt += 32;
+      wi++;
+      int past = lastw - wi;  // (< 0: past the data; a sign, not a compare
+      ms_opaque(past);        // result, which would go through the VALU)
+      nxm = ~(uint32_t)(past >> 31);
+      nx = w[(uint32_t)min(wi, lastw)];
+    }
+  }
+  __device__ __forceinline__ uint32_t hi32() const { return (uint32_t)(buf >> 32); }
+  __device__ __forceinline__ uint32_t peek16() const { return hi32() >> 16; }
+  __device__ __forceinline__ int take_ext(int s) {
+    uint32_t h = hi32();
+    ms_opaque(h);
+    const int v = (int)(h >> (32 - s));
+    skip(s);
+    return (int32_t)h < 0 ? v : v + 1 - (1 << s);
+  }
+  __device__ __forceinline__ uint32_t take_bit() {
+    uint32_t h = hi32();
+    ms_opaque(h);
+    skip(1);
+    return h >> 31;
+  }
+  __device__ __forceinline__ void skip(int n) {
+    buf <<= n;
+    cnt -= n;
+  }
+  __device__ __forceinline__ uint32_t take(int n) {
+    const uint32_t v = hi32() >> (32 - n);
+    skip(n);
+    return v;
+  }
+  __device__ __forceinline__ uint32_t get(int n) {
+    if (n == 0) return 0u;
+    need();
+    return take(n);
+  }
+  __device__ __forceinline__ bool truncated() const { return 32 * wi - cnt > nbits; }
+};
+
+template <class A, class B>
+struct ms_same {
+  static constexpr bool value = false;
+};
+template <class A>
+struct ms_same<A, A> {
+  static constexpr bool value = true;
+};
+
 // A Huffman table held in four VGPRs (one entry per lane):
 //   l1   lane p: the code starting with the 6-bit prefix p, len | symbol << 8
 //        (0: the code is longer than 6 bits)
@@ -2015,7 +2096,8 @@ __device__ __forceinline__ int ms_div(int x, int d) {
 
 // c correction bits appended MSB-first to corr (bit order of the stream:
 // the block's i-th non-zero history coefficient of n takes bit n - 1 - i)
-__device__ __forceinline__ void ms_take_corr(MsBits& br, int c, uint64_t& corr) {
+template <class Rd>
+__device__ __forceinline__ void ms_take_corr(Rd& br, int c, uint64_t& corr) {
   while (c > 0) {
     const int t = c < 32 ? c : 32;
     corr = (corr << t) | br.get(t);
@@ -2060,6 +2142,10 @@ __device__ __forceinline__ void ms_take_corr_long(MsBits& br, int c, uint64_t& c
   br.n0 = ms_u(st.f.n0);
   br.n1 = ms_u(st.f.n1);
   corr = ms_u64(st.corr);
+}
+
+__device__ __forceinline__ void ms_take_corr_long(MsWBits& br, int c, uint64_t& corr) {
+  ms_take_corr(br, c, corr);
 }
 
 enum { kScanSeq = 0, kScanDcFirst, kScanDcRefine, kScanAcFirst, kScanAcRefine };
@@ -2192,10 +2278,10 @@ __device__ __forceinline__ void ms_put(int i, int32_t (&v)[kMaxComp], int32_t x)
 // lv: the image's levels (64 int32 per block, zig-zag); masks: per block the
 // coefficients non-zero so far (AC bands of progressive images); soft: the
 // running scans this one trails (AC scans).
-template <int kind>
+template <int kind, class Rd>
 __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft, const MsGeo& g,
                                               const ImageInfo& in, const uint8_t* __restrict__ d,
-                                              int size, int32_t* __restrict__ lv,
+                                              const uint8_t* cl, int size, int32_t* __restrict__ lv,
                                               uint64_t* __restrict__ masks, int lane, int& nsym,
                                               int64_t (&prof)[3]) {
   const MsScan& scl = S.scan[si];
@@ -2235,11 +2321,16 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
   const int hc1 = g.ncomp == 1 ? 1 : g.h(c1), vc1 = g.ncomp == 1 ? 1 : g.v(c1);
   int b01 = 0;  // blocks of the components before c1 in an MCU
   for (int k = 0; k < c1; k++) b01 += g.h(k) * g.v(k);
-  MsBits br;
-  br.w = (MsWords)(const void*)d;
-  br.size = size;
-  br.lastw = (size - 1) >> 2;
-  br.start(sc.start, sc.end);
+  constexpr bool kWord = ms_same<Rd, MsWBits>::value;
+  Rd br;
+  if constexpr (kWord) {
+    br.init(cl + ((sc.start + 3) & ~3), ms_i(S.dlen[si]));
+  } else {
+    br.w = (MsWords)(const void*)d;
+    br.size = size;
+    br.lastw = (size - 1) >> 2;
+    br.start(sc.start, sc.end);
+  }
   int32_t pred[kMaxComp] = {0, 0, 0, 0};
   int eobrun = 0;
   const int al = sc.al, ss = sc.ss, se = sc.se;
@@ -2299,6 +2390,7 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
     } else {
       if (mcu >= nmcu) break;
     }
+    if constexpr (!kWord)  // (the word reader takes scans without restart markers)
     if (sc.ri && mcu && rpos == 0) {
       if (br.truncated()) {
         rc = kErrTruncated;
@@ -2361,7 +2453,10 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
           if (ms_lane0()) blev[0] = (int32_t)((uint32_t)pr << al);
         } else if constexpr (kind == kScanDcRefine) {
           br.need();
-          if (br.take_bit() && ms_lane0()) atomicOr(reinterpret_cast<unsigned int*>(blev), 1u << al);
+          const uint32_t bit = br.take_bit();
+          if (bit) {  // (uniform; then lane 0)
+            if (ms_lane0()) atomicOr(reinterpret_cast<unsigned int*>(blev), 1u << al);
+          }
         } else if constexpr (kind == kScanAcFirst) {
           if (eobrun > 0) {
             eobrun--;
@@ -2579,6 +2674,7 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
 }
 
 __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restrict__ bytes,
+                                                        uint8_t* __restrict__ clean,
                                                         const ImageDesc* __restrict__ desc,
                                                         ImageInfo* __restrict__ infos,
                                                         uint32_t* __restrict__ ents,
@@ -2749,6 +2845,83 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
     S.err = err;
   }
   __syncthreads();
+  // ---- each scan without restart markers destuffed into `clean` (the
+  // image's offsets; the scan's start rounded up to 4, so the scans' copies
+  // never overlap: headers >= 10 bytes lie between them), bytes reversed in
+  // each dword so that a dword load is the big-endian bit order.  Each thread
+  // takes a contiguous slice: count the kept bytes (a 0x00 after 0xFF is
+  // dropped), scan the counts, write.  A 0xFF followed by anything but 0x00
+  // inside the scan (fill bytes before the marker, a stray marker) leaves
+  // the scan to the stuffed reader, which stops there. ----
+  uint8_t* cl = clean + dd.in_off;
+  const int lane0 = tid & 63, wid = tid >> 6;
+  for (int i = 0; i < S.nscans && S.err == kOk; i++) {
+    const int s0 = S.scan[i].start, e0 = S.scan[i].end;
+    if (S.scan[i].ri != 0) {
+      if (tid == 0) S.dlen[i] = -1;
+      continue;
+    }
+    if (tid == 0) S.dodd = 0;
+    const int per = ((e0 - s0 + nt - 1) / nt + 15) & ~15;
+    const int cs = min(s0 + tid * per, e0), ce = min(cs + per, e0);
+    uint8_t* out = cl + ((s0 + 3) & ~3);
+    int kept = 0, off = 0;
+    bool odd = false;
+    for (int pass = 0; pass < 2; pass++) {
+      uint32_t prev = cs > s0 ? d[cs - 1] : 0u;
+      int o = off;
+      for (int a = cs & ~15; a < ce; a += 16) {
+        uint32_t w4[4];
+        if (a + 16 <= size) {
+          const uint4 q = *reinterpret_cast<const uint4*>(d + a);
+          w4[0] = q.x, w4[1] = q.y, w4[2] = q.z, w4[3] = q.w;
+        } else {
+          for (int k = 0; k < 4; k++) w4[k] = 0;
+          for (int k = 0; k < 16 && a + k < size; k++) w4[k >> 2] |= (uint32_t)d[a + k] << (8 * (k & 3));
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          const int p = a + k;
+          const uint32_t c = (w4[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+          if (p >= cs && p < ce) {
+            const bool ff = prev == 0xFFu;
+            if (ff && c != 0u) odd = true;
+            if (!(ff && c == 0u)) {
+              if (pass) out[o ^ 3] = (uint8_t)c;
+              o++;
+            }
+            prev = c;
+          }
+        }
+      }
+      if (ce == e0 && ce > cs && prev == 0xFFu) odd = true;  // (0xFF as the scan's last byte)
+      if (pass == 0) {
+        kept = o;
+        // exclusive scan of the slices' counts
+        const int inc = wave_incl_scan(kept);
+        if (lane0 == 63) S.wtot[wid] = inc;
+        if (odd) S.dodd = 1;
+        __syncthreads();
+        int wb = 0;
+        for (int k = 0; k < wid; k++) wb += S.wtot[k];
+        off = wb + inc - kept;
+        if (S.dodd) break;  // (uniform: every thread read it after the barrier)
+      }
+    }
+    const int total = S.wtot[0] + S.wtot[1] + S.wtot[2] + S.wtot[3];
+    __syncthreads();
+    if (tid == 0) {
+      if (S.dodd) {
+        S.dlen[i] = -1;
+      } else {
+        for (int k = total; k & 3; k++) out[k ^ 3] = 0;  // (the last dword's tail)
+        S.dlen[i] = total;
+      }
+    }
+    __syncthreads();
+  }
+  __threadfence();  // (the copies before any decoder wave reads them)
+  __syncthreads();
   tph[0] = wall_clock64() - t0;  // marker candidates + segment walk
   // ---- scan dependencies: a scan waits for every earlier scan that shares
   // a component and overlaps its coefficient band -- to finish, or, when
@@ -2850,16 +3023,22 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
       const uint64_t soft = ms_u64(S.soft[si]);
       int rc, nsym = 0;
       int64_t prof[3] = {0, 0, 0};
+      const bool wr = ms_i(S.dlen[si]) >= 0;  // destuffed copy (else the stuffed reader)
+#define HJ_MS_SCAN(K)                                                                      \
+  (wr ? ms_decode_scan<K, MsWBits>(S, si, soft, geo, in, d, cl, sizeu, lv, masks, lane, nsym, \
+                                   prof)                                                     \
+      : ms_decode_scan<K, MsBits>(S, si, soft, geo, in, d, cl, sizeu, lv, masks, lane, nsym, prof))
       if (!progu)
-        rc = ms_decode_scan<kScanSeq>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
+        rc = HJ_MS_SCAN(kScanSeq);
       else if (bd.ss == 0 && bd.ah == 0)
-        rc = ms_decode_scan<kScanDcFirst>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
+        rc = HJ_MS_SCAN(kScanDcFirst);
       else if (bd.ss == 0)
-        rc = ms_decode_scan<kScanDcRefine>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
+        rc = HJ_MS_SCAN(kScanDcRefine);
       else if (bd.ah == 0)
-        rc = ms_decode_scan<kScanAcFirst>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
+        rc = HJ_MS_SCAN(kScanAcFirst);
       else
-        rc = ms_decode_scan<kScanAcRefine>(S, si, soft, geo, in, d, sizeu, lv, masks, lane, nsym, prof);
+        rc = HJ_MS_SCAN(kScanAcRefine);
+#undef HJ_MS_SCAN
       // the scan's stores are visible before it counts as done
       ms_publish(S, si, 1 << 30);
       if (ms_lane0() && si < 16) {
@@ -2934,9 +3113,10 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   }
 }
 
-hipError_t launch_multiscan(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
-                            uint32_t* ents, uint2* bdesc, int n, hipStream_t st) {
-  hipLaunchKernelGGL(multiscan_kernel, dim3(n), dim3(256), 0, st, bytes, desc, infos, ents, bdesc);
+hipError_t launch_multiscan(const uint8_t* bytes, uint8_t* clean, const ImageDesc* desc,
+                            ImageInfo* infos, uint32_t* ents, uint2* bdesc, int n, hipStream_t st) {
+  hipLaunchKernelGGL(multiscan_kernel, dim3(n), dim3(256), 0, st, bytes, clean, desc, infos, ents,
+                     bdesc);
   return hipGetLastError();
 }
 
