@@ -2578,9 +2578,11 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
               nsg |= (uint64_t)(m1 & neg) << p;
               k = p + 1;
               zi = t + 1;
-              uint32_t dk = (uint32_t)(se - k);
+              // (k <= se, i.e. p < se: a sign bit)
+              uint32_t dk = (uint32_t)(p - se);
               ms_opaque(dk);
-              cont = live & (int)((dk >> 31) ^ 1u);
+              cont = live & (int)(dk >> 31);
+              ms_opaque(cont);
               br.need();
             } while (__builtin_expect(cont, 1));
             const int rs = (int)e >> 16, r = rs >> 4, s = rs & 15;
