@@ -310,6 +310,22 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
   }
 }
 
+// The first SOF of a file that probe() accepted is SOF2 (progressive).
+bool is_progressive(const uint8_t* d, size_t size) {
+  size_t pos = 2;
+  while (pos + 4 <= size) {
+    while (pos < size && d[pos] != 0xFF) pos++;
+    while (pos < size && d[pos] == 0xFF) pos++;
+    if (pos + 3 > size) return false;
+    const int m = d[pos++];
+    if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+    if (m == 0xC0 || m == 0xC1 || m == 0xC2) return m == 0xC2;
+    if (m == 0xD9 || m == 0xDA) return false;
+    pos += (size_t)((d[pos] << 8) | d[pos + 1]);
+  }
+  return false;
+}
+
 // ---- geometry (FFmpeg scale/pad/crop semantics; see oracle jo_geometry) ----
 int64_t rescale_rnd(int64_t a, int64_t b, int64_t c) { return (a * b + c / 2) / c; }
 
@@ -512,6 +528,10 @@ struct Layout {
   bool fuse_ok = true;      // ... with standard 4:2:0 / 4:2:2 MCUs (idct_rgb_kernel)
   int64_t cmyk_px = 0;      // 4-component images needing cmyk_kernel's K transform: max pixels
   int fused_tiles = 0;      // idct_rgb_kernel workgroups per image (max)
+  // a progressive (SOF2) image is in the batch: multiscan_kernel runs on a
+  // side stream beside destuff + entropy (only the host-bytes entry points
+  // see the headers; elsewhere it runs after entropy on the lane's stream)
+  bool ms_side = false;
 };
 
 int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_image_info* infos,
@@ -681,6 +701,10 @@ struct Workspace {
   DevBuf clean, segs, desc, info, luts, ents, bdesc, planes, wts, recs, dschunks;
   hipEvent_t done = nullptr;      // the workspace is free after this
   hipStream_t stream = nullptr;   // lanes > 1 only
+  // multiscan_kernel beside the baseline stages (batches with a progressive
+  // image, host-bytes entry points): created on first use
+  hipStream_t side = nullptr;
+  hipEvent_t ev_parsed = nullptr, ev_ms = nullptr;
 };
 
 struct spdl_hj_ctx {
@@ -883,6 +907,18 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                       static_cast<HuffTable*>(W.luts.p), hs ? slot.pin_tables.dev : nullptr,
                       W.wts.p, hs ? (int64_t)tb : 0, n, st));
   mark(ctx, slot, 2, st);
+  const bool ms_side = L.ms_side && !(ctx->debug_mask & 0x10000);
+  if (ms_side) {
+    if (!W.side) HJ_HIP(hipStreamCreateWithFlags(&W.side, hipStreamNonBlocking));
+    if (!W.ev_parsed) HJ_HIP(hipEventCreateWithFlags(&W.ev_parsed, hipEventDisableTiming));
+    if (!W.ev_ms) HJ_HIP(hipEventCreateWithFlags(&W.ev_ms, hipEventDisableTiming));
+    HJ_HIP(hipEventRecord(W.ev_parsed, st));
+    HJ_HIP(hipStreamWaitEvent(W.side, W.ev_parsed, 0));
+    HJ_HIP(launch_multiscan(d_bytes, static_cast<uint8_t*>(W.clean.p), desc, infos,
+                            static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p), n,
+                            W.side));
+    HJ_HIP(hipEventRecord(W.ev_ms, W.side));
+  }
   HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<DsChunk*>(W.dschunks.p),
                         static_cast<uint8_t*>(W.clean.p), static_cast<uint32_t*>(W.segs.p),
                         L.max_chunks, n, st));
@@ -901,7 +937,9 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   // progressive / non-interleaved images (the kernels above skipped them)
   // (debug_mask 0x10000 / 0x20000 / 0x40000: timing ablations that skip the
   // multiscan / IDCT / output launch; the output is wrong)
-  if (!(ctx->debug_mask & 0x10000))
+  if (ms_side)
+    HJ_HIP(hipStreamWaitEvent(st, W.ev_ms, 0));
+  else if (!(ctx->debug_mask & 0x10000))
     HJ_HIP(launch_multiscan(d_bytes, static_cast<uint8_t*>(W.clean.p), desc, infos,
                             static_cast<uint32_t*>(W.ents.p),
                             static_cast<uint2*>(W.bdesc.p), n, st));
@@ -1129,6 +1167,9 @@ void spdl_hj_destroy(spdl_hj_ctx* c) {
     for (DevBuf* b : bufs) b->release();
     if (w.done) (void)hipEventDestroy(w.done);
     if (w.stream) (void)hipStreamDestroy(w.stream);
+    if (w.ev_parsed) (void)hipEventDestroy(w.ev_parsed);
+    if (w.ev_ms) (void)hipEventDestroy(w.ev_ms);
+    if (w.side) (void)hipStreamDestroy(w.side);
   }
   for (Slot& s : c->slots) {
     s.bytes.release();
@@ -1160,8 +1201,10 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
   std::vector<int64_t> offs(n), szs(n);
   std::vector<CopyItem> items(n);
   int64_t total = 0;
+  bool prog = false;
   for (int i = 0; i < n; i++) {
     int rc = probe(data[i], sizes[i], &infos[i]);
+    if (!rc) prog = prog || is_progressive(data[i], sizes[i]);
     if (status) status[i] = rc;
     if (rc) {
       set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, status_str(rc));
@@ -1177,6 +1220,7 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
   int rc = build_layout(offs.data(), szs.data(), infos.data(), n, out, ctx->sub_bits, L, status, err,
                         errlen, &ctx->plans);
   if (rc) return rc;
+  L.ms_side = prog;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
   if (rc) return rc;
@@ -1330,10 +1374,12 @@ int spdl_hj_decode_staged(spdl_hj_ctx* ctx, int64_t ticket, size_t len, const in
   hipStream_t st = static_cast<hipStream_t>(stream);
   const uint8_t* host = static_cast<const uint8_t*>(s->pin_in.p);
   std::vector<spdl_hj_image_info> infos(n);
+  bool prog = false;
   for (int i = 0; i < n; i++) {
     int rc = SPDL_HJ_ERR_INVALID_ARG;
     if (offsets[i] >= 0 && sizes[i] >= 0 && (size_t)(offsets[i] + sizes[i]) <= len)
       rc = probe(host + offsets[i], (size_t)sizes[i], &infos[i]);
+    if (!rc) prog = prog || is_progressive(host + offsets[i], (size_t)sizes[i]);
     if (status) status[i] = rc;
     if (rc) {
       set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, status_str(rc));
@@ -1348,6 +1394,7 @@ int spdl_hj_decode_staged(spdl_hj_ctx* ctx, int64_t ticket, size_t len, const in
     s->ticket = 0;
     return rc;
   }
+  L.ms_side = prog;
   memset(static_cast<uint8_t*>(s->pin_in.p) + len, 0, 512);  // tail read slack
   hipStream_t xs;
   rc = exec_stream(ctx, *s, st, &xs, err, errlen);
