@@ -1126,7 +1126,8 @@ static int decode_planes_info(const uint8_t* d, size_t size, const jo_info* info
 
 /* FFmpeg mjpegdec's in-decoder conversion of 4-component frames (the end of
  * ff_mjpeg_decode_frame / receive_frame, as recalled; parity UNPINNED):
- *   Adobe transform 0 (or no marker), pix_fmt GBRAP -- inverted CMYK to RGB:
+ *   Adobe transform 0, pix_fmt GBRAP -- inverted CMYK to RGB (no Adobe marker:
+ *   YCbCr + K, jo_frame_color, left as transform 1):
  *     R = c k 257 >> 16, G = m k 257 >> 16, B = y k 257 >> 16
  *   transform 2, YUVA444P -- YCCK to YCbCr:
  *     Y = (255 - y) k 257 >> 16, Cb = ((128 - cb) k 257 >> 16) + 128, Cr likewise

@@ -907,7 +907,8 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                       static_cast<HuffTable*>(W.luts.p), hs ? slot.pin_tables.dev : nullptr,
                       W.wts.p, hs ? (int64_t)tb : 0, n, st));
   mark(ctx, slot, 2, st);
-  const bool ms_side = L.ms_side && !(ctx->debug_mask & 0x10000);
+  const bool ms_side = L.ms_side && !(ctx->debug_mask & 0x10000) &&
+                       2 * ctx->lanes + 1 <= ctx->hw_queues;
   if (ms_side) {
     if (!W.side) HJ_HIP(hipStreamCreateWithFlags(&W.side, hipStreamNonBlocking));
     if (!W.ev_parsed) HJ_HIP(hipEventCreateWithFlags(&W.ev_parsed, hipEventDisableTiming));
@@ -918,6 +919,22 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                             static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p), n,
                             W.side));
     HJ_HIP(hipEventRecord(W.ev_ms, W.side));
+  }
+  // If a launch below fails and returns early, the lane's stream still joins
+  // the side stream and re-records W.done, so the next batch on this
+  // workspace cannot reuse clean / ents / bdesc while multiscan writes them.
+  struct SideJoin {
+    hipStream_t st = nullptr;
+    Workspace* w = nullptr;
+    ~SideJoin() {
+      if (!w) return;
+      (void)hipStreamWaitEvent(st, w->ev_ms, 0);
+      (void)hipEventRecord(w->done, st);
+    }
+  } side_join;
+  if (ms_side) {
+    side_join.st = st;
+    side_join.w = &W;
   }
   HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<DsChunk*>(W.dschunks.p),
                         static_cast<uint8_t*>(W.clean.p), static_cast<uint32_t*>(W.segs.p),
@@ -937,9 +954,10 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   // progressive / non-interleaved images (the kernels above skipped them)
   // (debug_mask 0x10000 / 0x20000 / 0x40000: timing ablations that skip the
   // multiscan / IDCT / output launch; the output is wrong)
-  if (ms_side)
+  if (ms_side) {
+    side_join.w = nullptr;
     HJ_HIP(hipStreamWaitEvent(st, W.ev_ms, 0));
-  else if (!(ctx->debug_mask & 0x10000))
+  } else if (!(ctx->debug_mask & 0x10000))
     HJ_HIP(launch_multiscan(d_bytes, static_cast<uint8_t*>(W.clean.p), desc, infos,
                             static_cast<uint32_t*>(W.ents.p),
                             static_cast<uint2*>(W.bdesc.p), n, st));
@@ -1749,6 +1767,9 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"warmup_slots", ctx->warm_slots >= 0 ? ctx->warm_slots : (ent <= 256 ? 6 : 12)},
       {"lanes", ctx->lanes},
       {"hw_queues", ctx->hw_queues},
+      // streams a batch holding a progressive image may use: one per lane, a
+      // multiscan side stream per lane when the queues allow it, the copy stream
+      {"streams", ctx->lanes * (2 * ctx->lanes + 1 <= ctx->hw_queues ? 2 : 1) + 1},
       {"output_path", ctx->output_path},
       {"host_staging", ctx->host_staging},
       {"copy_threads", ctx->pool ? ctx->pool->workers() : copy_workers() + 1},

@@ -1324,25 +1324,41 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       d.pos = 0;
       d.z = d.bs = 0;
       bool have = false;
-      for (int k = r0; k < r1; k++) {
-        if (slot_empty(k)) {
+      // the run's slots, one segment piece at a time: [k, k2] = its slots
+      // in segment s that hold bits
+      for (int k = r0; k < r1;) {
+        const int s = slot_seg(k);
+        const uint32_t s0 = seg_start_bits(s), se = seg_end_bits(s);
+        const int jlast = se > s0 ? (int)((se - s0 - 1) / N) : 0;
+        const int k2 = min(r1 - 1, (s - seg_lo) * cmax + jlast);
+        if (k > k2) {  // past the segment's bits: empty slots
           have = false;
+          k = min(r1, (s - seg_lo + 1) * cmax);
           continue;
         }
+        const uint32_t ss = s0 + (uint32_t)slot_j(k) * N;
         if (slot_known(k)) {
-          dec_init<NT>(d, win, words, slot_start(k), 0, 0);
+          dec_init<NT>(d, win, words, ss, 0, 0);
         } else if (!have) {
           // warm-up: guess a state warm_slots slots earlier (or take the
           // segment start, which is exact) and decode up to the slot, so the
           // run's first state is usually already synchronised and the sync
           // rounds below have short chains to settle
-          const uint32_t ss = slot_start(k), s0 = seg_start_bits(slot_seg(k));
           const uint32_t wb = (uint32_t)warm_slots * N;
           dec_init<NT>(d, win, words, ss - s0 > wb ? ss - wb : s0, 0, 0);
           decode_state<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, ss);
         }
-        decode_k(d, k);
+        // one decode_state call per slot (measured: a single loop over the
+        // piece that records each slot as it crosses the boundary ran 20 %
+        // slower than these per-slot loops), the slot ends precomputed
+        for (uint32_t kk = k, be = ss + N; (int)kk <= k2; kk++, be += N) {
+          const uint32_t p0 = d.pos, zb0 = d.z | (d.bs << 8);
+          const int nblk = decode_state<NT, kSlow>(S, d, win, words, bcomp, tmap,
+                                                   2u * (uint32_t)bpm, min(be, se));
+          sst[kk] = make_uint4(p0, zb0, (uint32_t)nblk, d.z);
+        }
         have = true;
+        k = k2 + 1;
       }
       S.run_pos[tid] = d.pos;
       S.run_zb[tid] = (have && r0 < r1) ? (d.z | (d.bs << 8)) : 0xFFFFFFFFu;
@@ -1468,32 +1484,40 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
 #pragma unroll
       for (uint32_t i = 0; i < 4; i++) o.pk[i] = 0u;
       Dec d;
-      for (int k = r0; k < r1 && rc == kOk; k++) {
-        if (slot_empty(k)) {
+      // one decode_write call per segment piece of the run (its slots [k,
+      // k2] in segment s that hold bits), to the piece's end
+      for (int k = r0; k < r1 && rc == kOk;) {
+        const int s = slot_seg(k);
+        const uint32_t s0 = seg_start_bits(s), se = seg_end_bits(s);
+        const int jlast = se > s0 ? (int)((se - s0 - 1) / N) : 0;
+        const int k2 = min(r1 - 1, (s - seg_lo) * cmax + jlast);
+        if (k > k2) {  // past the segment's bits: empty slots
           have = false;
+          k = min(r1, (s - seg_lo + 1) * cmax);
           continue;
         }
-        const int s = slot_seg(k);
         if (slot_known(k)) {
           nb = seg_first_blk(s);
           done = false;
-          dec_init<NT>(d, win, words, slot_start(k), 0, 0);
+          dec_init<NT>(d, win, words, s0, 0, 0);
           have = true;
         } else if (!have) {
           const uint4 q = sst[k];
           dec_init<NT>(d, win, words, q.x, q.y & 0xFF, q.y >> 8);
-          skip_open_block<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm,
-                                     seg_end_bits(s));
+          skip_open_block<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, se);
           have = true;
         }
-        if (done) continue;
-        const int seb = seg_end_blk(s);
-        rc = decode_write<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm,
-                                     slot_end(k), seg_end_bits(s), seb, o, nb, done);
-        // last slot of its segment: every block of the segment must be done
-        const bool last = (k + 1 >= nslots) || slot_j(k + 1) == 0 || slot_empty(k + 1);
-        if (rc == kOk && !done && last && (nb < seb || (nb == seb && d.z != 0)))
-          rc = kErrTruncated;
+        if (!done) {
+          const int seb = seg_end_blk(s);
+          const uint32_t pend = min(s0 + (uint32_t)(slot_j(k2) + 1) * N, se);
+          rc = decode_write<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, pend, se,
+                                       seb, o, nb, done);
+          // the piece ends its segment: every block of the segment must be done
+          const bool last = (k2 + 1 >= nslots) || slot_j(k2 + 1) == 0 || pend >= se;
+          if (rc == kOk && !done && last && (nb < seb || (nb == seb && d.z != 0)))
+            rc = kErrTruncated;
+        }
+        k = k2 + 1;
       }
       flush_tail(o);
       if (rc != kOk) atomicCAS(&S.err, kOk, rc);
@@ -1649,6 +1673,7 @@ struct MsShared {
   int32_t prog[kMsMaxScans];   // blocks a scan has finished, in scan order
   int32_t prio[kMsMaxScans];   // claim priority (bytes of its heaviest dependent chain)
   int32_t dlen[kMsMaxScans];   // destuffed bytes in `clean` (-1: the stuffed reader)
+  int32_t dbase[kMsMaxScans];  // their offset from the image's start (a multiple of 4)
   int32_t wtot[4], dodd;       // destuff scratch
   uint64_t claimed, done;      // scans taken by a decoder wave / finished
   int64_t tkind[4];            // diagnostics: decode ticks by scan kind
@@ -2324,7 +2349,7 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
   constexpr bool kWord = ms_same<Rd, MsWBits>::value;
   Rd br;
   if constexpr (kWord) {
-    br.init(cl + ((sc.start + 3) & ~3), ms_i(S.dlen[si]));
+    br.init(cl + ms_i(S.dbase[si]), ms_i(S.dlen[si]));
   } else {
     br.w = (MsWords)(const void*)d;
     br.size = size;
@@ -2848,7 +2873,7 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   }
   __syncthreads();
   // ---- each scan without restart markers destuffed into `clean` (the
-  // image's offsets; the scan's start rounded up to 4, so the scans' copies
+  // image's offsets; the scan's start rounded down to 4, so the scans' copies
   // never overlap: headers >= 10 bytes lie between them), bytes reversed in
   // each dword so that a dword load is the big-endian bit order.  Each thread
   // takes a contiguous slice: count the kept bytes (a 0x00 after 0xFF is
@@ -2866,7 +2891,13 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
     if (tid == 0) S.dodd = 0;
     const int per = ((e0 - s0 + nt - 1) / nt + 15) & ~15;
     const int cs = min(s0 + tid * per, e0), ce = min(cs + per, e0);
-    uint8_t* out = cl + ((s0 + 3) & ~3);
+    // The copy's dwords stay inside the image's own bytes (a tightly packed
+    // next image may follow at in_size while its destuff / entropy run on
+    // another stream): base = the scan start rounded down to 4, lowered
+    // further when the last (byte-reversed) dword would pass in_size.  It
+    // stays past the previous scan's copy: >= 10 header bytes separate them.
+    uint8_t* out = cl;
+    int base = 0;
     int kept = 0, off = 0;
     bool odd = false;
     for (int pass = 0; pass < 2; pass++) {
@@ -2908,16 +2939,21 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
         for (int k = 0; k < wid; k++) wb += S.wtot[k];
         off = wb + inc - kept;
         if (S.dodd) break;  // (uniform: every thread read it after the barrier)
+        const int tot = S.wtot[0] + S.wtot[1] + S.wtot[2] + S.wtot[3];
+        base = min(s0 & ~3, ((int)dd.in_size - ((tot + 3) & ~3)) & ~3);
+        out = cl + base;
+        if (base < 0) break;  // (cannot happen: total <= e0 - s0; uniform)
       }
     }
     const int total = S.wtot[0] + S.wtot[1] + S.wtot[2] + S.wtot[3];
     __syncthreads();
     if (tid == 0) {
-      if (S.dodd) {
+      if (S.dodd || base < 0) {
         S.dlen[i] = -1;
       } else {
         for (int k = total; k & 3; k++) out[k ^ 3] = 0;  // (the last dword's tail)
         S.dlen[i] = total;
+        S.dbase[i] = base;
       }
     }
     __syncthreads();
@@ -3126,20 +3162,67 @@ hipError_t launch_multiscan(const uint8_t* bytes, uint8_t* clean, const ImageDes
 // idct_kernel
 // ---------------------------------------------------------------------------
 
-// Per-thread dense block in LDS: 64 int16 in natural order in a 144-byte
-// slot (36 words: the uint4 accesses of 16 consecutive threads fall on
-// disjoint banks).
+// Per-thread dense block in LDS, word-major: word w of thread t's block at
+// [w][t] (32 words of int16 pairs in the IDCT slot order, kSlotOrder), so any
+// access of a wave in which each lane touches its own block -- the scatter of
+// a list entry into an arbitrary slot included -- falls on 64 distinct banks
+// (a block-major layout took ~4 bank-conflict cycles per LDS instruction in
+// the scatter).  Word kBlkWords is a per-thread dummy that takes the
+// scatter's stores past the end of a list.
 #ifndef HJ_IDCT_THREADS
 #define HJ_IDCT_THREADS 256
 #endif
 constexpr int kIdctThreads = HJ_IDCT_THREADS;
-// 0 1: wave-uniform sparse transforms (below).  Off: on the
-// bench images 468-470 k vs 474 k img/s (the four variants take 136 VGPRs,
-// or spill under a 4-waves/SIMD cap; r02_v7/ab_idct_sparse/)
-constexpr int kBlkWords = 36;
+constexpr int kBlkWords = 32;
 
-// One block of the entropy kernel's coefficient lists -> 8x8 pixels (u8
-// values in int32), through the thread's LDS slot `my_blk` (kBlkWords words).
+// (a coefficient's int16 store into the block words: may_alias, or the
+// compiler may forward the zeroing word stores to the transform's word loads)
+typedef int16_t __attribute__((may_alias)) hj_i16_alias;
+
+// byte offset of IDCT slot s (kSlotOrder) in the word-major block of NT threads
+template <int NT>
+__device__ __forceinline__ uint32_t slot_byte(uint32_t s) {
+  return (s >> 1) * (uint32_t)NT * 4u + ((s & 1u) << 1);
+}
+
+// One block of the entropy kernel's coefficient lists (see BlockOut: DC
+// final, AC dequantised with their IDCT slot) into the thread's word-major
+// block (b32: its word 0; zeroed here).  (A list may start inside a 16-byte
+// group: a run's lists are packed back to back; entries [lo, lo + count) of
+// the groups from `start`.)
+template <int NT>
+__device__ __forceinline__ void list_block(const uint32_t* __restrict__ ents, const uint2 bd,
+                                           const int64_t coef_off, const int nblocks,
+                                           uint32_t* b32) {
+#pragma unroll
+  for (int w = 0; w < kBlkWords; w++) b32[w * NT] = w == 0 ? (bd.y >> 16) : 0u;
+  uint8_t* blk = reinterpret_cast<uint8_t*>(b32);
+  uint8_t* dummy = reinterpret_cast<uint8_t*>(b32 + kBlkWords * NT);
+  const uint32_t cap = (uint32_t)nblocks * 64u;
+  const uint32_t lo = bd.x & 3u, start = bd.x & ~3u;
+  uint32_t count = min(bd.y & 0xFFFFu, 63u);
+  if (start > cap - 64u) count = 0;  // only an unwritten list (a failed scan)
+  const uint32_t hi_e = lo + count;
+  const uint4* e4 = reinterpret_cast<const uint4*>(ents + (size_t)coef_off * 64 + start);
+  const uint32_t n4 = (hi_e + 3u) >> 2;
+  for (uint32_t i = 0; i < n4; i += 4) {
+    // unconditional loads (index clamped into the list), then the scatter
+    uint4 q[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) q[u] = e4[min(i + u, n4 - 1u)];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+      for (int h = 0; h < 4; h++) {  // (outside the list: into the dummy word)
+        const uint32_t k = 4u * (i + u) + h;
+        uint8_t* dst = k >= lo && k < hi_e ? blk + slot_byte<NT>(w[h] & 63u) : dummy;
+        *reinterpret_cast<hj_i16_alias*>(dst) = (int16_t)(w[h] >> 16);
+      }
+    }
+  }
+}
+
 // FFmpeg simple_idct (8-bit) on packed int16 pairs with v_dot2_i32_i16: a
 // row of the slot block is (x0, x2), (x4, x6), (x1, x3), (x5, x7), so each
 // even / odd partial sum of a pass is two dot2 steps.  The products and
@@ -3169,14 +3252,21 @@ __device__ __forceinline__ void sidct8(uint32_t e0, uint32_t e1, uint32_t o0, ui
   b[2] = dot2(o1, pk16(kW7, kW3), dot2(o0, pk16(kW5, -kW1), 0));
   b[3] = dot2(o1, pk16(kW3, -kW1), dot2(o0, pk16(kW7, -kW5), 0));
 }
-// blk: the slot block (8 rows of 4 words); px: 64 pixels, row-major
-__device__ __forceinline__ void simple_idct_slots(const uint4* blk, int32_t (&px)[64]) {
+// row i of the word-major block: words 4i..4i+3
+template <int NT>
+__device__ __forceinline__ uint4 blk_row(const uint32_t* b32, int i) {
+  return make_uint4(b32[(4 * i) * NT], b32[(4 * i + 1) * NT], b32[(4 * i + 2) * NT],
+                    b32[(4 * i + 3) * NT]);
+}
+// b32: the thread's word 0 of the word-major block; px: 64 pixels, row-major
+template <int NT>
+__device__ __forceinline__ void simple_idct_slots(const uint32_t* b32, int32_t (&px)[64]) {
   // rows: results truncated to int16 (FFmpeg keeps them in the int16 block);
   // only their low halves are used, packed below.  DC-only rows: x0 << 3.
   uint32_t r[8][8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const uint4 q = blk[i];
+    const uint4 q = blk_row<NT>(b32, i);
     int32_t a[4], b[4];
     sidct8(q.x, q.y, q.z, q.w, 1 << 10, a, b);
     const bool dc_only = ((q.x >> 16) | q.y | q.z | q.w) == 0u;
@@ -3207,50 +3297,19 @@ __device__ __forceinline__ void simple_idct_slots(const uint4* blk, int32_t (&px
   }
 }
 
-template <int IDCT>
-__device__ __forceinline__ void idct_list_block(const uint32_t* __restrict__ ents, const uint2 bd,
-                                                const int64_t coef_off, const int nblocks,
-                                                uint32_t* my_blk, int32_t (&px)[64]) {
-  // The entropy kernel's list for this block (see BlockOut): DC final, AC
-  // dequantised with their IDCT slot (kSlotOrder); placed in the thread's LDS block.
-  // (a list may start inside a 16-byte group: the run's lists are packed
-  // back to back; entries [lo, lo + count) of the groups from `start`)
-  const uint32_t cap = (uint32_t)nblocks * 64u;
-  const uint32_t lo = bd.x & 3u, start = bd.x & ~3u;
-  uint32_t count = min(bd.y & 0xFFFFu, 63u);
-  if (start > cap - 64u) count = 0;  // only an unwritten list (a failed scan)
-  const uint32_t hi_e = lo + count;
-  const uint4* e4 = reinterpret_cast<const uint4*>(ents + (size_t)coef_off * 64 + start);
-  uint4* my4 = reinterpret_cast<uint4*>(my_blk);
-#pragma unroll
-  for (int i = 0; i < 8; i++) my4[i] = make_uint4(0u, 0u, 0u, 0u);
-  int16_t* my16 = reinterpret_cast<int16_t*>(my_blk);
-  my16[0] = (int16_t)(bd.y >> 16);
-  const uint32_t n4 = (hi_e + 3u) >> 2;
-  for (uint32_t i = 0; i < n4; i += 4) {
-    // unconditional loads (index clamped into the list), then the scatter
-    uint4 q[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) q[u] = e4[min(i + u, n4 - 1u)];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
-#pragma unroll
-      for (int h = 0; h < 4; h++) {  // (outside the list: into the slot's padding)
-        const uint32_t k = 4u * (i + u) + h;
-        my16[k >= lo && k < hi_e ? (w[h] & 63u) : 64u] = (int16_t)(w[h] >> 16);
-      }
-    }
-  }
+// The thread's LDS block (b32: its word 0) -> 8x8 pixels (u8 values in
+// int32), row-major.
+template <int NT, int IDCT>
+__device__ __forceinline__ void idct_block(const uint32_t* b32, int32_t (&px)[64]) {
   if (IDCT == 0) {
-    simple_idct_slots(my4, px);
+    simple_idct_slots<NT>(b32, px);
     return;
   }
   // natural order from the slot layout (a compile-time permutation)
   int32_t blk[64];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const uint4 q = my4[i];
+    const uint4 q = blk_row<NT>(b32, i);
     blk[8 * i + 0] = sext16(q.x);
     blk[8 * i + 2] = sext16(q.x >> 16);
     blk[8 * i + 4] = sext16(q.y);
@@ -3274,7 +3333,7 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
                                                             const ImageDesc* __restrict__ desc,
                                                             const ImageInfo* __restrict__ infos,
                                                             uint8_t* __restrict__ planes) {
-  __shared__ __attribute__((aligned(16))) uint32_t sblk[kIdctThreads][kBlkWords];
+  __shared__ __attribute__((aligned(16))) uint32_t sblk[kBlkWords + 1][kIdctThreads];
   const int img = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const ImageInfo& in = infos[img];
@@ -3292,9 +3351,10 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
     bx = mx * in.comp_h[c] + in.mcu_dx[b];
     by = my * in.comp_v[c] + in.mcu_dy[b];
   }
+  uint32_t* b32 = &sblk[0][threadIdx.x];
+  list_block<kIdctThreads>(ents, bdesc[(size_t)dd.coef_off + j], dd.coef_off, in.nblocks, b32);
   int32_t px[64];
-  idct_list_block<IDCT>(ents, bdesc[(size_t)dd.coef_off + j], dd.coef_off, in.nblocks,
-                        sblk[threadIdx.x], px);
+  idct_block<kIdctThreads, IDCT>(b32, px);
   const int stride = dd.plane_stride[c];
   uint8_t* dst = planes + dd.plane_off[c] + (size_t)by * 8 * stride + bx * 8;
 #pragma unroll
@@ -3963,7 +4023,7 @@ __global__ void __launch_bounds__(256) rgb_unscaled_kernel(const uint8_t* __rest
 }
 
 // Full resolution, fused: one workgroup transforms a run of MCUs of one MCU
-// row into LDS (idct_list_block, the IDCT slots then reused as the plane
+// row into LDS (list_block + idct_block, the blocks' LDS then reused as the plane
 // tile) and converts it with swscale's unscaled converter straight from LDS
 // (rgbu_group) -- the planes never go through HBM.  Standard 4:2:0 / 4:2:2
 // MCUs only (Y 2x2 or 2x1 blocks, then U, V 1x1: bpm 6 or 4); the host checks
@@ -3976,7 +4036,7 @@ __global__ void __launch_bounds__(kFusedThreads) idct_rgb_kernel(const uint32_t*
                                                        uint8_t* __restrict__ out,
                                                        const BatchParams p,
                                                        int32_t* __restrict__ host_status) {
-  __shared__ __attribute__((aligned(16))) uint32_t sblk[kFusedThreads][kBlkWords];
+  __shared__ __attribute__((aligned(16))) uint32_t sblk[kBlkWords + 1][kFusedThreads];
   const int img = blockIdx.y, tid = threadIdx.x;
   const ImageInfo& in = infos[img];
   if (host_status && blockIdx.x == 0 && tid == 0) host_status[img] = in.status;
@@ -3995,8 +4055,9 @@ __global__ void __launch_bounds__(kFusedThreads) idct_rgb_kernel(const uint32_t*
   int32_t px[64];
   if (act) {
     const int j = (my * in.mcux + mx0 + m) * bpm + b;
-    idct_list_block<IDCT>(ents, bdesc[(size_t)dd.coef_off + j], dd.coef_off, in.nblocks, sblk[tid],
-                          px);
+    list_block<kFusedThreads>(ents, bdesc[(size_t)dd.coef_off + j], dd.coef_off, in.nblocks,
+                              &sblk[0][tid]);
+    idct_block<kFusedThreads, IDCT>(&sblk[0][tid], px);
   }
   __syncthreads();  // every slot read: the tile takes their place
   uint8_t* tl = reinterpret_cast<uint8_t*>(&sblk[0][0]);  // hy x ys luma, then 8 x cs U, V
@@ -4067,10 +4128,13 @@ hipError_t launch_rgb_unscaled(const uint8_t* planes, const ImageDesc* desc,
 
 // FFmpeg mjpeg's in-decoder conversion of a 4-component frame (oracle
 // jo_cmyk_transform; parity unpinned), in place on the IDCT planes:
-//   Adobe 0 / no marker (GBRAP): inverted CMYK -> RGB, R = c k 257 >> 16 ...
+//   Adobe 0 (GBRAP): inverted CMYK -> RGB, R = c k 257 >> 16 ...
 //   Adobe 2 (YUVA444P): YCCK -> YCbCr, Y = (255 - y) k 257 >> 16,
 //                       Cb = ((128 - cb) k 257 >> 16) + 128, Cr likewise
-// Adobe 1 is YCbCr + K already (K dropped).  Four pixels per thread: one
+// Adobe 1, another transform or no Adobe marker: YCbCr + K (frame_color
+// kColorYcbcrk; K dropped, this kernel skips the image).  The colour models
+// are restated from mjpegdec as recalled: parity unpinned (no fixture the
+// reference holds covers them).  Four pixels per thread: one
 // 32-bit load from each plane, three stores (HBM-bound: 4 B in, 3 B out per
 // pixel); the planes are 1x1-sampled, so one stride serves all four.
 __global__ void __launch_bounds__(256) cmyk_kernel(const ImageDesc* __restrict__ desc,

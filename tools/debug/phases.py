@@ -1,0 +1,20 @@
+"""Entropy-kernel phase timers (wall_clock64 ticks -> us) of single images per
+workgroup size: round 0 | sync rounds | block scan | mark pass, DC pass ticks."""
+import sys
+
+sys.path.insert(0, ".")
+from oracle import oracle as O  # noqa: E402
+from spdl_amd._lib import Decoder  # noqa: E402
+from tests import cases  # noqa: E402
+
+for threads in (256, 512):
+    dec = Decoder(0)
+    dec.set_param("entropy_threads", threads)
+    for name in ["q90_420", "large_1080p"]:
+        d = cases.case(name)
+        info = O.parse(d)
+        for _ in range(3):
+            coefs, clean, diag = dec.debug_entropy(d, info.nblocks)
+        print(f"T={threads} {name} phases_us={diag['phase_us']} rounds={diag['sync_rounds']} "
+              f"dc_us={diag['dbg'][0] / 100.0:.1f}", flush=True)
+    dec.close()
