@@ -28,8 +28,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# spdl_amd first: it exports GPU_MAX_HW_QUEUES (one hardware queue per
-# pipeline lane) before torch can initialise HIP
+# --hw-queues Q: the regime of a drop-in imported after the trainer touched
+# the GPU -- HIP initialised (through torch) with GPU_MAX_HW_QUEUES=Q before
+# spdl_amd is imported, so the decoder sees Q queues.  Otherwise spdl_amd
+# comes first and exports GPU_MAX_HW_QUEUES=16 before HIP starts.
+if "--hw-queues" in sys.argv:
+    os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
+    import torch  # noqa: E402
+
+    torch.cuda.init()
 import spdl_amd  # noqa: E402,F401
 
 import numpy as np  # noqa: E402
@@ -168,8 +175,11 @@ def _args():
     p.add_argument("--norm-dtype", choices=["float16", "bfloat16"], default="float16")
     p.add_argument("--inflight", type=int, default=0, choices=range(0, 11),
                    help="batches submitted ahead before waiting the oldest (0: lanes + 2; the ring holds 10)")
-    p.add_argument("--lanes", type=int, default=4,
-                   help="concurrent decode pipelines in the context (1-8)")
+    p.add_argument("--lanes", type=int, default=0,
+                   help="concurrent decode pipelines in the context (1-8; 0: the library default)")
+    p.add_argument("--hw-queues", type=int, default=0,
+                   help="initialise HIP with this many hardware queues before importing spdl_amd "
+                        "(the late-import regime of a drop-in)")
     p.add_argument("--sync-steps", action="store_true",
                    help="one synchronous call per step (no overlap of host work)")
     p.add_argument("--with-copies", action="store_true",
@@ -322,8 +332,6 @@ def _dry_run(a, rank: int, world: int) -> None:
 
 def main():
     a = _args()
-    if a.inflight == 0:
-        a.inflight = min(10, max(2, a.lanes + 2))
     rank, world, local = launched_world()
     if a.gpus > 1 and world == 1:
         # one process per GPU, started before anything touches a device
@@ -351,7 +359,10 @@ def main():
         dec.set_param("entropy_lds_pad", a.entropy_lds_pad)
     if a.warm_slots >= 0:
         dec.set_param("warmup_slots", a.warm_slots)
-    dec.set_param("lanes", a.lanes)
+    dec.set_param("lanes", a.lanes)  # (0: the library's choice for the queues in effect)
+    a.lanes = dec.get_param("lanes")
+    if a.inflight == 0:
+        a.inflight = min(10, max(2, a.lanes + 2))
     for kv in a.param:
         k, v = kv.split("=", 1)
         dec.set_param(k, int(v))

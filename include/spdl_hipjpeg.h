@@ -279,7 +279,8 @@ const char* spdl_hj_stage_name(int32_t i);
  * default 384), "entropy_threads" (256/512/1024; default 512 with one lane,
  * 256 with more), "warmup_slots" (0-64: slots a Huffman run decodes from a
  * guessed state before its own first slot; default 6 with 256 threads, 12
- * with more), "lanes" (1-8 concurrent pipelines: with N > 1, successive
+ * with more), "lanes" (1-8 concurrent pipelines, 0 = automatic: 4, or one
+ * per hardware queue beside the caller's when fewer; with N > 1, successive
  * batches rotate over N device workspaces and run on the context's own N
  * streams, each ordered after the caller's stream at submission; completion
  * is then observed through the ticket -- spdl_hj_wait / spdl_hj_stream_wait

@@ -1723,7 +1723,10 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "lanes")) {  // concurrent pipelines (workspaces + streams)
-    if (value < 1 || value > kMaxLanes) return SPDL_HJ_ERR_INVALID_ARG;
+    if (value < 0 || value > kMaxLanes) return SPDL_HJ_ERR_INVALID_ARG;
+    // 0: automatic -- four lanes when the process has the hardware queues
+    // for them beside the caller's stream, else one per spare queue
+    if (value == 0) value = std::max(1, std::min(4, ctx->hw_queues - 1));
     // lanes beyond the process's hardware queues would share queues and
     // serialise: clamp (spdl_hj_get_param reports the lanes in effect)
     const int lanes = std::min((int)value, std::max(1, ctx->hw_queues));

@@ -493,7 +493,7 @@ __global__ void __launch_bounds__(256) lut_kernel(const uint8_t* __restrict__ by
       if (code <= maxcode[l]) {
         const int sym = vals[valoff[l] + code];
         const int sz = is_dc ? sym : (sym & 15);
-        if (is_dc && sym > 15) return 0u;  // invalid size -> slow path reports it
+        if (is_dc && sym > 15) return 0u;  // invalid size (stored as 1: see below)
         if (l + sz <= full_max) {
           int v = 0;
           if (sz) {
@@ -512,13 +512,14 @@ __global__ void __launch_bounds__(256) lut_kernel(const uint8_t* __restrict__ by
     uint32_t e = entry16((uint32_t)idx << kSubBits, kLutBits, kLutBits);
     if (e == 0u && idx >= p_lo && idx <= p_hi)
       e = sub_ok ? ((kKindSub << 5) | ((uint32_t)(idx - p_lo) << kEntHiShift)) : 0u;
-    T.lut[idx] = e;
+    T.lut[idx] = e ? e : 1u;  // invalid: kind Slow, one bit (the decode loops' step)
   }
   if (sub_ok)
     for (int i = tid; i < nsub << kSubBits; i += blockDim.x)
-      T.sub[i] = entry16(((uint32_t)(p_lo + (i >> kSubBits)) << kSubBits) |
-                             (uint32_t)(i & ((1 << kSubBits) - 1)),
-                         16, 16);
+      T.sub[i] = max(entry16(((uint32_t)(p_lo + (i >> kSubBits)) << kSubBits) |
+                                 (uint32_t)(i & ((1 << kSubBits) - 1)),
+                             16, 16),
+                     1u);
   if (tid == 0) {
     T.nsub = sub_ok ? nsub : 0;
     T.long_slow = sub_ok ? 0 : 1;  // long codes left to the canonical path
@@ -827,17 +828,28 @@ static_assert(sizeof(EntShared<256, 4>) <= 160 * 1024 / 3,
 //
 // The state is the bit position alone; each step reads the two window words
 // holding bits [pos, pos + 32) (one ds_read2st64) and shifts them -- no bit
-// buffer to refill, no branch.  The window is stored in reverse word order
-// so the pair lands in a register pair as (lo, hi) = (word w + 1, word w),
-// ready for one 64-bit shift.
+// buffer to refill, no branch.  (A 64-bit register bit buffer refilled from
+// the window one word ahead takes the window read off the symbol's
+// dependency chain, but its refill selects cost more issue than the read's
+// latency: round 0 +11 %, r04 A/B.)  The decode loops are issue-bound as much
+// as latency-bound, so the step is written for instruction count: the
+// window position as a bit offset from the window's first bit (`wbit`), the
+// table of a step from one packed map per symbol class (TabMap).
 struct Dec {
-  uint32_t wb;   // absolute word index of the window's first word
-  uint32_t pos;  // absolute bit position of the next symbol
-  uint32_t z;    // next coefficient index (0 = DC)
-  uint32_t bs;   // 2 * block-in-MCU
+  uint32_t wbit;  // absolute bit position of the window's first word
+  uint32_t pos;   // absolute bit position of the next symbol
+  uint32_t z;     // next coefficient index (0 = DC)
+  uint32_t bs;    // 3 * block-in-MCU
 };
 
-__device__ __forceinline__ constexpr int win_slot(int i) { return kWinWords - 1 - i; }
+// The Huffman table slots and component of each block of the MCU, packed
+// 3 bits per block-in-MCU b at bit 3b (Dec::bs), and the MCU's end.
+struct TabMap {
+  uint32_t dmap;    // LDS table slot of b's DC table
+  uint32_t amap;    // ... of its AC table
+  uint32_t cmap;    // its component
+  uint32_t bs_end;  // 3 * blocks per MCU
+};
 
 template <int NT>
 __device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, uint32_t wb) {
@@ -850,19 +862,18 @@ __device__ __forceinline__ void win_stage(uint32_t* win, const uint32_t* words, 
   // stored MSB-first (byte-swapped once here instead of at every read)
 #pragma unroll
   for (int i = 0; i < kWinWords / 4; i++) {
-    win[win_slot(4 * i + 0) * NT] = __builtin_bswap32(q[i].x);
-    win[win_slot(4 * i + 1) * NT] = __builtin_bswap32(q[i].y);
-    win[win_slot(4 * i + 2) * NT] = __builtin_bswap32(q[i].z);
-    win[win_slot(4 * i + 3) * NT] = __builtin_bswap32(q[i].w);
+    win[(kWinWords - 1 - 4 * i) * NT] = __builtin_bswap32(q[i].x);
+    win[(kWinWords - 2 - 4 * i) * NT] = __builtin_bswap32(q[i].y);
+    win[(kWinWords - 3 - 4 * i) * NT] = __builtin_bswap32(q[i].z);
+    win[(kWinWords - 4 - 4 * i) * NT] = __builtin_bswap32(q[i].w);
   }
 }
-
 
 template <int NT>
 __device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* words, uint32_t p,
                                          uint32_t z, uint32_t bs) {
-  d.wb = p >> 5;  // the word holding the position: a full window of runway
-  win_stage<NT>(win, words, d.wb);
+  d.wbit = p & ~31u;  // the word holding the position: a full window of runway
+  win_stage<NT>(win, words, p >> 5);
   d.pos = p;
   d.z = z;
   d.bs = bs;
@@ -874,18 +885,28 @@ __device__ __forceinline__ void dec_init(Dec& d, uint32_t* win, const uint32_t* 
 // per ~25 symbol steps of the wave.
 template <int NT>
 __device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32_t* words) {
-  uint32_t w = (d.pos >> 5) - d.wb;
-  if (__any(w >= (uint32_t)(kWinWords - 1))) {
-    d.wb = d.pos >> 5;
-    win_stage<NT>(win, words, d.wb);
-    w = (d.pos >> 5) - d.wb;
+  uint32_t rel = d.pos - d.wbit;
+  if (__any(rel >= 32u * (kWinWords - 1))) {
+    d.wbit = d.pos & ~31u;
+    win_stage<NT>(win, words, d.pos >> 5);
+    rel = d.pos - d.wbit;
   }
-  const uint32_t* pw = win + (kWinWords - 2 - (int)w) * NT;  // word w + 1, then word w
+  // (the window is stored in reverse word order, so the pair lands in a
+  // register pair as (lo, hi) = (word w + 1, word w), ready for one shift)
+  const uint32_t* pw = win + (kWinWords - 2 - (int)(rel >> 5)) * NT;
   const uint64_t lohi = (uint64_t)pw[0] | ((uint64_t)pw[NT] << 32);
-  return (uint32_t)((lohi << (d.pos & 31u)) >> 32);
+  return (uint32_t)((lohi << (rel & 31u)) >> 32);
 }
 
 __device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) { d.pos += nbits; }
+
+// the LDS table of the next symbol, and the block-in-MCU advance at a block end
+__device__ __forceinline__ uint32_t tab_slot(const TabMap& m, const Dec& d, bool is_dc) {
+  return __builtin_amdgcn_ubfe(is_dc ? m.dmap : m.amap, d.bs, 3);
+}
+__device__ __forceinline__ uint32_t next_bs(const TabMap& m, uint32_t bs) {
+  return bs + 3u == m.bs_end ? 0u : bs + 3u;
+}
 
 // Canonical decode of a code that is not fully resolved by the LUT (longer
 // than kLutBits, or a DC size > 15): returns a kKindCode entry, 0 if invalid.
@@ -900,11 +921,11 @@ __device__ __attribute__((noinline)) uint32_t slow_symbol(const SH& S, int t, ui
     const int code = (int)(w16 >> (16 - l));
     if (code <= (g ? G->maxcode[l] : S.maxcode[tl][l])) {
       const int sym = g ? G->vals[G->valoff[l] + code] : S.vals[tl][S.valoff[tl][l] + code];
-      if (is_dc && sym > 15) return 0;
+      if (is_dc && sym > 15) return 1;
       return hj_entry(kKindCode, l, sym, is_dc, 0);
     }
   }
-  return 0;
+  return 1;
 }
 
 // The entry of the symbol at the head of `hi` in table slot t (two-level LUT,
@@ -944,27 +965,28 @@ __device__ __forceinline__ uint32_t lookup(const SH& S, uint32_t t, uint32_t hi,
 // a wave decode 64 unrelated streams).  Returns the blocks started.
 template <int NT, bool SLOW, class SH>
 __device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
-                            const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
-                            const uint32_t end) {
-  int nblk = 0;
+                            const TabMap& m, const uint32_t end) {
+  // blocks started = blocks ended + (a block open at the end) - (one open at
+  // the start): counting ends is one add per step
+  int nend = 0;
+  const int open0 = d.z != 0u;
   while (d.pos < end) {
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
-    const bool is_dc = z == 0;
-    const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
-    const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 12u) + c * 3u, 3);
-    const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
-    // entry 0 (invalid) takes one bit, advances nothing and starts no block
-    const uint32_t nbits = max(e & 31u, 1u);  // code + value bits, <= 31
-    nblk += is_dc ? (int)__builtin_amdgcn_ubfe(e, 19, 1) : 0;  // DC: coef bit = valid
+    const uint32_t t = tab_slot(m, d, z == 0u);
+    const uint32_t e = lookup<SLOW>(S, t, hi, z == 0u);
+    // an invalid code's entry (1) takes one bit, advances nothing and starts
+    // no block
+    const uint32_t nbits = e & 31u;  // code + value bits, <= 31
     dec_skip(d, nbits);
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool bend = zn >= 64u;
-    const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
+    nend += bend ? 1 : 0;
+    const uint32_t bsn = next_bs(m, d.bs);
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
-  return nblk;
+  return nend + (d.z != 0u ? 1 : 0) - open0;
 }
 
 // The block in progress at a run's synchronised start belongs to the run
@@ -972,19 +994,16 @@ __device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
 // rest of it, state only, bounded by the segment end.
 template <int NT, bool SLOW, class SH>
 __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
-                                const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
-                                const uint32_t seg_end) {
+                                const TabMap& m, const uint32_t seg_end) {
   while (d.z != 0u && d.pos < seg_end) {
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
-    const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
-    const uint32_t t = __builtin_amdgcn_ubfe(tmap, 12u + c * 3u, 3);
-    const uint32_t e = lookup<SLOW>(S, t, hi, false);
-    const uint32_t nbits = max(e & 31u, 1u);
+    const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, false), hi, false);
+    const uint32_t nbits = e & 31u;
     dec_skip(d, nbits);
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool bend = zn >= 64u;
-    const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
+    const uint32_t bsn = next_bs(m, d.bs);
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
@@ -1001,6 +1020,17 @@ __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32
 // so no buffer needs clearing and nothing is scattered: HBM sees ~4 bytes per
 // non-zero coefficient.
 
+// The symbol's value: the entry's own (Full) plus the sz value bits that
+// follow the code (Code), JPEG EXTEND -- a field whose top bit is clear is
+// negative, raw - (2^sz - 1).  (sz = 0: the top-bit extract reads bit 31 of
+// raw, which is 0, and the mask is empty.)
+__device__ __forceinline__ int sym_value(uint32_t e, uint32_t hi, uint32_t nbits, uint32_t sz) {
+  const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
+  const uint32_t top = (uint32_t)__builtin_amdgcn_sbfe((int)raw, sz - 1u, 1);  // ~0: positive
+  const uint32_t neg = ~top & ((1u << sz) - 1u);
+  return ((int32_t)e >> kEntHiShift) + (int)(raw - neg);
+}
+
 struct BlockOut {
   uint32_t* ents;
   uint2* bdesc;
@@ -1009,21 +1039,20 @@ struct BlockOut {
   uint32_t bstart;  // first entry of the open block
   int dcv;          // its DC difference
   bool open;        // a block of this run is being decoded
-  uint32_t pk[4];   // entries of the current 16-byte group not yet stored
+  uint32_t pk[4];   // the last four entries (a shift register: pk[3] the newest)
 };
 
-
-__device__ __forceinline__ void store_pack(BlockOut& o) {
-  const uint32_t base = min(o.cur & ~3u, o.last & ~3u);
-  *reinterpret_cast<uint4*>(o.ents + base) = make_uint4(o.pk[0], o.pk[1], o.pk[2], o.pk[3]);
-}
-
-// entry e at o.cur (the caller advances o.cur); four entries per 16-byte store
-__device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e) {
-  const uint32_t k = o.cur & 3u;
-#pragma unroll
-  for (uint32_t i = 0; i < 4; i++) o.pk[i] = k == i ? e : o.pk[i];
-  if (k == 3u) store_pack(o);
+// entry e at o.cur when `put` (the caller advances o.cur): shifted into pk,
+// and the group of four leaves as one 16-byte store when it completes
+__device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e, bool put) {
+  o.pk[0] = put ? o.pk[1] : o.pk[0];
+  o.pk[1] = put ? o.pk[2] : o.pk[1];
+  o.pk[2] = put ? o.pk[3] : o.pk[2];
+  o.pk[3] = put ? e : o.pk[3];
+  if (put && (o.cur & 3u) == 3u) {
+    const uint32_t base = min(o.cur & ~3u, o.last & ~3u);
+    *reinterpret_cast<uint4*>(o.ents + base) = make_uint4(o.pk[0], o.pk[1], o.pk[2], o.pk[3]);
+  }
 }
 
 // a run's lists go back to back: the next list continues the current group,
@@ -1034,8 +1063,21 @@ __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
   o.open = false;
 }
 
+// the run's last r = cur & 3 entries, pk[4 - r .. 3], to the group at cur & ~3
 __device__ __forceinline__ void flush_tail(BlockOut& o) {
-  if (o.cur & 3u) store_pack(o);
+  const uint32_t r = o.cur & 3u;
+  if (r == 0u) return;
+  const uint32_t base = min(o.cur & ~3u, o.last & ~3u);
+  // (masks, not selects: a select chain over pk becomes a dynamic index
+  // and puts the BlockOut in scratch)
+  const uint32_t m1 = 0u - (uint32_t)(r == 1u), m2 = 0u - (uint32_t)(r == 2u);
+  const uint32_t m3 = ~(m1 | m2);
+  uint4 q;
+  q.x = (o.pk[3] & m1) | (o.pk[2] & m2) | (o.pk[1] & m3);
+  q.y = (o.pk[3] & m2) | (o.pk[2] & m3);
+  q.z = o.pk[3];
+  q.w = 0u;
+  *reinterpret_cast<uint4*>(o.ents + base) = q;
 }
 
 // Full decode from a synchronised state (z == 0: at a block start) of the
@@ -1046,63 +1088,58 @@ __device__ __forceinline__ void flush_tail(BlockOut& o) {
 // segment's last block is complete.
 template <int NT, bool SLOW, class SH>
 __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* words,
-                            const uint32_t bcomp, const uint32_t tmap, const uint32_t bs_end,
-                            const uint32_t end, const uint32_t seg_end, const int seg_end_blk,
-                            BlockOut& o, int& nb, bool& done) {
+                            const TabMap& m, const uint32_t end, const uint32_t seg_end,
+                            const int seg_end_blk, BlockOut& o, int& nb, bool& done) {
   int rc = kOk;
   // Fast path, straight-line: a symbol that can trigger none of the rules
-  // below -- a valid code, no run past coefficient 63, not running past the
-  // segment end, not a DC symbol once the segment's last block started -- is
-  // decoded without them.  A lane leaves at the first symbol that could,
-  // before consuming it, and the careful loop continues from that state.
+  // below -- a valid code, no run past coefficient 63, not within 32 bits of
+  // the segment end, not a DC symbol once the segment's last block started
+  // -- is decoded without them.  A lane leaves at the first symbol that
+  // could, before consuming it, and the careful loop continues from that
+  // state.  (In the fast path a block is open exactly while z != 0.)
+  const uint32_t fast_end = seg_end > 32u ? seg_end - 32u : 0u;
   for (;;) {
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
-    if (is_dc & ((d.pos >= end) | (nb >= seg_end_blk))) break;
+    if ((is_dc & ((d.pos >= end) | (nb >= seg_end_blk))) | (d.pos > fast_end)) break;
     const uint32_t hi = dec_peek<NT>(d, win, words);
-    const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
-    const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 12u) + c * 3u, 3);
-    const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
+    const uint32_t c = __builtin_amdgcn_ubfe(m.cmap, d.bs, 2);
+    const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, is_dc), hi, is_dc);
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
     const uint32_t nbits = e & 31u;
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool coef = (e >> 19) & 1u;
-    // (bitwise, not short-circuit: one exit test instead of nested branches)
-    if ((e == 0u) | (((e >> 20) & 1u) != 0u) | (coef & (zn > 64u)) | (d.pos + nbits > seg_end))
-      break;
-    const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
-    const uint32_t msk = (1u << sz) - 1u;
-    const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
+    // valid (kind != Slow) and not an AC size-0 symbol other than EOB / ZRL:
+    // (e & (bad | kind)) in {0x20, 0x40, 0x60}
+    const bool ok = ((e & 0x100060u) - 1u) < 0x60u;
+    if (!ok | (coef & (zn > 64u))) break;
+    const int v = sym_value(e, hi, nbits, sz);
     dec_skip(d, nbits);
     const bool ac = coef & !is_dc;
-    if (ac) {
-      const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-      put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
-    }
+    const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
+    // (16-bit multiply: the low half is exact)
+    put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u), ac);
     o.cur += ac ? 1u : 0u;
     o.bstart = is_dc ? o.cur : o.bstart;
     o.dcv = is_dc ? v : o.dcv;
     nb += is_dc ? 1 : 0;
     const bool bend = zn >= 64u;
     if (bend) close_block(o, nb - 1);
-    o.open = !bend;
-    const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
+    const uint32_t bsn = next_bs(m, d.bs);
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
+  o.open = d.z != 0u;
   while (!done && rc == kOk && !(d.z == 0u && d.pos >= end)) {
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
-    const uint32_t c = __builtin_amdgcn_ubfe(bcomp, d.bs, 2);
-    const uint32_t t = __builtin_amdgcn_ubfe(tmap, (is_dc ? 0u : 12u) + c * 3u, 3);
-    const uint32_t e = lookup<SLOW>(S, t, hi, is_dc);
-    const bool valid = e != 0u;
+    const uint32_t c = __builtin_amdgcn_ubfe(m.cmap, d.bs, 2);
+    const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, is_dc), hi, is_dc);
+    const bool valid = (e & 0x60u) != 0u;
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
-    const uint32_t nbits = valid ? e & 31u : 1u;
-    const uint32_t raw = __builtin_amdgcn_ubfe(hi, 32u - nbits, sz);
-    const uint32_t msk = (1u << sz) - 1u;
-    const int v = ((int32_t)e >> kEntHiShift) + (int)raw - (int)(raw <= (msk >> 1) ? msk : 0u);
+    const uint32_t nbits = e & 31u;
+    const int v = sym_value(e, hi, nbits, sz);
     dec_skip(d, nbits);
     const uint32_t zinc = __builtin_amdgcn_ubfe(e, 12, 7);
     const bool coef = valid && ((e >> 19) & 1u);
@@ -1120,11 +1157,10 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
       o.dcv = v;
       o.open = true;
     }
-    if (wr && !is_dc) {
-      const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-      put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u));  // (16-bit multiply: the low half is exact)
-      o.cur++;
-    }
+    const bool put = wr && !is_dc;
+    const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
+    put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u), put);
+    o.cur += put ? 1u : 0u;
     nb += (wr && is_dc) ? 1 : 0;
     // a symbol running past the segment end (after the rule above)
     const bool trunc = !bad && !stop && d.pos > seg_end;
@@ -1133,7 +1169,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     rc = (bad && !past_a) ? kErrBadHuffman : ((trunc && !past_b) ? kErrTruncated : kOk);
     const bool bend = zn >= 64u;
     if (bend && !stop && o.open) close_block(o, nb - 1);
-    const uint32_t bsn = d.bs + 2u == bs_end ? 0u : d.bs + 2u;
+    const uint32_t bsn = next_bs(m, d.bs);
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
   }
@@ -1200,9 +1236,10 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   const int nseg = ri > 0 ? (nmcu + ri - 1) / ri : 1;
 
   // ---- tables into LDS (dedup table slots per component) ----
-  // 2-bit component per block-in-MCU; 3-bit LDS table slots: DC of component
-  // c at bit 3c, AC at 12 + 3c
-  uint32_t bcomp = 0, tmap = 0;
+  // table slots and components per block-in-MCU (TabMap); the DC pass
+  // keeps a 2-bit component map
+  uint32_t bcomp = 0;  // 2-bit component per block-in-MCU (DC pass)
+  TabMap tm{0u, 0u, 0u, 0u};
   {
     int slots[kMaxTabs], ns = 0, ldc[kMaxComp] = {}, lac[kMaxComp] = {};
     for (int c = 0; c < in.ncomp; c++) {
@@ -1233,7 +1270,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       if (fits) pool += nsub;
       for (int k = tid; k < kLutSize; k += NT) {
         uint32_t e = T.lut[k];
-        if ((e >> 5 & 3) == kKindSub) e = fits ? e + ((uint32_t)base << kEntHiShift) : 0u;
+        if ((e >> 5 & 3) == kKindSub) e = fits ? e + ((uint32_t)base << kEntHiShift) : 1u;
         S.lut[i][k] = e;
       }
       if (fits)
@@ -1247,9 +1284,14 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       if (k % 64 == 0) S.qdc[k / 64] = in.qt[k / 64][0];
       S.qn[k / 64][k % 64] = kSlotOrder[k % 64] | ((uint32_t)in.qt[k / 64][k % 64] << 16);
     }
-    for (int b = 0; b < bpm; b++) bcomp |= (uint32_t)in.mcu_comp[b] << (2 * b);
-    for (int c = 0; c < kMaxComp; c++)
-      tmap |= ((uint32_t)ldc[c] << (3 * c)) | ((uint32_t)lac[c] << (12 + 3 * c));
+    for (int b = 0; b < bpm; b++) {
+      const int c = in.mcu_comp[b];
+      bcomp |= (uint32_t)c << (2 * b);
+      tm.dmap |= (uint32_t)ldc[c] << (3 * b);
+      tm.amap |= (uint32_t)lac[c] << (3 * b);
+      tm.cmap |= (uint32_t)c << (3 * b);
+    }
+    tm.bs_end = 3u * (uint32_t)bpm;
     if (tid == 0) S.err = kOk;
   }
   if (nseg_found < nseg) {
@@ -1313,8 +1355,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
     auto slot_known = [&](int k) { return slot_j(k) == 0; };
     auto decode_k = [&](Dec& d, int k) {
       const uint32_t p0 = d.pos, zb0 = d.z | (d.bs << 8);
-      const int nblk = decode_state<NT, kSlow>(S, d, win, words, bcomp, tmap,
-                                               2u * (uint32_t)bpm, slot_end(k));
+      const int nblk = decode_state<NT, kSlow>(S, d, win, words, tm, slot_end(k));
       sst[k] = make_uint4(p0, zb0, (uint32_t)nblk, d.z);
     };
 
@@ -1346,15 +1387,14 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
           // rounds below have short chains to settle
           const uint32_t wb = (uint32_t)warm_slots * N;
           dec_init<NT>(d, win, words, ss - s0 > wb ? ss - wb : s0, 0, 0);
-          decode_state<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, ss);
+          decode_state<NT, kSlow>(S, d, win, words, tm, ss);
         }
         // one decode_state call per slot (measured: a single loop over the
         // piece that records each slot as it crosses the boundary ran 20 %
         // slower than these per-slot loops), the slot ends precomputed
         for (uint32_t kk = k, be = ss + N; (int)kk <= k2; kk++, be += N) {
           const uint32_t p0 = d.pos, zb0 = d.z | (d.bs << 8);
-          const int nblk = decode_state<NT, kSlow>(S, d, win, words, bcomp, tmap,
-                                                   2u * (uint32_t)bpm, min(be, se));
+          const int nblk = decode_state<NT, kSlow>(S, d, win, words, tm, min(be, se));
           sst[kk] = make_uint4(p0, zb0, (uint32_t)nblk, d.z);
         }
         have = true;
@@ -1504,14 +1544,13 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
         } else if (!have) {
           const uint4 q = sst[k];
           dec_init<NT>(d, win, words, q.x, q.y & 0xFF, q.y >> 8);
-          skip_open_block<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, se);
+          skip_open_block<NT, kSlow>(S, d, win, words, tm, se);
           have = true;
         }
         if (!done) {
           const int seb = seg_end_blk(s);
           const uint32_t pend = min(s0 + (uint32_t)(slot_j(k2) + 1) * N, se);
-          rc = decode_write<NT, kSlow>(S, d, win, words, bcomp, tmap, 2u * (uint32_t)bpm, pend, se,
-                                       seb, o, nb, done);
+          rc = decode_write<NT, kSlow>(S, d, win, words, tm, pend, se, seb, o, nb, done);
           // the piece ends its segment: every block of the segment must be done
           const bool last = (k2 + 1 >= nslots) || slot_j(k2 + 1) == 0 || pend >= se;
           if (rc == kOk && !done && last && (nb < seb || (nb == seb && d.z != 0)))
