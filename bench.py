@@ -60,10 +60,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # committed rocprofv3 --pmc passes of this same command (tools/pmc_round.sh:
 # tools/pmc_traffic.py, tools/pmc_issue.py): counters cannot be read from
 # inside the timed process.
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r03", "final")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r04", "final")
 PMC_TRAFFIC = os.path.join(PROFILE_DIR, "traffic.json")
 PMC_ISSUE = os.path.join(PROFILE_DIR, "issue.json")
 # rocprofv3 --kernel-trace --stats of this command (tools/profile_round.sh)
+# union of each kernel's launch intervals per step in the kernel traces of
+# the KSTATS runs (tools/kernel_busy.py)
+BUSY = os.path.join(PROFILE_DIR, "kernel_busy.json")
 KSTATS = {4: os.path.join(PROFILE_DIR, "kernel_stats_lanes4.csv"),
           1: os.path.join(PROFILE_DIR, "kernel_stats_lanes1.csv")}
 # bench stage -> kernels launched in it
@@ -108,14 +111,43 @@ def _rocprof_ms(lanes: int, stage: str) -> float | None:
     return None
 
 
-def _limiter(issue: dict | None) -> str:
-    """What bounds the dominant kernel, from its SQ counters: the share of
-    wave time spent issuing VALU work vs waiting (tools/pmc_issue.py)."""
+def _kernel_busy_ms(lanes: int, stage: str) -> float | None:
+    """The device time per bench step during which `stage`'s kernel runs (the
+    union of its launches' intervals / steps) in the committed kernel trace
+    of the bench at `lanes` lanes (tools/kernel_busy.py)."""
+    try:
+        with open(BUSY) as f:
+            rec = json.load(f)
+    except OSError:
+        return None
+    for name, v in rec.get(str(lanes), {}).items():
+        if any(name.startswith(k) for k in STAGE_KERNELS.get(stage, [])):
+            return v["busy_ms_per_step"]
+    return None
+
+
+def _limiter(issue: dict | None, hbm_frac: float | None) -> str:
+    """What bounds the dominant kernel, derived from its measured shares
+    (SQ counters, tools/pmc_issue.py; HBM traffic over the kernel's time):
+    HBM when its traffic runs at >= 60 % of peak, VALU issue when its waves
+    issue VALU >= 50 % of their cycles, latency when they wait >= 40 %,
+    otherwise mixed issue."""
     if not issue:
         return "unmeasured (no PMC record for this configuration)"
-    return (f"latency/issue, not HBM: waves issue VALU {issue['valu_share']:.0%} and wait "
-            f"{issue['wait_share']:.0%} of their cycles ({issue['waves']} waves per launch, "
-            f"{issue['lds_conflict_per_lds_inst']:.1f} LDS bank-conflict cycles per LDS instruction)")
+    v, w = issue["valu_share"], issue["wait_share"]
+    shares = (f"waves issue VALU {v:.0%} and wait {w:.0%} of their cycles; {issue['waves']} "
+              f"waves per launch; {issue['lds_conflict_per_lds_inst']:.2f} LDS bank-conflict "
+              f"cycles per LDS instruction"
+              + (f"; PMC HBM traffic at {hbm_frac:.1%} of peak" if hbm_frac is not None else ""))
+    if hbm_frac is not None and hbm_frac >= 0.6:
+        kind = "HBM bandwidth"
+    elif v >= 0.5:
+        kind = "VALU issue"
+    elif w >= 0.4:
+        kind = "latency (dependent LDS / VALU chains, barriers)"
+    else:
+        kind = "instruction issue (VALU, SALU and LDS mixed)"
+    return f"{kind}: {shares}"
 
 
 BATCH = 256
@@ -450,8 +482,6 @@ def main():
     # §8(d): compressed in + RGB224 out (u8: 150,528 B; fp16/bf16: 301,056 B)
     per_image_bytes = comp_bytes + nbytes_out / a.batch
     launch_bytes = per_image_bytes * a.batch
-    dom_s = kernels[dominant] / 1000.0
-    achieved = launch_bytes / dom_s / 1e9
 
     # The dominant kernel alone: with several lanes its launches share the CUs
     # with the other lanes' kernels, so the per-launch time above is a shared
@@ -515,6 +545,15 @@ def main():
     if a.workload == "pad224" and a.lanes == 4:  # the configuration the PMC passes ran
         traffic = _pmc(PMC_TRAFFIC, dominant, a.batch)
         issue = _pmc(PMC_ISSUE, dominant, a.batch)
+    # `achieved` and `frac` from the kernel's average duration in the committed
+    # rocprofv3 kernel-trace summary of this configuration (rocprof_source)
+    # when one exists, else from the HIP events of this run (time_source says
+    # which); the other figure rides along.
+    kernel_ms = rocprof_ms if rocprof_ms else kernels[dominant]
+    achieved = launch_bytes / (kernel_ms / 1e3) / 1e9
+    hbm_frac = (traffic["traffic_bytes"] / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS
+                if traffic else None)
+    busy = _kernel_busy_ms(a.lanes, dominant) if a.workload == "pad224" else None
     if rank == 0:
         value = world * a.batch * a.steps / elapsed
         rec = {
@@ -547,7 +586,7 @@ def main():
             },
             "roofline": {
                 # the roofline the path is priced against (no MFMA work); what
-                # actually limits the kernel is `limiter`
+                # the counters say limits the kernel is `limiter`
                 "bound": "hbm",
                 "kernel": dominant,
                 "achieved": round(achieved, 3),
@@ -560,18 +599,25 @@ def main():
                                   if traffic else None,
                 "algorithmic_bytes_per_image": round(per_image_bytes, 1),
                 "launch_images": a.batch,
-                "formula": "achieved = algorithmic_bytes_per_image x launch_images / mean "
-                           "HIP-event duration of the kernel's launches in the timed steps",
-                # the same kernel's average in the committed rocprofv3 summary of
-                # this configuration: the HIP events above also count the time a
-                # launch waits for CUs the other lanes hold
+                "formula": "achieved = algorithmic_bytes_per_image x launch_images / kernel_ms; "
+                           "frac = achieved / peak",
+                "kernel_ms": round(kernel_ms, 4),
+                "time_source": (f"rocprofv3 average duration, {os.path.relpath(KSTATS[a.lanes], ROOT)}"
+                                if rocprof_ms else "HIP events around the kernel's launches in the "
+                                                   "timed steps (no committed rocprof summary for "
+                                                   "this configuration)"),
+                # with several lanes a launch's duration is a shared wall
+                # time (it waits for CUs the other lanes hold), so it can
+                # exceed ms_per_step; the device time per step the kernel
+                # occupies is the union of its launches' intervals per step
                 "kernel_ms_hip_events": round(kernels[dominant], 4),
-                "kernel_ms_rocprof": rocprof_ms,
-                "frac_rocprof": (round(launch_bytes / (rocprof_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 6)
-                                 if rocprof_ms else None),
-                "rocprof_source": (os.path.relpath(KSTATS[a.lanes], ROOT)
-                                   if rocprof_ms else None),
-                "limiter": _limiter(issue),
+                "frac_hip_events": round(launch_bytes / (kernels[dominant] / 1e3) / 1e9
+                                         / HBM_PEAK_GBS, 6),
+                "kernel_busy_ms_per_step": busy,
+                "kernel_busy_source": (f"{os.path.relpath(BUSY, ROOT)}: union of the kernel's "
+                                       f"launch intervals in the rocprofv3 kernel trace / steps"
+                                       if busy is not None else None),
+                "limiter": _limiter(issue, hbm_frac),
                 "pipeline_GBps": round(launch_bytes / (elapsed / a.steps) / 1e9, 3),
                 "lanes1": lanes1,
             },

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SPDL_HJ_ABI_VERSION 4
+#define SPDL_HJ_ABI_VERSION 5
 
 enum spdl_hj_status {
   SPDL_HJ_OK = 0,
@@ -121,6 +121,11 @@ typedef struct spdl_hj_image_info {
   int32_t width, height, ncomp;
   int32_t h_samp[4], v_samp[4];
   int32_t color;  /* enum spdl_hj_color, since ABI 4 */
+  /* 1: the multi-scan path decodes the file -- progressive (SOF2), or a
+   * first scan holding fewer components than the frame (since ABI 5).  A
+   * batch holding such a file runs that path on a side stream beside the
+   * baseline stages (spdl_hj_decode_batch_device included). */
+  int32_t multiscan;
 } spdl_hj_image_info;
 
 typedef struct spdl_hj_ctx spdl_hj_ctx;
@@ -279,8 +284,8 @@ const char* spdl_hj_stage_name(int32_t i);
  * default 384), "entropy_threads" (256/512/1024; default 512 with one lane,
  * 256 with more), "warmup_slots" (0-64: slots a Huffman run decodes from a
  * guessed state before its own first slot; default 6 with 256 threads, 12
- * with more), "lanes" (1-8 concurrent pipelines, 0 = automatic: 4, or one
- * per hardware queue beside the caller's when fewer; with N > 1, successive
+ * with more), "lanes" (1-8 concurrent pipelines, 0 = automatic: 4, or the
+ * hardware queues when fewer; with N > 1, successive
  * batches rotate over N device workspaces and run on the context's own N
  * streams, each ordered after the caller's stream at submission; completion
  * is then observed through the ticket -- spdl_hj_wait / spdl_hj_stream_wait

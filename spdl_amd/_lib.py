@@ -15,7 +15,7 @@ from dataclasses import dataclass
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPDL_AMD_LIB") or os.path.join(_HERE, "lib", "libspdl_hipjpeg.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # enums (mirror include/spdl_hipjpeg.h)
 PIX_FMTS = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
@@ -62,6 +62,7 @@ class ImageInfo(ctypes.Structure):
         ("h_samp", ctypes.c_int32 * 4),
         ("v_samp", ctypes.c_int32 * 4),
         ("color", ctypes.c_int32),  # spdl_hj_color: GRAY YCBCR RGB CMYK YCCK YCBCRK
+        ("multiscan", ctypes.c_int32),  # progressive or non-interleaved (ABI 5)
     ]
 
 

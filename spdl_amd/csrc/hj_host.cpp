@@ -257,6 +257,21 @@ void parallel_pack(CopyPool* pool, uint8_t* base, const std::vector<CopyItem>& i
   else pool->run(body);
 }
 
+// Components of the first scan (SOS Ns) after `pos`; 255 when no SOS header
+// follows (the device parse then reports the file).
+int first_scan_components(const uint8_t* d, size_t size, size_t pos) {
+  for (;;) {
+    while (pos < size && d[pos] != 0xFF) pos++;
+    while (pos < size && d[pos] == 0xFF) pos++;
+    if (pos >= size) return 255;
+    const int m = d[pos++];
+    if (m == 0x01 || (m >= 0xD0 && m <= 0xD8)) continue;
+    if (m == 0xD9 || pos + 3 > size) return 255;
+    if (m == 0xDA) return d[pos + 2];
+    pos += (size_t)((d[pos] << 8) | d[pos + 1]);
+  }
+}
+
 // ---- host SOF probe (replaces nvjpegGetImageInfo) --------------------------
 // The SOF fields and the frame's colour model (frame_color: the APP14 Adobe
 // flag seen before the SOF, the component ids).
@@ -302,28 +317,15 @@ int probe(const uint8_t* d, size_t size, spdl_hj_image_info* info) {
       }
       if (!frame_color(info->ncomp, info->h_samp, info->v_samp, ids, adobe, &info->color))
         return SPDL_HJ_ERR_UNSUPPORTED;
+      // the scan structure: progressive, or a first scan with fewer
+      // components than the frame (the multi-scan path decodes both)
+      info->multiscan = m == 0xC2 || first_scan_components(d, size, pos) < info->ncomp;
       return SPDL_HJ_OK;
     }
     if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
         (m >= 0xCD && m <= 0xCF))
       return SPDL_HJ_ERR_UNSUPPORTED;  // lossless, hierarchical, arithmetic
   }
-}
-
-// The first SOF of a file that probe() accepted is SOF2 (progressive).
-bool is_progressive(const uint8_t* d, size_t size) {
-  size_t pos = 2;
-  while (pos + 4 <= size) {
-    while (pos < size && d[pos] != 0xFF) pos++;
-    while (pos < size && d[pos] == 0xFF) pos++;
-    if (pos + 3 > size) return false;
-    const int m = d[pos++];
-    if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
-    if (m == 0xC0 || m == 0xC1 || m == 0xC2) return m == 0xC2;
-    if (m == 0xD9 || m == 0xDA) return false;
-    pos += (size_t)((d[pos] << 8) | d[pos + 1]);
-  }
-  return false;
 }
 
 // ---- geometry (FFmpeg scale/pad/crop semantics; see oracle jo_geometry) ----
@@ -1222,7 +1224,7 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
   bool prog = false;
   for (int i = 0; i < n; i++) {
     int rc = probe(data[i], sizes[i], &infos[i]);
-    if (!rc) prog = prog || is_progressive(data[i], sizes[i]);
+    if (!rc) prog = prog || infos[i].multiscan;
     if (status) status[i] = rc;
     if (rc) {
       set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, status_str(rc));
@@ -1269,6 +1271,8 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
   int rc = build_layout(offsets, sizes, infos, n, out, ctx->sub_bits, L, status, err, errlen,
                         &ctx->plans);
   if (rc) return rc;
+  // the caller's probe says which files take the multi-scan path (ABI 5)
+  for (int i = 0; i < n; i++) L.ms_side = L.ms_side || infos[i].multiscan != 0;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
   if (rc) return rc;
@@ -1397,7 +1401,7 @@ int spdl_hj_decode_staged(spdl_hj_ctx* ctx, int64_t ticket, size_t len, const in
     int rc = SPDL_HJ_ERR_INVALID_ARG;
     if (offsets[i] >= 0 && sizes[i] >= 0 && (size_t)(offsets[i] + sizes[i]) <= len)
       rc = probe(host + offsets[i], (size_t)sizes[i], &infos[i]);
-    if (!rc) prog = prog || is_progressive(host + offsets[i], (size_t)sizes[i]);
+    if (!rc) prog = prog || infos[i].multiscan;
     if (status) status[i] = rc;
     if (rc) {
       set_err(err, errlen, "Failed to decode an image. (image %d: %s)", i, status_str(rc));
@@ -1724,9 +1728,9 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
   }
   if (!strcmp(name, "lanes")) {  // concurrent pipelines (workspaces + streams)
     if (value < 0 || value > kMaxLanes) return SPDL_HJ_ERR_INVALID_ARG;
-    // 0: automatic -- four lanes when the process has the hardware queues
-    // for them beside the caller's stream, else one per spare queue
-    if (value == 0) value = std::max(1, std::min(4, ctx->hw_queues - 1));
+    // 0: automatic -- four lanes, fewer only with fewer hardware queues
+    // (measured with 4 queues: 2 or 4 lanes 401k img/s, 3 lanes 326k)
+    if (value == 0) value = std::max(1, std::min(4, ctx->hw_queues));
     // lanes beyond the process's hardware queues would share queues and
     // serialise: clamp (spdl_hj_get_param reports the lanes in effect)
     const int lanes = std::min((int)value, std::max(1, ctx->hw_queues));

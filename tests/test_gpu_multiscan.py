@@ -160,3 +160,52 @@ def test_progressive_with_ff_metadata(oracle, name):
     hyp = _lib.thread_decoder(0).decode_planes(d)
     for c in range(len(ref)):
         np.testing.assert_array_equal(hyp[c], ref[c], strict=True)
+
+
+def test_probe_flags_the_multiscan_path():
+    """spdl_hj_image_info.multiscan (ABI 5): what lets the device-resident
+    entry point run the multi-scan decoder beside the baseline stages."""
+    for n in ["q90_420", "q90_444", "gray", "odd_227x333"]:
+        assert _lib.get_image_info(cases.case(n)).multiscan == 0, n
+    for n in ["prog_420", "prog_gray", "multiscan_420", "multiscan_cmyk", "prog_restart"]:
+        assert _lib.get_image_info(cases.case(n)).multiscan == 1, n
+
+
+def _with_size_mod(d: bytes, mod: int) -> bytes:
+    """d with a COM segment after SOI sized so that len % 256 == mod."""
+    need = (mod - (len(d) + 4)) % 256
+    return d[:2] + b"\xff\xfe" + (need + 2).to_bytes(2, "big") + b"\x00" * need + d[2:]
+
+
+@pytest.mark.parametrize("mod", [252, 253, 254, 255, 0])
+def test_tightly_packed_device_batch(oracle, mod):
+    """Images back to back at 256-byte offsets (no slack after a file): the
+    multi-scan decoder's destuffed copy (side stream) must stay inside its
+    own image's bytes while the next image is destuffed and decoded."""
+    prog = [_with_size_mod(cases.case(n), mod) for n in ["prog_420", "multiscan_420",
+                                                          "prog_optimized"]]
+    base = [cases.case(n) for n in ["q90_420", "q90_444", "q75_420"]]
+    datas = [x for pair in zip(prog * 4, base * 4) for x in pair]
+    assert all(len(d) % 256 == mod for d in datas[::2])
+    offs, total = [], 0
+    for d in datas:
+        offs.append(total)
+        total = (total + len(d) + 255) // 256 * 256
+    host = np.zeros(total + 512, np.uint8)
+    for o, d in zip(offs, datas):
+        host[o:o + len(d)] = np.frombuffer(d, np.uint8)
+    dev = torch.from_numpy(host).to("cuda:0")
+    infos = [_lib.get_image_info(d) for d in datas]
+    assert sum(i.multiscan for i in infos) == len(datas) // 2
+    spec = Output(pix_fmt="rgb24", resize=True, **PAD224)
+    dec = _lib.Decoder(0)
+    out = torch.zeros((len(datas), 224, 224, 3), dtype=torch.uint8, device="cuda:0")
+    for _ in range(3):
+        assert not any(dec.decode_batch_device(dev.data_ptr(), dev.numel(), offs,
+                                               [len(d) for d in datas], infos, spec,
+                                               out.data_ptr(), out.numel()))
+    rs = oracle.Resize(**PAD224)
+    hyp = out.cpu().numpy()
+    for i, d in enumerate(datas):
+        np.testing.assert_array_equal(hyp[i], oracle.decode_resize(d, rs, "rgb24"), strict=True)
+    dec.close()
