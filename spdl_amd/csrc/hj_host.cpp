@@ -1608,24 +1608,28 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   for (int i = 0; i < 4; i++) diag[4 + i] = (int32_t)hi.tphase[i];
   for (int i = 0; i < 4; i++) diag[8 + i] = (int32_t)hi.dbg[i];
   for (int i = 0; i < 48; i++) diag[12 + i] = hi.sdiag[i];
-  // expand the coefficient lists (see BlockOut in hj_kernels.hip) to the dense
+  // expand the coefficient lists (see BlockOut in hj_kernels.hip: entries
+  // level << 16 | zig-zag index, dequantised as the IDCT does) to the dense
   // natural-order blocks the IDCT consumes
   const size_t nbk = (size_t)L.desc[0].nblocks;
   if (coefs && hi.status == SPDL_HJ_OK) {
+    static const uint8_t kNatural[64] = {
+        0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+        41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+        30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
     std::vector<uint2> bd(nbk);
     std::vector<uint32_t> ents(nbk * 64);
     HJ_HIP(hipMemcpy(bd.data(), W.bdesc.p, nbk * sizeof(uint2), hipMemcpyDeviceToHost));
     HJ_HIP(hipMemcpy(ents.data(), W.ents.p, nbk * 256, hipMemcpyDeviceToHost));
     std::vector<int16_t> dense(nbk * 64, 0);
     for (size_t j = 0; j < nbk; j++) {
+      const int c = hi.mcu_comp[j % (size_t)hi.bpm];
       dense[j * 64] = (int16_t)(bd[j].y >> 16);
       const uint32_t cnt = bd[j].y & 0xFFFFu;
       for (uint32_t i = 0; i < cnt && bd[j].x + i < nbk * 64; i++) {
         const uint32_t e = ents[bd[j].x + i];
-        // the entry's IDCT slot (kSlotOrder in hj_kernels.hip) -> natural index
-        const uint32_t sl = e & 63u, q = sl & 7u;
-        const uint32_t nat = (sl & 56u) | (q < 4u ? 2u * q : 2u * (q - 4u) + 1u);
-        dense[j * 64 + nat] = (int16_t)(e >> 16);  // dequantised
+        const uint32_t zz = e & 63u;
+        dense[j * 64 + kNatural[zz]] = (int16_t)(uint16_t)((e >> 16) * hi.qt[c][zz]);
       }
     }
     memcpy(coefs, dense.data(), 2 * (dense.size() < coef_cap ? dense.size() : coef_cap));

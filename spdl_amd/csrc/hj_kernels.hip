@@ -794,7 +794,6 @@ struct EntShared {
   uint32_t run_pos[NT];
   uint32_t run_zb[NT];
   uint32_t qdc[kMaxComp];  // DC quantiser per component
-  uint32_t qn[kMaxComp][64];  // per zig-zag index: IDCT slot (kSlotOrder) | quantiser << 16
   // The bit-reader windows are dead outside round 0 / the sync rounds, so the
   // reduction and scan scratch share their storage (keeps the workgroup at
   // <= 80 KiB of LDS: two entropy workgroups -- e.g. of two concurrent
@@ -1103,7 +1102,6 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const bool is_dc = z == 0;
     if ((is_dc & ((d.pos >= end) | (nb >= seg_end_blk))) | (d.pos > fast_end)) break;
     const uint32_t hi = dec_peek<NT>(d, win, words);
-    const uint32_t c = __builtin_amdgcn_ubfe(m.cmap, d.bs, 2);
     const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, is_dc), hi, is_dc);
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
     const uint32_t nbits = e & 31u;
@@ -1116,9 +1114,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const int v = sym_value(e, hi, nbits, sz);
     dec_skip(d, nbits);
     const bool ac = coef & !is_dc;
-    const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-    // (16-bit multiply: the low half is exact)
-    put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u), ac);
+    put_entry(o, (uint32_t)v << 16 | ((zn - 1u) & 63u), ac);
     o.cur += ac ? 1u : 0u;
     o.bstart = is_dc ? o.cur : o.bstart;
     o.dcv = is_dc ? v : o.dcv;
@@ -1134,7 +1130,6 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
-    const uint32_t c = __builtin_amdgcn_ubfe(m.cmap, d.bs, 2);
     const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, is_dc), hi, is_dc);
     const bool valid = (e & 0x60u) != 0u;
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
@@ -1158,8 +1153,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
       o.open = true;
     }
     const bool put = wr && !is_dc;
-    const uint32_t qn = S.qn[c][(zn - 1u) & 63u];
-    put_entry(o, pk_mul_lo16((uint32_t)v, qn >> 16) << 16 | (qn & 63u), put);
+    put_entry(o, (uint32_t)v << 16 | ((zn - 1u) & 63u), put);
     o.cur += put ? 1u : 0u;
     nb += (wr && is_dc) ? 1 : 0;
     // a symbol running past the segment end (after the rule above)
@@ -1280,10 +1274,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       if (tid < 17) S.valoff[i][tid] = T.valoff[tid];
       if (tid < 256) S.vals[i][tid] = T.vals[tid];
     }
-    for (int k = tid; k < kMaxComp * 64; k += NT) {
-      if (k % 64 == 0) S.qdc[k / 64] = in.qt[k / 64][0];
-      S.qn[k / 64][k % 64] = kSlotOrder[k % 64] | ((uint32_t)in.qt[k / 64][k % 64] << 16);
-    }
+    if (tid < kMaxComp) S.qdc[tid] = in.qt[tid][0];
     for (int b = 0; b < bpm; b++) {
       const int c = in.mcu_comp[b];
       bcomp |= (uint32_t)c << (2 * b);
@@ -3153,7 +3144,7 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
     if (tid == 0) in.status = S.err;
     return;
   }
-  // ---- levels -> coefficient lists (BlockOut layout), dequantised ----
+  // ---- levels -> coefficient lists (BlockOut layout; dequantised by the IDCT) ----
   for (int j = tid; j < nblocks; j += nt) {
     const int c = in.mcu_comp[j % in.bpm];
     uint4 q[16];
@@ -3173,8 +3164,7 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
 #pragma unroll
     for (int k = 1; k < 64; k++) {
       if (l[k] != 0) {
-        const uint32_t v = (uint32_t)l[k] * (uint32_t)in.qt[c][k];
-        out[n++] = (v << 16) | kSlotOrder[k];
+        out[n++] = ((uint32_t)l[k] << 16) | (uint32_t)k;
       }
     }
     const int32_t dc = (int32_t)(int16_t)(uint16_t)((uint32_t)kDcBias + (uint32_t)l[0] * in.qt[c][0]);
@@ -3224,15 +3214,26 @@ __device__ __forceinline__ uint32_t slot_byte(uint32_t s) {
   return (s >> 1) * (uint32_t)NT * 4u + ((s & 1u) << 1);
 }
 
-// One block of the entropy kernel's coefficient lists (see BlockOut: DC
-// final, AC dequantised with their IDCT slot) into the thread's word-major
-// block (b32: its word 0; zeroed here).  (A list may start inside a 16-byte
-// group: a run's lists are packed back to back; entries [lo, lo + count) of
-// the groups from `start`.)
+// The IDCT kernels' dequantisation table, per component and zig-zag index:
+// the coefficient's byte offset in the word-major block (its IDCT slot,
+// kSlotOrder) | quantiser << 16.  Filled by the workgroup before its blocks.
+template <int NT>
+__device__ __forceinline__ void load_dequant(uint32_t (&sq)[kMaxComp][64], const ImageInfo& in,
+                                             int tid) {
+  for (int k = tid; k < kMaxComp * 64; k += NT)
+    sq[k >> 6][k & 63] = slot_byte<NT>(kSlotOrder[k & 63]) | ((uint32_t)in.qt[k >> 6][k & 63] << 16);
+}
+
+// One block's coefficient list (see BlockOut: DC final in bd; AC entries
+// level << 16 | zig-zag index) into the thread's word-major block (b32: its
+// word 0; zeroed here), dequantised on the way (sqc: the component's row of
+// the dequantisation table).  (A list may start inside a 16-byte group: a
+// run's lists are packed back to back; entries [lo, lo + count) of the groups
+// from `start`.)
 template <int NT>
 __device__ __forceinline__ void list_block(const uint32_t* __restrict__ ents, const uint2 bd,
                                            const int64_t coef_off, const int nblocks,
-                                           uint32_t* b32) {
+                                           const uint32_t* sqc, uint32_t* b32) {
 #pragma unroll
   for (int w = 0; w < kBlkWords; w++) b32[w * NT] = w == 0 ? (bd.y >> 16) : 0u;
   uint8_t* blk = reinterpret_cast<uint8_t*>(b32);
@@ -3255,8 +3256,10 @@ __device__ __forceinline__ void list_block(const uint32_t* __restrict__ ents, co
 #pragma unroll
       for (int h = 0; h < 4; h++) {  // (outside the list: into the dummy word)
         const uint32_t k = 4u * (i + u) + h;
-        uint8_t* dst = k >= lo && k < hi_e ? blk + slot_byte<NT>(w[h] & 63u) : dummy;
-        *reinterpret_cast<hj_i16_alias*>(dst) = (int16_t)(w[h] >> 16);
+        const uint32_t qs = sqc[w[h] & 63u];
+        uint8_t* dst = k >= lo && k < hi_e ? blk + (qs & 0xFFFFu) : dummy;
+        // (16-bit multiply: the low half is the sequential decoder's int16 product)
+        *reinterpret_cast<hj_i16_alias*>(dst) = (int16_t)pk_mul_lo16(w[h] >> 16, qs >> 16);
       }
     }
   }
@@ -3373,10 +3376,14 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
                                                             const ImageInfo* __restrict__ infos,
                                                             uint8_t* __restrict__ planes) {
   __shared__ __attribute__((aligned(16))) uint32_t sblk[kBlkWords + 1][kIdctThreads];
+  __shared__ uint32_t sq[kMaxComp][64];
   const int img = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const ImageInfo& in = infos[img];
-  if (in.status != kOk || j >= in.nblocks) return;
+  if (in.status != kOk || (int)(blockIdx.x * blockDim.x) >= in.nblocks) return;
+  load_dequant<kIdctThreads>(sq, in, threadIdx.x);
+  __syncthreads();
+  if (j >= in.nblocks) return;
   const ImageDesc& dd = desc[img];
   const int bpm = in.bpm;
   const int mcu = j / bpm, b = j - mcu * bpm;
@@ -3391,7 +3398,8 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
     by = my * in.comp_v[c] + in.mcu_dy[b];
   }
   uint32_t* b32 = &sblk[0][threadIdx.x];
-  list_block<kIdctThreads>(ents, bdesc[(size_t)dd.coef_off + j], dd.coef_off, in.nblocks, b32);
+  list_block<kIdctThreads>(ents, bdesc[(size_t)dd.coef_off + j], dd.coef_off, in.nblocks, sq[c],
+                           b32);
   int32_t px[64];
   idct_block<kIdctThreads, IDCT>(b32, px);
   const int stride = dd.plane_stride[c];
@@ -4076,6 +4084,7 @@ __global__ void __launch_bounds__(kFusedThreads) idct_rgb_kernel(const uint32_t*
                                                        const BatchParams p,
                                                        int32_t* __restrict__ host_status) {
   __shared__ __attribute__((aligned(16))) uint32_t sblk[kBlkWords + 1][kFusedThreads];
+  __shared__ uint32_t sq[kMaxComp][64];
   const int img = blockIdx.y, tid = threadIdx.x;
   const ImageInfo& in = infos[img];
   if (host_status && blockIdx.x == 0 && tid == 0) host_status[img] = in.status;
@@ -4091,11 +4100,13 @@ __global__ void __launch_bounds__(kFusedThreads) idct_rgb_kernel(const uint32_t*
   const int ys = tw * 16, cs = tw * 8;                 // tile row strides (bytes)
   const bool act = tid < nm * bpm;
   const int m = tid / bpm, b = tid - m * bpm;
+  load_dequant<kFusedThreads>(sq, in, tid);
+  __syncthreads();
   int32_t px[64];
   if (act) {
     const int j = (my * in.mcux + mx0 + m) * bpm + b;
     list_block<kFusedThreads>(ents, bdesc[(size_t)dd.coef_off + j], dd.coef_off, in.nblocks,
-                              &sblk[0][tid]);
+                              sq[in.mcu_comp[b]], &sblk[0][tid]);
     idct_block<kFusedThreads, IDCT>(&sblk[0][tid], px);
   }
   __syncthreads();  // every slot read: the tile takes their place

@@ -77,3 +77,30 @@ def test_configs4_stream_ranks_rehearsed(oracle, tmp_path):
             i = int(str(name).rsplit("/", 1)[1][:-4])
             np.testing.assert_array_equal(rgb, oracle.decode_resize(datas[i], rs, "rgb24"),
                                           strict=True)
+
+
+def test_configs4_stream_eight_ranks_rehearsed(oracle, tmp_path):
+    """configs[4] as the driver would launch it on an 8-GPU node (8 stream
+    ranks, each its own shard of the tar stream, pinned ring, copy pool sized
+    for LOCAL_WORLD_SIZE=8), rehearsed on one GPU; every rank's samples of
+    its last timed pass checked against the oracle."""
+    from spdl_amd.synthetic import synthetic_batch
+
+    out = str(tmp_path / "stream8")
+    rec = _run(["bench_stream.py", "--gpus", "8", "--rehearse-one-gpu", "--images", "512",
+                "--passes", "1", "--warmup-passes", "1", "--sample-out", out,
+                "--sample-images", "8"], 900)
+    assert rec["n_gpus"] == 8 and len(rec["ranks"]) == 8
+    datas = synthetic_batch(512, distinct=32)
+    rs = oracle.Resize(**PAD224)
+    refs = {}
+    files = sorted(glob.glob(out + ".r*.npz"))
+    assert len(files) == 8
+    for f in files:
+        z = np.load(f)
+        assert len(z["names"]) > 0
+        for name, rgb in zip(z["names"], z["rgb"]):
+            i = int(str(name).rsplit("/", 1)[1][:-4])
+            if i not in refs:
+                refs[i] = oracle.decode_resize(datas[i], rs, "rgb24")
+            np.testing.assert_array_equal(rgb, refs[i], strict=True)

@@ -14,6 +14,10 @@ for l in 4 1; do
     -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --lanes1-steps 0 --lanes $l \
     > "$out/ktrace_l$l.log" 2>&1 || { echo "kernel trace lanes $l failed"; exit 1; }
 done
+python3 tools/kernel_busy.py "$out/kernel_busy.json" \
+  "4:$(find "$out/ktrace_l4" -name '*kernel_trace.csv' | head -1)" \
+  "1:$(find "$out/ktrace_l1" -name '*kernel_trace.csv' | head -1)" > "$out/kernel_busy.txt" || exit 1
+cat "$out/kernel_busy.txt"
 python3 tools/pmc_traffic.py "$out/traffic.json" "$out/pmc/pmc_1" "$out/pmc/pmc_2" \
   --calib "$out/calib/calibration.json" > "$out/traffic.txt" || exit 1
 cat "$out/traffic.txt" "$out/pmc/issue.txt" "$out/calib/calibration.txt"
