@@ -1107,14 +1107,18 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t nbits = e & 31u;
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
     const bool coef = (e >> 19) & 1u;
-    // valid (kind != Slow) and not an AC size-0 symbol other than EOB / ZRL:
-    // (e & (bad | kind)) in {0x20, 0x40, 0x60}
-    const bool ok = ((e & 0x100060u) - 1u) < 0x60u;
-    if (!ok | (coef & (zn > 64u))) break;
+    // One unsigned test for the three rules: the entry is valid (kind !=
+    // Slow) and not an AC size-0 symbol other than EOB / ZRL -- (e & (bad |
+    // kind)) - 0x20 in {0, 0x20, 0x40} -- and a coefficient does not run
+    // past 63: bit 31 of (64 - zn) & (e << 12) is (zn > 64) & coef (an EOB
+    // also has zn > 64: only bit 31 counts).
+    const uint32_t rules =
+        ((64u - zn) & ((e & 0x80000u) << 12)) | ((e & 0x100060u) - 0x20u);
+    if (rules > 0x40u) break;
     const int v = sym_value(e, hi, nbits, sz);
     dec_skip(d, nbits);
     const bool ac = coef & !is_dc;
-    put_entry(o, (uint32_t)v << 16 | ((zn - 1u) & 63u), ac);
+    put_entry(o, (uint32_t)v << 16 | (zn - 1u), ac);  // (zn <= 64 for a coefficient)
     o.cur += ac ? 1u : 0u;
     o.bstart = is_dc ? o.cur : o.bstart;
     o.dcv = is_dc ? v : o.dcv;
