@@ -1574,20 +1574,30 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       // (selects over the components, not a dynamically indexed array: that
       // would live in scratch)
       int v[kMaxComp] = {}, flag = 0;
+      // (blocks in groups of kG: the group's descriptor loads are issued
+      // back to back, so one memory latency is exposed per group)
+      constexpr int kG = 8;
       {
         int bs = bs0, reset = first_reset;
-        for (int b = b0; b < b1; b++) {
-          if (b == reset) {
-            flag = 1;
+        for (int b = b0; b < b1; b += kG) {
+          uint32_t ys[kG];
 #pragma unroll
-            for (int i = 0; i < kMaxComp; i++) v[i] = 0;
-            reset += rblk;
+          for (int g = 0; g < kG; g++) ys[g] = bdesc_img[min(b + g, b1 - 1)].y;
+#pragma unroll
+          for (int g = 0; g < kG; g++) {
+            if (b + g >= b1) break;
+            if (b + g == reset) {
+              flag = 1;
+#pragma unroll
+              for (int i = 0; i < kMaxComp; i++) v[i] = 0;
+              reset += rblk;
+            }
+            const uint32_t c = __builtin_amdgcn_ubfe(bcomp, 2u * (uint32_t)bs, 2);
+            const int dv = (int32_t)ys[g] >> 16;
+#pragma unroll
+            for (int i = 0; i < kMaxComp; i++) v[i] += c == (uint32_t)i ? dv : 0;
+            bs = bs + 1 == bpm ? 0 : bs + 1;
           }
-          const uint32_t c = __builtin_amdgcn_ubfe(bcomp, 2u * (uint32_t)bs, 2);
-          const int dv = (int32_t)bdesc_img[b].y >> 16;
-#pragma unroll
-          for (int i = 0; i < kMaxComp; i++) v[i] += c == (uint32_t)i ? dv : 0;
-          bs = bs + 1 == bpm ? 0 : bs + 1;
         }
       }
       seg_scan<NT, kMaxComp>(S, tid, flag, v);
@@ -1598,25 +1608,31 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       }
       __syncthreads();
       int bs = bs0, reset = first_reset;
-      for (int b = b0; b < b1; b++) {
-        if (b == reset) {
+      for (int b = b0; b < b1; b += kG) {
+        uint32_t ys[kG];
 #pragma unroll
-          for (int i = 0; i < kMaxComp; i++) pr[i] = 0;
-          reset += rblk;
+        for (int g = 0; g < kG; g++) ys[g] = bdesc_img[min(b + g, b1 - 1)].y;
+#pragma unroll
+        for (int g = 0; g < kG; g++) {
+          if (b + g >= b1) break;
+          if (b + g == reset) {
+#pragma unroll
+            for (int i = 0; i < kMaxComp; i++) pr[i] = 0;
+            reset += rblk;
+          }
+          const uint32_t c = __builtin_amdgcn_ubfe(bcomp, 2u * (uint32_t)bs, 2);
+          const uint32_t by = ys[g];
+          int cur = (int32_t)by >> 16;
+#pragma unroll
+          for (int i = 0; i < kMaxComp; i++) cur += c == (uint32_t)i ? pr[i] : 0;
+#pragma unroll
+          for (int i = 0; i < kMaxComp; i++) pr[i] = c == (uint32_t)i ? cur : pr[i];
+          const uint32_t q = S.qdc[c];
+          const int32_t dqi = (int32_t)((uint32_t)kDcBias + q * (uint32_t)cur);
+          const int32_t dc = dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi);
+          bdesc_img[b + g].y = (by & 0xFFFFu) | ((uint32_t)dc << 16);
+          bs = bs + 1 == bpm ? 0 : bs + 1;
         }
-        const uint32_t c = __builtin_amdgcn_ubfe(bcomp, 2u * (uint32_t)bs, 2);
-        const uint32_t by = bdesc_img[b].y;
-        const int dv = (int32_t)by >> 16;
-        int cur = dv;
-#pragma unroll
-        for (int i = 0; i < kMaxComp; i++) cur += c == (uint32_t)i ? pr[i] : 0;
-#pragma unroll
-        for (int i = 0; i < kMaxComp; i++) pr[i] = c == (uint32_t)i ? cur : pr[i];
-        const uint32_t q = S.qdc[c];
-        const int32_t dqi = (int32_t)((uint32_t)kDcBias + q * (uint32_t)cur);
-        const int32_t dc = dqi < -32768 ? -32768 : (dqi > 32767 ? 32767 : dqi);
-        bdesc_img[b].y = (by & 0xFFFFu) | ((uint32_t)dc << 16);
-        bs = bs + 1 == bpm ? 0 : bs + 1;
       }
     }
     {
