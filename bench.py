@@ -22,16 +22,18 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# --hw-queues Q: the regime of a drop-in imported after the trainer touched
-# the GPU -- HIP initialised (through torch) with GPU_MAX_HW_QUEUES=Q before
-# spdl_amd is imported, so the decoder sees Q queues.  Otherwise spdl_amd
-# comes first and exports GPU_MAX_HW_QUEUES=16 before HIP starts.
+# --hw-queues Q: HIP initialised (through torch) with GPU_MAX_HW_QUEUES=Q
+# before spdl_amd is imported (the regime of a drop-in imported after the
+# trainer touched the GPU).  Without it HIP takes the environment's value
+# (its own default: 4).  The lanes' low-priority streams make the rate
+# independent of Q; the record carries the rate at the other setting too.
 if "--hw-queues" in sys.argv:
     os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
     import torch  # noqa: E402
@@ -212,6 +214,8 @@ def _args():
     p.add_argument("--hw-queues", type=int, default=0,
                    help="initialise HIP with this many hardware queues before importing spdl_amd "
                         "(the late-import regime of a drop-in)")
+    p.add_argument("--no-queue-compare", action="store_true",
+                   help="skip the child run at the other GPU_MAX_HW_QUEUES setting (4 <-> 16)")
     p.add_argument("--sync-steps", action="store_true",
                    help="one synchronous call per step (no overlap of host work)")
     p.add_argument("--with-copies", action="store_true",
@@ -539,6 +543,27 @@ def main():
         threads = a.cpu_threads or _cpu_cores()["usable"]
         cpu = _cpu_baseline(datas, threads, a.cpu_images, a.cpu_images // 2, a.cpu_runs)
 
+    # the same bench in a child process whose HIP starts with the other
+    # hardware-queue count (4 <-> 16): the record carries both rates
+    queues = None
+    hwq = dec.get_param("hw_queues")
+    if (rank == 0 and world == 1 and not a.no_queue_compare and not a.debug_mask
+            and a.workload == "pad224"):
+        other = 16 if hwq != 16 else 4
+        cmd = [sys.executable, os.path.abspath(__file__), "--hw-queues", str(other),
+               "--steps", str(a.steps), "--warmup", str(a.warmup), "--batch", str(a.batch),
+               "--lanes", str(a.lanes), "--no-cpu-baseline", "--lanes1-steps", "0",
+               "--no-queue-compare", "--oracle-check", "8"]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        child = [json.loads(line) for line in r.stdout.splitlines() if line.startswith('{"metric"')]
+        if r.returncode != 0 or not child:
+            raise SystemExit(f"queue-compare child failed ({r.returncode}): {r.stderr[-2000:]}")
+        c = child[-1]
+        queues = {"this_run": {"hw_queues": hwq, "value": None},
+                  "other": {"hw_queues": c["config"]["hw_queues"], "value": c["value"],
+                            "lanes": c["config"]["lanes"], "steps": c["steps"],
+                            "oracle_check": c["oracle_check"]}}
+
     traffic = issue = rocprof_ms = None
     if a.workload == "pad224" and a.lanes in KSTATS and a.batch == BATCH:
         rocprof_ms = _rocprof_ms(a.lanes, dominant)
@@ -626,6 +651,10 @@ def main():
             "ranks": ranks,
             "cpu_baseline": cpu,
         }
+        if queues is not None:
+            queues["this_run"]["value"] = rec["value"]
+            queues["other_over_this"] = round(queues["other"]["value"] / rec["value"], 4)
+            rec["hw_queue_regimes"] = queues
         if copies is not None:
             rec["with_copies_images_per_sec"] = round(copies, 1)
         print(json.dumps(rec), flush=True)

@@ -291,9 +291,13 @@ const char* spdl_hj_stage_name(int32_t i);
  * is then observed through the ticket -- spdl_hj_wait / spdl_hj_stream_wait
  * -- not by the caller's stream; each lane wants a hardware queue of its own,
  * so the value is clamped to "hw_queues"; a lane's stream is created when
- * first enabled), "hw_queues" (the hardware queues HIP gave this process:
+ * first enabled), "lane_priority" (stream priority of the lanes: 1 = low,
+ * the default, 0 = normal, -1 = high; HIP keeps up to "hw_queues" hardware
+ * queues per priority, so low-priority lanes get queues of their own beside
+ * the normal-priority null / torch streams; changing it re-creates the lane
+ * streams after their work), "hw_queues" (hardware queues per priority pool:
  * read from GPU_MAX_HW_QUEUES at spdl_hj_create, default 4; set it when HIP
- * initialised before that variable was exported), "output_path" (0 = by
+ * initialised with another value), "output_path" (0 = by
  * batch, 1 = the generic swscale kernel, 2 = separate IDCT + unscaled
  * converter at full resolution: byte-identical outputs, for A/B and tests).
  * Builds with -DHJ_ABLATIONS=1 also take "debug_mask" (timing ablations that

@@ -8,25 +8,12 @@ hand-written HIP kernels of ``spdl_amd/csrc`` through the C-ABI in
 """
 
 import os as _os
-import sys as _sys
 
-# Each decode pipeline lane is a HIP stream of its own, beside the copy stream
-# and the caller's: with HIP's default of 4 hardware queues per process, three
-# or more lanes share queues and serialise (measured: 4 lanes 348k img/s with
-# 4 queues, 439k with 16).  HIP reads the variable when it initialises, so
-# this only works when spdl_amd is imported before the first GPU call.
-# HW_QUEUES is the value in effect; HW_QUEUES_LATE says HIP had already
-# initialised (through torch) with the previous value, and decoders then
-# clamp their lanes to it (spdl_hj_set_param "hw_queues").
-_prev = int(_os.environ.get("GPU_MAX_HW_QUEUES") or 0)
-_torch = _sys.modules.get("torch")
-HW_QUEUES_LATE = bool(_torch is not None and hasattr(_torch, "cuda")
-                      and _torch.cuda.is_initialized())
-if HW_QUEUES_LATE:
-    HW_QUEUES = _prev or 4
-else:
-    HW_QUEUES = max(16, _prev)
-    _os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
-del _torch
+# Each decode pipeline lane is a HIP stream of its own.  Lane streams are
+# created at low priority: HIP keeps a pool of GPU_MAX_HW_QUEUES hardware
+# queues per stream priority, so the lanes get queues of their own whatever
+# the variable's value (4, HIP's default, included) and whether or not torch
+# initialised HIP first.  HW_QUEUES is the per-pool queue count in effect.
+HW_QUEUES = int(_os.environ.get("GPU_MAX_HW_QUEUES") or 0) or 4
 
 __version__ = "0.1.0"

@@ -318,10 +318,6 @@ class Decoder:
             raise RuntimeError(f"spdl_amd: cannot create decoder: {err.value.decode()}")
         self._h = h
         self.device_index = int(device_index)
-        from . import HW_QUEUES, HW_QUEUES_LATE
-
-        if HW_QUEUES_LATE:  # HIP initialised before spdl_amd exported the variable
-            self.set_param("hw_queues", HW_QUEUES)
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -722,6 +722,15 @@ struct spdl_hj_ctx {
   // hardware queues HIP gives this process (GPU_MAX_HW_QUEUES when HIP
   // initialised; 4 is HIP's default): each lane's stream wants one of its own
   int hw_queues = 4;
+  // stream priority of the lanes' streams: 1 low (default), 0 normal, -1
+  // high.  HIP keeps a pool of up to GPU_MAX_HW_QUEUES hardware queues per
+  // priority, so low-priority lanes get queues of their own beside the
+  // normal-priority pool that the null stream, torch's streams and the copy
+  // stream share (measured with 4 queues, 4 lanes: 408k img/s at normal
+  // priority -- the lanes landed on two queues -- 508k at low, as with 16).
+  // Multiscan side streams are high priority (a third pool): they carry the
+  // mixed batch's critical path.
+  int lane_priority = 1;
   // output kernels: 0 = by batch (fused IDCT + converter at full resolution
   // when possible), 1 = the generic swscale kernel, 2 = separate IDCT +
   // unscaled converter -- byte-identical outputs (tests compare them)
@@ -767,14 +776,26 @@ CopyPool* copy_pool(spdl_hj_ctx* c) {
   return c->pool;
 }
 
+hipError_t create_stream(hipStream_t* s, int priority) {
+  int least = 0, greatest = 0;
+  (void)hipDeviceGetStreamPriorityRange(&least, &greatest);  // (1, -1) on gfx950
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking,
+                                     std::max(greatest, std::min(least, priority)));
+}
+
+// side streams (multiscan beside the lanes' stages) have queues to spare: the
+// high-priority pool holds them alone unless the lanes are high priority too
+bool side_streams_fit(const spdl_hj_ctx* c) {
+  return (c->lane_priority < 0 ? 2 * c->lanes : c->lanes) <= c->hw_queues;
+}
+
 // Workspaces [0, n) get their completion event and (n > 1) their stream.
 bool ensure_lanes(spdl_hj_ctx* c, int n) {
   DeviceGuard g(c->device);
   for (int i = c->lanes_ready; i < n; i++) {
     Workspace& w = c->ws[i];
     if (!w.done && hipEventCreateWithFlags(&w.done, hipEventDisableTiming) != hipSuccess) return false;
-    if (!w.stream && hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess)
-      return false;
+    if (!w.stream && create_stream(&w.stream, c->lane_priority) != hipSuccess) return false;
     c->lanes_ready = i + 1;
   }
   return true;
@@ -909,10 +930,9 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                       static_cast<HuffTable*>(W.luts.p), hs ? slot.pin_tables.dev : nullptr,
                       W.wts.p, hs ? (int64_t)tb : 0, n, st));
   mark(ctx, slot, 2, st);
-  const bool ms_side = L.ms_side && !(ctx->debug_mask & 0x10000) &&
-                       2 * ctx->lanes + 1 <= ctx->hw_queues;
+  const bool ms_side = L.ms_side && !(ctx->debug_mask & 0x10000) && side_streams_fit(ctx);
   if (ms_side) {
-    if (!W.side) HJ_HIP(hipStreamCreateWithFlags(&W.side, hipStreamNonBlocking));
+    if (!W.side) HJ_HIP(create_stream(&W.side, -1));
     if (!W.ev_parsed) HJ_HIP(hipEventCreateWithFlags(&W.ev_parsed, hipEventDisableTiming));
     if (!W.ev_ms) HJ_HIP(hipEventCreateWithFlags(&W.ev_ms, hipEventDisableTiming));
     HJ_HIP(hipEventRecord(W.ev_parsed, st));
@@ -1064,6 +1084,8 @@ int exec_stream(spdl_hj_ctx* ctx, Slot& slot, hipStream_t st, hipStream_t* xs, c
 // H2D of the slot's staged bytes on the copy stream; `st` waits for it.
 int stage_h2d(spdl_hj_ctx* ctx, Slot& s, size_t total, hipStream_t st, char* err, size_t errlen) {
   HJ_HIP(s.bytes.ensure(total + 512));
+  // (created on first use: device-resident batches never take its queue)
+  if (!ctx->copy) HJ_HIP(hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking));
   mark(ctx, s, 0, ctx->copy);
   HJ_HIP(hipMemcpyAsync(s.bytes.p, s.pin_in.p, total, hipMemcpyHostToDevice, ctx->copy));
   HJ_HIP(hipEventRecord(s.h2d_done, ctx->copy));
@@ -1155,8 +1177,7 @@ spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen) {
   auto* c = new spdl_hj_ctx();
   c->device = device;
   if (const char* q = getenv("GPU_MAX_HW_QUEUES")) c->hw_queues = atoi(q) > 0 ? atoi(q) : 4;
-  bool ok = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) == hipSuccess;
-  ok = ok && ensure_lanes(c, 1);
+  bool ok = ensure_lanes(c, 1);
   for (int i = 0; ok && i < kSlots; i++)
     ok = hipEventCreateWithFlags(&c->slots[i].h2d_done, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->slots[i].done, hipEventDisableTiming) == hipSuccess &&
@@ -1733,14 +1754,29 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "lanes")) {  // concurrent pipelines (workspaces + streams)
     if (value < 0 || value > kMaxLanes) return SPDL_HJ_ERR_INVALID_ARG;
     // 0: automatic -- four lanes, fewer only with fewer hardware queues
-    // (measured with 4 queues: 2 or 4 lanes 401k img/s, 3 lanes 326k)
+    // (r04 sweep, 4-lane bench: 3 lanes 447k img/s, 4 479k, 5 431k, 8 471k)
     if (value == 0) value = std::max(1, std::min(4, ctx->hw_queues));
-    // lanes beyond the process's hardware queues would share queues and
-    // serialise: clamp (spdl_hj_get_param reports the lanes in effect)
+    // lanes beyond the hardware queues of their priority's pool would share
+    // queues and serialise: clamp (spdl_hj_get_param reports the lanes in effect)
     const int lanes = std::min((int)value, std::max(1, ctx->hw_queues));
     if (!ensure_lanes(ctx, lanes)) return SPDL_HJ_ERR_HIP;
     ctx->lanes = lanes;
     return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "lane_priority")) {  // 1 low (own queue pool), 0 normal, -1 high
+    if (value < -1 || value > 1) return SPDL_HJ_ERR_INVALID_ARG;
+    if (value == ctx->lane_priority) return SPDL_HJ_OK;
+    // the lanes' streams are re-created at the new priority (after their work)
+    DeviceGuard g(ctx->device);
+    for (Workspace& w : ctx->ws)
+      if (w.stream) {
+        if (hipStreamSynchronize(w.stream) != hipSuccess) return SPDL_HJ_ERR_HIP;
+        (void)hipStreamDestroy(w.stream);
+        w.stream = nullptr;
+      }
+    ctx->lane_priority = (int)value;
+    ctx->lanes_ready = 0;
+    return ensure_lanes(ctx, std::max(1, ctx->lanes)) ? SPDL_HJ_OK : SPDL_HJ_ERR_HIP;
   }
   if (!strcmp(name, "hw_queues")) {  // the caller knows HIP initialised with another value
     if (value < 1 || value > 32) return SPDL_HJ_ERR_INVALID_ARG;
@@ -1780,7 +1816,8 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"hw_queues", ctx->hw_queues},
       // streams a batch holding a progressive image may use: one per lane, a
       // multiscan side stream per lane when the queues allow it, the copy stream
-      {"streams", ctx->lanes * (2 * ctx->lanes + 1 <= ctx->hw_queues ? 2 : 1) + 1},
+      {"streams", ctx->lanes * (side_streams_fit(ctx) ? 2 : 1) + 1},
+      {"lane_priority", ctx->lane_priority},
       {"output_path", ctx->output_path},
       {"host_staging", ctx->host_staging},
       {"copy_threads", ctx->pool ? ctx->pool->workers() : copy_workers() + 1},

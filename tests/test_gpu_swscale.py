@@ -158,18 +158,21 @@ def bench_batch(oracle):
     return dev, np.asarray(offs, np.int64), np.asarray(sizes, np.int64), infos, refs
 
 
-@pytest.mark.parametrize("lanes,inflight,warm", [
-    (1, 2, 0), (1, 2, 8), (1, 2, 64), (2, 2, 0), (2, 2, 8), (2, 2, 64),
-    (4, 6, -1),  # the driver's bench configuration: 4 lanes, lanes + 2 in flight
+@pytest.mark.parametrize("lanes,inflight,warm,prio", [
+    (1, 2, 0, 1), (1, 2, 8, 1), (1, 2, 64, 1), (2, 2, 0, 1), (2, 2, 8, 1), (2, 2, 64, 1),
+    (4, 6, -1, 1),  # the driver's bench configuration: 4 lanes, lanes + 2 in flight
+    (4, 6, -1, 0), (4, 6, -1, -1),  # lanes at normal / high stream priority
 ])
-def test_bench_path_bit_exact(bench_batch, lanes, inflight, warm):
+def test_bench_path_bit_exact(bench_batch, lanes, inflight, warm, prio):
     """decode_batch_device exactly as bench.py drives it: async submissions,
     `inflight` batches in flight on `lanes` pipelines, then every image of
     every batch against the oracle."""
     dev, offs, sizes, infos, refs = bench_batch
     dec = _lib.Decoder(0)
     dec.set_param("lanes", lanes)
-    assert dec.get_param("lanes") == lanes  # the box exports 16 hardware queues
+    assert dec.get_param("lanes") == lanes  # <= 4: HIP's default queues per priority pool
+    dec.set_param("lane_priority", prio)
+    assert dec.get_param("lane_priority") == prio
     if warm >= 0:
         dec.set_param("warmup_slots", warm)
     spec = Output(pix_fmt="rgb24", resize=True, **PAD224)
