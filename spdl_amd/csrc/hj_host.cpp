@@ -1737,7 +1737,8 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "entropy_threads")) {  // workgroup size of the Huffman kernel
-    if (value != 0 && value != 256 && value != 512 && value != 1024) return SPDL_HJ_ERR_INVALID_ARG;
+    if (value != 0 && value != 128 && value != 256 && value != 512 && value != 1024)
+      return SPDL_HJ_ERR_INVALID_ARG;
     ctx->entropy_threads = (int)value;
     return SPDL_HJ_OK;
   }

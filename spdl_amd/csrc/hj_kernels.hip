@@ -778,7 +778,12 @@ __constant__ uint8_t kSlotOrder[64] = {
     0,  4,  8,  16, 12, 1,  5,  9,  20, 24, 32, 28, 17, 13, 2,  6,  10, 21, 25, 36, 40, 48,
     44, 33, 29, 18, 14, 3,  7,  11, 22, 26, 37, 41, 52, 56, 60, 49, 45, 34, 30, 19, 15, 23,
     27, 38, 42, 53, 57, 61, 50, 46, 35, 31, 39, 43, 54, 58, 62, 51, 47, 55, 59, 63};
-constexpr int kWinWords = 8;  // bit-reader window per thread (words)
+#ifndef HJ_WIN_WORDS
+#define HJ_WIN_WORDS 12
+#endif
+// bit-reader window per thread (words): 12 restages a lane every ~8-11 words
+// (r04 A/B, 4-lane bench: 8 words 507.5k img/s, 12 515.1k, 16 514.1k)
+constexpr int kWinWords = HJ_WIN_WORDS;
 
 // NTAB = distinct Huffman tables the workgroup holds in LDS: 4 covers luma +
 // chroma DC/AC (gray: 2) and keeps three entropy workgroups per CU; a scan
@@ -819,8 +824,8 @@ static_assert(sizeof(EntShared<256, 4>) <= 160 * 1024 / 3,
               "entropy LDS must allow 3 workgroups per CU at 256 threads");
 
 // Per-thread bit reader over the destuffed stream (big-endian bytes read as
-// 32-bit words).  Words come from an 8-word LDS window per thread
-// ([word][thread], conflict-free), restaged from HBM once every 4-7 words:
+// 32-bit words).  Words come from a kWinWords LDS window per thread
+// ([word][thread], conflict-free), restaged from HBM once every 8-11 words:
 // the decode loop itself issues no global load, so its coefficient stores
 // never stall it (on gfx9 a vmcnt wait for a load also waits for older
 // stores).
@@ -1276,7 +1281,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
           S.sub[(base << kSubBits) + k] = T.sub[k];
       if (tid < 18) S.maxcode[i][tid] = T.maxcode[tid];
       if (tid < 17) S.valoff[i][tid] = T.valoff[tid];
-      if (tid < 256) S.vals[i][tid] = T.vals[tid];
+      for (int k = tid; k < 256; k += NT) S.vals[i][k] = T.vals[k];
     }
     if (tid < kMaxComp) S.qdc[tid] = in.qt[tid][0];
     for (int b = 0; b < bpm; b++) {
@@ -4288,6 +4293,8 @@ hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const Imag
     HJ_ENT(1024, 4);
   } else if (threads == 512) {
     HJ_ENT(512, 4);
+  } else if (threads == 128) {
+    HJ_ENT(128, 4);
   } else {
     HJ_ENT(256, 4);
   }

@@ -248,7 +248,7 @@ def test_corrupt_streams_agree_with_oracle(decoder, oracle, seed):
         np.testing.assert_array_equal(t.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("threads", [256, 512, 1024])
+@pytest.mark.parametrize("threads", [128, 256, 512, 1024])
 @pytest.mark.parametrize("sub_bits", [32, 64, 256, 1024, 8192])
 def test_subsequence_sizes(oracle, sub_bits, threads):
     """The sync result must not depend on the subsequence size or on the

@@ -6,7 +6,7 @@ for r in $(seq ${REPS:-3}); do
   for v in $VARIANTS; do
     lib=spdl_amd/lib/libspdl_hipjpeg.so
     [ "$v" != base ] && lib=spdl_amd/lib/variants/libspdl_hipjpeg_$v.so
-    SPDL_AMD_LIB=$lib timeout -k 10 150 python -u bench.py --steps 80 --warmup 5 --no-cpu-baseline --oracle-check 0 $1 > gpurun_out/abr/${v}_r$r.log 2>&1 || { echo "fail $v"; exit 1; }
+    SPDL_AMD_LIB=$lib timeout -k 10 150 python -u bench.py --steps 200 --warmup 10 --no-cpu-baseline --no-queue-compare --lanes1-steps 0 --oracle-check 0 $1 > gpurun_out/abr/${v}_r$r.log 2>&1 || { echo "fail $v"; exit 1; }
   done
 done
 python - <<'PY'

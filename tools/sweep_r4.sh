@@ -3,7 +3,7 @@
 set -o pipefail
 IFS=';' read -ra CASES <<< "$SWEEP"
 for args in "${CASES[@]}"; do
-  timeout -k 10 150 python -u bench.py --steps 200 --warmup 10 --no-cpu-baseline --lanes1-steps 0 $args > gpurun_out/sw.log 2>&1 || { tail -5 gpurun_out/sw.log; exit 1; }
+  timeout -k 10 150 python -u bench.py --steps 200 --warmup 10 --no-cpu-baseline --lanes1-steps 0 --no-queue-compare $args > gpurun_out/sw.log 2>&1 || { tail -5 gpurun_out/sw.log; exit 1; }
   python -c "
 import json
 for l in open('gpurun_out/sw.log'):
