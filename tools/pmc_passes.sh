@@ -12,5 +12,5 @@ for grp in "$@"; do
   i=$((i+1))
   echo "== pmc pass $i: $grp"
   timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $grp -d "$out/pmc_$i" -o run --output-format csv \
-    -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --lanes1-steps 0 > "$out/pmc_$i.log" 2>&1 || { echo "pass $i rc=$?"; exit 1; }
+    -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-queue-compare --lanes1-steps 0 > "$out/pmc_$i.log" 2>&1 || { echo "pass $i rc=$?"; exit 1; }
 done

@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 for l in 4 1; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/ktrace_l$l" -o run --output-format csv \
-    -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --lanes1-steps 0 --lanes $l \
+    -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-queue-compare --lanes1-steps 0 --lanes $l \
     > "$out/ktrace_l$l.log" 2>&1 || { echo "kernel trace lanes $l failed"; exit 1; }
 done
 python3 tools/kernel_busy.py "$out/kernel_busy.json" \
