@@ -119,6 +119,7 @@ struct HuffTable {
   uint32_t sub[kMaxSub << kSubBits];  // second level for codes of 11..16 bits
   int32_t nsub;
   int32_t long_slow;    // codes > kLutBits without sub-tables (canonical decode)
+  int32_t sub_lo;       // the first level-1 index with a sub-table (its sub-table 0)
   int32_t maxcode[18];  // max code of length l (-1 if none), [17] sentinel
   int32_t valoff[17];
   uint8_t vals[256];

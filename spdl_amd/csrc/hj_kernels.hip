@@ -523,6 +523,7 @@ __global__ void __launch_bounds__(256) lut_kernel(const uint8_t* __restrict__ by
   if (tid == 0) {
     T.nsub = sub_ok ? nsub : 0;
     T.long_slow = sub_ok ? 0 : 1;  // long codes left to the canonical path
+    T.sub_lo = sub_ok ? p_lo : 0;
   }
   if (tid < 18) T.maxcode[tid] = maxcode[tid];
   if (tid < 17) T.valoff[tid] = valoff[tid];
@@ -853,6 +854,10 @@ struct TabMap {
   uint32_t amap;    // ... of its AC table
   uint32_t cmap;    // its component
   uint32_t bs_end;  // 3 * blocks per MCU
+  // per LDS table slot t (16 bits each): (pool base - sub_lo) * 64, so a
+  // code's second-level entry is sub[(top 16 bits + soff_t) mod pool] --
+  // computable from the bits alone, without the level-1 entry
+  uint64_t soff;
 };
 
 template <int NT>
@@ -937,7 +942,8 @@ __device__ __attribute__((noinline)) uint32_t slow_symbol(const SH& S, int t, ui
 // SLOW = false: every table's long codes are in LDS sub-tables, so a Slow
 // entry is 0 (invalid code) and the canonical fallback is not needed.
 template <bool SLOW, class SH>
-__device__ __forceinline__ uint32_t lookup(const SH& S, uint32_t t, uint32_t hi, bool is_dc) {
+__device__ __forceinline__ uint32_t lookup(const SH& S, uint32_t t, uint32_t hi, bool is_dc,
+                                           uint64_t soff) {
   if constexpr (SLOW) {
     if (t >= (uint32_t)SH::kTabs) {  // a table past the LDS slots: its HBM copy
       const HuffTable& G = S.gtab[S.gslot[t]];
@@ -950,6 +956,14 @@ __device__ __forceinline__ uint32_t lookup(const SH& S, uint32_t t, uint32_t hi,
     }
   }
   uint32_t e = S.lut[t][hi >> (32 - kLutBits)];
+  if constexpr (!SLOW) {
+    // both levels read back to back (the second address from the bits and
+    // the slot's offset, not from the first entry), one LDS latency per
+    // symbol instead of two whenever any lane of the wave has a long code
+    const uint32_t a2 = ((hi >> 16) + (uint32_t)(soff >> (16u * t))) & (uint32_t)(kSubPool - 1);
+    const uint32_t e2 = S.sub[a2];
+    return ((e >> 5) & 3) == kKindSub ? e2 : e;
+  }
   if (((e >> 5) & 3) == kKindSub)
     e = S.sub[((e >> kEntHiShift) << kSubBits) |
               ((hi >> (32 - kLutBits - kSubBits)) & ((1u << kSubBits) - 1))];
@@ -978,7 +992,7 @@ __device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
     const uint32_t t = tab_slot(m, d, z == 0u);
-    const uint32_t e = lookup<SLOW>(S, t, hi, z == 0u);
+    const uint32_t e = lookup<SLOW>(S, t, hi, z == 0u, m.soff);
     // an invalid code's entry (1) takes one bit, advances nothing and starts
     // no block
     const uint32_t nbits = e & 31u;  // code + value bits, <= 31
@@ -1002,7 +1016,7 @@ __device__ void skip_open_block(const SH& S, Dec& d, uint32_t* win, const uint32
   while (d.z != 0u && d.pos < seg_end) {
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
-    const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, false), hi, false);
+    const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, false), hi, false, m.soff);
     const uint32_t nbits = e & 31u;
     dec_skip(d, nbits);
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
@@ -1107,7 +1121,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const bool is_dc = z == 0;
     if ((is_dc & ((d.pos >= end) | (nb >= seg_end_blk))) | (d.pos > fast_end)) break;
     const uint32_t hi = dec_peek<NT>(d, win, words);
-    const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, is_dc), hi, is_dc);
+    const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, is_dc), hi, is_dc, m.soff);
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
     const uint32_t nbits = e & 31u;
     const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
@@ -1139,7 +1153,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
-    const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, is_dc), hi, is_dc);
+    const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, is_dc), hi, is_dc, m.soff);
     const bool valid = (e & 0x60u) != 0u;
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
     const uint32_t nbits = e & 31u;
@@ -1242,7 +1256,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   // table slots and components per block-in-MCU (TabMap); the DC pass
   // keeps a 2-bit component map
   uint32_t bcomp = 0;  // 2-bit component per block-in-MCU (DC pass)
-  TabMap tm{0u, 0u, 0u, 0u};
+  TabMap tm{0u, 0u, 0u, 0u, 0ull};
   {
     int slots[kMaxTabs], ns = 0, ldc[kMaxComp] = {}, lac[kMaxComp] = {};
     for (int c = 0; c < in.ncomp; c++) {
@@ -1271,6 +1285,8 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       const bool fits = (pool + nsub) << kSubBits <= kSubPool;
       const int base = pool;
       if (fits) pool += nsub;
+      if (fits && nsub > 0)
+        tm.soff |= (uint64_t)((uint32_t)((base - T.sub_lo) << kSubBits) & 0xFFFFu) << (16 * i);
       for (int k = tid; k < kLutSize; k += NT) {
         uint32_t e = T.lut[k];
         if ((e >> 5 & 3) == kKindSub) e = fits ? e + ((uint32_t)base << kEntHiShift) : 1u;
