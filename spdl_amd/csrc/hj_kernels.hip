@@ -909,6 +909,25 @@ __device__ __forceinline__ uint32_t dec_peek(Dec& d, uint32_t* win, const uint32
 
 __device__ __forceinline__ void dec_skip(Dec& d, uint32_t nbits) { d.pos += nbits; }
 
+// Three window words from the one holding d.pos, as the pairs (w0, w1) and
+// (w1, w2) (hi word first): bits [pos, pos + 64) for two symbol steps from one
+// window read.  Returns the bit offset of pos in w0.
+template <int NT>
+__device__ __forceinline__ uint32_t dec_peek3(Dec& d, uint32_t* win, const uint32_t* words,
+                                              uint64_t& p01, uint64_t& p12) {
+  uint32_t rel = d.pos - d.wbit;
+  if (__any(rel >= 32u * (kWinWords - 2))) {
+    d.wbit = d.pos & ~31u;
+    win_stage<NT>(win, words, d.pos >> 5);
+    rel = d.pos - d.wbit;
+  }
+  const uint32_t* pw = win + (kWinWords - 3 - (int)(rel >> 5)) * NT;
+  const uint32_t w2 = pw[0], w1 = pw[NT], w0 = pw[2 * NT];
+  p01 = (uint64_t)w1 | ((uint64_t)w0 << 32);
+  p12 = (uint64_t)w2 | ((uint64_t)w1 << 32);
+  return rel & 31u;
+}
+
 // the LDS table of the next symbol, and the block-in-MCU advance at a block end
 __device__ __forceinline__ uint32_t tab_slot(const TabMap& m, const Dec& d, bool is_dc) {
   return __builtin_amdgcn_ubfe(is_dc ? m.dmap : m.amap, d.bs, 3);
@@ -988,21 +1007,46 @@ __device__ int decode_state(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
   // the start): counting ends is one add per step
   int nend = 0;
   const int open0 = d.z != 0u;
+  // two symbol steps per window read (a step takes <= 31 bits, so both lie in
+  // the three words from the one holding pos): the second step's LUT read
+  // waits for the first entry only, not for another window read
   while (d.pos < end) {
-    const uint32_t hi = dec_peek<NT>(d, win, words);
-    const uint32_t z = d.z;
-    const uint32_t t = tab_slot(m, d, z == 0u);
-    const uint32_t e = lookup<SLOW>(S, t, hi, z == 0u, m.soff);
-    // an invalid code's entry (1) takes one bit, advances nothing and starts
-    // no block
-    const uint32_t nbits = e & 31u;  // code + value bits, <= 31
-    dec_skip(d, nbits);
-    const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
-    const bool bend = zn >= 64u;
-    nend += bend ? 1 : 0;
-    const uint32_t bsn = next_bs(m, d.bs);
-    d.z = bend ? 0u : zn;
-    d.bs = bend ? bsn : d.bs;
+    uint64_t p01, p12;
+    const uint32_t r = dec_peek3<NT>(d, win, words, p01, p12);
+    uint32_t nbits;
+    {
+      const uint32_t hi = (uint32_t)((p01 << r) >> 32);
+      const uint32_t z = d.z;
+      const uint32_t t = tab_slot(m, d, z == 0u);
+      const uint32_t e = lookup<SLOW>(S, t, hi, z == 0u, m.soff);
+      // an invalid code's entry (1) takes one bit, advances nothing and
+      // starts no block
+      nbits = e & 31u;  // code + value bits, <= 31
+      dec_skip(d, nbits);
+      const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
+      const bool bend = zn >= 64u;
+      nend += bend ? 1 : 0;
+      const uint32_t bsn = next_bs(m, d.bs);
+      d.z = bend ? 0u : zn;
+      d.bs = bend ? bsn : d.bs;
+    }
+    {
+      const bool more = d.pos < end;
+      const uint32_t r2 = r + nbits;  // < 63
+      const uint64_t pr = r2 < 32u ? p01 : p12;
+      const uint32_t hi = (uint32_t)((pr << (r2 & 31u)) >> 32);
+      const uint32_t z = d.z;
+      const uint32_t t = tab_slot(m, d, z == 0u);
+      const uint32_t e = lookup<SLOW>(S, t, hi, z == 0u, m.soff);
+      const uint32_t n2 = more ? (e & 31u) : 0u;
+      dec_skip(d, n2);
+      const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
+      const bool bend = more && zn >= 64u;
+      nend += bend ? 1 : 0;
+      const uint32_t bsn = next_bs(m, d.bs);
+      d.z = bend ? 0u : (more ? zn : z);
+      d.bs = bend ? bsn : d.bs;
+    }
   }
   return nend + (d.z != 0u ? 1 : 0) - open0;
 }
@@ -1116,11 +1160,11 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
   // could, before consuming it, and the careful loop continues from that
   // state.  (In the fast path a block is open exactly while z != 0.)
   const uint32_t fast_end = seg_end > 32u ? seg_end - 32u : 0u;
-  for (;;) {
+  // one fast-path step on the 32 bits `hi` at d.pos: false (nothing
+  // consumed) when the symbol could trigger a rule
+  auto fast_step = [&](const uint32_t hi) -> bool {
     const uint32_t z = d.z;
     const bool is_dc = z == 0;
-    if ((is_dc & ((d.pos >= end) | (nb >= seg_end_blk))) | (d.pos > fast_end)) break;
-    const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t e = lookup<SLOW>(S, tab_slot(m, d, is_dc), hi, is_dc, m.soff);
     const uint32_t sz = __builtin_amdgcn_ubfe(e, 7, 5);
     const uint32_t nbits = e & 31u;
@@ -1133,7 +1177,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     // also has zn > 64: only bit 31 counts).
     const uint32_t rules =
         ((64u - zn) & ((e & 0x80000u) << 12)) | ((e & 0x100060u) - 0x20u);
-    if (rules > 0x40u) break;
+    if (rules > 0x40u) return false;
     const int v = sym_value(e, hi, nbits, sz);
     dec_skip(d, nbits);
     const bool ac = coef & !is_dc;
@@ -1147,6 +1191,23 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint32_t bsn = next_bs(m, d.bs);
     d.z = bend ? 0u : zn;
     d.bs = bend ? bsn : d.bs;
+    return true;
+  };
+  auto fast_stop = [&]() -> bool {
+    const bool is_dc = d.z == 0u;
+    return (is_dc & ((d.pos >= end) | (nb >= seg_end_blk))) | (d.pos > fast_end);
+  };
+  // two steps per window read (as decode_state)
+  for (;;) {
+    if (fast_stop()) break;
+    uint64_t p01, p12;
+    const uint32_t r = dec_peek3<NT>(d, win, words, p01, p12);
+    const uint32_t pos0 = d.pos;
+    if (!fast_step((uint32_t)((p01 << r) >> 32))) break;
+    if (fast_stop()) break;
+    const uint32_t r2 = r + (d.pos - pos0);  // < 63
+    const uint64_t pr = r2 < 32u ? p01 : p12;
+    if (!fast_step((uint32_t)((pr << (r2 & 31u)) >> 32))) break;
   }
   o.open = d.z != 0u;
   while (!done && rc == kOk && !(d.z == 0u && d.pos >= end)) {
