@@ -455,13 +455,16 @@ def main():
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     pending = []
+    host_submit = 0.0  # host time inside the asynchronous submissions
     for _ in range(a.steps):
         if a.sync_steps:
             submit(True)
             for k, v in dec.last_timings().items():
                 stages[k] = stages.get(k, 0.0) + v
             continue
+        ts = time.perf_counter()
         pending.append(submit(False))
+        host_submit += time.perf_counter() - ts
         if len(pending) > a.inflight - 1:  # wait the oldest (the ring holds 10)
             collect(pending.pop(0))
     for t in pending:
@@ -647,6 +650,9 @@ def main():
                 "lanes1": lanes1,
             },
             "stages_ms": {k: round(v, 4) for k, v in stages_ms.items()},
+            # host time of one asynchronous batch submission (layout, pinned
+            # staging, launches): the device-resident path's host budget
+            "host_submit_ms": round(host_submit / a.steps * 1000.0, 4) if not a.sync_steps else None,
             "oracle_check": checked,
             "ranks": ranks,
             "cpu_baseline": cpu,
