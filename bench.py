@@ -128,6 +128,29 @@ def _kernel_busy_ms(lanes: int, stage: str) -> float | None:
     return None
 
 
+def _lib_hash() -> str | None:
+    """sha256 of the loaded decode library (the build a profile belongs to)."""
+    import hashlib
+
+    try:
+        with open(_lib.LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except (OSError, AttributeError):
+        return None
+
+
+def _profile_build_match() -> bool | None:
+    """Whether the committed profile set was taken on the library now loaded
+    (PROFILE_DIR/lib_sha256.txt, written by tools/profile_round.sh); None
+    when the profile set records no hash."""
+    try:
+        with open(os.path.join(PROFILE_DIR, "lib_sha256.txt")) as f:
+            want = f.read().split()[0]
+    except (OSError, IndexError):
+        return None
+    return want == _lib_hash()
+
+
 def _limiter(issue: dict | None, hbm_frac: float | None) -> str:
     """What bounds the dominant kernel, derived from its measured shares
     (SQ counters, tools/pmc_issue.py; HBM traffic over the kernel's time):
@@ -573,13 +596,15 @@ def main():
     if a.workload == "pad224" and a.lanes == 4:  # the configuration the PMC passes ran
         traffic = _pmc(PMC_TRAFFIC, dominant, a.batch)
         issue = _pmc(PMC_ISSUE, dominant, a.batch)
-    # `achieved` and `frac` from the kernel's average duration in the committed
-    # rocprofv3 kernel-trace summary of this configuration (rocprof_source)
-    # when one exists, else from the HIP events of this run (time_source says
-    # which); the other figure rides along.
-    kernel_ms = rocprof_ms if rocprof_ms else kernels[dominant]
+    # `achieved` and `frac` from this run's own HIP-event duration of the
+    # dominant kernel (events recorded on the lane streams the kernel runs
+    # on), so a kernel change shows in the headline fields at once.  The
+    # committed rocprofv3 summary of this configuration rides along under
+    # `profile`, with whether it was taken on this very library build.
+    kernel_ms = kernels[dominant]
     achieved = launch_bytes / (kernel_ms / 1e3) / 1e9
-    hbm_frac = (traffic["traffic_bytes"] / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS
+    prof_match = _profile_build_match()
+    hbm_frac = (traffic["traffic_bytes"] / ((rocprof_ms or kernel_ms) / 1e3) / 1e9 / HBM_PEAK_GBS
                 if traffic else None)
     busy = _kernel_busy_ms(a.lanes, dominant) if a.workload == "pad224" else None
     if rank == 0:
@@ -630,17 +655,21 @@ def main():
                 "formula": "achieved = algorithmic_bytes_per_image x launch_images / kernel_ms; "
                            "frac = achieved / peak",
                 "kernel_ms": round(kernel_ms, 4),
-                "time_source": (f"rocprofv3 average duration, {os.path.relpath(KSTATS[a.lanes], ROOT)}"
-                                if rocprof_ms else "HIP events around the kernel's launches in the "
-                                                   "timed steps (no committed rocprof summary for "
-                                                   "this configuration)"),
-                # with several lanes a launch's duration is a shared wall
-                # time (it waits for CUs the other lanes hold), so it can
-                # exceed ms_per_step; the device time per step the kernel
-                # occupies is the union of its launches' intervals per step
-                "kernel_ms_hip_events": round(kernels[dominant], 4),
-                "frac_hip_events": round(launch_bytes / (kernels[dominant] / 1e3) / 1e9
-                                         / HBM_PEAK_GBS, 6),
+                "time_source": "HIP events around the kernel's launches in the timed steps "
+                               "(this run)",
+                # the committed rocprofv3 kernel-trace average of this
+                # configuration; with several lanes a launch's duration is a
+                # shared wall time (it waits for CUs the other lanes hold), so
+                # it can exceed ms_per_step; the device time per step the
+                # kernel occupies is the union of its launches' intervals
+                "profile": {
+                    "dir": os.path.relpath(PROFILE_DIR, ROOT),
+                    "build_match": prof_match,
+                    "kernel_ms_rocprof": round(rocprof_ms, 4) if rocprof_ms else None,
+                    "frac_rocprof": (round(launch_bytes / (rocprof_ms / 1e3) / 1e9
+                                           / HBM_PEAK_GBS, 6) if rocprof_ms else None),
+                    "source": (os.path.relpath(KSTATS[a.lanes], ROOT) if rocprof_ms else None),
+                },
                 "kernel_busy_ms_per_step": busy,
                 "kernel_busy_source": (f"{os.path.relpath(BUSY, ROOT)}: union of the kernel's "
                                        f"launch intervals in the rocprofv3 kernel trace / steps"

@@ -1767,11 +1767,14 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
   if (!strcmp(name, "lane_priority")) {  // 1 low (own queue pool), 0 normal, -1 high
     if (value < -1 || value > 1) return SPDL_HJ_ERR_INVALID_ARG;
     if (value == ctx->lane_priority) return SPDL_HJ_OK;
-    // the lanes' streams are re-created at the new priority (after their work)
+    // the lanes' streams are re-created at the new priority (after their
+    // work): every stream is drained first, so a failure leaves all of them
+    // in place (none destroyed while lanes_ready still counts it)
     DeviceGuard g(ctx->device);
     for (Workspace& w : ctx->ws)
+      if (w.stream && hipStreamSynchronize(w.stream) != hipSuccess) return SPDL_HJ_ERR_HIP;
+    for (Workspace& w : ctx->ws)
       if (w.stream) {
-        if (hipStreamSynchronize(w.stream) != hipSuccess) return SPDL_HJ_ERR_HIP;
         (void)hipStreamDestroy(w.stream);
         w.stream = nullptr;
       }

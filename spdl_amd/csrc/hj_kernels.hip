@@ -1098,6 +1098,7 @@ struct BlockOut {
   uint2* bdesc;
   uint32_t cur;   // next entry
   uint32_t last;  // the image's last entry (a clamp that keeps a failed scan's stores in place)
+  uint32_t nblk;  // the image's blocks: descriptor stores past them are dropped
   uint32_t bstart;  // first entry of the open block
   int dcv;          // its DC difference
   bool open;        // a block of this run is being decoded
@@ -1120,8 +1121,11 @@ __device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e, bool put) {
 // a run's lists go back to back: the next list continues the current group,
 // so a block end stores nothing but its descriptor (the run's last, partial
 // group leaves in flush_tail)
+// (a block index past the image -- a run counting blocks in trailing garbage
+// or a failed scan -- is dropped: the next image's descriptors follow)
 __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
-  o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
+  if ((uint32_t)blk < o.nblk)
+    o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
   o.open = false;
 }
 
@@ -1159,7 +1163,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
   // -- is decoded without them.  A lane leaves at the first symbol that
   // could, before consuming it, and the careful loop continues from that
   // state.  (In the fast path a block is open exactly while z != 0.)
-  const uint32_t fast_end = seg_end > 32u ? seg_end - 32u : 0u;
+  const int nb_entry = nb;
   // one fast-path step on the 32 bits `hi` at d.pos: false (nothing
   // consumed) when the symbol could trigger a rule
   auto fast_step = [&](const uint32_t hi) -> bool {
@@ -1195,7 +1199,7 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
   };
   auto fast_stop = [&]() -> bool {
     const bool is_dc = d.z == 0u;
-    return (is_dc & ((d.pos >= end) | (nb >= seg_end_blk))) | (d.pos > fast_end);
+    return (is_dc & ((d.pos >= end) | (nb >= seg_end_blk))) | (d.pos + 32u > seg_end);
   };
   // two steps per window read (as decode_state)
   for (;;) {
@@ -1209,7 +1213,10 @@ __device__ int decode_write(const SH& S, Dec& d, uint32_t* win, const uint32_t* 
     const uint64_t pr = r2 < 32u ? p01 : p12;
     if (!fast_step((uint32_t)((pr << (r2 & 31u)) >> 32))) break;
   }
-  o.open = d.z != 0u;
+  // a block in progress is this run's only if the fast path started it (a
+  // run that entered inside the previous run's block -- skip_open_block
+  // stopped at the segment end -- owns nothing yet)
+  o.open = d.z != 0u && nb > nb_entry;
   while (!done && rc == kOk && !(d.z == 0u && d.pos >= end)) {
     const uint32_t hi = dec_peek<NT>(d, win, words);
     const uint32_t z = d.z;
@@ -1295,7 +1302,10 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   const int tid = threadIdx.x;
   // warm_param: warm-up slots; bits 16-19 = timing ablations (BatchParams
   // debug_mask >> 12: 1 skips the write and DC passes, 2 the sync rounds,
-  // 4 round 0, 8 the DC pass; outputs are wrong)
+  // 8 the DC pass; outputs are wrong.  Round 0 always runs: the sync rounds
+  // and the block scan read the slot records it writes -- a round-4 mask
+  // that skipped it left them unwritten, and the write pass then stored
+  // descriptors at garbage block indices)
   const int warm_slots = warm_param & 0xFFFF;
   const int dbg = warm_param >> 16;
   uint32_t* win = &S.win[0][tid];
@@ -1437,7 +1447,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
     };
 
     // ---- round 0: every run from a guess at its first slot ----
-    if (!(dbg & 4)) {
+    {
       Dec d;
       d.pos = 0;
       d.z = d.bs = 0;
@@ -1595,6 +1605,7 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       o.bdesc = bdesc_img;
       o.cur = (uint32_t)b0 * 64u;
       o.last = (uint32_t)nblocks * 64u - 1u;
+      o.nblk = (uint32_t)nblocks;
       o.bstart = o.cur;
       o.dcv = 0;
       o.open = false;

@@ -313,3 +313,44 @@ def _with_segment(data: bytes, marker: int, payload: bytes, before_sos: int) -> 
     for _ in range(before_sos + 1):
         pos = data.index(b"\xff\xda", pos + 1)
     return data[:pos] + seg + data[pos:]
+
+
+def _scan_span(d: bytes) -> tuple[int, int]:
+    """[start, end) of the (first) scan's entropy-coded bytes: after its SOS
+    header, up to the EOI marker."""
+    sos = d.index(b"\xff\xda")
+    start = sos + 2 + int.from_bytes(d[sos + 2 : sos + 4], "big")
+    return start, d.rindex(b"\xff\xd9")
+
+
+def trailing_scan(name: str = "q90_420", copies: int = 1) -> bytes:
+    """A sequential file whose scan is followed, before EOI, by `copies` more
+    copies of its own entropy-coded bytes: valid Huffman symbols past the
+    frame's last block, so the parallel decoder's runs there count blocks
+    beyond the image's.  The sequential decoder stops at the last block and
+    ignores them (libjpeg: extraneous data; FFmpeg likewise)."""
+    d = case(name)
+    s, e = _scan_span(d)
+    return d[:e] + d[s:e] * copies + d[e:]
+
+
+def junk_before_rst(seed: int = 0, name: str = "restart_rows", n: int = 24) -> bytes:
+    """A restart-interval file with `n` random bytes (no 0xFF) inserted before
+    every RSTn marker: garbage after each segment's last block, which the
+    sequential decoder never reads."""
+    d = case(name)
+    rng = np.random.default_rng(500 + seed)
+    s, e = _scan_span(d)
+    out = bytearray(d[:s])
+    i = s  # next byte of d to copy
+    j = s
+    while True:
+        j = d.find(b"\xff", j)
+        if j == -1 or j >= e:
+            break
+        if 0xD0 <= d[j + 1] <= 0xD7:  # RSTn: junk in front of it
+            out += d[i:j] + bytes(rng.integers(0, 255, size=n, dtype=np.uint8))
+            i = j
+        j += 2
+    out += d[i:]
+    return bytes(out)

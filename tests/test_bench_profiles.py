@@ -50,17 +50,21 @@ def test_committed_line_reproducible(bench):
     rec = _line("bench_default.json")
     r = rec["roofline"]
     assert r["kernel"] == "entropy" and r["bound"] == "hbm"
-    ms = bench._rocprof_ms(rec["config"]["lanes"], "entropy")
-    assert r["kernel_ms"] == pytest.approx(ms, abs=1e-4)
+    # headline: this run's HIP-event duration (round 5 on); round-4 lines
+    # carried the committed rocprof average there
+    ms = r["kernel_ms"]
     achieved = r["algorithmic_bytes_per_image"] * r["launch_images"] / (ms / 1e3) / 1e9
     assert r["achieved"] == pytest.approx(achieved, rel=1e-3)
     assert r["frac"] == pytest.approx(achieved / r["peak"], rel=1e-3)
+    prof_ms = bench._rocprof_ms(rec["config"]["lanes"], "entropy")
+    rocprof = r.get("profile", {}).get("kernel_ms_rocprof", r.get("kernel_ms"))
+    assert rocprof == pytest.approx(prof_ms, abs=1e-4)
     assert r["kernel_busy_ms_per_step"] == pytest.approx(
         bench._kernel_busy_ms(rec["config"]["lanes"], "entropy"), abs=1e-5)
     traffic = bench._pmc(bench.PMC_TRAFFIC, "entropy", rec["config"]["per_gpu_batch"])
     assert r["traffic"] == traffic["traffic_bytes"]
     issue = bench._pmc(bench.PMC_ISSUE, "entropy", rec["config"]["per_gpu_batch"])
-    hbm = traffic["traffic_bytes"] / (ms / 1e3) / 1e9 / bench.HBM_PEAK_GBS
+    hbm = traffic["traffic_bytes"] / (prof_ms / 1e3) / 1e9 / bench.HBM_PEAK_GBS
     assert r["limiter"] == bench._limiter(issue, hbm)
     # lanes=1 figure from the one-lane trace
     assert r["lanes1"]["kernel_ms_rocprof"] == pytest.approx(bench._rocprof_ms(1, "entropy"))
