@@ -191,6 +191,11 @@ WORKLOADS = {
                "224x224 u8 (scale bicubic decrease + centred pad, rgb24)"),
     "imagenet": ("configs[3]: synthetic 480x640 q90 4:2:0 baseline JPEG resident in HBM -> "
                  "scale 256 decrease + pad 256 + crop 224, (x/255-mean)/std fused, NCHW {dt}"),
+    "mixed": ("heterogeneous ImageNet-shaped batch resident in HBM (spdl_amd.synthetic.mixed_spec: "
+              "0.02-12 MP log-normal around 0.19 MP, 4:2:0/4:2:2/4:4:4, q60-95, 30% optimised "
+              "Huffman tables, 10% restart intervals) -> RGB 224x224 u8 pad"),
+    "big1": ("one 4000x3000 q90 4:2:0 JPEG (~4 MB) + 255 configs[1] images resident in HBM -> "
+             "RGB 224x224 u8 pad (size-adaptive entropy decode)"),
 }
 
 
@@ -229,6 +234,9 @@ def _args():
     p.add_argument("--warm-slots", type=int, default=-1,
                    help="entropy round-0 warm-up slots before each run (-1: library default)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="pad224")
+    p.add_argument("--piece-bytes", type=int, default=-1,
+                   help="entropy_piece_bytes (size-adaptive entropy decode; 0: off; -1: library "
+                        "default)")
     p.add_argument("--norm-dtype", choices=["float16", "bfloat16"], default="float16")
     p.add_argument("--inflight", type=int, default=0, choices=range(0, 11),
                    help="batches submitted ahead before waiting the oldest (0: lanes + 2; the ring holds 10)")
@@ -407,7 +415,21 @@ def main():
 
     # this rank's contiguous slice of the global batch (configs[2]: 2048 -> 8 x 256)
     sl = contiguous_shard(world * a.batch, rank, world)
-    datas = synthetic_slice(sl, distinct=a.distinct)
+    if a.workload == "mixed":
+        from spdl_amd.synthetic import mixed_jpeg
+
+        cache: dict[int, bytes] = {}
+        datas = []
+        for i in sl:  # 64 distinct images of the mixed set, cycled
+            if i % 64 not in cache:
+                cache[i % 64] = mixed_jpeg(i % 64)
+            datas.append(cache[i % 64])
+    elif a.workload == "big1":
+        from spdl_amd.synthetic import big_batch
+
+        datas = big_batch(a.batch, a.distinct)
+    else:
+        datas = synthetic_slice(sl, distinct=a.distinct)
     dev, offs, sizes, infos = _pack_device(datas, device)
     dec = _lib.Decoder(device.index)
     if a.sub_bits:
@@ -418,6 +440,8 @@ def main():
         dec.set_param("entropy_lds_pad", a.entropy_lds_pad)
     if a.warm_slots >= 0:
         dec.set_param("warmup_slots", a.warm_slots)
+    if a.piece_bytes >= 0:
+        dec.set_param("entropy_piece_bytes", a.piece_bytes)
     dec.set_param("lanes", a.lanes)  # (0: the library's choice for the queues in effect)
     a.lanes = dec.get_param("lanes")
     if a.inflight == 0:
@@ -440,7 +464,7 @@ def main():
         spec = FULLRES_SPEC
         outs = [torch.empty((a.batch, 480, 640, 3), dtype=torch.uint8, device=device)
                 for _ in range(max(3, a.inflight))]
-    else:
+    else:  # pad224, mixed, big1
         spec = OUT_SPEC
         outs = [torch.empty((a.batch, 224, 224, 3), dtype=torch.uint8, device=device)
                 for _ in range(max(3, a.inflight))]
@@ -520,6 +544,8 @@ def main():
     if a.lanes1_steps > 0 and not a.debug_mask:
         dec1 = _lib.Decoder(device.index)
         dec1.set_param("lanes", 1)
+        if a.piece_bytes >= 0:
+            dec1.set_param("entropy_piece_bytes", a.piece_bytes)
         dec1.set_profiling(True)
         acc = {}
         for i in range(a.lanes1_steps + 2):
@@ -620,7 +646,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8" if a.workload in ("pad224", "fullres") else
+            "dtype": "u8" if a.workload in ("pad224", "fullres", "mixed", "big1") else
                      {"float16": "f16", "bfloat16": "bf16"}[a.norm_dtype] + " out (int decode, f32 normalise)",
             "data": "synthetic",
             "config": {
@@ -634,6 +660,8 @@ def main():
                 "lanes": dec.get_param("lanes"),
                 "hw_queues": dec.get_param("hw_queues"),
                 "entropy_threads": dec.get_param("entropy_threads"),
+                "entropy_piece_bytes": dec.get_param("entropy_piece_bytes"),
+                "compressed_GBps": round(world * float(np.sum(sizes)) * a.steps / elapsed / 1e9, 3),
                 **({"rehearsal": f"{world} ranks sharing ONE GPU (launch-path check, not a "
                                  f"multi-GPU rate)"} if a.rehearse_one_gpu else {}),
             },

@@ -351,7 +351,9 @@ class Decoder:
         return {lib().spdl_hj_stage_name(i).decode(): buf[i] for i in range(n.value)}
 
     def decode_batch(self, datas, out: Output, out_ptr: int, out_bytes: int, stream=None,
-                     sync: bool = True) -> list[int]:
+                     sync: bool = True, check: bool = True) -> list[int]:
+        """Per-image statuses.  A failed image raises RuntimeError unless
+        ``check`` is False (synchronous calls), which returns the statuses."""
         n = len(datas)
         if n == 0:
             raise RuntimeError("Failed to decode an image. (the batch is empty)")
@@ -372,7 +374,7 @@ class Decoder:
             self._h, ptrs, sizes, n, ctypes.byref(spec), out_ptr, out_bytes,
             _stream_handle(stream), int(bool(sync)), status, err, 1024,
         )
-        if rc:
+        if rc and not (not check and sync and any(status)):
             raise RuntimeError(err.value.decode() or f"Failed to decode an image. ({rc})")
         return list(status)
 

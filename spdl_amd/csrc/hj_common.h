@@ -58,10 +58,32 @@ constexpr int kDcBias = 1024;  // FFmpeg mjpegdec last_dc start value (4 << bits
 constexpr int kMaxSlots = 2048;
 constexpr int kRecPad = 4;
 constexpr int kMaxEntropyThreads = 1024;  // largest entropy workgroup
-// N for a scan whose longest segment has `maxbits` bits (host and device
-// agree; `maxbits` <= 8 * compressed size bounds it on the host)
-inline HJ_HD uint32_t slot_bits(uint32_t maxbits, int sub_bits) {
-  uint32_t need = (maxbits + kMaxSlots - 1) / kMaxSlots;
+
+// Size-adaptive entropy decode: an image whose file holds more than the
+// context's piece size (spdl_hj_set_param "entropy_piece_bytes") is decoded
+// by P = ceil(bytes / piece) workgroups ("pieces"), at most kMaxPieces.
+//  - with restart markers: piece p takes restart segments [p nseg / P,
+//    (p + 1) nseg / P) -- independent, no hand-off;
+//  - without: the P workgroups act as one workgroup of P x NT runs over the
+//    one segment; the run-boundary states, block counts and DC sums cross
+//    pieces through per-piece records of 8-byte {tag, value} granules
+//    (EntChain) in the workspace's chain buffer, zeroed by parse_kernel.
+// Work items (image | piece << 24) are handed out by a ticket counter, so a
+// piece only ever waits for pieces of lower tickets, which are running.
+constexpr int kMaxPieces = 64;
+constexpr int kChainGranules = 16;  // per piece
+constexpr int kChainHead = 32;      // granules before the first record (the ticket counter)
+enum ChainSlot {
+  kChG0 = 0, kChG1, kChL0, kChL1, kChT,  // rec1: first run's start state, last run's end state,
+                                         // blocks started (the piece decoded from its own guess)
+  kChE0, kChE1, kChB,                    // rec2: final end state, blocks through this piece
+  kChDc = 8,                             // recDC: the piece's DC-difference sums, 4 components
+};
+enum ChainTag : uint32_t { kTagRec1 = 1, kTagRec2 = 2, kTagDc = 3, kTagFail = 0xFA11u };
+// N for a scan whose longest segment has `maxbits` bits, at most `budget`
+// slots per segment (kMaxSlots per workgroup decoding the segment)
+inline HJ_HD uint32_t slot_bits(uint32_t maxbits, int sub_bits, uint32_t budget = kMaxSlots) {
+  uint32_t need = (uint32_t)(((uint64_t)maxbits + budget - 1) / budget);
   need = (need + 31) & ~31u;
   const uint32_t n = (uint32_t)sub_bits;
   return need > n ? need : n;
@@ -166,6 +188,8 @@ struct ImageDesc {      // host-filled per image
   int32_t color;        // spdl_hj_color (host probe)
   int64_t rec_off;      // entropy symbol records: offset (u32 units) and capacity
   int64_t rec_cap;
+  int32_t pieces;       // entropy workgroups decoding this image (kMaxPieces)
+  int32_t chain_off;    // its first piece record in the chain buffer (granules)
 };
 
 // sws_kernel LDS budget per workgroup (bytes): the horizontal-pass columns of
@@ -246,6 +270,7 @@ enum Status {
   kErrTruncated = 5,
   kErrBadRestart = 6,
   kErrBadGeometry = 7,
+  kErrDevice = 9,  // SPDL_HJ_ERR_HIP: a device-side hand-off gave up (bounded wait)
 };
 
 }  // namespace hj

@@ -33,13 +33,14 @@
 
 namespace hj {
 hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageDesc*, ImageInfo*, HuffTable*,
-                        const void*, void*, int64_t, int, hipStream_t);
+                        const void*, void*, int64_t, const uint32_t*, uint32_t*, int, uint64_t*, int,
+                        hipStream_t);
 hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, DsChunk*, uint8_t*,
                           uint32_t*, int, int,
                           hipStream_t);
 hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
-                          const HuffTable*, uint32_t*, uint2*, uint32_t*, int, int, int, int, int,
-                          hipStream_t);
+                          const HuffTable*, uint32_t*, uint2*, uint32_t*, const uint32_t*, uint64_t*,
+                          int, int, int, int, int, hipStream_t);
 hipError_t launch_idct(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, uint8_t*,
                        int, int, int, hipStream_t);
 hipError_t launch_multiscan(const uint8_t*, uint8_t*, const ImageDesc*, ImageInfo*, uint32_t*, uint2*, int,
@@ -530,6 +531,10 @@ struct Layout {
   bool fuse_ok = true;      // ... with standard 4:2:0 / 4:2:2 MCUs (idct_rgb_kernel)
   int64_t cmyk_px = 0;      // 4-component images needing cmyk_kernel's K transform: max pixels
   int fused_tiles = 0;      // idct_rgb_kernel workgroups per image (max)
+  // entropy work items (image | piece << 24), the images with the most
+  // pieces first, and the granules of their hand-off records (hj_common.h)
+  std::vector<uint32_t> work;
+  int64_t chain_granules = 0;
   // a progressive (SOF2) image is in the batch: multiscan_kernel runs on a
   // side stream beside destuff + entropy (only the host-bytes entry points
   // see the headers; elsewhere it runs after entropy on the lane's stream)
@@ -537,8 +542,8 @@ struct Layout {
 };
 
 int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_image_info* infos,
-                 int n, const spdl_hj_output* out, int sub_bits, Layout& L, int32_t* status,
-                 char* err, size_t errlen, PlanCache* plans) {
+                 int n, const spdl_hj_output* out, int sub_bits, int64_t piece_bytes, Layout& L,
+                 int32_t* status, char* err, size_t errlen, PlanCache* plans) {
   L.desc.assign(n, ImageDesc{});
   // plan -> offset in L.tables.  `alive` holds every placed plan until the
   // layout is built: the cache may evict (and free) a plan mid-batch, and a
@@ -609,8 +614,17 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     d.ds_off = L.total_ds;
     L.total_ds += d.ds_cap;
     if (d.ds_cap > L.max_chunks) L.max_chunks = d.ds_cap;
-    // entropy slot state (u32 units): two uint4 per slot
-    d.rec_cap = (int64_t)kMaxSlots * 8;
+    // size-adaptive entropy decode: a file larger than piece_bytes is
+    // decoded by ceil(size / piece_bytes) workgroups (progressive and
+    // multi-scan images take multiscan_kernel: one)
+    int pieces = 1;
+    if (piece_bytes > 0 && !p.multiscan && sizes[i] > piece_bytes)
+      pieces = (int)std::min<int64_t>(kMaxPieces, (sizes[i] + piece_bytes - 1) / piece_bytes);
+    d.pieces = pieces;
+    d.chain_off = pieces > 1 ? (int32_t)L.chain_granules : 0;
+    if (pieces > 1) L.chain_granules += (int64_t)pieces * kChainGranules;
+    // entropy slot state (u32 units): kMaxSlots uint4 + slack per piece
+    d.rec_cap = (int64_t)kMaxSlots * 8 * pieces;
     d.rec_off = L.total_recs;
     L.total_recs += d.rec_cap;
     Geom g;
@@ -668,6 +682,15 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
   }
   L.out_elems_per_image = (int64_t)L.ow * L.oh * 3;
   for (int i = 0; i < n; i++) L.desc[i].out_off = (int64_t)i * L.out_elems_per_image;
+  // entropy work list: the images with the most pieces first (their pieces
+  // start early and in ticket order), each image's pieces in order
+  std::vector<int> order(n);
+  for (int i = 0; i < n; i++) order[i] = i;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return L.desc[a].pieces > L.desc[b].pieces; });
+  L.work.clear();
+  for (int i : order)
+    for (int q = 0; q < L.desc[i].pieces; q++) L.work.push_back((uint32_t)i | ((uint32_t)q << 24));
   return SPDL_HJ_OK;
 }
 
@@ -701,6 +724,7 @@ constexpr int kMaxLanes = 8;
 
 struct Workspace {
   DevBuf clean, segs, desc, info, luts, ents, bdesc, planes, wts, recs, dschunks;
+  DevBuf chain;  // entropy ticket counter + piece hand-off records (hj_common.h)
   hipEvent_t done = nullptr;      // the workspace is free after this
   hipStream_t stream = nullptr;   // lanes > 1 only
   // multiscan_kernel beside the baseline stages (batches with a progressive
@@ -751,6 +775,9 @@ struct spdl_hj_ctx {
   // workgroup size: 12 with 512+ threads, 6 with 256 (each run then spans
   // twice the slots; 4-lane A/B: 459-461k vs 450-454k img/s, r02_v5)
   int warm_slots = -1;
+  // entropy piece size: a file larger than this is decoded by several
+  // workgroups (hj_common.h kMaxPieces); 0 = one workgroup per image
+  int64_t piece_bytes = 128 * 1024;
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
   PlanCache plans;          // swscale plans per distinct geometry
 };
@@ -899,7 +926,10 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   HJ_HIP(W.clean.ensure((size_t)max_end + 512));
   HJ_HIP(W.segs.ensure((size_t)L.total_segs * 4 + 64));
   HJ_HIP(W.dschunks.ensure((size_t)L.total_ds * sizeof(DsChunk) + 64));
-  HJ_HIP(W.desc.ensure(sizeof(ImageDesc) * n));
+  const int nwork = (int)L.work.size();
+  const size_t desc_bytes = sizeof(ImageDesc) * n + sizeof(uint32_t) * nwork;  // + work list
+  HJ_HIP(W.desc.ensure(desc_bytes));
+  HJ_HIP(W.chain.ensure((size_t)(kChainHead + L.chain_granules) * 8 + 64));
   HJ_HIP(W.info.ensure(sizeof(ImageInfo) * n));
   HJ_HIP(W.luts.ensure(sizeof(HuffTable) * 8 * n));
   HJ_HIP(W.ents.ensure((size_t)L.total_blocks * 256 + 256));
@@ -907,10 +937,11 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   HJ_HIP(W.planes.ensure((size_t)L.total_planes + 256));
   HJ_HIP(W.recs.ensure((size_t)L.total_recs * 4 + 256));
   HJ_HIP(W.wts.ensure(L.tables.size() * 4 + 256));
-  HJ_HIP(slot.pin_desc.ensure(sizeof(ImageDesc) * n));
+  HJ_HIP(slot.pin_desc.ensure(desc_bytes));
   HJ_HIP(slot.pin_status.ensure(sizeof(int32_t) * n));
   slot.n = n;
   memcpy(slot.pin_desc.p, L.desc.data(), sizeof(ImageDesc) * n);
+  memcpy(static_cast<ImageDesc*>(slot.pin_desc.p) + n, L.work.data(), sizeof(uint32_t) * nwork);
   // the batch's swscale tables travel with the descriptors
   const bool swscale = !planes_only && out->csc == SPDL_HJ_CSC_SWSCALE;
   const size_t tb = swscale ? L.tables.size() * 4 : 0;
@@ -918,17 +949,22 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   if (tb) memcpy(slot.pin_tables.p, L.tables.data(), tb);
   const bool hs = ctx->host_staging != 0;
   if (!hs) {
-    HJ_HIP(hipMemcpyAsync(W.desc.p, slot.pin_desc.p, sizeof(ImageDesc) * n,
-                          hipMemcpyHostToDevice, st));
+    HJ_HIP(hipMemcpyAsync(W.desc.p, slot.pin_desc.p, desc_bytes, hipMemcpyHostToDevice, st));
     if (tb) HJ_HIP(hipMemcpyAsync(W.wts.p, slot.pin_tables.p, tb, hipMemcpyHostToDevice, st));
   }
   mark(ctx, slot, 1, st);
   auto* desc = static_cast<const ImageDesc*>(W.desc.p);
   auto* infos = static_cast<ImageInfo*>(W.info.p);
+  auto* work = reinterpret_cast<uint32_t*>(static_cast<ImageDesc*>(W.desc.p) + n);
+  auto* chain = static_cast<uint64_t*>(W.chain.p);
   HJ_HIP(launch_parse(d_bytes, hs ? static_cast<const ImageDesc*>(slot.pin_desc.dev) : nullptr,
                       static_cast<ImageDesc*>(W.desc.p), infos,
                       static_cast<HuffTable*>(W.luts.p), hs ? slot.pin_tables.dev : nullptr,
-                      W.wts.p, hs ? (int64_t)tb : 0, n, st));
+                      W.wts.p, hs ? (int64_t)tb : 0,
+                      hs ? reinterpret_cast<const uint32_t*>(
+                               static_cast<const ImageDesc*>(slot.pin_desc.dev) + n)
+                         : nullptr,
+                      work, nwork, chain, n, st));
   mark(ctx, slot, 2, st);
   const bool ms_side = L.ms_side && !(ctx->debug_mask & 0x10000) && side_streams_fit(ctx);
   if (ms_side) {
@@ -969,10 +1005,9 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<const uint32_t*>(W.segs.p), desc, infos,
                         static_cast<const HuffTable*>(W.luts.p),
                         static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
-                        static_cast<uint32_t*>(W.recs.p),
+                        static_cast<uint32_t*>(W.recs.p), work, chain,
                         ctx->sub_bits, warm | (((ctx->debug_mask >> 12) & 0xF) << 16),
-                        ent_threads,
-                        ctx->entropy_lds_pad, n, st));
+                        ent_threads, ctx->entropy_lds_pad, nwork, st));
   // progressive / non-interleaved images (the kernels above skipped them)
   // (debug_mask 0x10000 / 0x20000 / 0x40000: timing ablations that skip the
   // multiscan / IDCT / output launch; the output is wrong)
@@ -1258,7 +1293,7 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
     total += padded;
   }
   Layout L;
-  int rc = build_layout(offs.data(), szs.data(), infos.data(), n, out, ctx->sub_bits, L, status, err,
+  int rc = build_layout(offs.data(), szs.data(), infos.data(), n, out, ctx->sub_bits, ctx->piece_bytes, L, status, err,
                         errlen, &ctx->plans);
   if (rc) return rc;
   L.ms_side = prog;
@@ -1289,7 +1324,7 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
   DeviceGuard g(ctx->device);
   hipStream_t st = static_cast<hipStream_t>(stream);
   Layout L;
-  int rc = build_layout(offsets, sizes, infos, n, out, ctx->sub_bits, L, status, err, errlen,
+  int rc = build_layout(offsets, sizes, infos, n, out, ctx->sub_bits, ctx->piece_bytes, L, status, err, errlen,
                         &ctx->plans);
   if (rc) return rc;
   // the caller's probe says which files take the multi-scan path (ABI 5)
@@ -1431,7 +1466,7 @@ int spdl_hj_decode_staged(spdl_hj_ctx* ctx, int64_t ticket, size_t len, const in
     }
   }
   Layout L;
-  int rc = build_layout(offsets, sizes, infos.data(), n, out, ctx->sub_bits, L, status, err, errlen,
+  int rc = build_layout(offsets, sizes, infos.data(), n, out, ctx->sub_bits, ctx->piece_bytes, L, status, err, errlen,
                         &ctx->plans);
   if (rc) {
     s->ticket = 0;
@@ -1552,7 +1587,7 @@ int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   o.idct = idct;
   int64_t off = 0, sz = (int64_t)size, total = round_up(sz + 64, 256);
   Layout L;
-  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen, nullptr);
+  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, ctx->piece_bytes, L, nullptr, err, errlen, nullptr);
   if (rc) return rc;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
@@ -1605,7 +1640,7 @@ int spdl_hj_debug_entropy(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   spdl_hj_output o{};
   int64_t off = 0, sz = (int64_t)size, total = round_up(sz + 64, 256);
   Layout L;
-  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, L, nullptr, err, errlen, nullptr);
+  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, ctx->piece_bytes, L, nullptr, err, errlen, nullptr);
   if (rc) return rc;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
@@ -1747,6 +1782,11 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     ctx->warm_slots = (int)value;
     return SPDL_HJ_OK;
   }
+  if (!strcmp(name, "entropy_piece_bytes")) {  // size-adaptive entropy decode; 0 = off
+    if (value < 0 || (value > 0 && value < 16 * 1024)) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->piece_bytes = value;
+    return SPDL_HJ_OK;
+  }
   if (!strcmp(name, "entropy_lds_pad")) {  // bytes; > ~26 KB leaves one entropy WG per CU
     if (value < 0 || value > 64 * 1024) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->entropy_lds_pad = (int)value;
@@ -1817,6 +1857,7 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"entropy_threads", ent},
       {"warmup_slots", ctx->warm_slots >= 0 ? ctx->warm_slots : (ent <= 256 ? 6 : 12)},
       {"lanes", ctx->lanes},
+      {"entropy_piece_bytes", ctx->piece_bytes},
       {"hw_queues", ctx->hw_queues},
       // streams a batch holding a progressive image may use: one per lane, a
       // multiscan side stream per lane when the queues allow it, the copy stream

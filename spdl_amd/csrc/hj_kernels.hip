@@ -249,7 +249,10 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
                                                     ImageInfo* __restrict__ infos,
                                                     HuffTable* __restrict__ luts,
                                                     const uint4* __restrict__ host_tables,
-                                                    uint4* __restrict__ tables, int64_t ntab16) {
+                                                    uint4* __restrict__ tables, int64_t ntab16,
+                                                    const uint32_t* __restrict__ host_work,
+                                                    uint32_t* __restrict__ work, int nwork,
+                                                    uint64_t* __restrict__ chain) {
   __shared__ ParseScratch s;
   __shared__ int st;
   __shared__ __attribute__((aligned(16))) uint8_t hdr[kHdrBytes];
@@ -262,8 +265,15 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     for (int64_t i = (int64_t)img * blockDim.x + tid; i < ntab16;
          i += (int64_t)gridDim.x * blockDim.x)
       tables[i] = host_tables[i];
+    for (int i = img * blockDim.x + tid; i < nwork; i += gridDim.x * blockDim.x)
+      work[i] = host_work[i];
   }
   const ImageDesc dd = (host_desc ? host_desc : desc)[img];
+  // the entropy kernel's ticket counter and this image's piece records
+  if (img == 0 && tid == 0) chain[0] = 0ull;
+  if (dd.pieces > 1)
+    for (int i = tid; i < dd.pieces * kChainGranules; i += blockDim.x)
+      chain[kChainHead + dd.chain_off + i] = 0ull;
   {
     int* z = reinterpret_cast<int*>(&s);
     for (int i = tid; i < (int)(sizeof(ParseScratch) / 4); i += blockDim.x) z[i] = 0;
@@ -814,6 +824,11 @@ struct EntShared {
   };
   int32_t flag;
   int32_t err;
+  // the left neighbour of run 0 (a piece's first run: the previous piece's
+  // end state once known; zb 0xFFFFFFFF = none) and a piece's hand-off results
+  uint32_t left_pos, left_zb;
+  int32_t lb_ok, lb_blocks;
+  int32_t lb_dc[kMaxComp];
   // tables past the NTAB LDS slots (5-6 distinct tables, rare): read from
   // the parse kernel's HBM copy
   const HuffTable* gtab;
@@ -1287,16 +1302,149 @@ __device__ void seg_scan(SH& S, int tid, int flag, const int (&v)[kMaxComp]) {
   }
 }
 
+// ---- piece hand-off (hj_common.h EntChain): 8-byte {tag, value} granules,
+// each written by ONE agent-scope relaxed (sc1, write-through) store and read
+// by agent-scope relaxed (sc1) loads, so a granule is its own flag -- no
+// fences (MI355X_MICROARCH.md, hand-off R2).  Every wait is bounded.
+typedef __attribute__((address_space(1))) unsigned long long hj_gu64;
+__device__ __forceinline__ void gran_put(uint64_t* c, int i, uint32_t tag, uint32_t v) {
+  __hip_atomic_store((hj_gu64*)(c + i), ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t gran_get(const uint64_t* c, int i) {
+  return __hip_atomic_load((hj_gu64*)(c + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int64_t kChainWaitTicks = 20000000;  // 200 ms of wall_clock64 (100 MHz)
+
+// A piece that cannot take part (failed image, bad restart count, a hand-off
+// that gave up): every granule it would publish carries kTagFail, so the
+// pieces waiting for it stop waiting and fail the image too.
+__device__ __forceinline__ void chain_fail(uint64_t* rec, int tid) {
+  if (tid < kChainGranules) gran_put(rec, tid, kTagFail, 0u);
+}
+
+// Look-back of piece p (> 0), wave 0: the end state and block count of piece
+// p - 1 as the sequential decoder sees them.  Lane l reads piece q = p-1-l.
+// The base is the nearest piece with its final record (rec2; piece 0 posts
+// one at once); from it the fold walks up through the pieces' own records
+// (rec1) while each one's guessed start equals the state handed to it (an
+// empty piece passes the state on); a piece whose guess was wrong has to post
+// its own rec2 first.  -> S.left_pos / left_zb / lb_blocks, S.lb_ok.
+template <class SH>
+__device__ void chain_lookback(SH& S, const uint64_t* chain, int p, int lane) {
+  const uint64_t* rec = chain + (int64_t)(p - 1 - lane) * kChainGranules;
+  const bool mine = lane < p;
+  const int64_t t0 = wall_clock64();
+  for (;;) {
+    uint64_t r[8] = {};
+    if (mine) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) r[i] = gran_get(rec, i);
+    }
+    bool fail = false, has1 = mine, has2 = mine;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t tag = (uint32_t)(r[i] >> 32);
+      fail |= tag == kTagFail;
+      if (i < 5) has1 = has1 && tag == kTagRec1;
+      else has2 = has2 && tag == kTagRec2;
+    }
+    if (__any(fail)) {
+      if (lane == 0) S.lb_ok = -1;
+      return;
+    }
+    const uint64_t m2 = __ballot(has2), m1 = __ballot(has1);
+    if (m2 != 0) {
+      const int lb = __builtin_ctzll(m2);
+      const uint64_t below = (1ull << lb) - 1ull;
+      if ((m1 & below) == below) {
+        uint32_t e0 = __shfl((uint32_t)r[kChE0], lb), e1 = __shfl((uint32_t)r[kChE1], lb);
+        int32_t b = (int32_t)__shfl((uint32_t)r[kChB], lb);
+        bool ok = true;
+        for (int l = lb - 1; l >= 0; l--) {  // wave-uniform fold
+          const uint32_t g0 = __shfl((uint32_t)r[kChG0], l), g1 = __shfl((uint32_t)r[kChG1], l);
+          if (g1 == 0xFFFFFFFFu) continue;  // an empty piece
+          if (g0 != e0 || g1 != e1) {
+            ok = false;  // started from a wrong guess: wait for its final record
+            break;
+          }
+          e0 = __shfl((uint32_t)r[kChL0], l);
+          e1 = __shfl((uint32_t)r[kChL1], l);
+          b += (int32_t)__shfl((uint32_t)r[kChT], l);
+        }
+        if (ok) {
+          if (lane == 0) {
+            S.left_pos = e0;
+            S.left_zb = e1;
+            S.lb_blocks = b;
+            S.lb_ok = 1;
+          }
+          return;
+        }
+      }
+    }
+    if (wall_clock64() - t0 > kChainWaitTicks) {
+      if (lane == 0) S.lb_ok = -2;  // gave up
+      return;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
+// DC predictors entering piece p: the sum of the DC-difference sums of
+// pieces 0 .. p-1 (one restart-free segment: no resets), wave 0.
+template <class SH>
+__device__ void chain_dc(SH& S, const uint64_t* chain, int p, int lane) {
+  const uint64_t* rec = chain + (int64_t)lane * kChainGranules + kChDc;
+  const bool mine = lane < p;
+  const int64_t t0 = wall_clock64();
+  for (;;) {
+    uint64_t r[kMaxComp] = {};
+    bool fail = false, have = true;
+    if (mine) {
+#pragma unroll
+      for (int i = 0; i < kMaxComp; i++) {
+        r[i] = gran_get(rec, i);
+        const uint32_t tag = (uint32_t)(r[i] >> 32);
+        fail |= tag == kTagFail;
+        have = have && tag == kTagDc;
+      }
+    }
+    if (__any(fail)) {
+      if (lane == 0) S.lb_ok = -1;
+      return;
+    }
+    if (__all(have)) {
+#pragma unroll
+      for (int i = 0; i < kMaxComp; i++) {
+        int32_t v = (int32_t)(uint32_t)r[i];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) S.lb_dc[i] = v;
+      }
+      if (lane == 0) S.lb_ok = 1;
+      return;
+    }
+    if (wall_clock64() - t0 > kChainWaitTicks) {
+      if (lane == 0) S.lb_ok = -2;  // gave up
+      return;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
 // One image's scan, decoded by the whole workgroup.  kSlow: the scan has
 // more distinct tables than LDS slots, or long codes outside the LDS
 // sub-table pool (parse_kernel's ent_wide): lookups may go to HBM copies
 // and the canonical fallback.
+// (always inlined: as a real call the kernel takes the call ABI's register
+// budget -- 248 VGPRs and scratch instead of ~100)
 template <int NT, int NTAB, bool kSlow>
-__device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
+__device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
                               const uint8_t* __restrict__ clean, const uint32_t* __restrict__ segs,
                               const ImageDesc* __restrict__ desc, ImageInfo* __restrict__ infos,
                               const HuffTable* __restrict__ luts, uint32_t* __restrict__ ents,
                               uint2* __restrict__ bdesc, uint32_t* __restrict__ recs,
+                              uint64_t* __restrict__ chain, const int piece,
                               const int sub_bits_param,
                               const int warm_param) {
   const int tid = threadIdx.x;
@@ -1309,9 +1457,20 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   const int warm_slots = warm_param & 0xFFFF;
   const int dbg = warm_param >> 16;
   uint32_t* win = &S.win[0][tid];
-  if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc dd = desc[img];
   const ImageInfo& in = infos[img];
+  // pieces of this image (hj_common.h): crec = piece 0's hand-off record
+  const int P = max(1, dd.pieces);
+  uint64_t* crec = chain + kChainHead + dd.chain_off;
+  uint64_t* myrec = crec + (int64_t)piece * kChainGranules;
+  // (the status is read once, by one lane: another piece of this image may
+  // write it while this one starts)
+  if (tid == 0) S.flag = (in.status != kOk || in.multiscan) ? 1 : 0;
+  __syncthreads();
+  if (S.flag) {
+    if (P > 1) chain_fail(myrec, tid);
+    return;
+  }
   // The NTAB = 4 instance takes the images whose scan uses <= 4 distinct
   // tables with every long code in sub-tables that fit the LDS pool (no
   // canonical fallback in its loops); the NTAB = 6 instance takes the rest.
@@ -1383,9 +1542,20 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   }
   if (nseg_found < nseg) {
     if (tid == 0) infos[img].status = kErrBadRestart;
+    if (P > 1) chain_fail(myrec, tid);
     return;
   }
   __syncthreads();
+
+  // ---- the image's pieces: restart segments split over P workgroups, or
+  // one restart-free segment decoded as one workgroup of P x NT runs, its
+  // run states, block counts and DC sums handed across pieces ----
+  const bool chained = P > 1 && ri == 0;
+  const int seg_a = (P > 1 && !chained) ? (int)((int64_t)piece * nseg / P) : 0;
+  const int seg_b = (P > 1 && !chained) ? (int)((int64_t)(piece + 1) * nseg / P) : nseg;
+  const int pc = chained ? piece : 0;  // this workgroup's share of the run space
+  const int nruns = chained ? P * NT : NT;
+  const uint32_t budget = (uint32_t)kMaxSlots * (chained ? P : 1);
 
   auto seg_start_bits = [&](int s) -> uint32_t { return sg[s] * 8u; };
   auto seg_end_bits = [&](int s) -> uint32_t {
@@ -1406,29 +1576,31 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   }
   maxbits = (uint32_t)S.sc.red[0];
   __syncthreads();
-  const uint32_t N = slot_bits(maxbits, sub_bits_param);
-  if ((int64_t)kMaxSlots * 8 > dd.rec_cap) {  // host-sized slot state
+  const uint32_t N = slot_bits(maxbits, sub_bits_param, budget);
+  if ((int64_t)kMaxSlots * 8 * P > dd.rec_cap) {  // host-sized slot state
     if (tid == 0) infos[img].status = kErrBadGeometry;
+    if (P > 1) chain_fail(myrec, tid);
     return;
   }
   const int cmax = max(1, (int)((maxbits + N - 1) / N));
-  const int seg_per_chunk = max(1, kMaxSlots / cmax);
+  const int seg_per_chunk = max(1, (int)(budget / (uint32_t)cmax));
   uint32_t* ents_img = ents + (size_t)dd.coef_off * 64;
   uint2* bdesc_img = bdesc + dd.coef_off;
   // per-slot state, one uint4 per slot: {start pos, start z | bs << 8, blocks
   // started, end z}; each slot is only ever touched by the thread that owns it
-  uint4* sst = reinterpret_cast<uint4*>(recs + dd.rec_off);
+  uint4* sst = reinterpret_cast<uint4*>(recs + dd.rec_off) +
+              (chained ? 0 : (size_t)piece * kMaxSlots * 2);
   auto seg_first_blk = [&](int s) { return ri > 0 ? s * ri * bpm : 0; };
   auto seg_end_blk = [&](int s) { return ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks; };
   int rounds_total = 0;
   int64_t tph[4] = {0, 0, 0, 0}, dcfix = 0;
   int64_t tstamp = wall_clock64();
 
-  for (int seg_lo = 0; seg_lo < nseg; seg_lo += seg_per_chunk) {
-    const int nsc = min(seg_per_chunk, nseg - seg_lo);
+  for (int seg_lo = seg_a; seg_lo < seg_b; seg_lo += seg_per_chunk) {
+    const int nsc = min(seg_per_chunk, seg_b - seg_lo);
     const int nslots = nsc * cmax;
-    const int K = (nslots + NT - 1) / NT;
-    const int r0 = min(tid * K, nslots), r1 = min(r0 + K, nslots);
+    const int K = (nslots + nruns - 1) / nruns;
+    const int r0 = min((pc * NT + tid) * K, nslots), r1 = min(r0 + K, nslots);
     auto slot_seg = [&](int k) { return seg_lo + k / cmax; };
     auto slot_j = [&](int k) { return k % cmax; };
     auto slot_start = [&](int k) { return seg_start_bits(slot_seg(k)) + (uint32_t)slot_j(k) * N; };
@@ -1497,66 +1669,71 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       tstamp = t;
     }
     // ---- sync rounds: re-decode a run from its left neighbour's end state
-    // until the trajectory merges with the stored one at a slot boundary ----
-    int rounds = 0;
-    for (; !(dbg & 2);) {
-      if (tid == 0) S.flag = 0;
-      __syncthreads();
-      bool redo = false;
-      uint32_t npos = 0, nzb = 0;
-      if (tid > 0 && r0 < r1 && !slot_known(r0) && !slot_empty(r0)) {
-        npos = S.run_pos[tid - 1];
-        nzb = S.run_zb[tid - 1];
-        if (nzb != 0xFFFFFFFFu) {
-          const uint4 q = sst[r0];
-          redo = npos != q.x || nzb != q.y;
-        }
-      }
-      __syncthreads();
-      if (redo) {
-        Dec d;
-        dec_init<NT>(d, win, words, npos, nzb & 0xFF, nzb >> 8);
-        bool merged = false;
-        for (int k = r0; k < r1; k++) {
-          if (slot_empty(k) || slot_known(k)) {
-            merged = true;
-            break;
+    // until the trajectory merges with the stored one at a slot boundary.
+    // Run 0's left neighbour is S.left (none, except for a later piece once
+    // the previous piece's end state is known) ----
+    if (tid == 0) {
+      S.left_pos = 0;
+      S.left_zb = 0xFFFFFFFFu;
+    }
+    auto sync_rounds = [&]() -> int {
+      int rounds = 0;
+      for (; !(dbg & 2);) {
+        if (tid == 0) S.flag = 0;
+        __syncthreads();
+        bool redo = false;
+        uint32_t npos = 0, nzb = 0;
+        if ((tid > 0 || S.left_zb != 0xFFFFFFFFu) && r0 < r1 && !slot_known(r0) &&
+            !slot_empty(r0)) {
+          npos = tid > 0 ? S.run_pos[tid - 1] : S.left_pos;
+          nzb = tid > 0 ? S.run_zb[tid - 1] : S.left_zb;
+          if (nzb != 0xFFFFFFFFu) {
+            const uint4 q = sst[r0];
+            redo = npos != q.x || nzb != q.y;
           }
-          const uint32_t zb = d.z | (d.bs << 8);
-          if (k > r0) {
-            const uint4 q = sst[k];
-            if (q.x == d.pos && q.y == zb) {
+        }
+        __syncthreads();
+        if (redo) {
+          Dec d;
+          dec_init<NT>(d, win, words, npos, nzb & 0xFF, nzb >> 8);
+          bool merged = false;
+          for (int k = r0; k < r1; k++) {
+            if (slot_empty(k) || slot_known(k)) {
               merged = true;
               break;
             }
+            const uint32_t zb = d.z | (d.bs << 8);
+            if (k > r0) {
+              const uint4 q = sst[k];
+              if (q.x == d.pos && q.y == zb) {
+                merged = true;
+                break;
+              }
+            }
+            decode_k(d, k);
           }
-          decode_k(d, k);
-        }
-        if (!merged) {
-          const uint32_t zb = d.z | (d.bs << 8);
-          if (S.run_pos[tid] != d.pos || S.run_zb[tid] != zb) {
-            S.run_pos[tid] = d.pos;
-            S.run_zb[tid] = zb;
-            S.flag = 1;
+          if (!merged) {
+            const uint32_t zb = d.z | (d.bs << 8);
+            if (S.run_pos[tid] != d.pos || S.run_zb[tid] != zb) {
+              S.run_pos[tid] = d.pos;
+              S.run_zb[tid] = zb;
+              S.flag = 1;
+            }
           }
         }
+        __syncthreads();
+        const int again = S.flag;
+        rounds++;
+        __syncthreads();
+        if (!again || rounds > NT + 2) break;
       }
-      __syncthreads();
-      const int again = S.flag;
-      rounds++;
-      __syncthreads();
-      if (!again || rounds > NT + 2) break;
-    }
-    rounds_total += rounds;
-    {
-      const int64_t t = wall_clock64();
-      tph[1] += t - tstamp;
-      tstamp = t;
-    }
-
+      return rounds;
+    };
     // ---- per-run block totals, then a segmented inclusive scan over runs:
-    // the absolute block index after each run ----
-    {
+    // the block index before (nb) and after (run_end_blk) each run, and the
+    // workgroup's total ----
+    int nb = 0, run_end_blk = 0, blk_total = 0;
+    auto block_scan = [&]() {
       int flag = 0, v[kMaxComp] = {};
       for (int k = r0; k < r1; k++) {
         if (slot_empty(k)) continue;
@@ -1567,17 +1744,93 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
         v[0] += (int)sst[k].z;
       }
       seg_scan<NT, 1>(S, tid, flag, v);
+      // the scan scratch shares LDS with the bit windows: take this thread's
+      // values before anything restages windows
+      nb = tid > 0 ? S.sc.scan_v[tid - 1][0] : 0;
+      run_end_blk = S.sc.scan_v[tid][0];
+      blk_total = S.sc.scan_v[NT - 1][0];
+      __syncthreads();
+    };
+    // Chained pieces: pass 0 decodes from this piece's own guess and posts
+    // it (rec1); a later piece then looks back for the previous piece's end
+    // state and, if its first run guessed wrong, runs pass 1 from the handed
+    // state.  (One call site each for the sync rounds and the block scan: the
+    // loops are inlined once.)
+    const int busy_runs = (int)(((int64_t)nslots + K - 1) / K);  // runs holding slots
+    const int t_last = min(NT - 1, busy_runs - 1 - pc * NT);     // < 0: an empty piece
+    for (int pass = 0;; pass++) {
+      rounds_total += sync_rounds();
+      if (pass == 0) {
+        const int64_t t = wall_clock64();
+        tph[1] += t - tstamp;
+        tstamp = t;
+      }
+      block_scan();
+      if (!chained || pass > 0) break;
+      if (tid == 0) {
+        uint32_t g0 = 0u, g1 = 0xFFFFFFFFu, l0 = 0u, l1 = 0u;
+        if (t_last >= 0) {
+          const uint4 q = sst[r0];
+          g0 = q.x;
+          g1 = q.y;
+          l0 = S.run_pos[t_last];
+          l1 = S.run_zb[t_last];
+        }
+        gran_put(myrec, kChG0, kTagRec1, g0);
+        gran_put(myrec, kChG1, kTagRec1, g1);
+        gran_put(myrec, kChL0, kTagRec1, l0);
+        gran_put(myrec, kChL1, kTagRec1, l1);
+        gran_put(myrec, kChT, kTagRec1, (uint32_t)blk_total);
+        if (pc == 0) {  // the first piece starts at the segment start: final at once
+          gran_put(myrec, kChE0, kTagRec2, l0);
+          gran_put(myrec, kChE1, kTagRec2, l1);
+          gran_put(myrec, kChB, kTagRec2, (uint32_t)blk_total);
+        }
+        S.lb_ok = 1;
+        S.lb_blocks = 0;
+      }
+      if (pc == 0) break;
+      // the previous piece's end state and block count as the sequential
+      // decoder sees them
+      if (tid < 64) chain_lookback(S, crec, pc, tid);
+      __syncthreads();
+      const int ok = S.lb_ok;
+      if (ok < 0) {
+        if (tid == 0 && ok == -2) infos[img].status = kErrDevice;
+        chain_fail(myrec, tid);
+        return;
+      }
+      // run 0 started from a wrong guess: the sync rounds again from the
+      // handed state (usually a short re-decode until it merges)
+      if (tid == 0) {
+        bool wrong = false;
+        if (t_last >= 0) {
+          const uint4 q = sst[r0];
+          wrong = q.x != S.left_pos || q.y != S.left_zb;
+        }
+        S.flag = wrong ? 1 : 0;
+      }
+      __syncthreads();
+      const bool resync = S.flag != 0;
+      __syncthreads();  // (sync_rounds rewrites S.flag)
+      if (!resync) break;
+    }
+    if (chained) {
+      if (pc > 0 && tid == 0) {  // rec2: final
+        const bool empty = t_last < 0;
+        gran_put(myrec, kChE0, kTagRec2, empty ? S.left_pos : S.run_pos[t_last]);
+        gran_put(myrec, kChE1, kTagRec2, empty ? S.left_zb : S.run_zb[t_last]);
+        gran_put(myrec, kChB, kTagRec2, (uint32_t)(S.lb_blocks + blk_total));
+      }
+      __syncthreads();
+      nb += S.lb_blocks;
+      run_end_blk += S.lb_blocks;
     }
     {
       const int64_t t = wall_clock64();
       tph[2] += t - tstamp;
       tstamp = t;
     }
-    // the scan scratch shares LDS with the bit windows: take this thread's
-    // values before the write pass restages windows
-    int nb = tid > 0 ? S.sc.scan_v[tid - 1][0] : 0;
-    const int run_end_blk = S.sc.scan_v[tid][0];
-    __syncthreads();
     // This run's blocks [b0, b1): those whose DC symbol lies in the run --
     // from its first slot's segment start (or the predecessor's end) to its
     // count end, clamped to its last segment's end (symbols decoded from the
@@ -1592,6 +1845,8 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
         b1 = min(min(run_end_blk, seg_end_blk(slot_seg(r1 - 1))), nblocks);
       }
     }
+    // (timing ablations: a later piece still needs this one's DC record)
+    if ((dbg & 9) && chained && tid < kMaxComp) gran_put(myrec, kChDc + tid, kTagDc, 0u);
     if (dbg & 1) continue;
     // ---- write pass: decode each run once more from its synchronised
     // start, appending its blocks' coefficient lists; the sequential decoder's
@@ -1699,7 +1954,21 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
 #pragma unroll
         for (int i = 0; i < kMaxComp; i++) pr[i] = S.sc.scan_v[tid - 1][i];
       }
+      if (chained && tid < kMaxComp)  // this piece's DC sums (no restarts: no resets)
+        gran_put(myrec, kChDc + tid, kTagDc, (uint32_t)S.sc.scan_v[NT - 1][tid]);
       __syncthreads();
+      if (chained && pc > 0) {
+        // the predictors entering this piece: the sums of all earlier pieces
+        if (tid < 64) chain_dc(S, crec, pc, tid);
+        __syncthreads();
+        const int ok = S.lb_ok;
+        if (ok < 0) {
+          if (tid == 0 && ok == -2) infos[img].status = kErrDevice;
+          return;  // (this piece's records are all posted)
+        }
+#pragma unroll
+        for (int i = 0; i < kMaxComp; i++) pr[i] += S.lb_dc[i];
+      }
       int bs = bs0, reset = first_reset;
       for (int b = b0; b < b1; b += kG) {
         uint32_t ys[kG];
@@ -1734,8 +2003,8 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
       tstamp = t;
     }
   }
-  if (tid == 0) {
-    if (S.err != kOk && !dbg) infos[img].status = S.err;
+  if (tid == 0 && S.err != kOk && !dbg) infos[img].status = S.err;
+  if (tid == 0 && piece == 0) {
     infos[img].sync_rounds = rounds_total;
     for (int i = 0; i < 4; i++) infos[img].tphase[i] = tph[i];
     for (int i = 0; i < 4; i++) infos[img].dbg[i] = 0;
@@ -1743,10 +2012,13 @@ __device__ void entropy_image(EntShared<NT, NTAB>& S, const int img,
   }
 }
 
-// One workgroup per image (grid-stride).  The common scan (<= 4 distinct
-// tables, every long code in the LDS sub-table pool) runs the LDS-only
-// decode loops; a wide one (parse_kernel's ent_wide) the loops that may read
-// HBM table copies and the canonical fallback.  One launch serves both.
+// One workgroup per work item: an image, or a piece of a large one
+// (hj_common.h).  Items are taken in ticket order (a device-scope counter
+// that parse_kernel zeroed), so a piece waits only for pieces of lower
+// tickets, which are already running: no dependence on dispatch order.  The
+// common scan (<= 4 distinct tables, every long code in the LDS sub-table
+// pool) runs the LDS-only decode loops; a wide one (parse_kernel's ent_wide)
+// the loops that may read HBM table copies and the canonical fallback.
 template <int NT, int NTAB>
 __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
                                                      const uint32_t* __restrict__ segs,
@@ -1756,18 +2028,27 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
                                                      uint32_t* __restrict__ ents,
                                                      uint2* __restrict__ bdesc,
                                                      uint32_t* __restrict__ recs,
+                                                     const uint32_t* __restrict__ work,
+                                                     uint64_t* __restrict__ chain,
                                                      const int sub_bits_param, const int warm_slots,
-                                                     const int n) {
+                                                     const int nwork) {
   __shared__ EntShared<NT, NTAB> S;
-  for (int img = blockIdx.x; img < n; img += gridDim.x) {
-    if (infos[img].ent_wide)
-      entropy_image<NT, NTAB, true>(S, img, clean, segs, desc, infos, luts, ents, bdesc, recs,
-                                    sub_bits_param, warm_slots);
-    else
-      entropy_image<NT, NTAB, false>(S, img, clean, segs, desc, infos, luts, ents, bdesc, recs,
-                                     sub_bits_param, warm_slots);
-    __syncthreads();  // LDS is reused by the next image
+  __shared__ uint32_t item;
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t*)chain,
+                                              1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    item = t < (uint32_t)nwork ? work[t] : 0xFFFFFFFFu;
   }
+  __syncthreads();
+  const uint32_t w = item;
+  if (w == 0xFFFFFFFFu) return;
+  const int img = (int)(w & 0xFFFFFFu), piece = (int)(w >> 24);
+  if (infos[img].ent_wide)
+    entropy_image<NT, NTAB, true>(S, img, clean, segs, desc, infos, luts, ents, bdesc, recs, chain,
+                                  piece, sub_bits_param, warm_slots);
+  else
+    entropy_image<NT, NTAB, false>(S, img, clean, segs, desc, infos, luts, ents, bdesc, recs,
+                                   chain, piece, sub_bits_param, warm_slots);
 }
 
 // ---------------------------------------------------------------------------
@@ -4351,10 +4632,11 @@ __global__ void __launch_bounds__(256) cmyk_kernel(const ImageDesc* __restrict__
 
 hipError_t launch_parse(const uint8_t* bytes, const ImageDesc* host_desc, ImageDesc* desc,
                         ImageInfo* infos, HuffTable* luts, const void* host_tables, void* tables,
-                        int64_t table_bytes, int n, hipStream_t st) {
+                        int64_t table_bytes, const uint32_t* host_work, uint32_t* work, int nwork,
+                        uint64_t* chain, int n, hipStream_t st) {
   hipLaunchKernelGGL(parse_kernel, dim3(n), dim3(256), 0, st, bytes, host_desc, desc, infos, luts,
                      static_cast<const uint4*>(host_tables), static_cast<uint4*>(tables),
-                     (table_bytes + 15) / 16);
+                     (table_bytes + 15) / 16, host_work, work, nwork, chain);
   hipLaunchKernelGGL(lut_kernel, dim3(8, n), dim3(256), 0, st, bytes, desc, infos, luts);
   return hipGetLastError();
 }
@@ -4370,13 +4652,14 @@ hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo
 }
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
                           ImageInfo* infos, const HuffTable* luts, uint32_t* ents, uint2* bdesc,
-                          uint32_t* recs, int sub_bits, int warm_slots, int threads, int lds_pad, int n,
-                          hipStream_t st) {
-  // one workgroup per image; wide scans take the HBM-table loops inside
-#define HJ_ENT(T, NTAB)                                                                   \
-  hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(n), dim3(T), lds_pad, st, clean, segs, \
-                     desc, infos, luts, ents, bdesc, recs,                                  \
-                     sub_bits, warm_slots, n)
+                          uint32_t* recs, const uint32_t* work, uint64_t* chain, int sub_bits,
+                          int warm_slots, int threads, int lds_pad, int nwork, hipStream_t st) {
+  // one workgroup per work item (image or piece); wide scans take the
+  // HBM-table loops inside
+#define HJ_ENT(T, NTAB)                                                                       \
+  hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(nwork), dim3(T), lds_pad, st, clean, segs, \
+                     desc, infos, luts, ents, bdesc, recs, work, chain, sub_bits, warm_slots,    \
+                     nwork)
   if (threads == 1024) {
     HJ_ENT(1024, 4);
   } else if (threads == 512) {
