@@ -165,6 +165,10 @@ struct SwsDesc {
   int32_t col_chunk;       // output columns per workgroup
   int32_t gbr;             // three RGB planes (CMYK after the K transform), each
                            // through the luma filters (oracle sws_scale_gbr)
+  // large downscale: the horizontal pass runs once per source row in
+  // hscale_kernel (pre_rl luma / pre_rc chroma rows, row-major int16 in the
+  // workspace's hbuf) and sws_kernel stages its bands from there
+  int32_t pre, pre_rl, pre_rc;
 };
 
 struct ImageDesc {      // host-filled per image
@@ -190,6 +194,12 @@ struct ImageDesc {      // host-filled per image
   int64_t rec_cap;
   int32_t pieces;       // entropy workgroups decoding this image (kMaxPieces)
   int32_t chain_off;    // its first piece record in the chain buffer (granules)
+  // flat grids: the image's first workgroup in the destuff-chunk and IDCT
+  // launches (one entry per workgroup in the dispatch maps, parse_kernel)
+  int32_t ds_wg0, idct_wg0;
+  int32_t hs_wg0, hs_wgs;  // hscale_kernel workgroups (SwsDesc::pre images)
+  int32_t sws_wg0, sws_bands, sws_chunks;  // sws_kernel tiles: bands x column chunks
+  int64_t hbuf_off;        // their horizontal-pass rows (int16 units)
 };
 
 // sws_kernel LDS budget per workgroup (bytes): the horizontal-pass columns of
@@ -242,6 +252,13 @@ struct ImageInfo {      // device-filled by the parse kernel
 
 // destuff: chunk-parallel over kDsChunk-byte chunks; per-chunk counts and prefixes
 constexpr int kDsChunk = 4096;
+// idct_kernel: one block per thread, kIdctThreads blocks per workgroup
+#ifndef HJ_IDCT_THREADS
+#define HJ_IDCT_THREADS 256
+#endif
+constexpr int kIdctThreads = HJ_IDCT_THREADS;
+// hscale_kernel: source rows of one plane per workgroup
+constexpr int kHsRows = 16;
 struct DsChunk {
   int32_t keep, rst, term;
   int32_t keep_pre, rst_pre;

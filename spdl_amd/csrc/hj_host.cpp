@@ -33,23 +33,23 @@
 
 namespace hj {
 hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageDesc*, ImageInfo*, HuffTable*,
-                        const void*, void*, int64_t, const uint32_t*, uint32_t*, int, uint64_t*, int,
-                        hipStream_t);
+                        const void*, void*, int64_t, const uint32_t*, uint32_t*, int, uint64_t*,
+                        uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, hipStream_t);
 hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, DsChunk*, uint8_t*,
-                          uint32_t*, int, int,
-                          hipStream_t);
+                          uint32_t*, const uint32_t*, int, int, hipStream_t);
 hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
                           const HuffTable*, uint32_t*, uint2*, uint32_t*, const uint32_t*, uint64_t*,
                           int, int, int, int, int, hipStream_t);
 hipError_t launch_idct(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, uint8_t*,
-                       int, int, int, hipStream_t);
+                       int, const uint32_t*, int, hipStream_t);
 hipError_t launch_multiscan(const uint8_t*, uint8_t*, const ImageDesc*, ImageInfo*, uint32_t*, uint2*, int,
                             hipStream_t);
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                       const BatchParams&, int64_t, int, int32_t*, hipStream_t);
 hipError_t launch_nv12(const uint8_t*, uint8_t*, int, int, int, int, int, hipStream_t);
 hipError_t launch_sws(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*, void*,
-                      const BatchParams&, int, int, int, int, int32_t*, hipStream_t);
+                      const BatchParams&, const uint32_t*, int, int, int32_t*, const uint32_t*, int,
+                      int16_t*, hipStream_t);
 hipError_t launch_rgb_unscaled(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                                const BatchParams&, int64_t, int, int32_t*, hipStream_t);
 hipError_t launch_idct_rgb(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, void*,
@@ -398,10 +398,20 @@ struct PackedPlan {
 
 class PlanCache {
  public:
+  // the horizontal pass of large downscales in hscale_kernel (SwsDesc::pre):
+  // -1 when the vertical ratio is >= kPreRatio or the luma filter is longer
+  // than the kernel's register buckets (64 taps), 0 never, 1 always
+  // (spdl_hj_set_param "sws_prepass"; outputs are identical)
+  static constexpr int kPreRatio = 4;
+  void set_pre_mode(int m) {
+    if (m != pre_mode_) map_.clear();
+    pre_mode_ = m;
+  }
+  int pre_mode() const { return pre_mode_; }
   std::shared_ptr<const PackedPlan> get(const PlanKey& k, int* rc) {
     auto it = map_.find(k);
     if (it != map_.end()) return it->second;
-    auto p = build(k, rc);
+    auto p = build(k, rc, pre_mode_);
     if (!p) return nullptr;
     if (map_.size() >= 512) map_.clear();  // bounded: a stream of odd sizes replans
     map_.emplace(k, p);
@@ -416,7 +426,7 @@ class PlanCache {
     if (bytes) memcpy(blob.data() + *off, data, bytes);
   }
 
-  static std::shared_ptr<const PackedPlan> build(const PlanKey& k, int* rc) {
+  static std::shared_ptr<const PackedPlan> build(const PlanKey& k, int* rc, int pre_mode) {
     SwsPlan pl;
     // gbr: the luma plan (gray) applied to each of the three RGB planes
     *rc = sws_plan(k.w, k.h, k.hsub, k.vsub, k.mode != kPlanYuv, k.sw, k.sh, k.filter, &pl);
@@ -452,6 +462,16 @@ class PlanCache {
       put(pp->blob, &d.off[2 * i + 1], rows.data(), rows.size() * 2);
     }
     put(pp->blob, &d.off[kVmode], pl.vmode.data(), pl.vmode.size() * 4);
+    // source rows the vertical filters reach (first tap + taps, max over rows)
+    auto reach = [](const SwsAxis& a) {
+      int r = 0;
+      for (int y = 0; y < a.n; y++) r = std::max(r, a.pos[y] + a.eff);
+      return r;
+    };
+    d.pre = pre_mode > 0 ||
+            (pre_mode < 0 && !pp->special && (k.h >= kPreRatio * k.sh || pl.hl.eff > 64));
+    d.pre_rl = d.pre ? reach(pl.vl) : 0;
+    d.pre_rc = d.pre && !pl.gray ? reach(pl.vc) : 0;
     // tiling: the tallest band (and widest column chunk) whose horizontal
     // pass rows (+ 4 slack rows) and u8 output tile fit the LDS budget;
     // bands are in output rows
@@ -478,7 +498,10 @@ class PlanCache {
         // + the u8 output tile and the band's staged vertical tables
         const int64_t tile = (((int64_t)rb * chunk * 3 + 15) & ~(int64_t)15) +
                              (int64_t)rb * (16 + 2 * (d.vl_size + d.vc_size));
-        if (lds + tile <= kSwsLdsBudget || (rb == 1 && lds + tile <= 64 * 1024)) {
+        // (the launch's LDS is the batch's largest plan's: a plan over the
+        // budget slows every image's tiles; only a one-row band of a plan
+        // without the hscale pre-pass may exceed it)
+        if (lds + tile <= kSwsLdsBudget || (!d.pre && rb == 1 && lds + tile <= 64 * 1024)) {
           d.rb = rb;
           d.col_chunk = chunk;
           pp->lds = (int)(lds + tile);
@@ -496,6 +519,7 @@ class PlanCache {
   }
 
   std::map<PlanKey, std::shared_ptr<const PackedPlan>> map_;
+  int pre_mode_ = -1;
 };
 
 // chroma subsampling shifts of the yuvj4xxp frame FFmpeg's mjpeg decoder
@@ -535,6 +559,11 @@ struct Layout {
   // pieces first, and the granules of their hand-off records (hj_common.h)
   std::vector<uint32_t> work;
   int64_t chain_granules = 0;
+  // flat destuff / IDCT grids: workgroups over the whole batch
+  int64_t ds_wgs = 0, idct_wgs = 0;
+  // hscale_kernel (large downscales): workgroups and int16 rows
+  int64_t hs_wgs = 0, total_hbuf = 0;
+  int64_t sws_wgs = 0;  // sws_kernel tiles over the batch (per-image plans)
   // a progressive (SOF2) image is in the batch: multiscan_kernel runs on a
   // side stream beside destuff + entropy (only the host-bytes entry points
   // see the headers; elsewhere it runs after entropy on the lane's stream)
@@ -613,6 +642,10 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     d.ds_cap = (int32_t)(sizes[i] / kDsChunk + 2);
     d.ds_off = L.total_ds;
     L.total_ds += d.ds_cap;
+    d.ds_wg0 = (int32_t)L.ds_wgs;
+    L.ds_wgs += d.ds_cap;
+    d.idct_wg0 = (int32_t)L.idct_wgs;
+    L.idct_wgs += (nblocks + kIdctThreads - 1) / kIdctThreads;
     if (d.ds_cap > L.max_chunks) L.max_chunks = d.ds_cap;
     // size-adaptive entropy decode: a file larger than piece_bytes is
     // decoded by ceil(size / piece_bytes) workgroups (progressive and
@@ -666,6 +699,18 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     }
     d.wt_off = it->second;
     d.sws = plan->d;
+    if (plan->d.pre) {  // hscale_kernel rows: luma, then the two chroma planes
+      const SwsDesc& sd = plan->d;
+      const int wc = sd.gbr ? sd.sw : sd.chr_w, rc = sd.gbr ? sd.pre_rl : sd.pre_rc;
+      const int tl = (sd.pre_rl + kHsRows - 1) / kHsRows;
+      const bool chroma = sd.gbr || !sd.gray;  // (gbr plans are gray plans on three planes)
+      const int tc = chroma ? (rc + kHsRows - 1) / kHsRows : 0;
+      d.hs_wg0 = (int32_t)L.hs_wgs;
+      d.hs_wgs = tl + 2 * tc;
+      L.hs_wgs += d.hs_wgs;
+      d.hbuf_off = L.total_hbuf;
+      L.total_hbuf += (int64_t)sd.pre_rl * sd.sw + (chroma ? 2 * (int64_t)rc * wc : 0);
+    }
     L.all_special = L.all_special && plan->special;
     // idct_rgb_kernel's MCU shapes: Y 2x2 or 2x1, U and V 1x1
     if (p.ncomp == 3 && p.h_samp[0] == 2 && (p.v_samp[0] == 1 || p.v_samp[0] == 2) &&
@@ -678,6 +723,10 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
     }
     L.sws_bands = std::max(L.sws_bands, plan->bands);
     L.sws_chunks = std::max(L.sws_chunks, plan->chunks);
+    d.sws_wg0 = (int32_t)L.sws_wgs;  // flat sws grid: this image's tiles only
+    d.sws_bands = plan->bands;
+    d.sws_chunks = plan->chunks;
+    L.sws_wgs += (int64_t)plan->bands * plan->chunks;
     L.sws_lds = std::max(L.sws_lds, plan->lds);
   }
   L.out_elems_per_image = (int64_t)L.ow * L.oh * 3;
@@ -725,6 +774,8 @@ constexpr int kMaxLanes = 8;
 struct Workspace {
   DevBuf clean, segs, desc, info, luts, ents, bdesc, planes, wts, recs, dschunks;
   DevBuf chain;  // entropy ticket counter + piece hand-off records (hj_common.h)
+  DevBuf maps;   // flat-grid dispatch maps: destuff chunks, IDCT tiles, hscale rows -> image
+  DevBuf hbuf;   // hscale_kernel's horizontal-pass rows (large downscales)
   hipEvent_t done = nullptr;      // the workspace is free after this
   hipStream_t stream = nullptr;   // lanes > 1 only
   // multiscan_kernel beside the baseline stages (batches with a progressive
@@ -930,6 +981,12 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   const size_t desc_bytes = sizeof(ImageDesc) * n + sizeof(uint32_t) * nwork;  // + work list
   HJ_HIP(W.desc.ensure(desc_bytes));
   HJ_HIP(W.chain.ensure((size_t)(kChainHead + L.chain_granules) * 8 + 64));
+  HJ_HIP(W.maps.ensure((size_t)(L.ds_wgs + L.idct_wgs + L.hs_wgs + L.sws_wgs) * 4 + 64));
+  HJ_HIP(W.hbuf.ensure((size_t)L.total_hbuf * 2 + 64));
+  auto* ds_map = static_cast<uint32_t*>(W.maps.p);
+  auto* idct_map = ds_map + L.ds_wgs;
+  auto* hs_map = idct_map + L.idct_wgs;
+  auto* sws_map = hs_map + L.hs_wgs;
   HJ_HIP(W.info.ensure(sizeof(ImageInfo) * n));
   HJ_HIP(W.luts.ensure(sizeof(HuffTable) * 8 * n));
   HJ_HIP(W.ents.ensure((size_t)L.total_blocks * 256 + 256));
@@ -964,7 +1021,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                       hs ? reinterpret_cast<const uint32_t*>(
                                static_cast<const ImageDesc*>(slot.pin_desc.dev) + n)
                          : nullptr,
-                      work, nwork, chain, n, st));
+                      work, nwork, chain, ds_map, idct_map, hs_map, sws_map, n, st));
   mark(ctx, slot, 2, st);
   const bool ms_side = L.ms_side && !(ctx->debug_mask & 0x10000) && side_streams_fit(ctx);
   if (ms_side) {
@@ -996,7 +1053,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   }
   HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<DsChunk*>(W.dschunks.p),
                         static_cast<uint8_t*>(W.clean.p), static_cast<uint32_t*>(W.segs.p),
-                        L.max_chunks, n, st));
+                        ds_map, (int)L.ds_wgs, n, st));
   mark(ctx, slot, 3, st);
   const int ent_threads =
       ctx->entropy_threads ? ctx->entropy_threads : (ctx->lanes > 1 ? 256 : 512);
@@ -1029,7 +1086,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   if (!(ctx->debug_mask & 0x20000) && !fused)
     HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
                      static_cast<const uint2*>(W.bdesc.p), desc, infos,
-                     static_cast<uint8_t*>(W.planes.p), idct_kind, L.max_blocks, n, st));
+                     static_cast<uint8_t*>(W.planes.p), idct_kind, idct_map, (int)L.idct_wgs, st));
   // 4-component frames: FFmpeg's K transform on the planes (not on the raw
   // planes surface, which returns the IDCT output as the oracle does)
   if (!planes_only && L.cmyk_px > 0)
@@ -1075,8 +1132,9 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                                  bp, L.max_px, n, hstat, st));
     } else if (swscale) {
       HJ_HIP(launch_sws(static_cast<const uint8_t*>(W.planes.p), desc, infos,
-                        static_cast<const int32_t*>(W.wts.p), out_dev, bp, L.sws_bands,
-                        L.sws_chunks, L.sws_lds, n, hstat, st));
+                        static_cast<const int32_t*>(W.wts.p), out_dev, bp, sws_map,
+                        (int)L.sws_wgs, L.sws_lds, hstat, hs_map, (int)L.hs_wgs,
+                        static_cast<int16_t*>(W.hbuf.p), st));
     } else {
       HJ_HIP(launch_csc(static_cast<const uint8_t*>(W.planes.p), desc, infos, out_dev, bp,
                         L.max_px, n, hstat, st));
@@ -1787,6 +1845,11 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     ctx->piece_bytes = value;
     return SPDL_HJ_OK;
   }
+  if (!strcmp(name, "sws_prepass")) {  // -1 auto, 0 never, 1 always (identical outputs)
+    if (value < -1 || value > 1) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->plans.set_pre_mode((int)value);
+    return SPDL_HJ_OK;
+  }
   if (!strcmp(name, "entropy_lds_pad")) {  // bytes; > ~26 KB leaves one entropy WG per CU
     if (value < 0 || value > 64 * 1024) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->entropy_lds_pad = (int)value;
@@ -1858,6 +1921,7 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"warmup_slots", ctx->warm_slots >= 0 ? ctx->warm_slots : (ent <= 256 ? 6 : 12)},
       {"lanes", ctx->lanes},
       {"entropy_piece_bytes", ctx->piece_bytes},
+      {"sws_prepass", ctx->plans.pre_mode()},
       {"hw_queues", ctx->hw_queues},
       // streams a batch holding a progressive image may use: one per lane, a
       // multiscan side stream per lane when the queues allow it, the copy stream

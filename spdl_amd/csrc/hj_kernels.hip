@@ -252,7 +252,11 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
                                                     uint4* __restrict__ tables, int64_t ntab16,
                                                     const uint32_t* __restrict__ host_work,
                                                     uint32_t* __restrict__ work, int nwork,
-                                                    uint64_t* __restrict__ chain) {
+                                                    uint64_t* __restrict__ chain,
+                                                    uint32_t* __restrict__ ds_map,
+                                                    uint32_t* __restrict__ idct_map,
+                                                    uint32_t* __restrict__ hs_map,
+                                                    uint32_t* __restrict__ sws_map) {
   __shared__ ParseScratch s;
   __shared__ int st;
   __shared__ __attribute__((aligned(16))) uint8_t hdr[kHdrBytes];
@@ -269,6 +273,14 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
       work[i] = host_work[i];
   }
   const ImageDesc dd = (host_desc ? host_desc : desc)[img];
+  // the flat grids' dispatch maps: this image's destuff-chunk and IDCT
+  // workgroups (written whatever the status: those kernels look it up)
+  for (int i = tid; i < dd.ds_cap; i += blockDim.x) ds_map[dd.ds_wg0 + i] = (uint32_t)img;
+  for (int i = tid; i < (dd.nblocks + kIdctThreads - 1) / kIdctThreads; i += blockDim.x)
+    idct_map[dd.idct_wg0 + i] = (uint32_t)img;
+  for (int i = tid; i < dd.hs_wgs; i += blockDim.x) hs_map[dd.hs_wg0 + i] = (uint32_t)img;
+  for (int i = tid; i < dd.sws_bands * dd.sws_chunks; i += blockDim.x)
+    sws_map[dd.sws_wg0 + i] = (uint32_t)img;
   // the entropy kernel's ticket counter and this image's piece records
   if (img == 0 && tid == 0) chain[0] = 0ull;
   if (dd.pieces > 1)
@@ -646,10 +658,13 @@ __device__ __forceinline__ void ds_classify(const uint8_t* __restrict__ d, int s
 // every image at once (chunk k of image i starts at (scan_start & ~15) + 4096 k).
 __global__ void __launch_bounds__(kDsThreads) destuff_count_kernel(
     const uint8_t* __restrict__ bytes, const ImageDesc* __restrict__ desc,
-    const ImageInfo* __restrict__ infos, DsChunk* __restrict__ chunks) {
+    const ImageInfo* __restrict__ infos, DsChunk* __restrict__ chunks,
+    const uint32_t* __restrict__ ds_map) {
   __shared__ int sh[8];
   __shared__ int shterm;
-  const int img = blockIdx.y, k = blockIdx.x, tid = threadIdx.x;
+  // flat grid over every image's chunks (ds_map: workgroup -> image)
+  const int img = (int)ds_map[blockIdx.x], k = (int)blockIdx.x - desc[img].ds_wg0,
+            tid = threadIdx.x;
   if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc& dd = desc[img];
   const int size = (int)dd.in_size, start = infos[img].scan_start;
@@ -711,10 +726,11 @@ __global__ void __launch_bounds__(kDsThreads) destuff_prefix_kernel(
 __global__ void __launch_bounds__(kDsThreads) destuff_write_kernel(
     const uint8_t* __restrict__ bytes, const ImageDesc* __restrict__ desc,
     ImageInfo* __restrict__ infos, const DsChunk* __restrict__ chunks, uint8_t* __restrict__ clean,
-    uint32_t* __restrict__ segs) {
+    uint32_t* __restrict__ segs, const uint32_t* __restrict__ ds_map) {
   __shared__ int sh[8];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kDsChunk];
-  const int img = blockIdx.y, k = blockIdx.x, tid = threadIdx.x;
+  const int img = (int)ds_map[blockIdx.x], k = (int)blockIdx.x - desc[img].ds_wg0,
+            tid = threadIdx.x;
   if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc& dd = desc[img];
   const int size = (int)dd.in_size, start = infos[img].scan_start, end = infos[img].scan_end;
@@ -3592,10 +3608,6 @@ hipError_t launch_multiscan(const uint8_t* bytes, uint8_t* clean, const ImageDes
 // (a block-major layout took ~4 bank-conflict cycles per LDS instruction in
 // the scatter).  Word kBlkWords is a per-thread dummy that takes the
 // scatter's stores past the end of a list.
-#ifndef HJ_IDCT_THREADS
-#define HJ_IDCT_THREADS 256
-#endif
-constexpr int kIdctThreads = HJ_IDCT_THREADS;
 constexpr int kBlkWords = 32;
 
 // (a coefficient's int16 store into the block words: may_alias, or the
@@ -3768,13 +3780,16 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
                                                             const uint2* __restrict__ bdesc,
                                                             const ImageDesc* __restrict__ desc,
                                                             const ImageInfo* __restrict__ infos,
-                                                            uint8_t* __restrict__ planes) {
+                                                            uint8_t* __restrict__ planes,
+                                                            const uint32_t* __restrict__ idct_map) {
   __shared__ __attribute__((aligned(16))) uint32_t sblk[kBlkWords + 1][kIdctThreads];
   __shared__ uint32_t sq[kMaxComp][64];
-  const int img = blockIdx.y;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  // flat grid over every image's block tiles (idct_map: workgroup -> image)
+  const int img = (int)idct_map[blockIdx.x];
+  const int tile = (int)blockIdx.x - desc[img].idct_wg0;
+  const int j = tile * kIdctThreads + threadIdx.x;
   const ImageInfo& in = infos[img];
-  if (in.status != kOk || (int)(blockIdx.x * blockDim.x) >= in.nblocks) return;
+  if (in.status != kOk || tile * kIdctThreads >= in.nblocks) return;
   load_dequant<kIdctThreads>(sq, in, threadIdx.x);
   __syncthreads();
   if (j >= in.nblocks) return;
@@ -3959,7 +3974,7 @@ __device__ __forceinline__ int16_t h15(int32_t h) {  // hScale8To15: (sum >> 7),
 template <int NQ>
 __device__ __forceinline__ void hpass_cols(const uint8_t* plane, int stride, int ph, const int32_t* pos,
                            const int16_t* coef, int cstride, int c0, int ncols, int r0, int r1,
-                           int16_t* lds, int cst, int tid, int nthreads) {
+                           int16_t* lds, int cst, int tid, int nthreads, int rst = 1) {
   constexpr int NW = (NQ + 1 + 3) / 4 * 4;
   for (int c = tid; c < ncols; c += nthreads) {
     const int x = c0 + c;
@@ -3985,7 +4000,7 @@ __device__ __forceinline__ void hpass_cols(const uint8_t* plane, int stride, int
         if (r + g < r1) load_words<NW>(base + (int64_t)min(r + g, ph - 1) * stride, w[g]);
 #pragma unroll
       for (int g = 0; g < G; g++)
-        if (r + g < r1) out[r + g - r0] = h15(hdot<NQ>(w[g], sh, wp));
+        if (r + g < r1) out[(r + g - r0) * rst] = h15(hdot<NQ>(w[g], sh, wp));
     }
   }
 }
@@ -3993,7 +4008,8 @@ __device__ __forceinline__ void hpass_cols(const uint8_t* plane, int stride, int
 // taps beyond 64: a plain loop over the table
 __device__ __forceinline__ void hpass_cols_long(const uint8_t* plane, int stride, int ph, const int32_t* pos,
                                 const int16_t* coef, int cstride, int taps, int c0, int ncols,
-                                int r0, int r1, int16_t* lds, int cst, int tid, int nthreads) {
+                                int r0, int r1, int16_t* lds, int cst, int tid, int nthreads,
+                                int rst = 1) {
   for (int c = tid; c < ncols; c += nthreads) {
     const int x = c0 + c;
     const int p = pos[x];
@@ -4002,17 +4018,20 @@ __device__ __forceinline__ void hpass_cols_long(const uint8_t* plane, int stride
       const uint8_t* row = plane + (int64_t)min(r, ph - 1) * stride + p;
       int32_t v = 0;
       for (int t = 0; t < taps; t++) v += (int32_t)row[t] * cf[t];
-      lds[c * cst + (r - r0)] = h15(v);
+      lds[c * cst + (r - r0) * rst] = h15(v);
     }
   }
 }
 
+// (dst column c, row r at dst[c * cst + (r - r0) * rst]: column-major LDS by
+// default, row-major HBM for hscale_kernel)
 __device__ __forceinline__ void hpass(const uint8_t* plane, int stride, int ph, const int32_t* pos,
                       const int16_t* coef, int cstride, int taps, int c0, int ncols, int r0, int r1,
-                      int16_t* lds, int cst, int tid, int nthreads) {
+                      int16_t* lds, int cst, int tid, int nthreads, int rst = 1) {
   const int nq = (taps + 3) >> 2;
 #define HJ_HP(N) \
-  hpass_cols<N>(plane, stride, ph, pos, coef, cstride, c0, ncols, r0, r1, lds, cst, tid, nthreads)
+  hpass_cols<N>(plane, stride, ph, pos, coef, cstride, c0, ncols, r0, r1, lds, cst, tid, nthreads, \
+                rst)
   if (nq <= 1) HJ_HP(1);
   else if (nq <= 2) HJ_HP(2);
   else if (nq <= 3) HJ_HP(3);
@@ -4021,7 +4040,8 @@ __device__ __forceinline__ void hpass(const uint8_t* plane, int stride, int ph, 
   else if (nq <= 8) HJ_HP(8);
   else if (nq <= 12) HJ_HP(12);
   else if (nq <= 16) HJ_HP(16);
-  else hpass_cols_long(plane, stride, ph, pos, coef, cstride, taps, c0, ncols, r0, r1, lds, cst, tid, nthreads);
+  else hpass_cols_long(plane, stride, ph, pos, coef, cstride, taps, c0, ncols, r0, r1, lds, cst, tid,
+                       nthreads, rst);
 #undef HJ_HP
 }
 
@@ -4083,21 +4103,109 @@ __device__ __forceinline__ void full_rgb(const BatchParams& p, int Y, int U, int
   rgb[2] = B >> 22;
 }
 
+// hscale_kernel: swscale's horizontal pass (hScale8To15) of every source row
+// a large downscale reads, once, into a row-major int16 buffer (per image:
+// luma pre_rl x sw, then the two chroma planes pre_rc x chr_w -- gbr: three
+// planes through the luma filters).  sws_kernel then stages its bands from
+// there instead of re-filtering the rows its bands share: with a 17.9x
+// bicubic downscale (12 MP -> 224) each band's 72-tap window overlaps its
+// neighbours' 4x.  Flat grid (hs_map: workgroup -> image), kHsRows rows of
+// one plane per workgroup.  Arithmetic: hpass (oracle sws_oracle.c hscale).
+__global__ void __launch_bounds__(256) hscale_kernel(const uint8_t* __restrict__ planes,
+                                                     const ImageDesc* __restrict__ desc,
+                                                     const ImageInfo* __restrict__ infos,
+                                                     const int32_t* __restrict__ pool,
+                                                     const uint32_t* __restrict__ hs_map,
+                                                     int16_t* __restrict__ hbuf) {
+  const int img = (int)hs_map[blockIdx.x];
+  const ImageInfo& in = infos[img];
+  if (in.status != kOk) return;
+  const ImageDesc& dd = desc[img];
+  const SwsDesc& s = dd.sws;
+  const int32_t* T = pool + dd.wt_off;
+  const int tl = (s.pre_rl + kHsRows - 1) / kHsRows;  // luma tiles
+  // (a gbr plan is a gray one -- luma filters only -- applied to three planes)
+  const int tc = s.gbr ? tl : (s.gray ? 0 : (s.pre_rc + kHsRows - 1) / kHsRows);
+  int t = (int)blockIdx.x - dd.hs_wg0;
+  int c = 0;
+  if (t >= tl) {
+    t -= tl;
+    c = 1 + t / tc;
+    t %= tc;
+  }
+  const bool lumaf = c == 0 || s.gbr;  // luma filters
+  const int rows = lumaf ? s.pre_rl : s.pre_rc;
+  const int w = lumaf ? s.sw : s.chr_w;
+  const int r0 = t * kHsRows, r1 = min(r0 + kHsRows, rows);
+  const int64_t pbase = c == 0 ? 0 : (int64_t)s.pre_rl * s.sw + (c == 1 ? 0 : (int64_t)rows * w);
+  const uint8_t* plane = planes + dd.plane_off[c];
+  const int stride = dd.plane_stride[c], ph = in.comp_hpx[c];
+  const int32_t* pos = T + s.off[lumaf ? kHlPos : kHcPos];
+  const int16_t* coef = reinterpret_cast<const int16_t*>(T + s.off[lumaf ? kHlCoef : kHcCoef]);
+  const int cstride = lumaf ? s.hl_size : s.hc_size, taps = lumaf ? s.hl_taps : s.hc_taps;
+  int16_t* dst = hbuf + dd.hbuf_off + pbase + (int64_t)r0 * w;
+  if (taps <= 64) {  // the register-bucket kernels of sws_kernel's own pass
+    hpass(plane, stride, ph, pos, coef, cstride, taps, 0, w, r0, r1, dst, 1, threadIdx.x,
+          blockDim.x, w);
+    return;
+  }
+  // longer filters (downscales past ~16x): 64-tap chunks, the chunk's taps in
+  // registers, every row of the tile accumulated in registers across chunks
+  const int nch = (taps + 63) / 64;
+  for (int x = threadIdx.x; x < w; x += blockDim.x) {
+    const int p0 = pos[x];
+    const uint32_t sh = (uint32_t)(p0 & 3);
+    const uint8_t* base = plane + (p0 & ~3);
+    int32_t acc[kHsRows];
+#pragma unroll
+    for (int g = 0; g < kHsRows; g++) acc[g] = 0;
+    for (int k = 0; k < nch; k++) {
+      // taps [64k, 64k + 64): rows of the table are padded to a multiple of 4
+      // taps and the chunk past them reads zero taps of the next row's
+      // padding -- masked: a quad past `taps` is zeroed
+      uint32_t wp[32];
+      const uint2* cp = reinterpret_cast<const uint2*>(coef + (int64_t)x * cstride + 64 * k);
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const bool in_row = 64 * k + 4 * q < taps;
+        const uint2 t = in_row ? cp[q] : make_uint2(0u, 0u);
+        wp[2 * q] = t.x;
+        wp[2 * q + 1] = t.y;
+      }
+#pragma unroll
+      for (int g = 0; g < kHsRows; g++) {
+        if (r0 + g >= r1) break;
+        uint32_t wv[20];
+        load_words<20>(base + (int64_t)min(r0 + g, ph - 1) * stride + 64 * k, wv);
+        acc[g] += hdot<16>(wv, sh, wp);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < kHsRows; g++)
+      if (r0 + g < r1) dst[(int64_t)g * w + x] = h15(acc[g]);
+  }
+}
+
 __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ planes,
                                                   const ImageDesc* __restrict__ desc,
                                                   const ImageInfo* __restrict__ infos,
                                                   const int32_t* __restrict__ pool,
                                                   void* __restrict__ out, const BatchParams p,
-                                                  int32_t* __restrict__ host_status) {
+                                                  int32_t* __restrict__ host_status,
+                                                  const int16_t* __restrict__ hbuf,
+                                                  const uint32_t* __restrict__ sws_map) {
   extern __shared__ __attribute__((aligned(16))) int16_t sws_lds[];
-  const int img = blockIdx.z, tid = threadIdx.x, nt = blockDim.x;
+  // flat grid over every image's own tiles (sws_map: workgroup -> image)
+  const int img = (int)sws_map[blockIdx.x], tid = threadIdx.x, nt = blockDim.x;
+  const ImageDesc& dd = desc[img];
+  const int t = (int)blockIdx.x - dd.sws_wg0;
+  const int band = t / dd.sws_chunks, chunk = t - band * dd.sws_chunks;
   const ImageInfo& in = infos[img];
   // the image's final status, straight into the slot's pinned status array
-  if (host_status && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) host_status[img] = in.status;
+  if (host_status && t == 0 && tid == 0) host_status[img] = in.status;
   if (in.status != kOk) return;
-  const ImageDesc& dd = desc[img];
   const SwsDesc& s = dd.sws;
-  const int yo0 = (int)blockIdx.x * s.rb, xo0 = (int)blockIdx.y * s.col_chunk;
+  const int yo0 = band * s.rb, xo0 = chunk * s.col_chunk;
   if (yo0 >= dd.oh || xo0 >= dd.ow) return;
   const int yo1 = min(yo0 + s.rb, dd.oh), xo1 = min(xo0 + s.col_chunk, dd.ow);
   const int th = yo1 - yo0, tw = xo1 - xo0;
@@ -4190,7 +4298,44 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
       if (ys < 0 || ys >= s.sh || xs < 0 || xs >= s.sw) put(xo, yo, zero);
     }
   }
-  if (content && s.gbr) {
+  if (content && s.pre) {
+    // the horizontal pass was run once per source row by hscale_kernel
+    // (large downscales): copy the band's rows into the column-major LDS
+    const int16_t* hb = hbuf + dd.hbuf_off;
+    const int wl = s.sw, wc = s.gbr ? s.sw : s.chr_w;
+    const int64_t cbase = (int64_t)s.pre_rl * wl;
+    auto stage = [&](const int16_t* src, int w, int rows, int c0, int ncols, int r0, int r1,
+                     int16_t* dst, int cst_) {
+      // (4 elements per thread and step, the loads issued together)
+      const int nr = r1 - r0, ne = ncols * nr;
+      for (int i0 = tid; i0 < ne; i0 += 4 * nt) {
+        int16_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = min(i0 + u * nt, ne - 1);
+          const int r = i / ncols, c = i - r * ncols;
+          v[u] = src[(int64_t)min(r0 + r, rows - 1) * w + c0 + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = i0 + u * nt;
+          if (i < ne) {
+            const int r = i / ncols, c = i - r * ncols;
+            dst[c * cst_ + r] = v[u];
+          }
+        }
+      }
+    };
+    stage(hb, wl, s.pre_rl, xs0, ncl, lr0, lr1, hl, lst);
+    if (s.gbr) {
+      stage(hb + cbase, wl, s.pre_rl, xs0, ncl, lr0, lr1, hu, lst);
+      stage(hb + 2 * cbase, wl, s.pre_rl, xs0, ncl, lr0, lr1, hv, lst);
+    } else if (!s.gray) {
+      const int64_t cpl = (int64_t)s.pre_rc * wc;
+      stage(hb + cbase, wc, s.pre_rc, cx0, ncc, cr0, cr1, hu, cst);
+      stage(hb + cbase + cpl, wc, s.pre_rc, cx0, ncc, cr0, cr1, hv, cst);
+    }
+  } else if (content && s.gbr) {
     // three planes, a third of the threads each
     const int third = nt / 3, c = min(tid / third, 2), t3 = tid - c * third;
     if (tid < 3 * third)
@@ -4633,21 +4778,23 @@ __global__ void __launch_bounds__(256) cmyk_kernel(const ImageDesc* __restrict__
 hipError_t launch_parse(const uint8_t* bytes, const ImageDesc* host_desc, ImageDesc* desc,
                         ImageInfo* infos, HuffTable* luts, const void* host_tables, void* tables,
                         int64_t table_bytes, const uint32_t* host_work, uint32_t* work, int nwork,
-                        uint64_t* chain, int n, hipStream_t st) {
+                        uint64_t* chain, uint32_t* ds_map, uint32_t* idct_map, uint32_t* hs_map,
+                        uint32_t* sws_map, int n, hipStream_t st) {
   hipLaunchKernelGGL(parse_kernel, dim3(n), dim3(256), 0, st, bytes, host_desc, desc, infos, luts,
                      static_cast<const uint4*>(host_tables), static_cast<uint4*>(tables),
-                     (table_bytes + 15) / 16, host_work, work, nwork, chain);
+                     (table_bytes + 15) / 16, host_work, work, nwork, chain, ds_map, idct_map,
+                     hs_map, sws_map);
   hipLaunchKernelGGL(lut_kernel, dim3(8, n), dim3(256), 0, st, bytes, desc, infos, luts);
   return hipGetLastError();
 }
 hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
-                          DsChunk* chunks, uint8_t* clean, uint32_t* segs, int max_chunks, int n,
-                          hipStream_t st) {
-  hipLaunchKernelGGL(destuff_count_kernel, dim3(max_chunks, n), dim3(kDsThreads), 0, st, bytes,
-                     desc, infos, chunks);
+                          DsChunk* chunks, uint8_t* clean, uint32_t* segs, const uint32_t* ds_map,
+                          int ds_wgs, int n, hipStream_t st) {
+  hipLaunchKernelGGL(destuff_count_kernel, dim3(ds_wgs), dim3(kDsThreads), 0, st, bytes, desc,
+                     infos, chunks, ds_map);
   hipLaunchKernelGGL(destuff_prefix_kernel, dim3(n), dim3(kDsThreads), 0, st, desc, infos, chunks);
-  hipLaunchKernelGGL(destuff_write_kernel, dim3(max_chunks, n), dim3(kDsThreads), 0, st, bytes,
-                     desc, infos, chunks, clean, segs);
+  hipLaunchKernelGGL(destuff_write_kernel, dim3(ds_wgs), dim3(kDsThreads), 0, st, bytes, desc,
+                     infos, chunks, clean, segs, ds_map);
   return hipGetLastError();
 }
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
@@ -4673,18 +4820,18 @@ hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const Imag
   return hipGetLastError();
 }
 hipError_t launch_idct(const uint32_t* ents, const uint2* bdesc, const ImageDesc* desc,
-                       const ImageInfo* infos, uint8_t* planes, int idct, int max_blocks, int n,
-                       hipStream_t st) {
-  dim3 grid((max_blocks + kIdctThreads - 1) / kIdctThreads, n);
+                       const ImageInfo* infos, uint8_t* planes, int idct, const uint32_t* idct_map,
+                       int idct_wgs, hipStream_t st) {
+  const dim3 grid(idct_wgs);  // flat: every image's tiles, no empty workgroups
   if (idct == 2)  // timing ablation (debug_mask 0x800): no transform, wrong output
     hipLaunchKernelGGL(idct_kernel<2>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
-                       planes);
+                       planes, idct_map);
   else if (idct == 1)
     hipLaunchKernelGGL(idct_kernel<1>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
-                       planes);
+                       planes, idct_map);
   else
     hipLaunchKernelGGL(idct_kernel<0>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
-                       planes);
+                       planes, idct_map);
   return hipGetLastError();
 }
 hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
@@ -4757,10 +4904,14 @@ hipError_t launch_nv12(const uint8_t* src, uint8_t* dst, int frames, int height,
 }
 
 hipError_t launch_sws(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
-                      const int32_t* pool, void* out, const BatchParams& p, int bands, int chunks,
-                      int lds_bytes, int n, int32_t* host_status, hipStream_t st) {
-  hipLaunchKernelGGL(sws_kernel, dim3(bands, chunks, n), dim3(256), lds_bytes, st, planes, desc,
-                     infos, pool, out, p, host_status);
+                      const int32_t* pool, void* out, const BatchParams& p,
+                      const uint32_t* sws_map, int sws_wgs, int lds_bytes, int32_t* host_status,
+                      const uint32_t* hs_map, int hs_wgs, int16_t* hbuf, hipStream_t st) {
+  if (hs_wgs > 0)
+    hipLaunchKernelGGL(hscale_kernel, dim3(hs_wgs), dim3(256), 0, st, planes, desc, infos, pool,
+                       hs_map, hbuf);
+  hipLaunchKernelGGL(sws_kernel, dim3(sws_wgs), dim3(256), lds_bytes, st, planes, desc, infos,
+                     pool, out, p, host_status, hbuf, sws_map);
   return hipGetLastError();
 }
 hipError_t launch_cmyk(const ImageDesc* desc, const ImageInfo* infos, uint8_t* planes,

@@ -85,6 +85,27 @@ def test_resize_bit_exact(decoder, oracle, name, rk, filt):
     np.testing.assert_array_equal(hyp, ref, strict=True)
 
 
+@pytest.mark.parametrize("name", ["q90_420", "odd_227x333", "gray", "q90_444", "q90_422",
+                                  "large_1080p", "tiny_8x8", "cmyk_pillow_odd", "ycck_adobe",
+                                  "rgb_coded_odd_rst"])
+@pytest.mark.parametrize("rk", list(RESIZES))
+@pytest.mark.parametrize("filt", ["bicubic", "bilinear", "lanczos"])
+def test_resize_prepass_bit_exact(decoder, oracle, name, rk, filt):
+    """The same outputs with the horizontal pass forced into hscale_kernel
+    (sws_prepass=1: every source row filtered once into HBM, the bands
+    staged from there) -- the path large downscales take automatically."""
+    d = cases.case(name)
+    kw = RESIZES[rk]
+    ref = oracle.decode_resize(d, oracle.Resize(filter=filt, **kw), pix_fmt="rgb")
+    out = Output(pix_fmt="rgb", resize=True, filter=filt, **kw)
+    decoder.set_param("sws_prepass", 1)
+    try:
+        hyp = _decode(decoder, [d], out, ref.shape)[0].numpy()
+    finally:
+        decoder.set_param("sws_prepass", -1)
+    np.testing.assert_array_equal(hyp, ref, strict=True)
+
+
 @pytest.mark.parametrize("pix_fmt", ["rgb", "rgb24"])
 def test_normalize_fp16_bit_exact(decoder, oracle, pix_fmt):
     d = cases.case("q90_420")

@@ -135,3 +135,17 @@ def test_damaged_multi_piece_images_fail_cleanly(decoder, oracle):
         else:
             assert st[i] == 0, (i, st)
             np.testing.assert_array_equal(hyp[i], r, strict=True)
+
+
+def test_mixed_set_batch(decoder, oracle):
+    """The heterogeneous bench workload (bench.py --workload mixed: 64
+    ImageNet-shaped images, several samplings, qualities, optimised tables,
+    restart intervals; large downscales take hscale_kernel), every image
+    bit-exact at the default piece size."""
+    from spdl_amd.synthetic import mixed_jpeg
+
+    datas = [mixed_jpeg(i) for i in range(64)]
+    st, hyp = _decode224(decoder, datas, 128 * 1024, 4)
+    assert not any(st), st
+    for i, d in enumerate(datas):
+        np.testing.assert_array_equal(hyp[i], _ref224(oracle, d), strict=True, err_msg=f"image {i}")
