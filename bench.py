@@ -47,6 +47,7 @@ import torch  # noqa: E402
 from spdl_amd import _lib  # noqa: E402
 from spdl_amd._lib import Output  # noqa: E402
 from spdl_amd.distributed import (  # noqa: E402
+    bind_rank_cpus,
     barrier,
     contiguous_shard,
     init_host_group,
@@ -224,6 +225,9 @@ def _args():
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="run every rank on device 0 (a one-GPU rehearsal of the N-rank launch; "
                         "the record says so -- not a multi-GPU measurement)")
+    p.add_argument("--bind", choices=["node", "split", "none"], default="node",
+                   help="N > 1: each rank's threads on the cores of its GPU's NUMA node (node), on "
+                        "its own disjoint share of them (split), or left alone (none)")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU-only rehearsal of the multi-rank launch and timing reduction")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -412,6 +416,11 @@ def main():
         return
     device = torch.device("cuda", 0 if a.rehearse_one_gpu else local)
     torch.cuda.set_device(device)
+    bind = None
+    if world > 1 and a.bind != "none":
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        devices = [0] * lw if a.rehearse_one_gpu else list(range(lw))
+        bind = bind_rank_cpus(device.index, devices, local, a.bind)
 
     # this rank's contiguous slice of the global batch (configs[2]: 2048 -> 8 x 256)
     sl = contiguous_shard(world * a.batch, rank, world)
@@ -570,7 +579,7 @@ def main():
             "pci_bus_id": getattr(props, "pci_bus_id", None),
             "slice": [sl.start, sl.stop],
             "images_per_sec": round(a.batch * a.steps / own, 1),
-            "oracle_check": checked}
+            "oracle_check": checked, **(bind or {})}
     if world > 1:
         import torch.distributed as dist
 

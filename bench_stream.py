@@ -41,6 +41,7 @@ sys.path.insert(0, ROOT)
 
 import spdl_amd.io as sio  # noqa: E402
 from spdl_amd.distributed import (  # noqa: E402
+    bind_rank_cpus,
     barrier,
     init_host_group,
     launched_world,
@@ -62,6 +63,9 @@ def _args():
     p.add_argument("--source", choices=["file", "bytes"], default="file")
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="run every rank on device 0 (launch-path rehearsal, not a multi-GPU rate)")
+    p.add_argument("--bind", choices=["node", "split", "none"], default="node",
+                   help="N > 1: each rank's threads on the cores of its GPU's NUMA node (node), on "
+                        "its own disjoint share of them (split), or left alone (none)")
     p.add_argument("--depth", type=int, default=4,
                    help="batches in flight (= decode pipeline lanes), 1-8")
     p.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
@@ -92,10 +96,16 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     init_host_group()  # gloo: barrier + MAX of elapsed seconds only
+    lrank = local
     if a.rehearse_one_gpu:
         local = 0
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    bind = None
+    if world > 1 and a.bind != "none":
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        devices = [0] * lw if a.rehearse_one_gpu else list(range(lw))
+        bind = bind_rank_cpus(device.index, devices, lrank, a.bind)
 
     tmp = tempfile.mkdtemp(prefix=f"spdl_tar_r{rank}_")
     try:
@@ -155,7 +165,8 @@ def main():
         st.close()
         mine = {"rank": rank, "device": device.index, "images": total,
                 "pci_bus_id": getattr(torch.cuda.get_device_properties(device), "pci_bus_id", None),
-                "images_per_sec": round(total / own, 1)}
+                "images_per_sec": round(total / own, 1),
+                **(bind or {})}
         if a.sample_out and sample:
             import numpy as np
 

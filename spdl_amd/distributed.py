@@ -140,3 +140,100 @@ def reduce_sum(value: float, device=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+# ---- host-core binding per rank (configs[4]: the copy pool of each rank on
+# its GPU's NUMA node) -------------------------------------------------------
+# The reference binds its benchmark processes externally (`numactl --membind 0
+# --cpubind 0`, examples/benchmark_tarfile.py:28); here each rank binds
+# itself after choosing its device, within what the process may use.
+
+
+def _cpulist(text: str) -> set[int]:
+    """Parse a kernel cpulist ("0-3,8,10-11")."""
+    out: set[int] = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            out.update(range(int(a), int(b) + 1))
+        else:
+            out.add(int(part))
+    return out
+
+
+def device_numa(device_index: int) -> tuple[int, set[int]]:
+    """(NUMA node, local CPUs) of a GPU from its PCI address (sysfs); (-1,
+    empty) when unknown."""
+    import torch
+
+    p = torch.cuda.get_device_properties(device_index)
+    bdf = (f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
+           f"{getattr(p, 'pci_device_id', 0):02x}.0")
+    base = f"/sys/bus/pci/devices/{bdf}"
+    try:
+        with open(f"{base}/numa_node") as f:
+            node = int(f.read().strip())
+        with open(f"{base}/local_cpulist") as f:
+            cpus = _cpulist(f.read())
+    except (OSError, ValueError):
+        return -1, set()
+    return node, cpus
+
+
+def cpu_quota() -> int | None:
+    """Whole cores of the cgroup v2 CPU quota, or None when unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        return None
+
+
+def rank_cores(usable: set[int], nodes: Sequence[int], node_cpus: dict[int, set[int]],
+               local_rank: int, quota: int | None = None) -> list[int]:
+    """The cores of local rank `local_rank` among `len(nodes)` ranks of this
+    node, rank k's GPU on NUMA node nodes[k]: the ranks sharing a NUMA node
+    split the usable cores of that node (all usable cores when the node has
+    none of them) into equal disjoint runs; a CPU quota caps each rank at
+    quota / ranks cores."""
+    nranks = len(nodes)
+    mine = nodes[local_rank]
+    peers = [k for k in range(nranks) if nodes[k] == mine]
+    j = peers.index(local_rank)
+    cand = sorted(usable & node_cpus.get(mine, set())) or sorted(usable)
+    per = max(1, len(cand) // len(peers))
+    if quota is not None:
+        per = max(1, min(per, quota // nranks))
+    lo = (j * per) % max(1, len(cand))
+    return [cand[(lo + i) % len(cand)] for i in range(min(per, len(cand)))]
+
+
+def bind_rank_cpus(device_index: int, devices: Sequence[int], local_rank: int,
+                   policy: str = "node") -> dict:
+    """Pin every thread of this process to host cores near its GPU.
+    `devices[k]`: the device of local rank k.  policy "node": every usable
+    core of the GPU's NUMA node (shared by the ranks on that node); "split":
+    the rank's own disjoint share of them (rank_cores), the decoder's copy
+    pool sized to it.  Returns the record for the rank's JSON."""
+    usable = set(os.sched_getaffinity(0))
+    cache: dict[int, tuple[int, set[int]]] = {}
+    for d in set(devices):
+        cache[d] = device_numa(d)
+    nodes = [cache[d][0] for d in devices]
+    node_cpus = {cache[d][0]: cache[d][1] for d in cache}
+    if policy == "split":
+        cores = rank_cores(usable, nodes, node_cpus, local_rank, cpu_quota())
+    else:
+        cores = sorted(usable & node_cpus.get(nodes[local_rank], set())) or sorted(usable)
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            os.sched_setaffinity(int(tid), cores)
+        except OSError:
+            pass
+    if policy == "split":  # the copy pool (created on first use): a thread per core
+        os.environ["SPDL_HJ_COPY_THREADS"] = str(len(cores))
+    return {"numa_node": cache[device_index][0], "bind": policy,
+            "cpus": cores if len(cores) <= 32 else f"{len(cores)} cores {cores[0]}-{cores[-1]}"}

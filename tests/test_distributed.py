@@ -127,3 +127,31 @@ def test_spawn_ranks_fails_fast_when_a_later_rank_dies(tmp_path):
     t0 = time.perf_counter()
     assert spawn_ranks(2, [str(script)]) == 3
     assert time.perf_counter() - t0 < 60
+
+
+def test_rank_cores_split_a_numa_node():
+    from spdl_amd.distributed import rank_cores
+
+    usable = set(range(16))
+    sets = [set(rank_cores(usable, [0] * 8, {0: set(range(32))}, r)) for r in range(8)]
+    assert all(len(s) == 2 for s in sets)
+    assert len(set().union(*sets)) == 16  # disjoint, covering
+
+
+def test_rank_cores_follow_each_gpus_node_and_quota():
+    from spdl_amd.distributed import rank_cores
+
+    nodes = [0, 0, 0, 0, 1, 1, 1, 1]
+    cpus = {0: set(range(32)), 1: set(range(32, 64))}
+    sets = [rank_cores(set(range(64)), nodes, cpus, r, quota=16) for r in range(8)]
+    for r, s in enumerate(sets):
+        assert len(s) == 2 and all((c >= 32) == (nodes[r] == 1) for c in s), (r, s)
+    assert len({c for s in sets for c in s}) == 16
+    # a node with none of the usable cores: fall back to the usable set
+    assert rank_cores({1, 2}, [1], cpus, 0) == [1, 2]
+
+
+def test_cpulist_parse():
+    from spdl_amd.distributed import _cpulist
+
+    assert _cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}

@@ -49,7 +49,7 @@ def test_configs0_dataloading_1k_files_pixels(oracle, tmp_path):
 
 def test_configs2_eight_rank_launch_rehearsed(tmp_path):
     rec = _run(["bench.py", "--gpus", "8", "--batch", "256", "--rehearse-one-gpu", "--steps", "3",
-                "--warmup", "1", "--lanes1-steps", "0", "--no-cpu-baseline"], 600)
+                "--warmup", "1", "--lanes1-steps", "0", "--no-cpu-baseline", "--bind", "split"], 600)
     assert rec["n_gpus"] == 8 and rec["config"]["global_batch"] == 2048
     ranks = sorted(rec["ranks"], key=lambda r: r["rank"])
     assert [r["rank"] for r in ranks] == list(range(8))
@@ -58,6 +58,20 @@ def test_configs2_eight_rank_launch_rehearsed(tmp_path):
     for r in ranks:
         assert r["oracle_check"].endswith("bit-exact vs oracle"), r
         assert r["images_per_sec"] > 0
+    _assert_disjoint_cores(ranks)
+
+
+def _assert_disjoint_cores(ranks):
+    """Each rank bound itself to its own cores of its GPU's NUMA node
+    (spdl_amd.distributed.bind_rank_cpus), the sets pairwise disjoint when
+    the box has a core per rank."""
+    assert all(r["bind"] == "split" for r in ranks), ranks
+    sets = [set(r["cpus"]) for r in ranks]
+    assert all(sets), ranks
+    if sum(len(s) for s in sets) >= len(sets) and len(set().union(*sets)) >= len(sets):
+        for i in range(len(sets)):
+            for j in range(i + 1, len(sets)):
+                assert not (sets[i] & sets[j]), (i, j, sets)
 
 
 def test_configs4_stream_ranks_rehearsed(oracle, tmp_path):
@@ -89,8 +103,9 @@ def test_configs4_stream_eight_ranks_rehearsed(oracle, tmp_path):
     out = str(tmp_path / "stream8")
     rec = _run(["bench_stream.py", "--gpus", "8", "--rehearse-one-gpu", "--images", "512",
                 "--passes", "1", "--warmup-passes", "1", "--sample-out", out,
-                "--sample-images", "8"], 900)
+                "--sample-images", "8", "--bind", "split"], 900)
     assert rec["n_gpus"] == 8 and len(rec["ranks"]) == 8
+    _assert_disjoint_cores(rec["ranks"])
     datas = synthetic_batch(512, distinct=32)
     rs = oracle.Resize(**PAD224)
     refs = {}
