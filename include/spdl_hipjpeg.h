@@ -299,7 +299,13 @@ const char* spdl_hj_stage_name(int32_t i);
  * read from GPU_MAX_HW_QUEUES at spdl_hj_create, default 4; set it when HIP
  * initialised with another value), "output_path" (0 = by
  * batch, 1 = the generic swscale kernel, 2 = separate IDCT + unscaled
- * converter at full resolution: byte-identical outputs, for A/B and tests).
+ * converter at full resolution: byte-identical outputs, for A/B and tests),
+ * "entropy_piece_bytes" (size-adaptive Huffman decode: a file larger than
+ * this is decoded by ceil(size / value) workgroups, at most 64; default
+ * 131072, 0 = one workgroup per image; since ABI 5 round 5), "sws_prepass"
+ * (-1 = automatic: the horizontal scaling pass of a downscale by >= 4x or
+ * with a > 64-tap filter runs once per source row in its own kernel; 0 =
+ * never, 1 = always; byte-identical outputs).
  * Builds with -DHJ_ABLATIONS=1 also take "debug_mask" (timing ablations that
  * skip kernel phases; outputs wrong); release builds reject it. */
 int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value);
