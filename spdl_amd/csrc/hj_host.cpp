@@ -408,10 +408,17 @@ class PlanCache {
     pre_mode_ = m;
   }
   int pre_mode() const { return pre_mode_; }
+  // widest column chunk a tile may take (16-256; the tiler then picks the
+  // tallest band that fits the LDS budget)
+  void set_max_cols(int c) {
+    if (c != max_cols_) map_.clear();
+    max_cols_ = c;
+  }
+  int max_cols() const { return max_cols_; }
   std::shared_ptr<const PackedPlan> get(const PlanKey& k, int* rc) {
     auto it = map_.find(k);
     if (it != map_.end()) return it->second;
-    auto p = build(k, rc, pre_mode_);
+    auto p = build(k, rc, pre_mode_, max_cols_);
     if (!p) return nullptr;
     if (map_.size() >= 512) map_.clear();  // bounded: a stream of odd sizes replans
     map_.emplace(k, p);
@@ -426,7 +433,8 @@ class PlanCache {
     if (bytes) memcpy(blob.data() + *off, data, bytes);
   }
 
-  static std::shared_ptr<const PackedPlan> build(const PlanKey& k, int* rc, int pre_mode) {
+  static std::shared_ptr<const PackedPlan> build(const PlanKey& k, int* rc, int pre_mode,
+                                                 int max_cols) {
     SwsPlan pl;
     // gbr: the luma plan (gray) applied to each of the three RGB planes
     *rc = sws_plan(k.w, k.h, k.hsub, k.vsub, k.mode != kPlanYuv, k.sw, k.sh, k.filter, &pl);
@@ -475,7 +483,7 @@ class PlanCache {
     // tiling: the tallest band (and widest column chunk) whose horizontal
     // pass rows (+ 4 slack rows) and u8 output tile fit the LDS budget;
     // bands are in output rows
-    for (int cols = kSwsMaxCols; cols >= 16 && !pp->bands; cols /= 2) {
+    for (int cols = std::min(max_cols, kSwsMaxCols); cols >= 16 && !pp->bands; cols /= 2) {
       const int chunk = k.ow < cols ? k.ow : cols;
       static const int kRb[] = {32, 24, 16, 12, 8, 6, 4, 3, 2, 1};
       for (int rb : kRb) {
@@ -520,6 +528,7 @@ class PlanCache {
 
   std::map<PlanKey, std::shared_ptr<const PackedPlan>> map_;
   int pre_mode_ = -1;
+  int max_cols_ = kSwsMaxCols;
 };
 
 // chroma subsampling shifts of the yuvj4xxp frame FFmpeg's mjpeg decoder
@@ -829,6 +838,8 @@ struct spdl_hj_ctx {
   // entropy piece size: a file larger than this is decoded by several
   // workgroups (hj_common.h kMaxPieces); 0 = one workgroup per image
   int64_t piece_bytes = 128 * 1024;
+  // s_setprio of the entropy waves (0-3; A/B knob)
+  int entropy_prio = 0;
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
   PlanCache plans;          // swscale plans per distinct geometry
 };
@@ -1063,7 +1074,8 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<const HuffTable*>(W.luts.p),
                         static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
                         static_cast<uint32_t*>(W.recs.p), work, chain,
-                        ctx->sub_bits, warm | (((ctx->debug_mask >> 12) & 0xF) << 16),
+                        ctx->sub_bits,
+                        warm | (((ctx->debug_mask >> 12) & 0xF) << 16) | (ctx->entropy_prio << 24),
                         ent_threads, ctx->entropy_lds_pad, nwork, st));
   // progressive / non-interleaved images (the kernels above skipped them)
   // (debug_mask 0x10000 / 0x20000 / 0x40000: timing ablations that skip the
@@ -1845,6 +1857,16 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     ctx->piece_bytes = value;
     return SPDL_HJ_OK;
   }
+  if (!strcmp(name, "entropy_prio")) {
+    if (value < 0 || value > 3) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->entropy_prio = (int)value;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "sws_cols")) {  // widest swscale tile (16-256 columns; A/B knob)
+    if (value < 16 || value > kSwsMaxCols) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->plans.set_max_cols((int)value);
+    return SPDL_HJ_OK;
+  }
   if (!strcmp(name, "sws_prepass")) {  // -1 auto, 0 never, 1 always (identical outputs)
     if (value < -1 || value > 1) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->plans.set_pre_mode((int)value);
@@ -1922,6 +1944,8 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"lanes", ctx->lanes},
       {"entropy_piece_bytes", ctx->piece_bytes},
       {"sws_prepass", ctx->plans.pre_mode()},
+      {"entropy_prio", ctx->entropy_prio},
+      {"sws_cols", ctx->plans.max_cols()},
       {"hw_queues", ctx->hw_queues},
       // streams a batch holding a progressive image may use: one per lane, a
       // multiscan side stream per lane when the queues allow it, the copy stream

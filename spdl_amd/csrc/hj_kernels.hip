@@ -1471,7 +1471,7 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
   // that skipped it left them unwritten, and the write pass then stored
   // descriptors at garbage block indices)
   const int warm_slots = warm_param & 0xFFFF;
-  const int dbg = warm_param >> 16;
+  const int dbg = (warm_param >> 16) & 0xFF;
   uint32_t* win = &S.win[0][tid];
   const ImageDesc dd = desc[img];
   const ImageInfo& in = infos[img];
@@ -2050,6 +2050,12 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
                                                      const int nwork) {
   __shared__ EntShared<NT, NTAB> S;
   __shared__ uint32_t item;
+  // warm_slots bits 24+: wave priority (s_setprio) of the entropy waves
+  // (an A/B knob: flat at four lanes, r05 profiles/r05/ab_entropy_prio.txt)
+  const int prio = (warm_slots >> 24) & 3;
+  if (prio == 3) __builtin_amdgcn_s_setprio(3);
+  else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (prio == 1) __builtin_amdgcn_s_setprio(1);
   if (threadIdx.x == 0) {
     const uint32_t t = __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t*)chain,
                                               1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
