@@ -1075,7 +1075,10 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
                         static_cast<uint32_t*>(W.recs.p), work, chain,
                         ctx->sub_bits,
-                        warm | (((ctx->debug_mask >> 12) & 0xF) << 16) | (ctx->entropy_prio << 24),
+                        warm |
+                            ((((ctx->debug_mask >> 12) & 0xF) | (((ctx->debug_mask >> 19) & 1) << 4))
+                             << 16) |
+                            (ctx->entropy_prio << 24),
                         ent_threads, ctx->entropy_lds_pad, nwork, st));
   // progressive / non-interleaved images (the kernels above skipped them)
   // (debug_mask 0x10000 / 0x20000 / 0x40000: timing ablations that skip the

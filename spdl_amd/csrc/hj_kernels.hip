@@ -1134,6 +1134,9 @@ struct BlockOut {
   int dcv;          // its DC difference
   bool open;        // a block of this run is being decoded
   uint32_t pk[4];   // the last four entries (a shift register: pk[3] the newest)
+#if HJ_ABLATIONS
+  bool no_list, no_desc;  // store-site ablations (write-traffic accounting)
+#endif
 };
 
 // entry e at o.cur when `put` (the caller advances o.cur): shifted into pk,
@@ -1143,6 +1146,9 @@ __device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e, bool put) {
   o.pk[1] = put ? o.pk[2] : o.pk[1];
   o.pk[2] = put ? o.pk[3] : o.pk[2];
   o.pk[3] = put ? e : o.pk[3];
+#if HJ_ABLATIONS
+  if (o.no_list) return;
+#endif
   if (put && (o.cur & 3u) == 3u) {
     const uint32_t base = min(o.cur & ~3u, o.last & ~3u);
     *reinterpret_cast<uint4*>(o.ents + base) = make_uint4(o.pk[0], o.pk[1], o.pk[2], o.pk[3]);
@@ -1155,6 +1161,9 @@ __device__ __forceinline__ void put_entry(BlockOut& o, uint32_t e, bool put) {
 // (a block index past the image -- a run counting blocks in trailing garbage
 // or a failed scan -- is dropped: the next image's descriptors follow)
 __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
+#if HJ_ABLATIONS
+  if (o.no_desc) blk = -1;
+#endif
   if ((uint32_t)blk < o.nblk)
     o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
   o.open = false;
@@ -1164,6 +1173,9 @@ __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
 __device__ __forceinline__ void flush_tail(BlockOut& o) {
   const uint32_t r = o.cur & 3u;
   if (r == 0u) return;
+#if HJ_ABLATIONS
+  if (o.no_list) return;
+#endif
   const uint32_t base = min(o.cur & ~3u, o.last & ~3u);
   // (masks, not selects: a select chain over pk becomes a dynamic index
   // and puts the BlockOut in scratch)
@@ -1466,7 +1478,8 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
   const int tid = threadIdx.x;
   // warm_param: warm-up slots; bits 16-19 = timing ablations (BatchParams
   // debug_mask >> 12: 1 skips the write and DC passes, 2 the sync rounds,
-  // 8 the DC pass; outputs are wrong.  Round 0 always runs: the sync rounds
+  // 8 the DC pass, 4 the list stores, 16 (debug_mask 0x80000) the write
+  // pass's descriptor stores; outputs are wrong.  Round 0 always runs: the sync rounds
   // and the block scan read the slot records it writes -- a round-4 mask
   // that skipped it left them unwritten, and the write pass then stored
   // descriptors at garbage block indices)
@@ -1877,6 +1890,10 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
       o.cur = (uint32_t)b0 * 64u;
       o.last = (uint32_t)nblocks * 64u - 1u;
       o.nblk = (uint32_t)nblocks;
+#if HJ_ABLATIONS
+      o.no_list = (dbg & 4) != 0;
+      o.no_desc = (dbg & 16) != 0;
+#endif
       o.bstart = o.cur;
       o.dcv = 0;
       o.open = false;
