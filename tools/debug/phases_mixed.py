@@ -12,6 +12,8 @@ from spdl_amd.synthetic import mixed_jpeg, mixed_spec  # noqa: E402
 threads = int(os.environ.get("PH_THREADS", "512"))
 dec = Decoder(0)
 dec.set_param("entropy_threads", threads)
+if os.environ.get("PH_SUB"):
+    dec.set_param("sub_bits", int(os.environ["PH_SUB"]))
 if os.environ.get("PH_WARM"):
     dec.set_param("warmup_slots", int(os.environ["PH_WARM"]))
 rows = []

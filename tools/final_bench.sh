@@ -18,6 +18,8 @@ run bench_lanes1 200 python -u bench.py --lanes 1 --no-cpu-baseline --no-queue-c
 run bench_fullres 200 python -u bench.py --workload fullres --no-cpu-baseline --no-queue-compare
 run bench_imagenet_f16 200 python -u bench.py --workload imagenet --no-cpu-baseline --no-queue-compare
 run bench_imagenet_bf16 200 python -u bench.py --workload imagenet --norm-dtype bfloat16 --no-cpu-baseline --no-queue-compare
+run bench_mixed 200 python -u bench.py --workload mixed --no-cpu-baseline --no-queue-compare
+run bench_big1 200 python -u bench.py --workload big1 --no-cpu-baseline --no-queue-compare
 run bench_with_copies 300 python -u bench.py --with-copies --no-cpu-baseline --no-queue-compare
 run stream_bytes 300 python -u bench_stream.py --source bytes
 run stream_file 300 python -u bench_stream.py

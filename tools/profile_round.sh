@@ -9,10 +9,16 @@ bash tools/fetch_calib.sh "$out/calib" || exit 1
 bash tools/pmc_round.sh "$out/pmc" || exit 1
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
+sha256sum spdl_amd/lib/libspdl_hipjpeg.so | cut -d' ' -f1 > "$out/lib_sha256.txt"
 for l in 4 1; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/ktrace_l$l" -o run --output-format csv \
     -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-queue-compare --lanes1-steps 0 --lanes $l \
     > "$out/ktrace_l$l.log" 2>&1 || { echo "kernel trace lanes $l failed"; exit 1; }
+done
+for w in mixed big1; do
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/ktrace_$w" -o run --output-format csv \
+    -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-queue-compare --lanes1-steps 0 --workload $w \
+    > "$out/ktrace_$w.log" 2>&1 || { echo "kernel trace $w failed"; exit 1; }
 done
 python3 tools/kernel_busy.py "$out/kernel_busy.json" \
   "4:$(find "$out/ktrace_l4" -name '*kernel_trace.csv' | head -1)" \
