@@ -36,20 +36,20 @@ hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageDesc*, ImageInfo*
                         const void*, void*, int64_t, const uint32_t*, uint32_t*, int, uint64_t*,
                         uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, hipStream_t);
 hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, DsChunk*, uint8_t*,
-                          uint32_t*, const uint32_t*, int, int, hipStream_t);
+                          uint32_t*, const uint32_t*, int, int, int, hipStream_t);
 hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
                           const HuffTable*, uint32_t*, uint2*, uint32_t*, const uint32_t*, uint64_t*,
                           int, int, int, int, int, hipStream_t);
 hipError_t launch_idct(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, uint8_t*,
-                       int, const uint32_t*, int, hipStream_t);
+                       int, const uint32_t*, int, int, int, hipStream_t);
 hipError_t launch_multiscan(const uint8_t*, uint8_t*, const ImageDesc*, ImageInfo*, uint32_t*, uint2*, int,
                             hipStream_t);
 hipError_t launch_csc(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                       const BatchParams&, int64_t, int, int32_t*, hipStream_t);
 hipError_t launch_nv12(const uint8_t*, uint8_t*, int, int, int, int, int, hipStream_t);
 hipError_t launch_sws(const uint8_t*, const ImageDesc*, const ImageInfo*, const int32_t*, void*,
-                      const BatchParams&, const uint32_t*, int, int, int32_t*, const uint32_t*, int,
-                      int16_t*, hipStream_t);
+                      const BatchParams&, const uint32_t*, int, int, int, int, int, int32_t*,
+                      const uint32_t*, int, int16_t*, hipStream_t);
 hipError_t launch_rgb_unscaled(const uint8_t*, const ImageDesc*, const ImageInfo*, void*,
                                const BatchParams&, int64_t, int, int32_t*, hipStream_t);
 hipError_t launch_idct_rgb(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, void*,
@@ -998,6 +998,15 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   auto* idct_map = ds_map + L.ds_wgs;
   auto* hs_map = idct_map + L.idct_wgs;
   auto* sws_map = hs_map + L.hs_wgs;
+  // A grid is flat (one workgroup per image tile, through the map) when the
+  // (max tiles) x images grid would be mostly empty; a batch of similar
+  // images keeps the 2-D grid, whose workgroups need no map lookup
+  auto use_flat = [&](int64_t flat_wgs, int64_t max_tiles) {
+    return (double)max_tiles * n > 1.25 * (double)flat_wgs;
+  };
+  const bool ds_flat = use_flat(L.ds_wgs, L.max_chunks);
+  const bool idct_flat = use_flat(L.idct_wgs, (L.max_blocks + kIdctThreads - 1) / kIdctThreads);
+  const bool sws_flat = use_flat(L.sws_wgs, (int64_t)L.sws_bands * L.sws_chunks);
   HJ_HIP(W.info.ensure(sizeof(ImageInfo) * n));
   HJ_HIP(W.luts.ensure(sizeof(HuffTable) * 8 * n));
   HJ_HIP(W.ents.ensure((size_t)L.total_blocks * 256 + 256));
@@ -1064,7 +1073,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   }
   HJ_HIP(launch_destuff(d_bytes, desc, infos, static_cast<DsChunk*>(W.dschunks.p),
                         static_cast<uint8_t*>(W.clean.p), static_cast<uint32_t*>(W.segs.p),
-                        ds_map, (int)L.ds_wgs, n, st));
+                        ds_flat ? ds_map : nullptr, (int)L.ds_wgs, L.max_chunks, n, st));
   mark(ctx, slot, 3, st);
   const int ent_threads =
       ctx->entropy_threads ? ctx->entropy_threads : (ctx->lanes > 1 ? 256 : 512);
@@ -1101,7 +1110,8 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   if (!(ctx->debug_mask & 0x20000) && !fused)
     HJ_HIP(launch_idct(static_cast<const uint32_t*>(W.ents.p),
                      static_cast<const uint2*>(W.bdesc.p), desc, infos,
-                     static_cast<uint8_t*>(W.planes.p), idct_kind, idct_map, (int)L.idct_wgs, st));
+                     static_cast<uint8_t*>(W.planes.p), idct_kind, idct_flat ? idct_map : nullptr,
+                     (int)L.idct_wgs, L.max_blocks, n, st));
   // 4-component frames: FFmpeg's K transform on the planes (not on the raw
   // planes surface, which returns the IDCT output as the oracle does)
   if (!planes_only && L.cmyk_px > 0)
@@ -1147,8 +1157,9 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                                  bp, L.max_px, n, hstat, st));
     } else if (swscale) {
       HJ_HIP(launch_sws(static_cast<const uint8_t*>(W.planes.p), desc, infos,
-                        static_cast<const int32_t*>(W.wts.p), out_dev, bp, sws_map,
-                        (int)L.sws_wgs, L.sws_lds, hstat, hs_map, (int)L.hs_wgs,
+                        static_cast<const int32_t*>(W.wts.p), out_dev, bp,
+                        sws_flat ? sws_map : nullptr, (int)L.sws_wgs, L.sws_bands, L.sws_chunks, n,
+                        L.sws_lds, hstat, hs_map, (int)L.hs_wgs,
                         static_cast<int16_t*>(W.hbuf.p), st));
     } else {
       HJ_HIP(launch_csc(static_cast<const uint8_t*>(W.planes.p), desc, infos, out_dev, bp,

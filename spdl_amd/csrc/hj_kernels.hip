@@ -662,9 +662,11 @@ __global__ void __launch_bounds__(kDsThreads) destuff_count_kernel(
     const uint32_t* __restrict__ ds_map) {
   __shared__ int sh[8];
   __shared__ int shterm;
-  // flat grid over every image's chunks (ds_map: workgroup -> image)
-  const int img = (int)ds_map[blockIdx.x], k = (int)blockIdx.x - desc[img].ds_wg0,
-            tid = threadIdx.x;
+  // (chunk, image) grid, or a flat grid over every image's chunks (ds_map:
+  // workgroup -> image) when the batch's sizes differ widely
+  const bool flat = ds_map != nullptr;
+  const int img = flat ? (int)ds_map[blockIdx.x] : (int)blockIdx.y;
+  const int k = flat ? (int)blockIdx.x - desc[img].ds_wg0 : (int)blockIdx.x, tid = threadIdx.x;
   if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc& dd = desc[img];
   const int size = (int)dd.in_size, start = infos[img].scan_start;
@@ -729,8 +731,9 @@ __global__ void __launch_bounds__(kDsThreads) destuff_write_kernel(
     uint32_t* __restrict__ segs, const uint32_t* __restrict__ ds_map) {
   __shared__ int sh[8];
   __shared__ __attribute__((aligned(16))) uint8_t ob[kDsChunk];
-  const int img = (int)ds_map[blockIdx.x], k = (int)blockIdx.x - desc[img].ds_wg0,
-            tid = threadIdx.x;
+  const bool flat = ds_map != nullptr;
+  const int img = flat ? (int)ds_map[blockIdx.x] : (int)blockIdx.y;
+  const int k = flat ? (int)blockIdx.x - desc[img].ds_wg0 : (int)blockIdx.x, tid = threadIdx.x;
   if (infos[img].status != kOk || infos[img].multiscan) return;
   const ImageDesc& dd = desc[img];
   const int size = (int)dd.in_size, start = infos[img].scan_start, end = infos[img].scan_end;
@@ -3807,9 +3810,11 @@ __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __re
                                                             const uint32_t* __restrict__ idct_map) {
   __shared__ __attribute__((aligned(16))) uint32_t sblk[kBlkWords + 1][kIdctThreads];
   __shared__ uint32_t sq[kMaxComp][64];
-  // flat grid over every image's block tiles (idct_map: workgroup -> image)
-  const int img = (int)idct_map[blockIdx.x];
-  const int tile = (int)blockIdx.x - desc[img].idct_wg0;
+  // (tile, image) grid, or a flat grid over every image's block tiles
+  // (idct_map: workgroup -> image) when the batch's sizes differ widely
+  const bool flat = idct_map != nullptr;
+  const int img = flat ? (int)idct_map[blockIdx.x] : (int)blockIdx.y;
+  const int tile = flat ? (int)blockIdx.x - desc[img].idct_wg0 : (int)blockIdx.x;
   const int j = tile * kIdctThreads + threadIdx.x;
   const ImageInfo& in = infos[img];
   if (in.status != kOk || tile * kIdctThreads >= in.nblocks) return;
@@ -4218,11 +4223,15 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
                                                   const int16_t* __restrict__ hbuf,
                                                   const uint32_t* __restrict__ sws_map) {
   extern __shared__ __attribute__((aligned(16))) int16_t sws_lds[];
-  // flat grid over every image's own tiles (sws_map: workgroup -> image)
-  const int img = (int)sws_map[blockIdx.x], tid = threadIdx.x, nt = blockDim.x;
+  // (band, chunk, image) grid, or a flat grid over every image's own tiles
+  // (sws_map: workgroup -> image) when the batch's plans differ widely
+  const bool flat = sws_map != nullptr;
+  const int img = flat ? (int)sws_map[blockIdx.x] : (int)blockIdx.z, tid = threadIdx.x,
+            nt = blockDim.x;
   const ImageDesc& dd = desc[img];
-  const int t = (int)blockIdx.x - dd.sws_wg0;
-  const int band = t / dd.sws_chunks, chunk = t - band * dd.sws_chunks;
+  const int t = flat ? (int)blockIdx.x - dd.sws_wg0 : (int)(blockIdx.x * dd.sws_chunks + blockIdx.y);
+  const int band = flat ? t / dd.sws_chunks : (int)blockIdx.x;
+  const int chunk = flat ? t - band * dd.sws_chunks : (int)blockIdx.y;
   const ImageInfo& in = infos[img];
   // the image's final status, straight into the slot's pinned status array
   if (host_status && t == 0 && tid == 0) host_status[img] = in.status;
@@ -4812,12 +4821,14 @@ hipError_t launch_parse(const uint8_t* bytes, const ImageDesc* host_desc, ImageD
 }
 hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo* infos,
                           DsChunk* chunks, uint8_t* clean, uint32_t* segs, const uint32_t* ds_map,
-                          int ds_wgs, int n, hipStream_t st) {
-  hipLaunchKernelGGL(destuff_count_kernel, dim3(ds_wgs), dim3(kDsThreads), 0, st, bytes, desc,
-                     infos, chunks, ds_map);
+                          int ds_wgs, int max_chunks, int n, hipStream_t st) {
+  // ds_map null: the (max chunks, image) grid of a batch of similar sizes
+  const dim3 grid = ds_map ? dim3(ds_wgs) : dim3(max_chunks, n);
+  hipLaunchKernelGGL(destuff_count_kernel, grid, dim3(kDsThreads), 0, st, bytes, desc, infos,
+                     chunks, ds_map);
   hipLaunchKernelGGL(destuff_prefix_kernel, dim3(n), dim3(kDsThreads), 0, st, desc, infos, chunks);
-  hipLaunchKernelGGL(destuff_write_kernel, dim3(ds_wgs), dim3(kDsThreads), 0, st, bytes, desc,
-                     infos, chunks, clean, segs, ds_map);
+  hipLaunchKernelGGL(destuff_write_kernel, grid, dim3(kDsThreads), 0, st, bytes, desc, infos,
+                     chunks, clean, segs, ds_map);
   return hipGetLastError();
 }
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
@@ -4844,8 +4855,11 @@ hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const Imag
 }
 hipError_t launch_idct(const uint32_t* ents, const uint2* bdesc, const ImageDesc* desc,
                        const ImageInfo* infos, uint8_t* planes, int idct, const uint32_t* idct_map,
-                       int idct_wgs, hipStream_t st) {
-  const dim3 grid(idct_wgs);  // flat: every image's tiles, no empty workgroups
+                       int idct_wgs, int max_blocks, int n, hipStream_t st) {
+  // flat: every image's tiles, no empty workgroups; idct_map null: (max
+  // tiles, image)
+  const dim3 grid = idct_map ? dim3(idct_wgs)
+                             : dim3((max_blocks + kIdctThreads - 1) / kIdctThreads, n);
   if (idct == 2)  // timing ablation (debug_mask 0x800): no transform, wrong output
     hipLaunchKernelGGL(idct_kernel<2>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
                        planes, idct_map);
@@ -4928,13 +4942,15 @@ hipError_t launch_nv12(const uint8_t* src, uint8_t* dst, int frames, int height,
 
 hipError_t launch_sws(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,
                       const int32_t* pool, void* out, const BatchParams& p,
-                      const uint32_t* sws_map, int sws_wgs, int lds_bytes, int32_t* host_status,
-                      const uint32_t* hs_map, int hs_wgs, int16_t* hbuf, hipStream_t st) {
+                      const uint32_t* sws_map, int sws_wgs, int bands, int chunks, int n,
+                      int lds_bytes, int32_t* host_status, const uint32_t* hs_map, int hs_wgs,
+                      int16_t* hbuf, hipStream_t st) {
   if (hs_wgs > 0)
     hipLaunchKernelGGL(hscale_kernel, dim3(hs_wgs), dim3(256), 0, st, planes, desc, infos, pool,
                        hs_map, hbuf);
-  hipLaunchKernelGGL(sws_kernel, dim3(sws_wgs), dim3(256), lds_bytes, st, planes, desc, infos,
-                     pool, out, p, host_status, hbuf, sws_map);
+  const dim3 grid = sws_map ? dim3(sws_wgs) : dim3(bands, chunks, n);
+  hipLaunchKernelGGL(sws_kernel, grid, dim3(256), lds_bytes, st, planes, desc, infos, pool, out, p,
+                     host_status, hbuf, sws_map);
   return hipGetLastError();
 }
 hipError_t launch_cmyk(const ImageDesc* desc, const ImageInfo* infos, uint8_t* planes,
