@@ -34,7 +34,7 @@
 namespace hj {
 hipError_t launch_parse(const uint8_t*, const ImageDesc*, ImageDesc*, ImageInfo*, HuffTable*,
                         const void*, void*, int64_t, const uint32_t*, uint32_t*, int, uint64_t*,
-                        uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, hipStream_t);
+                        uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int, hipStream_t);
 hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, DsChunk*, uint8_t*,
                           uint32_t*, const uint32_t*, int, int, int, hipStream_t);
 hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
@@ -840,6 +840,8 @@ struct spdl_hj_ctx {
   int64_t piece_bytes = 128 * 1024;
   // s_setprio of the entropy waves (0-3; A/B knob)
   int entropy_prio = 0;
+  // parse_kernel workgroup size (its marker walk is one thread's)
+  int parse_threads = 64;  // (r05 A/B: 64 +1 % over 256 at four lanes)
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
   PlanCache plans;          // swscale plans per distinct geometry
 };
@@ -1041,7 +1043,8 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                       hs ? reinterpret_cast<const uint32_t*>(
                                static_cast<const ImageDesc*>(slot.pin_desc.dev) + n)
                          : nullptr,
-                      work, nwork, chain, ds_map, idct_map, hs_map, sws_map, n, st));
+                      work, nwork, chain, ds_map, idct_map, hs_map, sws_map, ctx->parse_threads, n,
+                      st));
   mark(ctx, slot, 2, st);
   const bool ms_side = L.ms_side && !(ctx->debug_mask & 0x10000) && side_streams_fit(ctx);
   if (ms_side) {
@@ -1871,6 +1874,11 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     ctx->piece_bytes = value;
     return SPDL_HJ_OK;
   }
+  if (!strcmp(name, "parse_threads")) {
+    if (value != 64 && value != 128 && value != 256) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->parse_threads = (int)value;
+    return SPDL_HJ_OK;
+  }
   if (!strcmp(name, "entropy_prio")) {
     if (value < 0 || value > 3) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->entropy_prio = (int)value;
@@ -1959,6 +1967,7 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"entropy_piece_bytes", ctx->piece_bytes},
       {"sws_prepass", ctx->plans.pre_mode()},
       {"entropy_prio", ctx->entropy_prio},
+      {"parse_threads", ctx->parse_threads},
       {"sws_cols", ctx->plans.max_cols()},
       {"hw_queues", ctx->hw_queues},
       // streams a batch holding a progressive image may use: one per lane, a

@@ -4819,8 +4819,8 @@ hipError_t launch_parse(const uint8_t* bytes, const ImageDesc* host_desc, ImageD
                         ImageInfo* infos, HuffTable* luts, const void* host_tables, void* tables,
                         int64_t table_bytes, const uint32_t* host_work, uint32_t* work, int nwork,
                         uint64_t* chain, uint32_t* ds_map, uint32_t* idct_map, uint32_t* hs_map,
-                        uint32_t* sws_map, int n, hipStream_t st) {
-  hipLaunchKernelGGL(parse_kernel, dim3(n), dim3(256), 0, st, bytes, host_desc, desc, infos, luts,
+                        uint32_t* sws_map, int threads, int n, hipStream_t st) {
+  hipLaunchKernelGGL(parse_kernel, dim3(n), dim3(threads), 0, st, bytes, host_desc, desc, infos, luts,
                      static_cast<const uint4*>(host_tables), static_cast<uint4*>(tables),
                      (table_bytes + 15) / 16, host_work, work, nwork, chain, ds_map, idct_map,
                      hs_map, sws_map);
