@@ -2512,14 +2512,22 @@ __device__ __forceinline__ uint32_t rt_entry(const RTab& t, uint32_t w16) {
 
 // AC refinement entries: the symbol's fields the symbol loop needs, unpacked
 // once per table instead of once per symbol:
-//   bits 0-4 code length (0: bad code), bit 5 s == 1 (a new coefficient),
-//   bit 6 stop (EOBr, or s > 1: an error), bits 8-11 r, bits 16-31 the
-//   symbol (-1: bad code)
+//   bits 0-5   code length + s (the bits before the correction bits: a
+//              64-bit shift by the entry itself skips them)
+//   bit 7      s == 1 (a new coefficient)
+//   bits 8-11  r;  bits 12-15  s
+//   bits 16-21 63 - code length (the sign bit's place in the 64-bit buffer)
+//   bits 22-26 code length (0: bad code)
+//   bit 31     stop: EOBr, s > 1 (an error) or a bad code -- so every entry
+//              the fast loop takes is > 0
 __device__ __forceinline__ uint32_t ms_ref_pack(uint32_t L, int sym) {
   const int s = sym & 15, r = sym >> 4;
   const uint32_t stop = ((s == 0 && r != 15) || s > 1) ? 1u : 0u;
-  return L | (s == 1 ? 32u : 0u) | stop << 6 | (uint32_t)(r & 15) << 8 | (uint32_t)sym << 16;
+  const uint32_t s1 = s == 1 ? 1u : 0u;
+  return (L + s1) | s1 << 7 | (uint32_t)r << 8 | (uint32_t)s << 12 | (63u - L) << 16 | L << 22 |
+         stop << 31;
 }
+constexpr uint32_t kRefBad = 0x8000F000u;  // bad code: length 0, s 15, stop
 // (per lane, on a built table's first level)
 __device__ __forceinline__ uint32_t ms_ref_l1(uint32_t e) {
   return e ? ms_ref_pack(e & 31u, (int)(e >> 8)) : 0u;
@@ -2533,10 +2541,154 @@ __device__ __forceinline__ uint32_t rt_entry_ref(const RTab& t, uint32_t w16) {
     const int Lc = L > 16 ? 16 : L;
     const uint32_t idx = ms_rl(t.voff, Lc) + (w16 >> (16 - Lc));
     const uint32_t sym = (ms_rl(t.vals, (int)((idx >> 2) & 63u)) >> (8 * (idx & 3u))) & 0xFFu;
-    e = L > 16 ? 0xFFFF0040u : ms_ref_pack((uint32_t)L, (int)sym);
+    e = L > 16 ? kRefBad : ms_ref_pack((uint32_t)L, (int)sym);
   }
   return e;
 }
+
+// The refinement symbol loop's common case in straight scalar code
+// (MsWBits reader): symbols with a code of <= 6 bits that do not run past
+// the band's zeros and take <= 15 correction bits, and the EOBr that ends a
+// block.  A symbol is two v_readlane (entry, zero place) and ~33 scalar
+// instructions, two symbols per taken branch; the compiled loop of the same
+// step took ~78 with register copies at its join points and a wait for the
+// refill's prefetch on every symbol.  The loop returns BEFORE a symbol it
+// does not take (the general step in ms_decode_scan decodes that one), or
+// after the symbol that ends the band (ended = 1) or an EOBr (ended = 2,
+// eobrun set); state in/out as MsWBits / the symbol loop keep it.  zpos
+// lanes >= nzero hold a sentinel > 63 + 15 + 15, so a run past the band's
+// zeros fails the <= 15 test (a zero index >= 64 reads lane t - 64, a zero
+// before k: the difference is negative, and fails it too).  Entry: >= 32
+// bits in the buffer.  The refill's scalar load is waited for before the
+// return (the compiler does not count the statement's loads).
+#define HJ_REF_SYM                                             \
+  /* entry of the code at the top 6 bits; <= 0: slow or stop */ \
+  "s_lshr_b32 %[i], s41, 26\n\t"                               \
+  "v_readlane_b32 %[e], %[l1], %[i]\n\t"                       \
+  "s_cmp_lt_i32 %[e], 1\n\t"                                   \
+  "s_cbranch_scc1 6f\n\t"                                      \
+  /* the new coefficient's place: the (zi + r)-th zero */       \
+  "s_bfe_u32 %[r], %[e], 0x40008\n\t"                          \
+  "s_add_i32 %[t], %[zi], %[r]\n\t"                            \
+  "v_readlane_b32 %[p], %[zpos], %[t]\n\t"                     \
+  /* correction bits: the history coefficients passed */       \
+  "s_sub_i32 %[c], %[p], %[k]\n\t"                             \
+  "s_sub_i32 %[c], %[c], %[r]\n\t"                             \
+  "s_cmp_gt_u32 %[c], 15\n\t"                                  \
+  "s_cbranch_scc1 9f\n\t"                                      \
+  /* new coefficient mask; its sign: bit 63 - len */           \
+  "s_bfe_u32 %[s1], %[e], 0x10007\n\t"                         \
+  "s_bfm_b64 %[x], %[s1], %[p]\n\t"                            \
+  "s_or_b64 %[nm], %[nm], %[x]\n\t"                            \
+  "s_bfe_u32 %[u], %[e], 0x60010\n\t"                          \
+  "s_bitcmp1_b64 s[40:41], %[u]\n\t"                           \
+  "s_cselect_b64 %[y], 0, %[x]\n\t"                            \
+  "s_or_b64 %[nsg], %[nsg], %[y]\n\t"                          \
+  /* past code + sign; the c correction bits, MSB-first */     \
+  "s_lshl_b64 %[q], s[40:41], %[e]\n\t"                        \
+  "s_sub_i32 %[o], 64, %[c]\n\t"                               \
+  "s_pack_ll_b32_b16 %[o], %[o], %[c]\n\t"                     \
+  "s_bfe_u64 %[x], %[q], %[o]\n\t"                             \
+  "s_lshl_b64 %[corr], %[corr], %[c]\n\t"                      \
+  "s_or_b64 %[corr], %[corr], %[x]\n\t"                        \
+  "s_lshl_b64 s[40:41], %[q], %[c]\n\t"                        \
+  "s_and_b32 %[u], %[e], 63\n\t"                               \
+  "s_add_i32 %[u], %[u], %[c]\n\t"                             \
+  "s_sub_i32 %[cnt], %[cnt], %[u]\n\t"                         \
+  "s_add_i32 %[k], %[p], 1\n\t"                                \
+  "s_add_i32 %[zi], %[t], 1\n\t"                               \
+  "s_add_i32 %[nsym], %[nsym], 1\n\t"                          \
+  /* the band ends after coefficient se */                     \
+  "s_cmp_ge_i32 %[p], %[se]\n\t"                               \
+  "s_cbranch_scc1 8f\n\t"
+
+__device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, uint32_t& nxm,
+                                            uint32_t& nx, MsWords w, int lastw, int& k, int& zi,
+                                            uint64_t& corr, uint64_t& nm, uint64_t& nsg,
+                                            int& nsym, int se, uint32_t l1, uint32_t zpos,
+                                            int& eobrun, int& ended) {
+  uint32_t i, e, r, t, p, c, o, u, s1;
+  uint64_t q, x, y;
+  // (all uniform; readfirstlane where the compiler's divergence analysis
+  // cannot see it -- no instruction for values already in SGPRs)
+  buf = ms_u64(buf);
+  cnt = ms_i(cnt);
+  wi = ms_i(wi);
+  nxm = ms_u(nxm);
+  nx = ms_u(nx);
+  k = ms_i(k);
+  zi = ms_i(zi);
+  corr = ms_u64(corr);
+  nm = ms_u64(nm);
+  nsg = ms_u64(nsg);
+  nsym = ms_i(nsym);
+  eobrun = ms_i(eobrun);
+  se = ms_i(se);
+  lastw = ms_i(lastw);
+  w = (MsWords)(const void*)(uintptr_t)ms_u64((uint64_t)(uintptr_t)(const void*)w);
+  asm volatile(
+      "s_mov_b32 %[ended], 0\n\t"
+      "s_nop 0\n"
+      "1:\n\t"
+      HJ_REF_SYM
+      "s_cmp_gt_i32 %[cnt], 31\n\t"
+      "s_cbranch_scc0 7f\n\t"
+      HJ_REF_SYM
+      "s_cmp_gt_i32 %[cnt], 31\n\t"
+      "s_cbranch_scc1 1b\n"
+      // refill (MsWBits::need): the prefetched dword enters the buffer
+      "7:\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_and_b32 s42, %[nx], %[nxm]\n\t"
+      "s_mov_b32 s43, 0\n\t"
+      "s_sub_i32 %[o], 32, %[cnt]\n\t"
+      "s_lshl_b64 s[42:43], s[42:43], %[o]\n\t"
+      "s_or_b64 s[40:41], s[40:41], s[42:43]\n\t"
+      "s_add_i32 %[cnt], %[cnt], 32\n\t"
+      "s_add_i32 %[wi], %[wi], 1\n\t"
+      "s_sub_i32 %[o], %[lastw], %[wi]\n\t"
+      "s_ashr_i32 %[o], %[o], 31\n\t"
+      "s_not_b32 %[nxm], %[o]\n\t"
+      "s_min_i32 %[o], %[wi], %[lastw]\n\t"
+      "s_lshl_b32 %[o], %[o], 2\n\t"
+      "s_load_dword %[nx], %[w], %[o]\n\t"
+      "s_branch 1b\n"
+      // a stop entry: EOBr (s = 0) ends the block with an EOB run of
+      // 2^r + r more bits (r <= 14: the code is <= 6 bits, so >= 26 bits
+      // are in the buffer); anything else is the general step's
+      "6:\n\t"
+      "s_cmp_eq_u32 %[e], 0\n\t"
+      "s_cbranch_scc1 9f\n\t"
+      "s_bfe_u32 %[u], %[e], 0x4000c\n\t"
+      "s_cmp_lg_u32 %[u], 0\n\t"
+      "s_cbranch_scc1 9f\n\t"
+      "s_bfe_u32 %[u], %[e], 0x50016\n\t"
+      "s_lshl_b64 s[40:41], s[40:41], %[u]\n\t"
+      "s_sub_i32 %[cnt], %[cnt], %[u]\n\t"
+      "s_bfe_u32 %[r], %[e], 0x40008\n\t"
+      "s_lshl_b32 %[eob], 1, %[r]\n\t"
+      "s_sub_i32 %[o], 64, %[r]\n\t"
+      "s_pack_ll_b32_b16 %[o], %[o], %[r]\n\t"
+      "s_bfe_u64 s[42:43], s[40:41], %[o]\n\t"
+      "s_add_i32 %[eob], %[eob], s42\n\t"
+      "s_lshl_b64 s[40:41], s[40:41], %[r]\n\t"
+      "s_sub_i32 %[cnt], %[cnt], %[r]\n\t"
+      "s_add_i32 %[nsym], %[nsym], 1\n\t"
+      "s_mov_b32 %[ended], 2\n\t"
+      "s_branch 9f\n"
+      "8:\n\t"
+      "s_mov_b32 %[ended], 1\n"
+      "9:\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      : "+{s[40:41]}"(buf), [cnt] "+s"(cnt), [wi] "+s"(wi), [nxm] "+s"(nxm), [nx] "+s"(nx),
+        [k] "+s"(k), [zi] "+s"(zi), [corr] "+s"(corr), [nm] "+s"(nm), [nsg] "+s"(nsg),
+        [nsym] "+s"(nsym), [eob] "+s"(eobrun), [ended] "=&s"(ended), [i] "=&s"(i), [e] "=&s"(e),
+        [r] "=&s"(r), [t] "=&s"(t), [p] "=&s"(p), [c] "=&s"(c), [o] "=&s"(o), [u] "=&s"(u),
+        [s1] "=&s"(s1), [q] "=&s"(q), [x] "=&s"(x), [y] "=&s"(y)
+      : [l1] "v"(l1), [zpos] "v"(zpos), [se] "s"(se), [lastw] "s"(lastw), [w] "s"(w)
+      : "s42", "s43", "scc", "memory");
+}
+#undef HJ_REF_SYM
 
 // bits k .. e (inclusive) of a coefficient mask; 0 when k > e
 __device__ __forceinline__ uint64_t ms_range(int k, int e) {
@@ -3016,8 +3168,9 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
             const int below = (int)__builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(hz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hz, 0u));
             const bool isz = (hz >> lane) & 1ull;
-            const uint32_t zpos = (uint32_t)__builtin_amdgcn_ds_permute(
+            uint32_t zpos = (uint32_t)__builtin_amdgcn_ds_permute(
                 (isz ? below : nzero + lane - below) << 2, lane);
+            zpos = lane < nzero ? zpos : 127u;  // (past the zeros: ms_ref_fast's sentinel)
             // One exit, at the bottom: the rare ends (EOBr, a run past se, a
             // bad code) only clear `live` and are sorted out after the loop,
             // so the symbol step is straight-line scalar code (flags as 0/1
@@ -3025,6 +3178,7 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
             int k = ss, zi = 0;  // next coefficient; zeros before it
             uint32_t e;
             int t, cont;
+            constexpr uint32_t kRefDone = 15u << 8;  // (s = 0, r = 15: no EOBr, no error)
             // zpos is waited for here, once: in the loop the LDS and scalar
             // load counters are one, and a wait for it there would also wait
             // for the bit reader's prefetch
@@ -3035,10 +3189,26 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
             // (the refill at the bottom: the common path falls through)
             br.need();
             do {
+              if constexpr (kWord) {
+                // the common symbols in ms_ref_fast; it returns before one it
+                // does not take, or after the one that ends the band
+                const int k0 = k;
+                int ended;
+                ms_ref_fast(br.buf, br.cnt, br.wi, br.nxm, br.nx, br.w, br.lastw, k, zi, corr, nm,
+                            nsg, nsym, se, atr.l1, zpos, eobrun, ended);
+                cb += __popcll(hist & ms_range(k0, k - 1));
+                if (ended) {  // (1: the band's end; 2: an EOBr, eobrun set)
+                  e = kRefDone;
+                  t = 0;
+                  break;
+                }
+              }
               e = rt_entry_ref(atr, br.peek16());
               nsym++;
-              br.skip((int)(e & 31u));
-              const int s1 = (int)((e >> 5) & 1u), stop = (int)((e >> 6) & 1u);
+              br.skip((int)((e >> 22) & 31u));
+              const int s1 = (int)((e >> 7) & 1u);
+              int stop = (int)(e >> 31);
+              ms_opaque(stop);  // (as a compare result it went through the VALU: illegal copy)
               const int r = (int)((e >> 8) & 15u);
               // the new coefficient's sign (bit 1: positive)
               uint32_t h = br.hi32();
@@ -3079,7 +3249,7 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
               ms_opaque(cont);
               br.need();
             } while (__builtin_expect(cont, 1));
-            const int rs = (int)e >> 16, r = rs >> 4, s = rs & 15;
+            const int r = (int)((e >> 8) & 15u), s = (int)((e >> 12) & 15u);
             if (s > 1 || (s == 1 && t >= nzero)) {
               rc = kErrBadHuffman;  // (a bad code, a value other than +-1, a new coefficient past se)
             } else if (s == 0 && r != 15) {  // EOBr
