@@ -2512,22 +2512,20 @@ __device__ __forceinline__ uint32_t rt_entry(const RTab& t, uint32_t w16) {
 
 // AC refinement entries: the symbol's fields the symbol loop needs, unpacked
 // once per table instead of once per symbol:
-//   bits 0-5   code length + s (the bits before the correction bits: a
-//              64-bit shift by the entry itself skips them)
+//   bits 0-5   code length (0: bad code): a 64-bit shift by the entry itself
+//              skips the code
+//   bit 6      stop: EOBr, or s > 1 (an error), or a bad code
 //   bit 7      s == 1 (a new coefficient)
 //   bits 8-11  r;  bits 12-15  s
-//   bits 16-21 63 - code length (the sign bit's place in the 64-bit buffer)
-//   bits 22-26 code length (0: bad code)
-//   bit 31     stop: EOBr, s > 1 (an error) or a bad code -- so every entry
-//              the fast loop takes is > 0
+//   bit 31     not a plain new-coefficient symbol (s != 1): ZRL, stop --
+//              so every entry ms_ref_fast takes is > 0
 __device__ __forceinline__ uint32_t ms_ref_pack(uint32_t L, int sym) {
   const int s = sym & 15, r = sym >> 4;
   const uint32_t stop = ((s == 0 && r != 15) || s > 1) ? 1u : 0u;
-  const uint32_t s1 = s == 1 ? 1u : 0u;
-  return (L + s1) | s1 << 7 | (uint32_t)r << 8 | (uint32_t)s << 12 | (63u - L) << 16 | L << 22 |
-         stop << 31;
+  return L | stop << 6 | (s == 1 ? 1u : 0u) << 7 | (uint32_t)r << 8 | (uint32_t)s << 12 |
+         (s != 1 ? 1u : 0u) << 31;
 }
-constexpr uint32_t kRefBad = 0x8000F000u;  // bad code: length 0, s 15, stop
+constexpr uint32_t kRefBad = 0x8000F040u;  // bad code: length 0, stop, s 15
 // (per lane, on a built table's first level)
 __device__ __forceinline__ uint32_t ms_ref_l1(uint32_t e) {
   return e ? ms_ref_pack(e & 31u, (int)(e >> 8)) : 0u;
@@ -2547,68 +2545,67 @@ __device__ __forceinline__ uint32_t rt_entry_ref(const RTab& t, uint32_t w16) {
 }
 
 // The refinement symbol loop's common case in straight scalar code
-// (MsWBits reader): symbols with a code of <= 6 bits that do not run past
-// the band's zeros and take <= 15 correction bits, and the EOBr that ends a
-// block.  A symbol is two v_readlane (entry, zero place) and ~33 scalar
-// instructions, two symbols per taken branch; the compiled loop of the same
-// step took ~78 with register copies at its join points and a wait for the
-// refill's prefetch on every symbol.  The loop returns BEFORE a symbol it
-// does not take (the general step in ms_decode_scan decodes that one), or
-// after the symbol that ends the band (ended = 1) or an EOBr (ended = 2,
-// eobrun set); state in/out as MsWBits / the symbol loop keep it.  zpos
-// lanes >= nzero hold a sentinel > 63 + 15 + 15, so a run past the band's
-// zeros fails the <= 15 test (a zero index >= 64 reads lane t - 64, a zero
-// before k: the difference is negative, and fails it too).  Entry: >= 32
-// bits in the buffer.  The refill's scalar load is waited for before the
-// return (the compiler does not count the statement's loads).
-#define HJ_REF_SYM                                             \
-  /* entry of the code at the top 6 bits; <= 0: slow or stop */ \
-  "s_lshr_b32 %[i], s41, 26\n\t"                               \
-  "v_readlane_b32 %[e], %[l1], %[i]\n\t"                       \
-  "s_cmp_lt_i32 %[e], 1\n\t"                                   \
-  "s_cbranch_scc1 6f\n\t"                                      \
-  /* the new coefficient's place: the (zi + r)-th zero */       \
-  "s_bfe_u32 %[r], %[e], 0x40008\n\t"                          \
-  "s_add_i32 %[t], %[zi], %[r]\n\t"                            \
-  "v_readlane_b32 %[p], %[zpos], %[t]\n\t"                     \
-  /* correction bits: the history coefficients passed */       \
-  "s_sub_i32 %[c], %[p], %[k]\n\t"                             \
-  "s_sub_i32 %[c], %[c], %[r]\n\t"                             \
-  "s_cmp_gt_u32 %[c], 15\n\t"                                  \
-  "s_cbranch_scc1 9f\n\t"                                      \
-  /* new coefficient mask; its sign: bit 63 - len */           \
-  "s_bfe_u32 %[s1], %[e], 0x10007\n\t"                         \
-  "s_bfm_b64 %[x], %[s1], %[p]\n\t"                            \
-  "s_or_b64 %[nm], %[nm], %[x]\n\t"                            \
-  "s_bfe_u32 %[u], %[e], 0x60010\n\t"                          \
-  "s_bitcmp1_b64 s[40:41], %[u]\n\t"                           \
-  "s_cselect_b64 %[y], 0, %[x]\n\t"                            \
-  "s_or_b64 %[nsg], %[nsg], %[y]\n\t"                          \
-  /* past code + sign; the c correction bits, MSB-first */     \
-  "s_lshl_b64 %[q], s[40:41], %[e]\n\t"                        \
-  "s_sub_i32 %[o], 64, %[c]\n\t"                               \
-  "s_pack_ll_b32_b16 %[o], %[o], %[c]\n\t"                     \
-  "s_bfe_u64 %[x], %[q], %[o]\n\t"                             \
-  "s_lshl_b64 %[corr], %[corr], %[c]\n\t"                      \
-  "s_or_b64 %[corr], %[corr], %[x]\n\t"                        \
-  "s_lshl_b64 s[40:41], %[q], %[c]\n\t"                        \
-  "s_and_b32 %[u], %[e], 63\n\t"                               \
-  "s_add_i32 %[u], %[u], %[c]\n\t"                             \
-  "s_sub_i32 %[cnt], %[cnt], %[u]\n\t"                         \
-  "s_add_i32 %[k], %[p], 1\n\t"                                \
-  "s_add_i32 %[zi], %[t], 1\n\t"                               \
-  "s_add_i32 %[nsym], %[nsym], 1\n\t"                          \
-  /* the band ends after coefficient se */                     \
-  "s_cmp_ge_i32 %[p], %[se]\n\t"                               \
-  "s_cbranch_scc1 8f\n\t"
+// (MsWBits reader): new-coefficient symbols (s = 1) with a code of <= 6
+// bits that do not run past the band's zeros and take <= 15 correction
+// bits, and the EOBr that ends a block.  A symbol is two v_readlane (entry,
+// zero place), ~29 scalar instructions and two conditional branches, two
+// symbols per taken branch; the compiled loop of the same step took ~78
+// instructions, with register copies at its join points and a wait for the
+// refill's prefetch on every symbol.  The buffer carries a marker bit right
+// below its valid bits (>= 32 valid bits <=> a non-zero low word), so the
+// loop keeps no bit count.  It returns BEFORE a symbol it does not take (the
+// general step in ms_decode_scan decodes that one), or after the symbol that
+// ends the band (ended = 1) or an EOBr (ended = 2, eobrun set); state in/out
+// as MsWBits / the symbol loop keep it.  zpos lanes >= nzero hold a sentinel
+// > 63 + 15 + 15, so a run past the band's zeros fails the <= 15 test (a zero
+// index >= 64 reads lane t - 64, a zero before k: the difference is
+// negative, and fails it too).  Entry: >= 32 bits in the buffer.  The
+// refill's scalar load is waited for before the return (the compiler does
+// not count the statement's loads).
+#define HJ_REF_SYM                                                      \
+  /* entry of the code at the top 6 bits; zero place (zi + r)-th */     \
+  "s_lshr_b32 %[i], s41, 26\n\t"                                        \
+  "v_readlane_b32 %[e], %[l1], %[i]\n\t"                                \
+  "s_bfe_u32 %[r], %[e], 0x40008\n\t"                                   \
+  "s_add_i32 %[t], %[zi], %[r]\n\t"                                     \
+  "v_readlane_b32 %[p], %[zpos], %[t]\n\t"                              \
+  /* correction bits: the history coefficients passed; leave if > 15 */ \
+  /* or the entry is not a plain symbol (<= 0) */                       \
+  "s_sub_i32 %[c], %[p], %[k]\n\t"                                      \
+  "s_sub_i32 %[c], %[c], %[r]\n\t"                                      \
+  "s_cmp_lt_i32 %[e], 1\n\t"                                            \
+  "s_cselect_b32 %[c], 64, %[c]\n\t"                                    \
+  "s_cmp_gt_u32 %[c], 15\n\t"                                           \
+  "s_cbranch_scc1 6f\n\t"                                               \
+  /* past the code: the sign bit on top (1: positive), then c bits */   \
+  "s_lshl_b64 s[42:43], s[40:41], %[e]\n\t"                             \
+  "s_lshl_b64 %[x], 1, %[p]\n\t"                                        \
+  "s_or_b64 %[nm], %[nm], %[x]\n\t"                                     \
+  "s_cmp_lt_i32 s43, 0\n\t"                                             \
+  "s_cselect_b64 %[y], 0, %[x]\n\t"                                     \
+  "s_or_b64 %[nsg], %[nsg], %[y]\n\t"                                   \
+  "s_sub_i32 %[o], 63, %[c]\n\t"                                        \
+  "s_pack_ll_b32_b16 %[o], %[o], %[c]\n\t"                              \
+  "s_bfe_u64 %[x], s[42:43], %[o]\n\t"                                  \
+  "s_lshl_b64 %[corr], %[corr], %[c]\n\t"                               \
+  "s_or_b64 %[corr], %[corr], %[x]\n\t"                                 \
+  "s_add_i32 %[u], %[c], 1\n\t"                                         \
+  "s_lshl_b64 s[40:41], s[42:43], %[u]\n\t"                             \
+  "s_add_i32 %[k], %[p], 1\n\t"                                         \
+  "s_add_i32 %[zi], %[t], 1\n\t"                                        \
+  "s_add_i32 %[nsym], %[nsym], 1\n\t"                                   \
+  /* on while the band goes on and >= 32 bits are left */              \
+  "s_cmp_ge_i32 %[p], %[se]\n\t"                                        \
+  "s_cselect_b32 %[u], 0, s40\n\t"                                      \
+  "s_cmp_lg_u32 %[u], 0\n\t"
 
 __device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, uint32_t& nxm,
                                             uint32_t& nx, MsWords w, int lastw, int& k, int& zi,
                                             uint64_t& corr, uint64_t& nm, uint64_t& nsg,
                                             int& nsym, int se, uint32_t l1, uint32_t zpos,
                                             int& eobrun, int& ended) {
-  uint32_t i, e, r, t, p, c, o, u, s1;
-  uint64_t q, x, y;
+  uint32_t i, e, r, t, p, c, o, u;
+  uint64_t x, y;
   // (all uniform; readfirstlane where the compiler's divergence analysis
   // cannot see it -- no instruction for values already in SGPRs)
   buf = ms_u64(buf);
@@ -2628,23 +2625,27 @@ __device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, ui
   w = (MsWords)(const void*)(uintptr_t)ms_u64((uint64_t)(uintptr_t)(const void*)w);
   asm volatile(
       "s_mov_b32 %[ended], 0\n\t"
-      "s_nop 0\n"
+      // the marker below the valid bits
+      "s_sub_i32 %[o], 63, %[cnt]\n\t"
+      "s_bitset1_b64 s[40:41], %[o]\n"
       "1:\n\t"
       HJ_REF_SYM
-      "s_cmp_gt_i32 %[cnt], 31\n\t"
       "s_cbranch_scc0 7f\n\t"
       HJ_REF_SYM
-      "s_cmp_gt_i32 %[cnt], 31\n\t"
       "s_cbranch_scc1 1b\n"
-      // refill (MsWBits::need): the prefetched dword enters the buffer
+      // the band's end, or a refill (MsWBits::need): the prefetched dword
+      // enters the buffer right below the valid bits, the marker below it
       "7:\n\t"
+      "s_cmp_ge_i32 %[p], %[se]\n\t"
+      "s_cbranch_scc1 8f\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
-      "s_and_b32 s42, %[nx], %[nxm]\n\t"
-      "s_mov_b32 s43, 0\n\t"
-      "s_sub_i32 %[o], 32, %[cnt]\n\t"
-      "s_lshl_b64 s[42:43], s[42:43], %[o]\n\t"
+      "s_ff1_i32_b64 %[o], s[40:41]\n\t"
+      "s_bitset0_b64 s[40:41], %[o]\n\t"
+      "s_sub_i32 %[o], 63, %[o]\n\t"
+      "s_and_b32 s43, %[nx], %[nxm]\n\t"
+      "s_brev_b32 s42, 1\n\t"
+      "s_lshr_b64 s[42:43], s[42:43], %[o]\n\t"
       "s_or_b64 s[40:41], s[40:41], s[42:43]\n\t"
-      "s_add_i32 %[cnt], %[cnt], 32\n\t"
       "s_add_i32 %[wi], %[wi], 1\n\t"
       "s_sub_i32 %[o], %[lastw], %[wi]\n\t"
       "s_ashr_i32 %[o], %[o], 31\n\t"
@@ -2653,38 +2654,38 @@ __device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, ui
       "s_lshl_b32 %[o], %[o], 2\n\t"
       "s_load_dword %[nx], %[w], %[o]\n\t"
       "s_branch 1b\n"
-      // a stop entry: EOBr (s = 0) ends the block with an EOB run of
+      // not taken: an EOBr (stop, s = 0) ends the block with an EOB run of
       // 2^r + r more bits (r <= 14: the code is <= 6 bits, so >= 26 bits
       // are in the buffer); anything else is the general step's
       "6:\n\t"
-      "s_cmp_eq_u32 %[e], 0\n\t"
-      "s_cbranch_scc1 9f\n\t"
+      "s_bitcmp1_b32 %[e], 6\n\t"
+      "s_cbranch_scc0 9f\n\t"
       "s_bfe_u32 %[u], %[e], 0x4000c\n\t"
       "s_cmp_lg_u32 %[u], 0\n\t"
       "s_cbranch_scc1 9f\n\t"
-      "s_bfe_u32 %[u], %[e], 0x50016\n\t"
-      "s_lshl_b64 s[40:41], s[40:41], %[u]\n\t"
-      "s_sub_i32 %[cnt], %[cnt], %[u]\n\t"
-      "s_bfe_u32 %[r], %[e], 0x40008\n\t"
+      "s_lshl_b64 s[40:41], s[40:41], %[e]\n\t"
       "s_lshl_b32 %[eob], 1, %[r]\n\t"
       "s_sub_i32 %[o], 64, %[r]\n\t"
       "s_pack_ll_b32_b16 %[o], %[o], %[r]\n\t"
       "s_bfe_u64 s[42:43], s[40:41], %[o]\n\t"
       "s_add_i32 %[eob], %[eob], s42\n\t"
       "s_lshl_b64 s[40:41], s[40:41], %[r]\n\t"
-      "s_sub_i32 %[cnt], %[cnt], %[r]\n\t"
       "s_add_i32 %[nsym], %[nsym], 1\n\t"
       "s_mov_b32 %[ended], 2\n\t"
       "s_branch 9f\n"
       "8:\n\t"
       "s_mov_b32 %[ended], 1\n"
       "9:\n\t"
+      // the bit count back from the marker
+      "s_ff1_i32_b64 %[o], s[40:41]\n\t"
+      "s_bitset0_b64 s[40:41], %[o]\n\t"
+      "s_sub_i32 %[cnt], 63, %[o]\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
       : "+{s[40:41]}"(buf), [cnt] "+s"(cnt), [wi] "+s"(wi), [nxm] "+s"(nxm), [nx] "+s"(nx),
         [k] "+s"(k), [zi] "+s"(zi), [corr] "+s"(corr), [nm] "+s"(nm), [nsg] "+s"(nsg),
         [nsym] "+s"(nsym), [eob] "+s"(eobrun), [ended] "=&s"(ended), [i] "=&s"(i), [e] "=&s"(e),
         [r] "=&s"(r), [t] "=&s"(t), [p] "=&s"(p), [c] "=&s"(c), [o] "=&s"(o), [u] "=&s"(u),
-        [s1] "=&s"(s1), [q] "=&s"(q), [x] "=&s"(x), [y] "=&s"(y)
+        [x] "=&s"(x), [y] "=&s"(y)
       : [l1] "v"(l1), [zpos] "v"(zpos), [se] "s"(se), [lastw] "s"(lastw), [w] "s"(w)
       : "s42", "s43", "scc", "memory");
 }
@@ -3205,9 +3206,9 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
               }
               e = rt_entry_ref(atr, br.peek16());
               nsym++;
-              br.skip((int)((e >> 22) & 31u));
+              br.skip((int)(e & 31u));
               const int s1 = (int)((e >> 7) & 1u);
-              int stop = (int)(e >> 31);
+              int stop = (int)((e >> 6) & 1u);
               ms_opaque(stop);  // (as a compare result it went through the VALU: illegal copy)
               const int r = (int)((e >> 8) & 15u);
               // the new coefficient's sign (bit 1: positive)
@@ -3337,6 +3338,31 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
   }
   if (rc == kOk) rc = br.truncated() ? kErrTruncated : kOk;
   return rc;
+}
+
+// The AC refinement scan decoder as a function of its own: inlined into the
+// kernel it shares the SGPR budget with every other scan kind and the
+// kernel's state (104 SGPRs, spilled to VGPR lanes around the symbol loop);
+// called, it gets the registers to itself (arguments arrive in VGPRs:
+// readfirstlane).  Returns {status, symbols}.
+template <class Rd>
+__device__ __noinline__ int2 ms_decode_refine(MsShared& S, int si, uint64_t soft, MsGeo g,
+                                              const ImageInfo& in, const uint8_t* d,
+                                              const uint8_t* cl, int size, int32_t* lv,
+                                              uint64_t* masks, int lane) {
+  g.ncomp = ms_i(g.ncomp);
+  g.mcux = ms_i(g.mcux);
+  g.bpm = ms_i(g.bpm);
+  g.hv = ms_u(g.hv);
+  const auto up = [](auto* q) {
+    return reinterpret_cast<decltype(q)>(ms_u64((uint64_t)(uintptr_t)q));
+  };
+  int nsym = 0;
+  int64_t prof[3] = {0, 0, 0};
+  const int rc = ms_decode_scan<kScanAcRefine, Rd>(S, ms_i(si), ms_u64(soft), g, *up(&in), up(d),
+                                                   up(cl), ms_i(size), up(lv), up(masks), lane,
+                                                   nsym, prof);
+  return make_int2(rc, nsym);
 }
 
 __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restrict__ bytes,
@@ -3719,7 +3745,18 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
       else if (bd.ah == 0)
         rc = HJ_MS_SCAN(kScanAcFirst);
       else
-        rc = HJ_MS_SCAN(kScanAcRefine);
+#ifdef HJ_MS_PROF
+        rc = HJ_MS_SCAN(kScanAcRefine);  // (the profile reads prof[])
+#else
+      {
+        const int2 rn = wr ? ms_decode_refine<MsWBits>(S, si, soft, geo, in, d, cl, sizeu, lv,
+                                                       masks, lane)
+                           : ms_decode_refine<MsBits>(S, si, soft, geo, in, d, cl, sizeu, lv,
+                                                      masks, lane);
+        rc = ms_i(rn.x);
+        nsym = ms_i(rn.y);
+      }
+#endif
 #undef HJ_MS_SCAN
       // the scan's stores are visible before it counts as done
       ms_publish(S, si, 1 << 30);
