@@ -2512,18 +2512,20 @@ __device__ __forceinline__ uint32_t rt_entry(const RTab& t, uint32_t w16) {
 
 // AC refinement entries: the symbol's fields the symbol loop needs, unpacked
 // once per table instead of once per symbol:
-//   bits 0-5   code length (0: bad code): a 64-bit shift by the entry itself
-//              skips the code
+//   bits 0-5   the bits before the sign bit: the code length, one less for
+//              ZRL (no sign bit: the "sign" read is the code's last bit and
+//              its new-coefficient flag is 0) -- a 64-bit shift by the
+//              entry itself takes them
 //   bit 6      stop: EOBr, or s > 1 (an error), or a bad code
 //   bit 7      s == 1 (a new coefficient)
-//   bits 8-11  r;  bits 12-15  s
-//   bit 31     not a plain new-coefficient symbol (s != 1): ZRL, stop --
-//              so every entry ms_ref_fast takes is > 0
+//   bits 8-11  r;  bits 12-15  s;  bits 16-20  the code length (0: bad)
+//   bit 31     stop -- every entry ms_ref_fast takes is > 0
 __device__ __forceinline__ uint32_t ms_ref_pack(uint32_t L, int sym) {
   const int s = sym & 15, r = sym >> 4;
-  const uint32_t stop = ((s == 0 && r != 15) || s > 1) ? 1u : 0u;
-  return L | stop << 6 | (s == 1 ? 1u : 0u) << 7 | (uint32_t)r << 8 | (uint32_t)s << 12 |
-         (s != 1 ? 1u : 0u) << 31;
+  const bool zrl = s == 0 && r == 15;
+  const uint32_t stop = (s > 1 || (s == 0 && !zrl)) ? 1u : 0u;
+  return (zrl ? L - 1u : L) | stop << 6 | (s == 1 ? 1u : 0u) << 7 | (uint32_t)r << 8 |
+         (uint32_t)s << 12 | L << 16 | stop << 31;
 }
 constexpr uint32_t kRefBad = 0x8000F040u;  // bad code: length 0, stop, s 15
 // (per lane, on a built table's first level)
@@ -2544,42 +2546,41 @@ __device__ __forceinline__ uint32_t rt_entry_ref(const RTab& t, uint32_t w16) {
   return e;
 }
 
-// The refinement symbol loop's common case in straight scalar code
-// (MsWBits reader): new-coefficient symbols (s = 1) with a code of <= 6
-// bits that do not run past the band's zeros and take <= 15 correction
-// bits, and the EOBr that ends a block.  A symbol is two v_readlane (entry,
-// zero place), ~29 scalar instructions and two conditional branches, two
-// symbols per taken branch; the compiled loop of the same step took ~78
-// instructions, with register copies at its join points and a wait for the
-// refill's prefetch on every symbol.  The buffer carries a marker bit right
-// below its valid bits (>= 32 valid bits <=> a non-zero low word), so the
-// loop keeps no bit count.  It returns BEFORE a symbol it does not take (the
-// general step in ms_decode_scan decodes that one), or after the symbol that
-// ends the band (ended = 1) or an EOBr (ended = 2, eobrun set); state in/out
-// as MsWBits / the symbol loop keep it.  zpos lanes >= nzero hold a sentinel
-// > 63 + 15 + 15, so a run past the band's zeros fails the <= 15 test (a zero
-// index >= 64 reads lane t - 64, a zero before k: the difference is
-// negative, and fails it too).  Entry: >= 32 bits in the buffer.  The
-// refill's scalar load is waited for before the return (the compiler does
-// not count the statement's loads).
-#define HJ_REF_SYM                                                      \
-  /* entry of the code at the top 6 bits; zero place (zi + r)-th */     \
-  "s_lshr_b32 %[i], s41, 26\n\t"                                        \
-  "v_readlane_b32 %[e], %[l1], %[i]\n\t"                                \
+// The refinement symbol loop in straight scalar code (MsWBits reader):
+// new-coefficient and ZRL symbols that do not run past the band's zeros and
+// take <= 15 correction bits, codes of <= 6 bits from the lane table, longer
+// ones by the canonical limits (one ballot), and the EOBr that ends a block.
+// A symbol is two v_readlane (entry, zero place), ~30 scalar instructions
+// and two conditional branches, two symbols per taken branch; the compiled
+// loop of the same step took ~78 instructions, with register copies at its
+// join points and a wait for the refill's prefetch on every symbol.  The
+// buffer carries a marker bit right below its valid bits (>= 32 valid bits
+// <=> a non-zero low word), so the loop keeps no bit count.  It returns
+// BEFORE a symbol it does not take (the general step in ms_decode_scan
+// decodes that one), or after the symbol that ends the band (ended = 1) or
+// an EOBr (ended = 2, eobrun set); state in/out as MsWBits / the symbol loop
+// keep it.  zpos lanes >= nzero hold a sentinel > 63 + 15 + 15, so a run past
+// the band's zeros fails the <= 15 test (a zero index >= 64 reads lane
+// t - 64, a zero before k: the difference is negative, and fails it too).
+// Entry: >= 32 bits in the buffer.  The refill's scalar load is waited for
+// before the return (the compiler does not count the statement's loads).
+#define HJ_REF_BODY(EXIT)                                               \
+  /* the new coefficient's place: the (zi + r)-th zero */               \
   "s_bfe_u32 %[r], %[e], 0x40008\n\t"                                   \
   "s_add_i32 %[t], %[zi], %[r]\n\t"                                     \
   "v_readlane_b32 %[p], %[zpos], %[t]\n\t"                              \
   /* correction bits: the history coefficients passed; leave if > 15 */ \
-  /* or the entry is not a plain symbol (<= 0) */                       \
+  /* or the entry is a stop or a long code (<= 0) */                    \
   "s_sub_i32 %[c], %[p], %[k]\n\t"                                      \
   "s_sub_i32 %[c], %[c], %[r]\n\t"                                      \
   "s_cmp_lt_i32 %[e], 1\n\t"                                            \
   "s_cselect_b32 %[c], 64, %[c]\n\t"                                    \
   "s_cmp_gt_u32 %[c], 15\n\t"                                           \
-  "s_cbranch_scc1 6f\n\t"                                               \
+  "s_cbranch_scc1 " EXIT "\n\t"                                         \
   /* past the code: the sign bit on top (1: positive), then c bits */   \
   "s_lshl_b64 s[42:43], s[40:41], %[e]\n\t"                             \
-  "s_lshl_b64 %[x], 1, %[p]\n\t"                                        \
+  "s_bfe_u32 %[u], %[e], 0x10007\n\t"                                   \
+  "s_bfm_b64 %[x], %[u], %[p]\n\t"                                      \
   "s_or_b64 %[nm], %[nm], %[x]\n\t"                                     \
   "s_cmp_lt_i32 s43, 0\n\t"                                             \
   "s_cselect_b64 %[y], 0, %[x]\n\t"                                     \
@@ -2598,11 +2599,16 @@ __device__ __forceinline__ uint32_t rt_entry_ref(const RTab& t, uint32_t w16) {
   "s_cmp_ge_i32 %[p], %[se]\n\t"                                        \
   "s_cselect_b32 %[u], 0, s40\n\t"                                      \
   "s_cmp_lg_u32 %[u], 0\n\t"
+#define HJ_REF_SYM                                                      \
+  /* entry of the code at the top 6 bits (0: a longer code) */          \
+  "s_lshr_b32 %[i], s41, 26\n\t"                                        \
+  "v_readlane_b32 %[e], %[l1], %[i]\n\t"                                \
+  HJ_REF_BODY("6f")
 
 __device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, uint32_t& nxm,
                                             uint32_t& nx, MsWords w, int lastw, int& k, int& zi,
                                             uint64_t& corr, uint64_t& nm, uint64_t& nsg,
-                                            int& nsym, int se, uint32_t l1, uint32_t zpos,
+                                            int& nsym, int se, const RTab& tab, uint32_t zpos,
                                             int& eobrun, int& ended) {
   uint32_t i, e, r, t, p, c, o, u;
   uint64_t x, y;
@@ -2654,10 +2660,41 @@ __device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, ui
       "s_lshl_b32 %[o], %[o], 2\n\t"
       "s_load_dword %[nx], %[w], %[o]\n\t"
       "s_branch 1b\n"
-      // not taken: an EOBr (stop, s = 0) ends the block with an EOB run of
+      // not taken: a code longer than 6 bits (e = 0) by the canonical
+      // limits -- length 1 + #{l : lim[l] <= w16} -- and its symbol; a
+      // plain (s = 1) symbol goes on in line, the rest is the general step's
+      "6:\n\t"
+      "s_cmp_eq_u32 %[e], 0\n\t"
+      "s_cbranch_scc0 5f\n\t"
+      "s_lshr_b32 %[i], s41, 16\n\t"
+      "v_cmp_ge_u32_e32 vcc, %[i], %[lim]\n\t"
+      "s_bcnt1_i32_b64 %[t], vcc\n\t"
+      "s_add_i32 %[t], %[t], 1\n\t"
+      "s_cmp_gt_u32 %[t], 16\n\t"
+      "s_cbranch_scc1 9f\n\t"
+      "v_readlane_b32 %[o], %[voff], %[t]\n\t"
+      "s_sub_i32 %[u], 16, %[t]\n\t"
+      "s_lshr_b32 %[i], %[i], %[u]\n\t"
+      "s_add_i32 %[i], %[i], %[o]\n\t"
+      "s_lshr_b32 %[u], %[i], 2\n\t"
+      "v_readlane_b32 %[o], %[vals], %[u]\n\t"
+      "s_and_b32 %[i], %[i], 3\n\t"
+      "s_lshl_b32 %[i], %[i], 3\n\t"
+      "s_lshr_b32 %[o], %[o], %[i]\n\t"
+      "s_and_b32 %[u], %[o], 15\n\t"
+      "s_cmp_eq_u32 %[u], 1\n\t"
+      "s_cbranch_scc0 9f\n\t"
+      "s_bfe_u32 %[e], %[o], 0x40004\n\t"
+      "s_lshl_b32 %[e], %[e], 8\n\t"
+      "s_or_b32 %[e], %[e], %[t]\n\t"
+      "s_or_b32 %[e], %[e], 0x80\n\t"
+      HJ_REF_BODY("6b")
+      "s_cbranch_scc1 1b\n\t"
+      "s_branch 7b\n"
+      // a stop entry: EOBr (s = 0) ends the block with an EOB run of
       // 2^r + r more bits (r <= 14: the code is <= 6 bits, so >= 26 bits
       // are in the buffer); anything else is the general step's
-      "6:\n\t"
+      "5:\n\t"
       "s_bitcmp1_b32 %[e], 6\n\t"
       "s_cbranch_scc0 9f\n\t"
       "s_bfe_u32 %[u], %[e], 0x4000c\n\t"
@@ -2686,10 +2723,12 @@ __device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, ui
         [nsym] "+s"(nsym), [eob] "+s"(eobrun), [ended] "=&s"(ended), [i] "=&s"(i), [e] "=&s"(e),
         [r] "=&s"(r), [t] "=&s"(t), [p] "=&s"(p), [c] "=&s"(c), [o] "=&s"(o), [u] "=&s"(u),
         [x] "=&s"(x), [y] "=&s"(y)
-      : [l1] "v"(l1), [zpos] "v"(zpos), [se] "s"(se), [lastw] "s"(lastw), [w] "s"(w)
-      : "s42", "s43", "scc", "memory");
+      : [l1] "v"(tab.l1), [lim] "v"(tab.lim), [voff] "v"(tab.voff), [vals] "v"(tab.vals),
+        [zpos] "v"(zpos), [se] "s"(se), [lastw] "s"(lastw), [w] "s"(w)
+      : "s42", "s43", "vcc", "scc", "memory");
 }
 #undef HJ_REF_SYM
+#undef HJ_REF_BODY
 
 // bits k .. e (inclusive) of a coefficient mask; 0 when k > e
 __device__ __forceinline__ uint64_t ms_range(int k, int e) {
@@ -3196,7 +3235,12 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
                 const int k0 = k;
                 int ended;
                 ms_ref_fast(br.buf, br.cnt, br.wi, br.nxm, br.nx, br.w, br.lastw, k, zi, corr, nm,
-                            nsg, nsym, se, atr.l1, zpos, eobrun, ended);
+                            nsg, nsym, se, atr, zpos, eobrun, ended);
+#ifdef HJ_MS_COUNT2
+                prof[0] += 0;
+#elif defined(HJ_MS_COUNT)
+                prof[0] += 256;  // (count build: fast-loop calls, blocks, general steps)
+#endif
                 cb += __popcll(hist & ms_range(k0, k - 1));
                 if (ended) {  // (1: the band's end; 2: an EOBr, eobrun set)
                   e = kRefDone;
@@ -3206,7 +3250,16 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
               }
               e = rt_entry_ref(atr, br.peek16());
               nsym++;
-              br.skip((int)(e & 31u));
+#ifdef HJ_MS_COUNT2
+              // (second count build: general steps by kind -- long code / ZRL /
+              // other)
+              if (((e >> 16) & 31u) > 6u) prof[0] += 256;
+              else if (((e >> 8) & 15u) == 15u && ((e >> 12) & 15u) == 0u) prof[1] += 256;
+              else prof[2] += 256;
+#elif defined(HJ_MS_COUNT)
+              prof[2] += 256;
+#endif
+              br.skip((int)((e >> 16) & 31u));
               const int s1 = (int)((e >> 7) & 1u);
               int stop = (int)((e >> 6) & 1u);
               ms_opaque(stop);  // (as a compare result it went through the VALU: illegal copy)
@@ -3272,7 +3325,11 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
           ch.whi = ms_wl(ch.whi, (uint32_t)(nm >> 32), j);
           ch.slo = ms_wl(ch.slo, (uint32_t)nsg, j);
           ch.shi = ms_wl(ch.shi, (uint32_t)(nsg >> 32), j);
-#ifdef HJ_MS_PROF
+#ifdef HJ_MS_COUNT
+#ifndef HJ_MS_COUNT2
+          prof[1] += 256;
+#endif
+#elif defined(HJ_MS_PROF)
           const int64_t pt3 = (int64_t)__builtin_amdgcn_s_memtime();
           prof[0] += pt1 - pt0;
           prof[1] += pt2 - pt1;
