@@ -2550,7 +2550,7 @@ __device__ __forceinline__ uint32_t rt_entry_ref(const RTab& t, uint32_t w16) {
 // new-coefficient and ZRL symbols that do not run past the band's zeros and
 // take <= 15 correction bits, codes of <= 6 bits from the lane table, longer
 // ones by the canonical limits (one ballot), and the EOBr that ends a block.
-// A symbol is two v_readlane (entry, zero place), ~30 scalar instructions
+// A symbol is two v_readlane (entry, zero place), ~29 scalar instructions
 // and two conditional branches, two symbols per taken branch; the compiled
 // loop of the same step took ~78 instructions, with register copies at its
 // join points and a wait for the refill's prefetch on every symbol.  The
@@ -2594,7 +2594,6 @@ __device__ __forceinline__ uint32_t rt_entry_ref(const RTab& t, uint32_t w16) {
   "s_lshl_b64 s[40:41], s[42:43], %[u]\n\t"                             \
   "s_add_i32 %[k], %[p], 1\n\t"                                         \
   "s_add_i32 %[zi], %[t], 1\n\t"                                        \
-  "s_add_i32 %[nsym], %[nsym], 1\n\t"                                   \
   /* on while the band goes on and >= 32 bits are left */              \
   "s_cmp_ge_i32 %[p], %[se]\n\t"                                        \
   "s_cselect_b32 %[u], 0, s40\n\t"                                      \
@@ -2960,6 +2959,166 @@ __device__ __forceinline__ void ms_put(int i, int32_t (&v)[kMaxComp], int32_t x)
   v[3] = i == 3 ? x : v[3];
 }
 
+// One block of an AC refinement scan against its history mask (lane j of
+// the chunk): the symbols, the correction bits, the records of lane j.
+template <class Rd>
+__device__ __forceinline__ int ms_refine_block(Rd& br, MsChunk& ch, const int j,
+                                               const uint64_t band, const int ss, const int se,
+                                               const int lane, const RTab& atr, int& eobrun,
+                                               int& nsym, int64_t (&prof)[3]) {
+  constexpr bool kWord = ms_same<Rd, MsWBits>::value;
+  int rc = kOk;
+  // against the block's non-zero mask (lane j of the chunk)
+#ifdef HJ_MS_PROF
+  const int64_t pt0 = (int64_t)__builtin_amdgcn_s_memtime();
+  int64_t pt1 = pt0;
+#endif
+  const uint64_t hist = ((uint64_t)ms_rl(ch.mhi, j) << 32 | ms_rl(ch.mlo, j)) & band;
+  const int htot = __popcll(hist);
+  uint64_t corr = 0, nm = 0, nsg = 0;
+  int cb = 0;  // correction bits taken (non-zero history coefficients passed)
+  if (eobrun <= 0) {
+    // zpos lane i: the place of the band's i-th coefficient that was
+    // zero before the scan (a lane permutation: the others go after)
+    const uint64_t hz = ~hist & band;
+    const int nzero = __popcll(hz);
+    const int below = (int)__builtin_amdgcn_mbcnt_hi(
+        (uint32_t)(hz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hz, 0u));
+    const bool isz = (hz >> lane) & 1ull;
+    uint32_t zpos = (uint32_t)__builtin_amdgcn_ds_permute(
+        (isz ? below : nzero + lane - below) << 2, lane);
+    zpos = lane < nzero ? zpos : 127u;  // (past the zeros: ms_ref_fast's sentinel)
+    // One exit, at the bottom: the rare ends (EOBr, a run past se, a
+    // bad code) only clear `live` and are sorted out after the loop,
+    // so the symbol step is straight-line scalar code (flags as 0/1
+    // integers, not compare results).
+    int k = ss, zi = 0;  // next coefficient; zeros before it
+    uint32_t e;
+    int t, cont;
+    constexpr uint32_t kRefDone = 15u << 8;  // (s = 0, r = 15: no EOBr, no error)
+    // zpos is waited for here, once: in the loop the LDS and scalar
+    // load counters are one, and a wait for it there would also wait
+    // for the bit reader's prefetch
+    asm volatile("" ::"s"(ms_rl(zpos, 0)));
+#ifdef HJ_MS_PROF
+    pt1 = (int64_t)__builtin_amdgcn_s_memtime();
+#endif
+    // (the refill at the bottom: the common path falls through)
+    br.need();
+    do {
+      if constexpr (kWord) {
+        // the common symbols in ms_ref_fast; it returns before one it
+        // does not take, or after the one that ends the band
+        const int k0 = k;
+        const uint64_t nm0 = nm;
+        int ended;
+        ms_ref_fast(br.buf, br.cnt, br.wi, br.nxm, br.nx, br.w, br.lastw, k, zi, corr, nm,
+                    nsg, nsym, se, atr, zpos, eobrun, ended);
+#ifdef HJ_MS_COUNT2
+        prof[0] += 0;
+#elif defined(HJ_MS_COUNT)
+        prof[0] += 256;  // (count build: fast-loop calls, blocks, general steps)
+#endif
+        cb += __popcll(hist & ms_range(k0, k - 1));
+        // (symbols: the loop counts only EOBr; its new coefficients
+        // here, its ZRL not at all)
+        nsym += __popcll(nm) - __popcll(nm0);
+        if (ended) {  // (1: the band's end; 2: an EOBr, eobrun set)
+          e = kRefDone;
+          t = 0;
+          break;
+        }
+      }
+      e = rt_entry_ref(atr, br.peek16());
+      nsym++;
+#ifdef HJ_MS_COUNT2
+      // (second count build: general steps by kind -- long code / ZRL /
+      // other)
+      if (((e >> 16) & 31u) > 6u) prof[0] += 256;
+      else if (((e >> 8) & 15u) == 15u && ((e >> 12) & 15u) == 0u) prof[1] += 256;
+      else prof[2] += 256;
+#elif defined(HJ_MS_COUNT)
+      prof[2] += 256;
+#endif
+      br.skip((int)((e >> 16) & 31u));
+      const int s1 = (int)((e >> 7) & 1u);
+      int stop = (int)((e >> 6) & 1u);
+      ms_opaque(stop);  // (as a compare result it went through the VALU: illegal copy)
+      const int r = (int)((e >> 8) & 15u);
+      // the new coefficient's sign (bit 1: positive)
+      uint32_t h = br.hi32();
+      ms_opaque(h);
+      const uint32_t neg = (~h >> 31) & (uint32_t)s1;
+      br.skip(s1);
+      // the (r + 1)-th coefficient from k that was zero before the
+      // scan is the new coefficient's place (ZRL: the 16th, left
+      // zero); each non-zero one passed on the way takes a
+      // correction bit
+      t = zi + r;
+      // (sign bits, not compares: a compare result the loop keeps
+      // would become a lane mask and go through the VALU)
+      uint32_t dz = (uint32_t)(t - nzero);
+      ms_opaque(dz);
+      const int live = (int)(dz >> 31) & (stop ^ 1);
+      const int lm = -live;
+      const int p = (int)ms_rl(zpos, t & lm);
+      const int c = (p - k - r) & lm;
+      if (__builtin_expect(c <= 15, 1)) {  // (>= 15 bits are left after a code and a sign)
+        uint32_t hc = br.hi32();
+        ms_opaque(hc);
+        corr = (corr << c) | ((hc >> 1) >> (31 - c));
+        br.skip(c);
+      } else {
+        ms_take_corr_long(br, c, corr);
+      }
+      cb += c;
+      const uint32_t m1 = (uint32_t)(s1 & live);
+      nm |= (uint64_t)m1 << p;
+      nsg |= (uint64_t)(m1 & neg) << p;
+      k = p + 1;
+      zi = t + 1;
+      // (k <= se, i.e. p < se: a sign bit)
+      uint32_t dk = (uint32_t)(p - se);
+      ms_opaque(dk);
+      cont = live & (int)(dk >> 31);
+      ms_opaque(cont);
+      br.need();
+    } while (__builtin_expect(cont, 1));
+    const int r = (int)((e >> 8) & 15u), s = (int)((e >> 12) & 15u);
+    if (s > 1 || (s == 1 && t >= nzero)) {
+      rc = kErrBadHuffman;  // (a bad code, a value other than +-1, a new coefficient past se)
+    } else if (s == 0 && r != 15) {  // EOBr
+      eobrun = 1 << r;
+      if (r) eobrun += (int)br.take(r);
+    }
+  }
+#ifdef HJ_MS_PROF
+  const int64_t pt2 = (int64_t)__builtin_amdgcn_s_memtime();
+#endif
+  if (rc != kOk) return rc;
+  // the history coefficients after the last symbol (an EOB run, or a
+  // run past se) take their correction bits
+  ms_take_corr(br, htot - cb, corr);
+  if (eobrun > 0) eobrun--;
+  ch.clo = ms_wl(ch.clo, (uint32_t)corr, j);
+  ch.chi = ms_wl(ch.chi, (uint32_t)(corr >> 32), j);
+  ch.wlo = ms_wl(ch.wlo, (uint32_t)nm, j);
+  ch.whi = ms_wl(ch.whi, (uint32_t)(nm >> 32), j);
+  ch.slo = ms_wl(ch.slo, (uint32_t)nsg, j);
+  ch.shi = ms_wl(ch.shi, (uint32_t)(nsg >> 32), j);
+#ifdef HJ_MS_COUNT
+#ifndef HJ_MS_COUNT2
+  prof[1] += 256;
+#endif
+#elif defined(HJ_MS_PROF)
+  const int64_t pt3 = (int64_t)__builtin_amdgcn_s_memtime();
+  prof[0] += pt1 - pt0;
+  prof[1] += pt2 - pt1;
+  prof[2] += pt3 - pt2;
+#endif
+  return rc;
+}
+
 // Decode one scan (a whole decoder wave, uniform control flow).
 // lv: the image's levels (64 int32 per block, zig-zag); masks: per block the
 // coefficients non-zero so far (AC bands of progressive images); soft: the
@@ -3190,151 +3349,9 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
           }
           if ((mcu & (kMsChunk - 1)) == kMsChunk - 1) ms_publish(S, si, mcu + 1);
         } else if constexpr (kind == kScanAcRefine) {
-          // against the block's non-zero mask (lane j of the chunk)
-#ifdef HJ_MS_PROF
-          const int64_t pt0 = (int64_t)__builtin_amdgcn_s_memtime();
-          int64_t pt1 = pt0;
-#endif
-          const int j = mcu & (kMsChunk - 1);
-          const uint64_t hist = ((uint64_t)ms_rl(ch.mhi, j) << 32 | ms_rl(ch.mlo, j)) & band;
-          const int htot = __popcll(hist);
-          uint64_t corr = 0, nm = 0, nsg = 0;
-          int cb = 0;  // correction bits taken (non-zero history coefficients passed)
-          if (eobrun <= 0) {
-            // zpos lane i: the place of the band's i-th coefficient that was
-            // zero before the scan (a lane permutation: the others go after)
-            const uint64_t hz = ~hist & band;
-            const int nzero = __popcll(hz);
-            const int below = (int)__builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(hz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hz, 0u));
-            const bool isz = (hz >> lane) & 1ull;
-            uint32_t zpos = (uint32_t)__builtin_amdgcn_ds_permute(
-                (isz ? below : nzero + lane - below) << 2, lane);
-            zpos = lane < nzero ? zpos : 127u;  // (past the zeros: ms_ref_fast's sentinel)
-            // One exit, at the bottom: the rare ends (EOBr, a run past se, a
-            // bad code) only clear `live` and are sorted out after the loop,
-            // so the symbol step is straight-line scalar code (flags as 0/1
-            // integers, not compare results).
-            int k = ss, zi = 0;  // next coefficient; zeros before it
-            uint32_t e;
-            int t, cont;
-            constexpr uint32_t kRefDone = 15u << 8;  // (s = 0, r = 15: no EOBr, no error)
-            // zpos is waited for here, once: in the loop the LDS and scalar
-            // load counters are one, and a wait for it there would also wait
-            // for the bit reader's prefetch
-            asm volatile("" ::"s"(ms_rl(zpos, 0)));
-#ifdef HJ_MS_PROF
-            pt1 = (int64_t)__builtin_amdgcn_s_memtime();
-#endif
-            // (the refill at the bottom: the common path falls through)
-            br.need();
-            do {
-              if constexpr (kWord) {
-                // the common symbols in ms_ref_fast; it returns before one it
-                // does not take, or after the one that ends the band
-                const int k0 = k;
-                int ended;
-                ms_ref_fast(br.buf, br.cnt, br.wi, br.nxm, br.nx, br.w, br.lastw, k, zi, corr, nm,
-                            nsg, nsym, se, atr, zpos, eobrun, ended);
-#ifdef HJ_MS_COUNT2
-                prof[0] += 0;
-#elif defined(HJ_MS_COUNT)
-                prof[0] += 256;  // (count build: fast-loop calls, blocks, general steps)
-#endif
-                cb += __popcll(hist & ms_range(k0, k - 1));
-                if (ended) {  // (1: the band's end; 2: an EOBr, eobrun set)
-                  e = kRefDone;
-                  t = 0;
-                  break;
-                }
-              }
-              e = rt_entry_ref(atr, br.peek16());
-              nsym++;
-#ifdef HJ_MS_COUNT2
-              // (second count build: general steps by kind -- long code / ZRL /
-              // other)
-              if (((e >> 16) & 31u) > 6u) prof[0] += 256;
-              else if (((e >> 8) & 15u) == 15u && ((e >> 12) & 15u) == 0u) prof[1] += 256;
-              else prof[2] += 256;
-#elif defined(HJ_MS_COUNT)
-              prof[2] += 256;
-#endif
-              br.skip((int)((e >> 16) & 31u));
-              const int s1 = (int)((e >> 7) & 1u);
-              int stop = (int)((e >> 6) & 1u);
-              ms_opaque(stop);  // (as a compare result it went through the VALU: illegal copy)
-              const int r = (int)((e >> 8) & 15u);
-              // the new coefficient's sign (bit 1: positive)
-              uint32_t h = br.hi32();
-              ms_opaque(h);
-              const uint32_t neg = (~h >> 31) & (uint32_t)s1;
-              br.skip(s1);
-              // the (r + 1)-th coefficient from k that was zero before the
-              // scan is the new coefficient's place (ZRL: the 16th, left
-              // zero); each non-zero one passed on the way takes a
-              // correction bit
-              t = zi + r;
-              // (sign bits, not compares: a compare result the loop keeps
-              // would become a lane mask and go through the VALU)
-              uint32_t dz = (uint32_t)(t - nzero);
-              ms_opaque(dz);
-              const int live = (int)(dz >> 31) & (stop ^ 1);
-              const int lm = -live;
-              const int p = (int)ms_rl(zpos, t & lm);
-              const int c = (p - k - r) & lm;
-              if (__builtin_expect(c <= 15, 1)) {  // (>= 15 bits are left after a code and a sign)
-                uint32_t hc = br.hi32();
-                ms_opaque(hc);
-                corr = (corr << c) | ((hc >> 1) >> (31 - c));
-                br.skip(c);
-              } else {
-                ms_take_corr_long(br, c, corr);
-              }
-              cb += c;
-              const uint32_t m1 = (uint32_t)(s1 & live);
-              nm |= (uint64_t)m1 << p;
-              nsg |= (uint64_t)(m1 & neg) << p;
-              k = p + 1;
-              zi = t + 1;
-              // (k <= se, i.e. p < se: a sign bit)
-              uint32_t dk = (uint32_t)(p - se);
-              ms_opaque(dk);
-              cont = live & (int)(dk >> 31);
-              ms_opaque(cont);
-              br.need();
-            } while (__builtin_expect(cont, 1));
-            const int r = (int)((e >> 8) & 15u), s = (int)((e >> 12) & 15u);
-            if (s > 1 || (s == 1 && t >= nzero)) {
-              rc = kErrBadHuffman;  // (a bad code, a value other than +-1, a new coefficient past se)
-            } else if (s == 0 && r != 15) {  // EOBr
-              eobrun = 1 << r;
-              if (r) eobrun += (int)br.take(r);
-            }
-          }
-#ifdef HJ_MS_PROF
-          const int64_t pt2 = (int64_t)__builtin_amdgcn_s_memtime();
-#endif
+          rc = ms_refine_block(br, ch, mcu & (kMsChunk - 1), band, ss, se, lane, atr, eobrun,
+                               nsym, prof);
           if (rc != kOk) break;
-          // the history coefficients after the last symbol (an EOB run, or a
-          // run past se) take their correction bits
-          ms_take_corr(br, htot - cb, corr);
-          if (eobrun > 0) eobrun--;
-          ch.clo = ms_wl(ch.clo, (uint32_t)corr, j);
-          ch.chi = ms_wl(ch.chi, (uint32_t)(corr >> 32), j);
-          ch.wlo = ms_wl(ch.wlo, (uint32_t)nm, j);
-          ch.whi = ms_wl(ch.whi, (uint32_t)(nm >> 32), j);
-          ch.slo = ms_wl(ch.slo, (uint32_t)nsg, j);
-          ch.shi = ms_wl(ch.shi, (uint32_t)(nsg >> 32), j);
-#ifdef HJ_MS_COUNT
-#ifndef HJ_MS_COUNT2
-          prof[1] += 256;
-#endif
-#elif defined(HJ_MS_PROF)
-          const int64_t pt3 = (int64_t)__builtin_amdgcn_s_memtime();
-          prof[0] += pt1 - pt0;
-          prof[1] += pt2 - pt1;
-          prof[2] += pt3 - pt2;
-#endif
         } else {  // sequential: the whole block
           br.need();
           int len;
@@ -3397,6 +3414,68 @@ __device__ __forceinline__ int ms_decode_scan(MsShared& S, int si, uint64_t soft
   return rc;
 }
 
+// An AC refinement scan over the destuffed copy (no restart markers): the
+// block loop of ms_decode_scan without its per-MCU bookkeeping (block
+// coordinates, predictors, restart intervals, scan components) -- a chunk of
+// kMsChunk blocks is loaded, decoded block by block, applied and published.
+__device__ __forceinline__ int ms_refine_word(MsShared& S, const int si, const uint64_t soft,
+                                              const MsGeo& g, const ImageInfo& in,
+                                              const uint8_t* __restrict__ d, const uint8_t* cl,
+                                              int32_t* __restrict__ lv,
+                                              uint64_t* __restrict__ masks, const int lane,
+                                              int& nsym, int64_t (&prof)[3]) {
+  const MsScan& scl = S.scan[si];
+  const MsBand sc = ms_band(scl);
+  const int o = ms_i(scl.dht[4 + ms_i(scl.ta[0])]);
+  if (o < 0) return kErrBadHeader;
+  bool bad = false;
+  RTab atr = rt_build(d, o, lane, bad);
+  if (bad) return kErrBadHeader;
+  atr.l1 = ms_ref_l1(atr.l1);
+  const int c1 = ms_i(scl.comp[0]);
+  const int bw1 = g.ncomp == 1 ? g.mcux : (ms_i(in.comp_w[c1]) + 7) / 8;
+  const int nmcu = bw1 * (g.ncomp == 1 ? ms_i(in.mcuy) : (ms_i(in.comp_hpx[c1]) + 7) / 8);
+  MsWBits br;
+  br.init(cl + ms_i(S.dbase[si]), ms_i(S.dlen[si]));
+  const int al = sc.al, ss = sc.ss, se = sc.se;
+  const uint64_t band = ms_range(ss, se);
+  int eobrun = 0, rc = kOk;
+  MsChunk ch;
+  ch.blk = -1;
+  bool have_next = false;
+  for (int m0 = 0; m0 < nmcu; m0 += kMsChunk) {
+    const int nxt = min(m0 + kMsChunk, nmcu);
+    // levels and masks of the chunk once the scans this one trails are past it
+    if (!have_next) {
+      if (!ms_wait(S, soft, nxt)) return kErrBadHuffman;  // (another scan failed)
+      ch.nblk = ms_lane_block(g, c1, bw1, nmcu, m0 + lane);
+      const uint64_t m = ch.nblk >= 0 ? masks[ch.nblk] : 0ull;
+      ch.nlo = (uint32_t)m;
+      ch.nhi = (uint32_t)(m >> 32);
+    }
+    ch.mlo = ch.nlo;
+    ch.mhi = ch.nhi;
+    ms_chunk_load(ch, lv, ch.nblk);
+    ch.clo = ch.chi = ch.wlo = ch.whi = ch.slo = ch.shi = 0;
+    // the next chunk's masks now, if its producers are already past it
+    have_next = nxt < nmcu && ms_reached(S, soft, min(nxt + kMsChunk, nmcu));
+    if (have_next) {
+      ch.nblk = ms_lane_block(g, c1, bw1, nmcu, nxt + lane);
+      const uint64_t m = ch.nblk >= 0 ? masks[ch.nblk] : 0ull;
+      ch.nlo = (uint32_t)m;
+      ch.nhi = (uint32_t)(m >> 32);
+    }
+    const int nb = nxt - m0;
+    for (int j = 0; j < nb; j++) {
+      rc = ms_refine_block(br, ch, j, band, ss, se, lane, atr, eobrun, nsym, prof);
+      if (rc != kOk) return rc;
+    }
+    ms_chunk_apply(ch, lv, masks, ss, se, al);
+    ms_publish(S, si, nxt);
+  }
+  return br.truncated() ? kErrTruncated : kOk;
+}
+
 // The AC refinement scan decoder as a function of its own: inlined into the
 // kernel it shares the SGPR budget with every other scan kind and the
 // kernel's state (104 SGPRs, spilled to VGPR lanes around the symbol loop);
@@ -3416,6 +3495,11 @@ __device__ __noinline__ int2 ms_decode_refine(MsShared& S, int si, uint64_t soft
   };
   int nsym = 0;
   int64_t prof[3] = {0, 0, 0};
+  if constexpr (ms_same<Rd, MsWBits>::value) {
+    const int rc = ms_refine_word(S, ms_i(si), ms_u64(soft), g, *up(&in), up(d), up(cl), up(lv),
+                                  up(masks), lane, nsym, prof);
+    return make_int2(rc, nsym);
+  }
   const int rc = ms_decode_scan<kScanAcRefine, Rd>(S, ms_i(si), ms_u64(soft), g, *up(&in), up(d),
                                                    up(cl), ms_i(size), up(lv), up(masks), lane,
                                                    nsym, prof);
