@@ -2512,20 +2512,19 @@ __device__ __forceinline__ uint32_t rt_entry(const RTab& t, uint32_t w16) {
 
 // AC refinement entries: the symbol's fields the symbol loop needs, unpacked
 // once per table instead of once per symbol:
-//   bits 0-5   the bits before the sign bit: the code length, one less for
-//              ZRL (no sign bit: the "sign" read is the code's last bit and
-//              its new-coefficient flag is 0) -- a 64-bit shift by the
-//              entry itself takes them
+//   bits 0-5   the code length: a 64-bit shift by the entry itself skips
+//              the code
 //   bit 6      stop: EOBr, or s > 1 (an error), or a bad code
 //   bit 7      s == 1 (a new coefficient)
 //   bits 8-11  r;  bits 12-15  s;  bits 16-20  the code length (0: bad)
-//   bit 31     stop -- every entry ms_ref_fast takes is > 0
+//   bit 31     not a new-coefficient symbol (stop or ZRL) -- every entry the
+//              fast loop's common step takes is > 0
 __device__ __forceinline__ uint32_t ms_ref_pack(uint32_t L, int sym) {
   const int s = sym & 15, r = sym >> 4;
   const bool zrl = s == 0 && r == 15;
   const uint32_t stop = (s > 1 || (s == 0 && !zrl)) ? 1u : 0u;
-  return (zrl ? L - 1u : L) | stop << 6 | (s == 1 ? 1u : 0u) << 7 | (uint32_t)r << 8 |
-         (uint32_t)s << 12 | L << 16 | stop << 31;
+  return L | stop << 6 | (s == 1 ? 1u : 0u) << 7 | (uint32_t)r << 8 | (uint32_t)s << 12 |
+         L << 16 | (s != 1 ? 1u : 0u) << 31;
 }
 constexpr uint32_t kRefBad = 0x8000F040u;  // bad code: length 0, stop, s 15
 // (per lane, on a built table's first level)
@@ -2547,13 +2546,14 @@ __device__ __forceinline__ uint32_t rt_entry_ref(const RTab& t, uint32_t w16) {
 }
 
 // The refinement symbol loop in straight scalar code (MsWBits reader):
-// new-coefficient and ZRL symbols that do not run past the band's zeros and
-// take <= 15 correction bits, codes of <= 6 bits from the lane table, longer
-// ones by the canonical limits (one ballot), and the EOBr that ends a block.
-// A symbol is two v_readlane (entry, zero place), ~29 scalar instructions
-// and two conditional branches, two symbols per taken branch; the compiled
-// loop of the same step took ~78 instructions, with register copies at its
-// join points and a wait for the refill's prefetch on every symbol.  The
+// new-coefficient symbols that do not run past the band's zeros and take
+// <= 15 correction bits, codes of <= 6 bits from the lane table, longer ones
+// by the canonical limits (one ballot); ZRL and the EOBr that ends a block on
+// side paths.  A symbol is two v_readlane (entry, zero place), ~27 scalar
+// instructions and two conditional branches, two symbols per taken branch;
+// the compiled loop of the same step took ~78 instructions, with register
+// copies at its join points and a wait for the refill's prefetch on every
+// symbol.  The
 // buffer carries a marker bit right below its valid bits (>= 32 valid bits
 // <=> a non-zero low word), so the loop keeps no bit count.  It returns
 // BEFORE a symbol it does not take (the general step in ms_decode_scan
@@ -2577,14 +2577,14 @@ __device__ __forceinline__ uint32_t rt_entry_ref(const RTab& t, uint32_t w16) {
   "s_cselect_b32 %[c], 64, %[c]\n\t"                                    \
   "s_cmp_gt_u32 %[c], 15\n\t"                                           \
   "s_cbranch_scc1 " EXIT "\n\t"                                         \
-  /* past the code: the sign bit on top (1: positive), then c bits */   \
+  /* past the code: the sign bit on top (1: positive), then c bits; */ \
+  /* a positive coefficient sets the sign mask's bit 0 (never a place */ \
+  /* of an AC band) */                                                  \
   "s_lshl_b64 s[42:43], s[40:41], %[e]\n\t"                             \
-  "s_bfe_u32 %[u], %[e], 0x10007\n\t"                                   \
-  "s_bfm_b64 %[x], %[u], %[p]\n\t"                                      \
-  "s_or_b64 %[nm], %[nm], %[x]\n\t"                                     \
+  "s_bitset1_b64 %[nm], %[p]\n\t"                                       \
   "s_cmp_lt_i32 s43, 0\n\t"                                             \
-  "s_cselect_b64 %[y], 0, %[x]\n\t"                                     \
-  "s_or_b64 %[nsg], %[nsg], %[y]\n\t"                                   \
+  "s_cselect_b32 %[u], 0, %[p]\n\t"                                     \
+  "s_bitset1_b64 %[nsg], %[u]\n\t"                                      \
   "s_sub_i32 %[o], 63, %[c]\n\t"                                        \
   "s_pack_ll_b32_b16 %[o], %[o], %[c]\n\t"                              \
   "s_bfe_u64 %[x], s[42:43], %[o]\n\t"                                  \
@@ -2610,7 +2610,7 @@ __device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, ui
                                             int& nsym, int se, const RTab& tab, uint32_t zpos,
                                             int& eobrun, int& ended) {
   uint32_t i, e, r, t, p, c, o, u;
-  uint64_t x, y;
+  uint64_t x;
   // (all uniform; readfirstlane where the compiler's divergence analysis
   // cannot see it -- no instruction for values already in SGPRs)
   buf = ms_u64(buf);
@@ -2690,12 +2690,38 @@ __device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, ui
       HJ_REF_BODY("6b")
       "s_cbranch_scc1 1b\n\t"
       "s_branch 7b\n"
-      // a stop entry: EOBr (s = 0) ends the block with an EOB run of
-      // 2^r + r more bits (r <= 14: the code is <= 6 bits, so >= 26 bits
-      // are in the buffer); anything else is the general step's
+      // an entry <= 0 from the lane table: stop or ZRL
       "5:\n\t"
       "s_bitcmp1_b32 %[e], 6\n\t"
-      "s_cbranch_scc0 9f\n\t"
+      "s_cbranch_scc1 3f\n\t"
+      // not a stop: a new-coefficient symbol with > 15 correction bits (the
+      // general step's), or ZRL: the 16th zero from k, its correction bits
+      "s_cmp_gt_i32 %[e], -1\n\t"
+      "s_cbranch_scc1 9f\n\t"
+      "s_add_i32 %[t], %[zi], 15\n\t"
+      "v_readlane_b32 %[p], %[zpos], %[t]\n\t"
+      "s_sub_i32 %[c], %[p], %[k]\n\t"
+      "s_sub_i32 %[c], %[c], 15\n\t"
+      "s_cmp_gt_u32 %[c], 15\n\t"
+      "s_cbranch_scc1 9f\n\t"
+      "s_lshl_b64 s[42:43], s[40:41], %[e]\n\t"
+      "s_sub_i32 %[o], 64, %[c]\n\t"
+      "s_pack_ll_b32_b16 %[o], %[o], %[c]\n\t"
+      "s_bfe_u64 %[x], s[42:43], %[o]\n\t"
+      "s_lshl_b64 %[corr], %[corr], %[c]\n\t"
+      "s_or_b64 %[corr], %[corr], %[x]\n\t"
+      "s_lshl_b64 s[40:41], s[42:43], %[c]\n\t"
+      "s_add_i32 %[k], %[p], 1\n\t"
+      "s_add_i32 %[zi], %[t], 1\n\t"
+      "s_cmp_ge_i32 %[p], %[se]\n\t"
+      "s_cselect_b32 %[u], 0, s40\n\t"
+      "s_cmp_lg_u32 %[u], 0\n\t"
+      "s_cbranch_scc1 1b\n\t"
+      "s_branch 7b\n"
+      // a stop: EOBr (s = 0) ends the block with an EOB run of 2^r + r
+      // more bits (r <= 14: the code is <= 6 bits, so >= 26 bits are in the
+      // buffer); anything else is the general step's
+      "3:\n\t"
       "s_bfe_u32 %[u], %[e], 0x4000c\n\t"
       "s_cmp_lg_u32 %[u], 0\n\t"
       "s_cbranch_scc1 9f\n\t"
@@ -2721,7 +2747,7 @@ __device__ __forceinline__ void ms_ref_fast(uint64_t& buf, int& cnt, int& wi, ui
         [k] "+s"(k), [zi] "+s"(zi), [corr] "+s"(corr), [nm] "+s"(nm), [nsg] "+s"(nsg),
         [nsym] "+s"(nsym), [eob] "+s"(eobrun), [ended] "=&s"(ended), [i] "=&s"(i), [e] "=&s"(e),
         [r] "=&s"(r), [t] "=&s"(t), [p] "=&s"(p), [c] "=&s"(c), [o] "=&s"(o), [u] "=&s"(u),
-        [x] "=&s"(x), [y] "=&s"(y)
+        [x] "=&s"(x)
       : [l1] "v"(tab.l1), [lim] "v"(tab.lim), [voff] "v"(tab.voff), [vals] "v"(tab.vals),
         [zpos] "v"(zpos), [se] "s"(se), [lastw] "s"(lastw), [w] "s"(w)
       : "s42", "s43", "vcc", "scc", "memory");
@@ -3887,7 +3913,9 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
         rc = HJ_MS_SCAN(kScanAcFirst);
       else
 #ifdef HJ_MS_PROF
-        rc = HJ_MS_SCAN(kScanAcRefine);  // (the profile reads prof[])
+        // (the profile reads prof[])
+        rc = wr ? ms_refine_word(S, si, soft, geo, in, d, cl, lv, masks, lane, nsym, prof)
+                : HJ_MS_SCAN(kScanAcRefine);
 #else
       {
         const int2 rn = wr ? ms_decode_refine<MsWBits>(S, si, soft, geo, in, d, cl, sizeu, lv,
