@@ -3830,11 +3830,20 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
     // wait for it (hard or trailing), so the chain that bounds the image --
     // for the libjpeg script the luma AC bands and the two refinement scans
     // trailing them -- takes the waves first
+    // (a scan's cost: its bytes plus a byte per block it visits -- the DC
+    // scans' per-block work is most of theirs: the DC chain, ~1 KB of bits
+    // over every block of the image, then starts before the chroma chains
+    // instead of after the luma AC bands)
     for (int i = S.nscans - 1; i >= 0; i--) {
       int down = 0;
       for (int j = i + 1; j < S.nscans; j++)
         if (((S.deps[j] | S.soft[j]) >> i) & 1ull) down = max(down, S.prio[j]);
-      S.prio[i] = S.scan[i].end - S.scan[i].start + down;
+      const MsScan& x = S.scan[i];
+      const int c0 = x.comp[0];
+      const int blocks = x.ns > 1 || in.ncomp == 1
+                             ? nblocks
+                             : ((in.comp_w[c0] + 7) / 8) * ((in.comp_hpx[c0] + 7) / 8);
+      S.prio[i] = x.end - x.start + blocks + down;
     }
     S.claimed = 0;
     S.done = 0;
