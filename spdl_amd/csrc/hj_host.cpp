@@ -1092,6 +1092,9 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                              << 16) |
                             (ctx->entropy_prio << 24),
                         ent_threads, ctx->entropy_lds_pad, nwork, st));
+  // (the entropy stage ends here: the multiscan launch or the wait for the
+  // side stream counts to the IDCT stage)
+  mark(ctx, slot, 4, st);
   // progressive / non-interleaved images (the kernels above skipped them)
   // (debug_mask 0x10000 / 0x20000 / 0x40000: timing ablations that skip the
   // multiscan / IDCT / output launch; the output is wrong)
@@ -1102,7 +1105,6 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
     HJ_HIP(launch_multiscan(d_bytes, static_cast<uint8_t*>(W.clean.p), desc, infos,
                             static_cast<uint32_t*>(W.ents.p),
                             static_cast<uint2*>(W.bdesc.p), n, st));
-  mark(ctx, slot, 4, st);
   // full resolution u8 through swscale's unscaled converter: IDCT and
   // conversion in one kernel (output_path 1: the generic sws_kernel, 2:
   // separate IDCT + rgb_unscaled_kernel)

@@ -92,6 +92,24 @@ def test_large_progressive_planes(oracle, name):
     np.testing.assert_array_equal(hyp.reshape(-1), ref, strict=True)
 
 
+@pytest.mark.parametrize("subsampling", [0, 2])
+@pytest.mark.parametrize("quality", [20, 50, 75, 90, 95, 100])
+def test_progressive_quality_sweep(oracle, quality, subsampling):
+    """The AC refinement scans' scalar symbol loop (ms_ref_fast) and its side
+    paths -- codes longer than 6 bits, ZRL, EOB runs, more than 15
+    correction bits (the general step) -- over the code tables and history
+    densities the encoder's quality produces, smooth and noise pixels:
+    planes bit-exact vs the oracle."""
+    from spdl_amd.synthetic import synthetic_pixels
+
+    for px in (synthetic_pixels(7, 240, 320), cases._noise(8, 96, 160)):
+        d = cases._enc(px, quality=quality, subsampling=subsampling, progressive=True)
+        assert _lib.get_image_info(d).multiscan == 1
+        hyp = sio.to_numpy(sio.load_image(d, filter_desc=None))
+        ref = np.concatenate([p.reshape(-1) for p in oracle.decode_planes(d)])
+        np.testing.assert_array_equal(hyp.reshape(-1), ref, strict=True)
+
+
 def test_large_progressive_batch_pad224(oracle):
     """Large progressive images mixed with baseline ones through the resize chain."""
     datas = [cases.case(n) for n in ("prog_large_420", "q90_420", "prog_large_restart",
