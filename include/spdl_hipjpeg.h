@@ -273,8 +273,9 @@ int spdl_hj_nv12_to_planar_rgb(const uint8_t* src_dev, int32_t num_frames, int32
 int spdl_hj_copy(void* dst, const void* src, size_t bytes, int32_t kind, int device, void* stream,
                  int32_t pinned, char* err, size_t errlen);
 
-/* Per-kernel timing of the last batch, in microseconds, measured with HIP
- * events on the decode stream (filled only when enabled). */
+/* Per-stage timing of the last batch, in microseconds, measured with HIP
+ * events on the decode stream (filled only when enabled).  The "idct" stage
+ * includes the multi-scan launch (or the wait for its side stream). */
 int spdl_hj_set_profiling(spdl_hj_ctx* ctx, int32_t enable);
 int spdl_hj_last_timings(spdl_hj_ctx* ctx, float* us, int32_t cap, int32_t* n_out);
 /* Names of the timed stages in the order spdl_hj_last_timings reports them. */
