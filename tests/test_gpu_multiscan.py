@@ -110,6 +110,29 @@ def test_progressive_quality_sweep(oracle, quality, subsampling):
         np.testing.assert_array_equal(hyp.reshape(-1), ref, strict=True)
 
 
+@pytest.mark.parametrize("blocks_wide,blocks_high", [(8, 8), (63, 1), (64, 1), (65, 1),
+                                                    (13, 5), (1, 1), (16, 9)])
+@pytest.mark.parametrize("gray", [True, False])
+def test_progressive_chunk_edges(oracle, blocks_wide, blocks_high, gray):
+    """Refinement scans visit a component's blocks in chunks of 64 (one per
+    lane: levels and masks loaded, records applied, progress published per
+    chunk): component block counts below, at and past a chunk, odd shapes
+    and a single block, gray and 4:2:0 (chroma with a quarter of the blocks):
+    planes bit-exact vs the oracle."""
+    rng = np.random.default_rng(blocks_wide * 100 + blocks_high)
+    h, w = 8 * blocks_high - (rng.integers(0, 4) if blocks_high > 1 else 0), 8 * blocks_wide
+    if gray:
+        px = rng.integers(0, 256, size=(h, w), dtype=np.uint8)
+        d = cases._enc(px, quality=92, progressive=True)
+    else:
+        px = rng.integers(0, 256, size=(2 * h, 2 * w, 3), dtype=np.uint8)
+        d = cases._enc(px, quality=92, subsampling=2, progressive=True)
+    assert _lib.get_image_info(d).multiscan == 1
+    hyp = sio.to_numpy(sio.load_image(d, filter_desc=None))
+    ref = np.concatenate([p.reshape(-1) for p in oracle.decode_planes(d)])
+    np.testing.assert_array_equal(hyp.reshape(-1), ref, strict=True)
+
+
 def test_large_progressive_batch_pad224(oracle):
     """Large progressive images mixed with baseline ones through the resize chain."""
     datas = [cases.case(n) for n in ("prog_large_420", "q90_420", "prog_large_restart",
