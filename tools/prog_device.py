@@ -8,6 +8,7 @@ progressive -- prints the time per batch of one synchronous batch and of a
 pipelined stream (4 lanes, 6 batches in flight), and checks the last batch's
 progressive image against the oracle.
 """
+import os
 import sys
 import time
 
@@ -81,15 +82,17 @@ def run(datas, lanes, inflight, nsteps):
     return sync_ms, stream_ms
 
 
+LANES = int(os.environ.get("PD_LANES", "4"))  # (A/B: lanes, batches in flight)
+INFLIGHT = int(os.environ.get("PD_INFLIGHT", "6"))
 base = [synthetic_jpeg(2000 + i % 32) for i in range(N)]
 prog1 = [synthetic_jpeg(2000, progressive=True)] + base[1:]
 allp = [synthetic_jpeg(2000 + i % 32, progressive=True) for i in range(N)]
 res = {}
 for name, datas, n in (("baseline", base, steps), ("one_progressive", prog1, steps),
                        ("all_progressive", allp, max(6, steps // 10))):
-    s1, sp = run(datas, 4, 6, n)
+    s1, sp = run(datas, LANES, INFLIGHT, n)
     res[name] = (s1, sp)
-    print(f"{name:16s} sync batch {s1:7.2f} ms   stream (4 lanes, 6 in flight) {sp:7.3f} ms/batch "
+    print(f"{name:16s} sync batch {s1:7.2f} ms   stream ({LANES} lanes, {INFLIGHT} in flight) {sp:7.3f} ms/batch "
           f"= {N / sp * 1e3:9.0f} img/s", flush=True)
 b = res["baseline"]
 o = res["one_progressive"]
