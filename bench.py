@@ -255,7 +255,24 @@ def _args():
                    help="one synchronous call per step (no overlap of host work)")
     p.add_argument("--with-copies", action="store_true",
                    help="also time the host-bytes path (pinned H2D + D2H of the output)")
+    p.add_argument("--warmup-mode", choices=["sync", "pipelined"], default="pipelined",
+                   help="warmup steps one synchronous batch at a time, or submitted as the timed "
+                        "steps are (the device is busy up to the timed region)")
+    p.add_argument("--timed-events", choices=["dominant", "stages", "off"], default="dominant",
+                   help="HIP events in the timed steps: around the dominant kernel's stage only "
+                        "(found by an untimed profiled pass first), around every stage, or none "
+                        "(A/B); the per-stage breakdown then comes from as many profiled steps "
+                        "after the timed region")
     return p.parse_args()
+
+
+def _param_or_none(dec, name: str):
+    """A decoder parameter, or None when the loaded library predates it (A/B
+    runs of older builds)."""
+    try:
+        return dec.get_param(name)
+    except ValueError:
+        return None
 
 
 def _pack_device(datas: list[bytes], device: torch.device):
@@ -495,9 +512,6 @@ def main():
     # layout and launches overlap the kernels, as in a data loader.  Each
     # batch is waited for (statuses checked) and its per-stage HIP-event
     # timings collected.
-    for _ in range(a.warmup):
-        submit(True)
-    dec.set_profiling(True)
     stages = {}
 
     def collect(ticket: int):
@@ -506,30 +520,65 @@ def main():
         for k, v in dec.last_timings().items():
             stages[k] = stages.get(k, 0.0) + v
 
+    def run_steps(k: int) -> float:
+        """k steps, up to --inflight batches in flight; returns the host time
+        spent inside the asynchronous submissions."""
+        pending = []
+        host = 0.0
+        for _ in range(k):
+            if a.sync_steps:
+                submit(True)
+                for kk, v in dec.last_timings().items():
+                    stages[kk] = stages.get(kk, 0.0) + v
+                continue
+            ts = time.perf_counter()
+            pending.append(submit(False))
+            host += time.perf_counter() - ts
+            if len(pending) > a.inflight - 1:  # wait the oldest (the ring holds 10)
+                collect(pending.pop(0))
+        for t in pending:
+            collect(t)
+        return host
+
+    # warmup: every lane's workspace sized and its kernels loaded; pipelined
+    # (the default), so the device runs at its working clocks up to the
+    # barrier that opens the timed region
+    if a.warmup_mode == "sync" or a.sync_steps:
+        for _ in range(a.warmup):
+            submit(True)
+    else:
+        for _ in range(min(a.warmup, a.lanes)):
+            submit(True)
+        run_steps(max(0, a.warmup - a.lanes))
+    stages.clear()
+    dom_stage = None
+    if a.timed_events == "dominant":
+        # which stage dominates: an untimed pass with every stage timed
+        dec.set_profiling(True)
+        run_steps(max(8, a.inflight))
+        ks = {k: v for k, v in stages.items() if k not in ("h2d", "d2h_status")}
+        dom_stage = max(ks, key=ks.get)
+        stages.clear()
+        dec.set_profiling(True, stages=[dom_stage])
+    else:
+        dec.set_profiling(a.timed_events == "stages")
+
     torch.cuda.synchronize(device)
     barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    pending = []
-    host_submit = 0.0  # host time inside the asynchronous submissions
-    for _ in range(a.steps):
-        if a.sync_steps:
-            submit(True)
-            for k, v in dec.last_timings().items():
-                stages[k] = stages.get(k, 0.0) + v
-            continue
-        ts = time.perf_counter()
-        pending.append(submit(False))
-        host_submit += time.perf_counter() - ts
-        if len(pending) > a.inflight - 1:  # wait the oldest (the ring holds 10)
-            collect(pending.pop(0))
-    for t in pending:
-        collect(t)
+    host_submit = run_steps(a.steps)  # host time inside the asynchronous submissions
     torch.cuda.synchronize(device)
     own = time.perf_counter() - t0
     barrier()
     torch.cuda.synchronize(device)
     elapsed = reduce_max(time.perf_counter() - t0)
+    timed_stages = dict(stages)  # the HIP-event times of the timed steps
+    if a.timed_events != "stages":
+        # the per-stage breakdown: as many profiled steps after the timed region
+        stages.clear()
+        dec.set_profiling(True)
+        run_steps(a.steps)
     dec.set_profiling(False)
 
     # correctness outside the timed region: the last timed batch against
@@ -540,7 +589,12 @@ def main():
 
     stages_ms = {k: v / a.steps / 1000.0 for k, v in stages.items()}
     kernels = {k: v for k, v in stages_ms.items() if k not in ("h2d", "d2h_status")}
-    dominant = max(kernels, key=kernels.get)
+    dominant = dom_stage or max(kernels, key=kernels.get)
+    # the dominant kernel's launch time inside the timed region (its own HIP
+    # events on its lane streams); with --timed-events off, from the
+    # profiled steps after it
+    timed_ms = {k: v / a.steps / 1000.0 for k, v in timed_stages.items()}
+    kernel_ms = timed_ms.get(dominant, kernels[dominant])
     comp_bytes = float(np.mean(sizes))
     # §8(d): compressed in + RGB224 out (u8: 150,528 B; fp16/bf16: 301,056 B)
     per_image_bytes = comp_bytes + nbytes_out / a.batch
@@ -636,10 +690,11 @@ def main():
     # on), so a kernel change shows in the headline fields at once.  The
     # committed rocprofv3 summary of this configuration rides along under
     # `profile`, with whether it was taken on this very library build.
-    kernel_ms = kernels[dominant]
     achieved = launch_bytes / (kernel_ms / 1e3) / 1e9
     prof_match = _profile_build_match()
-    hbm_frac = (traffic["traffic_bytes"] / ((rocprof_ms or kernel_ms) / 1e3) / 1e9 / HBM_PEAK_GBS
+    # (the PMC traffic per launch over this run's launch duration: the same
+    # time base as `achieved` / `frac`)
+    hbm_frac = (traffic["traffic_bytes"] / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS
                 if traffic else None)
     busy = _kernel_busy_ms(a.lanes, dominant) if a.workload == "pad224" else None
     if rank == 0:
@@ -669,7 +724,7 @@ def main():
                 "lanes": dec.get_param("lanes"),
                 "hw_queues": dec.get_param("hw_queues"),
                 "entropy_threads": dec.get_param("entropy_threads"),
-                "entropy_piece_bytes": dec.get_param("entropy_piece_bytes"),
+                "entropy_piece_bytes": _param_or_none(dec, "entropy_piece_bytes"),
                 "compressed_GBps": round(world * float(np.sum(sizes)) * a.steps / elapsed / 1e9, 3),
                 **({"rehearsal": f"{world} ranks sharing ONE GPU (launch-path check, not a "
                                  f"multi-GPU rate)"} if a.rehearse_one_gpu else {}),
@@ -692,8 +747,10 @@ def main():
                 "formula": "achieved = algorithmic_bytes_per_image x launch_images / kernel_ms; "
                            "frac = achieved / peak",
                 "kernel_ms": round(kernel_ms, 4),
-                "time_source": "HIP events around the kernel's launches in the timed steps "
-                               "(this run)",
+                "time_source": ("HIP events around the kernel's launches in the timed steps "
+                                "(this run)" if a.timed_events != "off" else
+                                "HIP events in profiled steps after the timed region (A/B mode)"),
+                "timed_events": a.timed_events,
                 # the committed rocprofv3 kernel-trace average of this
                 # configuration; with several lanes a launch's duration is a
                 # shared wall time (it waits for CUs the other lanes hold), so
@@ -712,10 +769,19 @@ def main():
                                        f"launch intervals in the rocprofv3 kernel trace / steps"
                                        if busy is not None else None),
                 "limiter": _limiter(issue, hbm_frac),
+                # the limiter's HBM share divides the committed PMC traffic by the
+                # same duration as `frac`
+                "limiter_time_base": "kernel_ms",
                 "pipeline_GBps": round(launch_bytes / (elapsed / a.steps) / 1e9, 3),
                 "lanes1": lanes1,
             },
             "stages_ms": {k: round(v, 4) for k, v in stages_ms.items()},
+            "stages_source": ("HIP events of every stage in the timed steps"
+                              if a.timed_events == "stages" else
+                              "HIP events of every stage in as many profiled steps after the "
+                              "timed region (" + ("the timed steps bracket the dominant kernel "
+                                                  "only)" if a.timed_events == "dominant" else
+                                                  "the timed steps record no events)")),
             # host time of one asynchronous batch submission (layout, pinned
             # staging, launches): the device-resident path's host budget
             "host_submit_ms": round(host_submit / a.steps * 1000.0, 4) if not a.sync_steps else None,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SPDL_HJ_ABI_VERSION 5
+#define SPDL_HJ_ABI_VERSION 6
 
 enum spdl_hj_status {
   SPDL_HJ_OK = 0,
@@ -44,6 +44,13 @@ enum spdl_hj_status {
   SPDL_HJ_ERR_INVALID_ARG = 8,
   SPDL_HJ_ERR_HIP = 9,
   SPDL_HJ_ERR_OOM = 10,
+  /* (since ABI 6) a large restart-free file is decoded by several entropy
+   * workgroups that hand run states across; a hand-off wait that polled
+   * "handoff_wait_us" with nothing arriving gives up with this status.  The
+   * library then re-decodes that image in one workgroup before reporting the
+   * batch (spdl_hj_wait / a sync call), so callers see it only if that
+   * re-decode itself fails to run. */
+  SPDL_HJ_ERR_HANDOFF = 11,
 };
 
 /* output pixel formats (reference nvjpeg/detail/utils.cpp:94-110):
@@ -274,7 +281,8 @@ int spdl_hj_copy(void* dst, const void* src, size_t bytes, int32_t kind, int dev
                  int32_t pinned, char* err, size_t errlen);
 
 /* Per-stage timing of the last batch, in microseconds, measured with HIP
- * events on the decode stream (filled only when enabled).  The "idct" stage
+ * events on the decode stream (filled only when enabled; -1 for a stage
+ * outside "profile_stages").  The "idct" stage
  * includes the multi-scan launch (or the wait for its side stream). */
 int spdl_hj_set_profiling(spdl_hj_ctx* ctx, int32_t enable);
 int spdl_hj_last_timings(spdl_hj_ctx* ctx, float* us, int32_t cap, int32_t* n_out);
@@ -306,7 +314,16 @@ const char* spdl_hj_stage_name(int32_t i);
  * 131072, 0 = one workgroup per image; since ABI 5 round 5), "sws_prepass"
  * (-1 = automatic: the horizontal scaling pass of a downscale by >= 4x or
  * with a > 64-tap filter runs once per source row in its own kernel; 0 =
- * never, 1 = always; byte-identical outputs).
+ * never, 1 = always; byte-identical outputs), "handoff_wait_us" (ABI 6: the
+ * bound of a piece hand-off wait, in microseconds of polling with no awaited
+ * record arriving -- time while the waves are switched out does not count;
+ * default 2000000; 0 gives up at once, which only tests use: every image
+ * whose pieces would have waited is re-decoded in one workgroup).
+ * "profile_stages" (ABI 6: bitmask of the stages, by spdl_hj_stage_name
+ * index, whose HIP events are recorded while profiling; default all; stages
+ * outside it report -1).
+ * Read-only (spdl_hj_get_param): "handoff_retries", images re-decoded after a
+ * hand-off gave up, since the context was created.
  * Builds with -DHJ_ABLATIONS=1 also take "debug_mask" (timing ablations that
  * skip kernel phases; outputs wrong); release builds reject it. */
 int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value);

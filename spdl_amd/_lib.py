@@ -15,7 +15,7 @@ from dataclasses import dataclass
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPDL_AMD_LIB") or os.path.join(_HERE, "lib", "libspdl_hipjpeg.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # enums (mirror include/spdl_hipjpeg.h)
 PIX_FMTS = {"rgb": 0, "bgr": 1, "rgb24": 2, "bgr24": 3}
@@ -215,7 +215,8 @@ def lib() -> ctypes.CDLL:
         ]
         L.spdl_hj_copy.argtypes = [vp, vp, sz, i32, ctypes.c_int, vp, i32, cp, sz]
         ver = L.spdl_hj_abi_version()
-        if ver != ABI_VERSION:
+        # (an explicitly chosen older build, ABI >= 5, loads for A/B runs)
+        if ver != ABI_VERSION and not (os.environ.get("SPDL_AMD_LIB") and 5 <= ver < ABI_VERSION):
             raise RuntimeError(f"libspdl_hipjpeg ABI {ver} != expected {ABI_VERSION}")
         _LIB = L
     return _LIB
@@ -341,14 +342,25 @@ class Decoder:
             raise ValueError(f"unknown decoder parameter {name}")
         return int(v.value)
 
-    def set_profiling(self, enable: bool) -> None:
+    def set_profiling(self, enable: bool, stages=None) -> None:
+        """HIP-event timing of every stage, or only of the named ones."""
+        if stages is not None:
+            names = [lib().spdl_hj_stage_name(i).decode() for i in range(16)]
+            self.set_param("profile_stages", sum(1 << names.index(s) for s in stages))
+        elif enable:
+            try:
+                self.set_param("profile_stages", 0xFF)
+            except ValueError:  # an A/B build from before ABI 6 times every stage anyway
+                pass
         lib().spdl_hj_set_profiling(self._h, int(bool(enable)))
 
     def last_timings(self) -> dict:
         buf = (ctypes.c_float * 16)()
         n = ctypes.c_int32()
         lib().spdl_hj_last_timings(self._h, buf, 16, ctypes.byref(n))
-        return {lib().spdl_hj_stage_name(i).decode(): buf[i] for i in range(n.value)}
+        # (stages outside "profile_stages" report -1: left out)
+        return {lib().spdl_hj_stage_name(i).decode(): buf[i] for i in range(n.value)
+                if buf[i] >= 0.0}
 
     def decode_batch(self, datas, out: Output, out_ptr: int, out_bytes: int, stream=None,
                      sync: bool = True, check: bool = True) -> list[int]:

@@ -287,7 +287,9 @@ enum Status {
   kErrTruncated = 5,
   kErrBadRestart = 6,
   kErrBadGeometry = 7,
-  kErrDevice = 9,  // SPDL_HJ_ERR_HIP: a device-side hand-off gave up (bounded wait)
+  kErrDevice = 9,    // SPDL_HJ_ERR_HIP
+  kErrHandoff = 11,  // SPDL_HJ_ERR_HANDOFF: a piece hand-off wait gave up; the host re-decodes
+                     // the image in one workgroup (spdl_hj_wait / collect_status)
 };
 
 }  // namespace hj

@@ -39,7 +39,7 @@ hipError_t launch_destuff(const uint8_t*, const ImageDesc*, ImageInfo*, DsChunk*
                           uint32_t*, const uint32_t*, int, int, int, hipStream_t);
 hipError_t launch_entropy(const uint8_t*, const uint32_t*, const ImageDesc*, ImageInfo*,
                           const HuffTable*, uint32_t*, uint2*, uint32_t*, const uint32_t*, uint64_t*,
-                          int, int, int, int, int, hipStream_t);
+                          int, int, int, int, int, int64_t, hipStream_t);
 hipError_t launch_idct(const uint32_t*, const uint2*, const ImageDesc*, const ImageInfo*, uint8_t*,
                        int, const uint32_t*, int, int, int, hipStream_t);
 hipError_t launch_multiscan(const uint8_t*, uint8_t*, const ImageDesc*, ImageInfo*, uint32_t*, uint2*, int,
@@ -86,6 +86,7 @@ const char* status_str(int s) {
     case SPDL_HJ_ERR_INVALID_ARG: return "invalid argument";
     case SPDL_HJ_ERR_HIP: return "HIP runtime error";
     case SPDL_HJ_ERR_OOM: return "out of device memory";
+    case SPDL_HJ_ERR_HANDOFF: return "entropy piece hand-off gave up";
     default: return "unknown error";
   }
 }
@@ -577,6 +578,9 @@ struct Layout {
   // side stream beside destuff + entropy (only the host-bytes entry points
   // see the headers; elsewhere it runs after entropy on the lane's stream)
   bool ms_side = false;
+  // images decoded by several entropy workgroups (hand-offs): their probes,
+  // for a one-workgroup re-decode should a hand-off give up
+  std::vector<std::pair<int, spdl_hj_image_info>> multi;
 };
 
 int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_image_info* infos,
@@ -664,7 +668,10 @@ int build_layout(const int64_t* offsets, const int64_t* sizes, const spdl_hj_ima
       pieces = (int)std::min<int64_t>(kMaxPieces, (sizes[i] + piece_bytes - 1) / piece_bytes);
     d.pieces = pieces;
     d.chain_off = pieces > 1 ? (int32_t)L.chain_granules : 0;
-    if (pieces > 1) L.chain_granules += (int64_t)pieces * kChainGranules;
+    if (pieces > 1) {
+      L.chain_granules += (int64_t)pieces * kChainGranules;
+      L.multi.emplace_back(i, p);
+    }
     // entropy slot state (u32 units): kMaxSlots uint4 + slack per piece
     d.rec_cap = (int64_t)kMaxSlots * 8 * pieces;
     d.rec_off = L.total_recs;
@@ -769,9 +776,22 @@ struct Slot {
   bool pending = false;           // submitted, not yet waited
   bool staged = false;            // acquired by spdl_hj_staging_acquire, not submitted
   bool profiled = false;          // ev[] were recorded for this batch
+  uint32_t profiled_stages = 0;   // ... for these stages
   hipEvent_t submitted = nullptr; // lanes > 1: the caller's stream reached the submit
   int n = 0;
   hipEvent_t ev[kStages + 1] = {};  // stage boundaries (profiling only)
+  // A batch with multi-piece images: what re-decoding one of them in one
+  // workgroup needs, should a piece hand-off give up (kErrHandoff)
+  struct Retry {
+    const uint8_t* bytes = nullptr;  // the batch's bytes in HBM
+    size_t len = 0;
+    spdl_hj_output out{};
+    uint8_t* out_dev = nullptr;
+    size_t img_bytes = 0;  // output bytes per image
+    std::vector<int> idx;
+    std::vector<int64_t> off, size;
+    std::vector<spdl_hj_image_info> info;
+  } retry;
 };
 
 // Device workspace of one pipeline "lane".  With lanes > 1 successive
@@ -820,6 +840,9 @@ struct spdl_hj_ctx {
   // unscaled converter -- byte-identical outputs (tests compare them)
   int output_path = 0;
   bool profiling = false;
+  // stages whose HIP events are recorded while profiling (bit i: stage i of
+  // kStageNames; a bench brackets only its dominant kernel in the timed steps)
+  uint32_t profile_stages = (1u << kStages) - 1u;
   float timings[kStages] = {};
   int ntimings = 0;
   int sub_bits = 384;
@@ -844,6 +867,10 @@ struct spdl_hj_ctx {
   int parse_threads = 64;  // (r05 A/B: 64 +1 % over 256 at four lanes)
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
   PlanCache plans;          // swscale plans per distinct geometry
+  // piece hand-off wait bound (us of polling with nothing arriving), and the
+  // images re-decoded in one workgroup after a wait gave up
+  int64_t handoff_wait_us = 2000000;
+  int64_t handoff_retries = 0;
 };
 
 namespace {
@@ -902,8 +929,11 @@ bool ensure_lanes(spdl_hj_ctx* c, int n) {
     }                                                                                    \
   } while (0)
 
+// stage boundary i: recorded when profiling and a profiled stage starts or
+// ends there ("profile_stages": stage i spans ev[i] .. ev[i + 1])
 inline void mark(spdl_hj_ctx* c, Slot& s, int i, hipStream_t st) {
-  if (c->profiling) (void)hipEventRecord(s.ev[i], st);
+  if (c->profiling && ((c->profile_stages | (c->profile_stages << 1)) >> i & 1u))
+    (void)hipEventRecord(s.ev[i], st);
 }
 
 // Take the next ring slot: its previous batch (if any) must have finished
@@ -929,25 +959,44 @@ Slot* find_slot(spdl_hj_ctx* ctx, int64_t ticket) {
   return s.ticket == ticket ? &s : nullptr;
 }
 
+int retry_image(spdl_hj_ctx* ctx, const Slot::Retry& r, int k);
+
 // Per-image statuses of a finished slot -> status[], first error -> err;
 // its stage timings -> ctx->timings when it was profiled.
 int collect_status(spdl_hj_ctx* ctx, Slot& s, int32_t* status, char* err, size_t errlen) {
   if (s.profiled) {
     ctx->ntimings = kStages;
     for (int i = 0; i < kStages; i++) {
-      float ms = 0.f;
-      if (hipEventElapsedTime(&ms, s.ev[i], s.ev[i + 1]) != hipSuccess) ms = -1.f;
-      ctx->timings[i] = ms * 1000.f;
+      float ms = -1.f;  // (stages not profiled, or a failed query: -1)
+      if (!(s.profiled_stages >> i & 1u) ||
+          hipEventElapsedTime(&ms, s.ev[i], s.ev[i + 1]) != hipSuccess)
+        ms = -1.f;
+      ctx->timings[i] = ms < 0.f ? -1.f : ms * 1000.f;
     }
     s.profiled = false;
   }
   const int32_t* stv = static_cast<const int32_t*>(s.pin_status.p);
+  s.pending = false;
+  bool handoff = false;
+  for (int i = 0; i < s.n && !handoff; i++) handoff = stv[i] == SPDL_HJ_ERR_HANDOFF;
+  std::vector<int32_t> fixed;
+  if (handoff && !s.retry.idx.empty()) {
+    // re-decode each image whose hand-off gave up in one workgroup (its
+    // output lands where the batch's would have); the statuses are copied
+    // first: the re-decode may take this very ring slot
+    fixed.assign(stv, stv + s.n);
+    Slot::Retry r = std::move(s.retry);
+    s.retry = Slot::Retry{};
+    for (size_t k = 0; k < r.idx.size(); k++)
+      if (fixed[r.idx[k]] == SPDL_HJ_ERR_HANDOFF) fixed[r.idx[k]] = retry_image(ctx, r, (int)k);
+    stv = fixed.data();
+  }
+  const int n = fixed.empty() ? s.n : (int)fixed.size();
   int first_bad = -1;
-  for (int i = 0; i < s.n; i++) {
+  for (int i = 0; i < n; i++) {
     if (status) status[i] = stv[i];
     if (stv[i] != SPDL_HJ_OK && first_bad < 0) first_bad = i;
   }
-  s.pending = false;
   if (first_bad >= 0) {
     set_err(err, errlen, "Failed to decode an image. (image %d: %s)", first_bad,
             status_str(stv[first_bad]));
@@ -1091,7 +1140,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                             ((((ctx->debug_mask >> 12) & 0xF) | (((ctx->debug_mask >> 19) & 1) << 4))
                              << 16) |
                             (ctx->entropy_prio << 24),
-                        ent_threads, ctx->entropy_lds_pad, nwork, st));
+                        ent_threads, ctx->entropy_lds_pad, nwork, ctx->handoff_wait_us * 100, st));
   // (the entropy stage ends here: the multiscan launch or the wait for the
   // side stream counts to the IDCT stage)
   mark(ctx, slot, 4, st);
@@ -1179,8 +1228,27 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   mark(ctx, slot, 8, st);
   HJ_HIP(hipEventRecord(W.done, st));
   HJ_HIP(hipEventRecord(slot.done, st));
+  Slot::Retry& R = slot.retry;
+  R.idx.clear();
+  R.off.clear();
+  R.size.clear();
+  R.info.clear();
+  if (!planes_only) {
+    for (const auto& m : L.multi) {
+      R.idx.push_back(m.first);
+      R.off.push_back(L.desc[m.first].in_off);
+      R.size.push_back(L.desc[m.first].in_size);
+      R.info.push_back(m.second);
+    }
+    R.bytes = d_bytes;
+    R.len = bytes_len;
+    R.out = *out;
+    R.out_dev = static_cast<uint8_t*>(out_dev);
+    R.img_bytes = (size_t)L.out_elems_per_image * esz;
+  }
   slot.pending = true;
   slot.profiled = ctx->profiling;
+  slot.profiled_stages = ctx->profile_stages;
   ctx->last_ticket = slot.ticket;
   if (!sync) return SPDL_HJ_OK;
   HJ_HIP(hipEventSynchronize(slot.done));
@@ -1203,6 +1271,29 @@ int exec_stream(spdl_hj_ctx* ctx, Slot& slot, hipStream_t st, hipStream_t* xs, c
   HJ_HIP(hipStreamWaitEvent(W.stream, slot.submitted, 0));
   *xs = W.stream;
   return SPDL_HJ_OK;
+}
+
+// Image r.idx[k] of a finished batch again, as a one-image batch decoded by
+// one entropy workgroup (no piece hand-off), synchronously, into its place in
+// the batch's output.  Returns its status.
+int retry_image(spdl_hj_ctx* ctx, const Slot::Retry& r, int k) {
+  char err[256];
+  const size_t errlen = sizeof(err);
+  Layout L;
+  int32_t st1 = SPDL_HJ_OK;
+  int rc = build_layout(&r.off[k], &r.size[k], &r.info[k], 1, &r.out, ctx->sub_bits, 0, L, &st1,
+                        err, errlen, &ctx->plans);
+  if (rc) return rc;
+  Slot* s = nullptr;
+  rc = acquire_slot(ctx, &s, err, errlen);
+  if (rc) return rc;
+  hipStream_t xs;
+  rc = exec_stream(ctx, *s, nullptr, &xs, err, errlen);
+  if (rc) return rc;
+  ctx->handoff_retries++;
+  rc = run_pipeline(ctx, *s, r.bytes, r.len, L, 1, &r.out, r.out_dev + (size_t)r.idx[k] * r.img_bytes,
+                    r.img_bytes, xs, 1, &st1, err, errlen, false);
+  return rc ? rc : st1;
 }
 
 // H2D of the slot's staged bytes on the copy stream; `st` waits for it.
@@ -1676,20 +1767,27 @@ int spdl_hj_decode_planes(spdl_hj_ctx* ctx, const uint8_t* data, size_t size, in
   o.idct = idct;
   int64_t off = 0, sz = (int64_t)size, total = round_up(sz + 64, 256);
   Layout L;
-  rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, ctx->piece_bytes, L, nullptr, err, errlen, nullptr);
-  if (rc) return rc;
   Slot* s = nullptr;
-  rc = acquire_slot(ctx, &s, err, errlen);
-  if (rc) return rc;
-  HJ_HIP(s->pin_in.ensure((size_t)total));
-  memcpy(s->pin_in.p, data, size);
-  memset(static_cast<uint8_t*>(s->pin_in.p) + size, 0, (size_t)(total - sz));
   hipStream_t xs;
-  rc = exec_stream(ctx, *s, st, &xs, err, errlen);
-  if (!rc) rc = stage_h2d(ctx, *s, (size_t)total, xs, err, errlen);
-  if (rc) return rc;
-  rc = run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), (size_t)total, L, 1, &o,
-                    nullptr, 0, xs, 1, nullptr, err, errlen, true);
+  // (a piece hand-off that gave up: once more in one entropy workgroup)
+  for (int64_t piece_bytes : {ctx->piece_bytes, (int64_t)0}) {
+    L = Layout{};
+    rc = build_layout(&off, &sz, &info, 1, &o, ctx->sub_bits, piece_bytes, L, nullptr, err, errlen,
+                      nullptr);
+    if (rc) return rc;
+    rc = acquire_slot(ctx, &s, err, errlen);
+    if (rc) return rc;
+    HJ_HIP(s->pin_in.ensure((size_t)total));
+    memcpy(s->pin_in.p, data, size);
+    memset(static_cast<uint8_t*>(s->pin_in.p) + size, 0, (size_t)(total - sz));
+    rc = exec_stream(ctx, *s, st, &xs, err, errlen);
+    if (!rc) rc = stage_h2d(ctx, *s, (size_t)total, xs, err, errlen);
+    if (rc) return rc;
+    rc = run_pipeline(ctx, *s, static_cast<const uint8_t*>(s->bytes.p), (size_t)total, L, 1, &o,
+                      nullptr, 0, xs, 1, nullptr, err, errlen, true);
+    if (rc != SPDL_HJ_ERR_HANDOFF || piece_bytes == 0) break;
+    ctx->handoff_retries++;
+  }
   if (rc) return rc;
   Workspace& W = ctx->ws[s->ticket % ctx->lanes];
   st = xs;
@@ -1942,6 +2040,16 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     ctx->output_path = (int)value;
     return SPDL_HJ_OK;
   }
+  if (!strcmp(name, "profile_stages")) {  // bitmask over spdl_hj_stage_name indices
+    if (value < 0 || value >= (1 << kStages)) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->profile_stages = (uint32_t)value;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "handoff_wait_us")) {  // piece hand-off wait bound (0: give up at once)
+    if (value < 0 || value > 60 * 1000 * 1000) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->handoff_wait_us = value;
+    return SPDL_HJ_OK;
+  }
   if (!strcmp(name, "host_staging")) {  // 1: kernels move descriptors / statuses; 0: DMA copies
     ctx->host_staging = value != 0;
     return SPDL_HJ_OK;
@@ -1980,6 +2088,9 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"host_staging", ctx->host_staging},
       {"copy_threads", ctx->pool ? ctx->pool->workers() : copy_workers() + 1},
       {"device", ctx->device},
+      {"handoff_wait_us", ctx->handoff_wait_us},
+      {"profile_stages", ctx->profile_stages},
+      {"handoff_retries", ctx->handoff_retries},
   };
   for (const auto& t : tab)
     if (!strcmp(name, t.n)) {

@@ -1345,7 +1345,33 @@ __device__ __forceinline__ void gran_put(uint64_t* c, int i, uint32_t tag, uint3
 __device__ __forceinline__ uint64_t gran_get(const uint64_t* c, int i) {
   return __hip_atomic_load((hj_gu64*)(c + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr int64_t kChainWaitTicks = 20000000;  // 200 ms of wall_clock64 (100 MHz)
+// Bounded waits, counted in polling time without progress (wall_clock64
+// ticks, 100 MHz).  The clock runs on while the queue's waves are switched
+// out (CWSR: the GPU shared with another process), so a gap between two polls
+// longer than kPollGapTicks is not waiting time; and any new granule among
+// those awaited restarts the count.  So only a wait that polled `limit`
+// ticks with nothing arriving gives up -- never a slow or preempted
+// predecessor (pieces take tickets in order: every awaited piece is running,
+// and piece 0 waits for nobody).  A wait that gives up fails its image with
+// kErrHandoff, which the host re-decodes in one workgroup (no hand-off).
+constexpr int64_t kPollGapTicks = 100000;  // 1 ms
+struct WaitBound {
+  int64_t last, idle;
+  int sig;
+};
+__device__ __forceinline__ WaitBound wait_begin() { return WaitBound{wall_clock64(), 0, -1}; }
+// sig: a wave-uniform count of the awaited granules present (grows with progress)
+__device__ __forceinline__ bool wait_expired(WaitBound& w, int sig, int64_t limit) {
+  const int64_t now = wall_clock64(), dt = now - w.last;
+  w.last = now;
+  if (sig != w.sig) {
+    w.sig = sig;
+    w.idle = 0;
+    return false;
+  }
+  if (dt < kPollGapTicks) w.idle += dt;
+  return w.idle >= limit;
+}
 
 // A piece that cannot take part (failed image, bad restart count, a hand-off
 // that gave up): every granule it would publish carries kTagFail, so the
@@ -1362,10 +1388,10 @@ __device__ __forceinline__ void chain_fail(uint64_t* rec, int tid) {
 // empty piece passes the state on); a piece whose guess was wrong has to post
 // its own rec2 first.  -> S.left_pos / left_zb / lb_blocks, S.lb_ok.
 template <class SH>
-__device__ void chain_lookback(SH& S, const uint64_t* chain, int p, int lane) {
+__device__ void chain_lookback(SH& S, const uint64_t* chain, int p, int lane, int64_t limit) {
   const uint64_t* rec = chain + (int64_t)(p - 1 - lane) * kChainGranules;
   const bool mine = lane < p;
-  const int64_t t0 = wall_clock64();
+  WaitBound wb = wait_begin();
   for (;;) {
     uint64_t r[8] = {};
     if (mine) {
@@ -1373,10 +1399,12 @@ __device__ void chain_lookback(SH& S, const uint64_t* chain, int p, int lane) {
       for (int i = 0; i < 8; i++) r[i] = gran_get(rec, i);
     }
     bool fail = false, has1 = mine, has2 = mine;
+    int present = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const uint32_t tag = (uint32_t)(r[i] >> 32);
       fail |= tag == kTagFail;
+      present += __popcll(__ballot(tag != 0u));
       if (i < 5) has1 = has1 && tag == kTagRec1;
       else has2 = has2 && tag == kTagRec2;
     }
@@ -1414,7 +1442,7 @@ __device__ void chain_lookback(SH& S, const uint64_t* chain, int p, int lane) {
         }
       }
     }
-    if (wall_clock64() - t0 > kChainWaitTicks) {
+    if (wait_expired(wb, present, limit)) {
       if (lane == 0) S.lb_ok = -2;  // gave up
       return;
     }
@@ -1425,13 +1453,14 @@ __device__ void chain_lookback(SH& S, const uint64_t* chain, int p, int lane) {
 // DC predictors entering piece p: the sum of the DC-difference sums of
 // pieces 0 .. p-1 (one restart-free segment: no resets), wave 0.
 template <class SH>
-__device__ void chain_dc(SH& S, const uint64_t* chain, int p, int lane) {
+__device__ void chain_dc(SH& S, const uint64_t* chain, int p, int lane, int64_t limit) {
   const uint64_t* rec = chain + (int64_t)lane * kChainGranules + kChDc;
   const bool mine = lane < p;
-  const int64_t t0 = wall_clock64();
+  WaitBound wb = wait_begin();
   for (;;) {
     uint64_t r[kMaxComp] = {};
     bool fail = false, have = true;
+    int got = 0;
     if (mine) {
 #pragma unroll
       for (int i = 0; i < kMaxComp; i++) {
@@ -1439,6 +1468,7 @@ __device__ void chain_dc(SH& S, const uint64_t* chain, int p, int lane) {
         const uint32_t tag = (uint32_t)(r[i] >> 32);
         fail |= tag == kTagFail;
         have = have && tag == kTagDc;
+        got += tag != 0u ? 1 : 0;
       }
     }
     if (__any(fail)) {
@@ -1455,7 +1485,9 @@ __device__ void chain_dc(SH& S, const uint64_t* chain, int p, int lane) {
       if (lane == 0) S.lb_ok = 1;
       return;
     }
-    if (wall_clock64() - t0 > kChainWaitTicks) {
+    int present = got;
+    for (int o = 32; o > 0; o >>= 1) present += __shfl_xor(present, o);
+    if (wait_expired(wb, present, limit)) {
       if (lane == 0) S.lb_ok = -2;  // gave up
       return;
     }
@@ -1477,7 +1509,7 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
                               uint2* __restrict__ bdesc, uint32_t* __restrict__ recs,
                               uint64_t* __restrict__ chain, const int piece,
                               const int sub_bits_param,
-                              const int warm_param) {
+                              const int warm_param, const int64_t handoff_ticks) {
   const int tid = threadIdx.x;
   // warm_param: warm-up slots; bits 16-19 = timing ablations (BatchParams
   // debug_mask >> 12: 1 skips the write and DC passes, 2 the sync rounds,
@@ -1824,11 +1856,11 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
       if (pc == 0) break;
       // the previous piece's end state and block count as the sequential
       // decoder sees them
-      if (tid < 64) chain_lookback(S, crec, pc, tid);
+      if (tid < 64) chain_lookback(S, crec, pc, tid, handoff_ticks);
       __syncthreads();
       const int ok = S.lb_ok;
       if (ok < 0) {
-        if (tid == 0 && ok == -2) infos[img].status = kErrDevice;
+        if (tid == 0 && ok == -2) infos[img].status = kErrHandoff;
         chain_fail(myrec, tid);
         return;
       }
@@ -1995,11 +2027,11 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
       __syncthreads();
       if (chained && pc > 0) {
         // the predictors entering this piece: the sums of all earlier pieces
-        if (tid < 64) chain_dc(S, crec, pc, tid);
+        if (tid < 64) chain_dc(S, crec, pc, tid, handoff_ticks);
         __syncthreads();
         const int ok = S.lb_ok;
         if (ok < 0) {
-          if (tid == 0 && ok == -2) infos[img].status = kErrDevice;
+          if (tid == 0 && ok == -2) infos[img].status = kErrHandoff;
           return;  // (this piece's records are all posted)
         }
 #pragma unroll
@@ -2067,7 +2099,7 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
                                                      const uint32_t* __restrict__ work,
                                                      uint64_t* __restrict__ chain,
                                                      const int sub_bits_param, const int warm_slots,
-                                                     const int nwork) {
+                                                     const int nwork, const int64_t handoff_ticks) {
   __shared__ EntShared<NT, NTAB> S;
   __shared__ uint32_t item;
   // warm_slots bits 24+: wave priority (s_setprio) of the entropy waves
@@ -2087,10 +2119,10 @@ __global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__
   const int img = (int)(w & 0xFFFFFFu), piece = (int)(w >> 24);
   if (infos[img].ent_wide)
     entropy_image<NT, NTAB, true>(S, img, clean, segs, desc, infos, luts, ents, bdesc, recs, chain,
-                                  piece, sub_bits_param, warm_slots);
+                                  piece, sub_bits_param, warm_slots, handoff_ticks);
   else
     entropy_image<NT, NTAB, false>(S, img, clean, segs, desc, infos, luts, ents, bdesc, recs,
-                                   chain, piece, sub_bits_param, warm_slots);
+                                   chain, piece, sub_bits_param, warm_slots, handoff_ticks);
 }
 
 // ---------------------------------------------------------------------------
@@ -5227,13 +5259,14 @@ hipError_t launch_destuff(const uint8_t* bytes, const ImageDesc* desc, ImageInfo
 hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const ImageDesc* desc,
                           ImageInfo* infos, const HuffTable* luts, uint32_t* ents, uint2* bdesc,
                           uint32_t* recs, const uint32_t* work, uint64_t* chain, int sub_bits,
-                          int warm_slots, int threads, int lds_pad, int nwork, hipStream_t st) {
+                          int warm_slots, int threads, int lds_pad, int nwork,
+                          int64_t handoff_ticks, hipStream_t st) {
   // one workgroup per work item (image or piece); wide scans take the
   // HBM-table loops inside
 #define HJ_ENT(T, NTAB)                                                                       \
   hipLaunchKernelGGL((entropy_kernel<T, NTAB>), dim3(nwork), dim3(T), lds_pad, st, clean, segs, \
                      desc, infos, luts, ents, bdesc, recs, work, chain, sub_bits, warm_slots,    \
-                     nwork)
+                     nwork, handoff_ticks)
   if (threads == 1024) {
     HJ_ENT(1024, 4);
   } else if (threads == 512) {

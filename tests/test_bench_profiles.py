@@ -64,7 +64,10 @@ def test_committed_line_reproducible(bench):
     traffic = bench._pmc(bench.PMC_TRAFFIC, "entropy", rec["config"]["per_gpu_batch"])
     assert r["traffic"] == traffic["traffic_bytes"]
     issue = bench._pmc(bench.PMC_ISSUE, "entropy", rec["config"]["per_gpu_batch"])
-    hbm = traffic["traffic_bytes"] / (prof_ms / 1e3) / 1e9 / bench.HBM_PEAK_GBS
+    # the limiter's HBM share: over this run's kernel_ms since round 6 (the
+    # time base of `frac`), over the committed rocprof average before
+    base_ms = ms if r.get("limiter_time_base") == "kernel_ms" else prof_ms
+    hbm = traffic["traffic_bytes"] / (base_ms / 1e3) / 1e9 / bench.HBM_PEAK_GBS
     assert r["limiter"] == bench._limiter(issue, hbm)
     # lanes=1 figure from the one-lane trace
     assert r["lanes1"]["kernel_ms_rocprof"] == pytest.approx(bench._rocprof_ms(1, "entropy"))

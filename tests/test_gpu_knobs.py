@@ -1,0 +1,45 @@
+"""Tuning knobs that change launch shapes but must not change a byte
+(ADVICE r05): swscale tile width (`sws_cols`), parse_kernel workgroup size
+(`parse_threads`) and the entropy waves' priority (`entropy_prio`), each
+bit-exact vs the oracle on a few resize cases in one batch.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from spdl_amd._lib import Output
+from tests import cases
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ["q90_420", "odd_227x333", "gray", "restart_rows", "large_1080p", "optimized"]
+SPECS = {
+    "pad224": dict(fit_w=224, fit_h=224, aspect="decrease", pad_w=224, pad_h=224),
+    "crop224": dict(fit_w=224, fit_h=224, aspect="increase", crop_w=224, crop_h=224),
+    "stretch160x120": dict(fit_w=160, fit_h=120),
+}
+
+
+@pytest.mark.parametrize("knob,value", [("sws_cols", 16), ("sws_cols", 64),
+                                        ("parse_threads", 128), ("parse_threads", 256),
+                                        ("entropy_prio", 3)])
+@pytest.mark.parametrize("sk", list(SPECS))
+def test_knob_bit_exact(decoder, oracle, knob, value, sk):
+    kw = SPECS[sk]
+    datas = [cases.case(n) for n in NAMES]
+    refs = [oracle.decode_resize(d, oracle.Resize(**kw), pix_fmt="rgb24") for d in datas]
+    out = Output(pix_fmt="rgb24", resize=True, **kw)
+    h, w = refs[0].shape[:2]
+    prev = decoder.get_param(knob)
+    decoder.set_param(knob, value)
+    try:
+        t = torch.empty((len(datas), h, w, 3), dtype=torch.uint8, device="cuda:0")
+        st = decoder.decode_batch(datas, out, t.data_ptr(), t.numel(),
+                                  stream=torch.cuda.current_stream())
+    finally:
+        decoder.set_param(knob, prev)
+    assert not any(st), st
+    hyp = t.cpu().numpy()
+    for i, r in enumerate(refs):
+        np.testing.assert_array_equal(hyp[i], r, strict=True, err_msg=f"{knob}={value} {NAMES[i]}")

@@ -7,8 +7,11 @@ bench.py with HIP initialised (through torch) at 4 queues -- the regime of a
 drop-in imported after a trainer touched the GPU -- and bench.py itself runs
 the same bench in a grandchild at 16 queues.  Here only the structural facts
 are asserted (4 lanes at 4 queues, both runs' last timed batch bit-exact vs
-the oracle); the two rates ride in the bench record's `hw_queue_regimes`
-(a throughput ratio is a measurement, not a correctness gate).
+the oracle), plus a loose rate bound: the 4-queue run reaches at least 80 %
+of the 16-queue one (HIP's default queue count must not serialise the lanes;
+at normal lane priority it fell to ~80 % of 508 k in round 4, so a real
+regression fails while run-to-run noise of a few percent does not).  The
+two rates ride in the bench record's `hw_queue_regimes`.
 """
 import json
 import os
@@ -21,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-def test_four_queue_rate_matches_sixteen():
+def test_four_queue_lanes_structure_and_rate():
     env = dict(os.environ)
     env["GPU_MAX_HW_QUEUES"] = "4"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--hw-queues", "4", "--steps", "40",
@@ -35,3 +38,4 @@ def test_four_queue_rate_matches_sixteen():
     assert rec["oracle_check"].endswith("bit-exact vs oracle"), rec["oracle_check"]
     assert q["other"]["oracle_check"].endswith("bit-exact vs oracle"), q["other"]
     assert q["this_run"]["value"] > 0 and q["other"]["value"] > 0
+    assert q["this_run"]["value"] >= 0.8 * q["other"]["value"], q
