@@ -241,6 +241,8 @@ def _args():
     p.add_argument("--piece-bytes", type=int, default=-1,
                    help="entropy_piece_bytes (size-adaptive entropy decode; 0: off; -1: library "
                         "default)")
+    p.add_argument("--mixed-skip", default="",
+                   help="A/B: comma-separated mixed-set images left out of --workload mixed")
     p.add_argument("--norm-dtype", choices=["float16", "bfloat16"], default="float16")
     p.add_argument("--inflight", type=int, default=0, choices=range(0, 11),
                    help="batches submitted ahead before waiting the oldest (0: lanes + 2; the ring holds 10)")
@@ -446,10 +448,13 @@ def main():
 
         cache: dict[int, bytes] = {}
         datas = []
+        skip = {int(x) for x in a.mixed_skip.split(",") if x}
+        keep = [j for j in range(64) if j not in skip]
         for i in sl:  # 64 distinct images of the mixed set, cycled
-            if i % 64 not in cache:
-                cache[i % 64] = mixed_jpeg(i % 64)
-            datas.append(cache[i % 64])
+            j = keep[i % len(keep)]
+            if j not in cache:
+                cache[j] = mixed_jpeg(j)
+            datas.append(cache[j])
     elif a.workload == "big1":
         from spdl_amd.synthetic import big_batch
 

@@ -319,6 +319,11 @@ const char* spdl_hj_stage_name(int32_t i);
  * record arriving -- time while the waves are switched out does not count;
  * default 2000000; 0 gives up at once, which only tests use: every image
  * whose pieces would have waited is re-decoded in one workgroup).
+ * "chain_after" (ABI 6: entropy sync rounds after which runs still out of
+ * step with their left neighbour are re-decoded chain by chain by whole
+ * waves; default 2, 0 = never; byte-identical outputs), "min_run_slots"
+ * (ABI 6: the fewest slots an entropy run decodes; default 0 = one run per
+ * thread; byte-identical outputs),
  * "profile_stages" (ABI 6: bitmask of the stages, by spdl_hj_stage_name
  * index, whose HIP events are recorded while profiling; default all; stages
  * outside it report -1).

@@ -861,6 +861,14 @@ struct spdl_hj_ctx {
   // entropy piece size: a file larger than this is decoded by several
   // workgroups (hj_common.h kMaxPieces); 0 = one workgroup per image
   int64_t piece_bytes = 128 * 1024;
+  // entropy runs hold at least this many slots (0: one run per thread)
+  int min_run_slots = 0;
+  // entropy sync rounds after which unresolved chains are re-decoded by
+  // whole waves (chain rounds; 0 = never).  r06: the mixed set's slowest
+  // image (q94, optimised tables, 11 sync rounds) 1.02 -> 0.63 ms alone,
+  // one-lane mixed entropy 0.90 -> 0.71 ms; uniform batches unchanged; 2
+  // beat 1 and 3 on that image (profiles/r06/chain/)
+  int chain_after = 2;
   // s_setprio of the entropy waves (0-3; A/B knob)
   int entropy_prio = 0;
   // parse_kernel workgroup size (its marker walk is one thread's)
@@ -1136,7 +1144,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
                         static_cast<uint32_t*>(W.recs.p), work, chain,
                         ctx->sub_bits,
-                        warm |
+                        warm | (ctx->min_run_slots << 8) | (ctx->chain_after << 26) |
                             ((((ctx->debug_mask >> 12) & 0xF) | (((ctx->debug_mask >> 19) & 1) << 4))
                              << 16) |
                             (ctx->entropy_prio << 24),
@@ -1974,6 +1982,16 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     ctx->piece_bytes = value;
     return SPDL_HJ_OK;
   }
+  if (!strcmp(name, "min_run_slots")) {  // entropy: fewest slots per run (0 = off)
+    if (value < 0 || value > 64) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->min_run_slots = (int)value;
+    return SPDL_HJ_OK;
+  }
+  if (!strcmp(name, "chain_after")) {  // entropy chain rounds after this many sync rounds
+    if (value < 0 || value > 15) return SPDL_HJ_ERR_INVALID_ARG;
+    ctx->chain_after = (int)value;
+    return SPDL_HJ_OK;
+  }
   if (!strcmp(name, "parse_threads")) {
     if (value != 64 && value != 128 && value != 256) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->parse_threads = (int)value;
@@ -2077,6 +2095,8 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"entropy_piece_bytes", ctx->piece_bytes},
       {"sws_prepass", ctx->plans.pre_mode()},
       {"entropy_prio", ctx->entropy_prio},
+      {"min_run_slots", ctx->min_run_slots},
+      {"chain_after", ctx->chain_after},
       {"parse_threads", ctx->parse_threads},
       {"sws_cols", ctx->plans.max_cols()},
       {"hw_queues", ctx->hw_queues},

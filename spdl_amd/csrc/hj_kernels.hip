@@ -843,6 +843,9 @@ struct EntShared {
   };
   int32_t flag;
   int32_t err;
+  // chain rounds: runs to re-decode, and the chains' heads (bit per run)
+  uint64_t cmask[NT / 64], hmask[NT / 64];
+  uint32_t chain_bits;  // bits the chain rounds decoded (diagnostics)
   // the left neighbour of run 0 (a piece's first run: the previous piece's
   // end state once known; zb 0xFFFFFFFF = none) and a piece's hand-off results
   uint32_t left_pos, left_zb;
@@ -1495,6 +1498,178 @@ __device__ void chain_dc(SH& S, const uint64_t* chain, int p, int lane, int64_t 
   }
 }
 
+// Slot geometry of one chunk of restart segments (entropy_image's slot_*
+// lambdas, for code outside it)
+// a wave-uniform value into an SGPR
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+struct SlotGeo {
+  const uint32_t* sg;  // segment start bytes
+  int seg_lo, cmax, nseg_found;
+  uint32_t N, clean_len;
+  __device__ uint32_t seg_start(int s) const { return sg[s] * 8u; }
+  __device__ uint32_t seg_end(int s) const {
+    return (s + 1 < nseg_found ? sg[s + 1] : clean_len) * 8u;
+  }
+  __device__ int seg(int k) const { return seg_lo + k / cmax; }
+  __device__ int j(int k) const { return k % cmax; }
+  __device__ uint32_t start(int k) const { return seg_start(seg(k)) + (uint32_t)j(k) * N; }
+  __device__ uint32_t end(int k) const {
+    const uint32_t a = start(k) + N, e = seg_end(seg(k));
+    return a < e ? a : e;
+  }
+  __device__ bool empty(int k) const { return j(k) > 0 && start(k) >= seg_end(seg(k)); }
+  __device__ bool known(int k) const { return j(k) == 0; }
+};
+
+// One chain of a chain round (entropy_image's chain_round): the wave decodes
+// from the true end state of run h - 1 through the slots of runs h, h + 1,
+// ... until the trajectory meets a recorded slot state, a segment start, or
+// the next head nh's first slot, rewriting the slot records (sst) and run end
+// states it passes -- decode_state's semantics symbol for symbol.  Lane l
+// looks up the symbol at bit l of a 64-bit window (the current block's AC
+// table; lane 0 the DC table at a block start); the wave walks the symbols
+// with v_readlane.  (Out of line: the rare path keeps its registers out of
+// the decode loops' budget.)
+template <int NT, bool kSlow, class SH>
+__device__ __forceinline__ uint32_t chain_sweep(SH& S, uint4* sst, const uint32_t* __restrict__ words,
+                                         TabMap tm, SlotGeo geo, int K, int pc, int nslots,
+                                         int h, int nh, const int lane, const int wave) {
+  // every scalar in SGPRs (a value the compiler cannot prove uniform would
+  // make the whole walk divergent in its eyes)
+  auto rfli = [](int v) { return (int)rfl((uint32_t)v); };
+  auto rflp = [](const uint32_t* p) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    return (const uint32_t*)(uintptr_t)((uint64_t)rfl((uint32_t)a) |
+                                        (uint64_t)rfl((uint32_t)(a >> 32)) << 32);
+  };
+  K = rfli(K);
+  pc = rfli(pc);
+  nslots = rfli(nslots);
+  h = rfli(h);
+  nh = rfli(nh);
+  tm.dmap = rfl(tm.dmap);
+  tm.amap = rfl(tm.amap);
+  tm.bs_end = rfl(tm.bs_end);
+  geo.sg = rflp(geo.sg);
+  geo.seg_lo = rfli(geo.seg_lo);
+  geo.cmax = rfli(geo.cmax);
+  geo.nseg_found = rfli(geo.nseg_found);
+  geo.N = rfl(geo.N);
+  geo.clean_len = rfl(geo.clean_len);
+  words = rflp(words);
+  auto run_first = [&](int u) { return min((pc * NT + u) * K, nslots); };
+  uint32_t* cw = &S.win[0][0] + wave * (kWinWords * 64);  // this wave's chunk of the stream
+  constexpr uint32_t kChunkBits = kWinWords * 64 * 32;
+  const uint32_t nwords = (geo.clean_len + 3u) / 4u;
+  const int kstop = run_first(nh);  // (nh == NT: the end of this workgroup's slots)
+  const int kh = run_first(h);
+  uint32_t pos = __builtin_amdgcn_readfirstlane(h > 0 ? S.run_pos[h - 1] : S.left_pos);
+  const uint32_t zb_in = __builtin_amdgcn_readfirstlane(h > 0 ? S.run_zb[h - 1] : S.left_zb);
+  uint32_t z = zb_in & 0xFFu, bs = zb_in >> 8;
+  uint32_t cbit = 0xFFFFFFFFu;  // first bit of the staged chunk (none yet)
+  uint32_t eL = 0;              // lane l: the entry of the symbol at window bit l
+  uint32_t o = 64;              // pos's bit in the window (>= 64: refill)
+  // lane lookups of the window starting at pos: the AC table of block-in-MCU
+  // bs, but lane 0 takes the DC table when the block's DC symbol is next
+  // (z == 0): a window is refilled at every block start
+  auto fill = [&]() {
+    if (cbit == 0xFFFFFFFFu || pos - cbit + 96u > kChunkBits) {
+      cbit = pos & ~31u;
+      const uint32_t w0 = cbit >> 5;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      // (one word in flight per lane at a time: this rare path must not
+      // raise the kernel's register count)
+#pragma unroll 1
+      for (int i = 0; i < kWinWords; i++) {
+        const uint32_t wi = w0 + (uint32_t)(i * 64 + lane);
+        cw[i * 64 + lane] = wi < nwords + 2u ? __builtin_bswap32(words[wi]) : 0u;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint32_t r = pos - cbit + (uint32_t)lane;
+    const uint64_t pr = ((uint64_t)cw[r >> 5] << 32) | cw[(r >> 5) + 1];
+    const uint32_t hi = (uint32_t)((pr << (r & 31u)) >> 32);
+    const bool dc = lane == 0 && z == 0u;
+    eL = lookup<kSlow>(S, __builtin_amdgcn_ubfe(dc ? tm.dmap : tm.amap, bs, 3), hi, dc, tm.soff);
+    o = 0;
+  };
+  pos = rfl(pos);
+  z = rfl(z);
+  bs = rfl(bs);
+  const uint32_t pos_in = pos;
+  int u = h;  // the run whose slots are being decoded
+  int cseg = -1;
+  uint32_t seg_s = 0, seg_e = 0;
+  // slot k + 1's recorded state, loaded a slot ahead (the merge test)
+  uint4 qn = kh + 1 < kstop ? sst[kh + 1] : make_uint4(0u, 0u, 0u, 0u);
+  for (int k = kh; k < kstop; k++) {
+    const int sk = geo.seg(k), jk = geo.j(k);
+    if (jk == 0) break;  // a segment start: its state is known
+    if (sk != cseg) {
+      cseg = sk;
+      seg_s = rfl(geo.seg_start(sk));
+      seg_e = rfl(geo.seg_end(sk));
+    }
+    const uint32_t st = seg_s + (uint32_t)jk * geo.N;
+    if (st >= seg_e) break;  // an empty slot past the segment's bits
+    const uint32_t zb0 = z | (bs << 8);
+    const uint4 q = qn;
+    if (k + 1 < kstop) qn = sst[k + 1];
+    if (k > kh && rfl(q.x) == pos && rfl(q.y) == zb0) break;  // met the recorded trajectory
+    const uint32_t p0 = pos, end = rfl(min(st + geo.N, seg_e));
+    int nend = 0;
+    while (pos < end) {
+      if (o >= 64u) fill();
+      // symbols until a block ends, the slot ends or the window runs out:
+      // the entry at the window bit o of lane o (one v_readlane), the
+      // position, window bit and coefficient index advanced in scalar code
+      uint32_t be, e, n, zi;
+      asm volatile(
+          "s_nop 4\n\t"  // (o may come from a VALU write: lane-select hazard)
+          "s_mov_b32 %[be], 0\n"
+          "1:\n\t"
+          "v_readlane_b32 %[e], %[v], %[o]\n\t"
+          "s_and_b32 %[n], %[e], 31\n\t"
+          "s_bfe_u32 %[zi], %[e], 0x7000c\n\t"
+          "s_add_u32 %[pos], %[pos], %[n]\n\t"
+          "s_add_u32 %[o], %[o], %[n]\n\t"
+          "s_add_u32 %[z], %[z], %[zi]\n\t"
+          "s_cmp_gt_u32 %[z], 63\n\t"
+          "s_cbranch_scc1 3f\n\t"
+          "s_cmp_ge_u32 %[pos], %[end]\n\t"
+          "s_cbranch_scc1 2f\n\t"
+          "s_cmp_lt_u32 %[o], 64\n\t"
+          "s_cbranch_scc1 1b\n\t"
+          "s_branch 2f\n"
+          "3:\n\t"
+          "s_mov_b32 %[be], 1\n"
+          "2:"
+          : [pos] "+s"(pos), [o] "+s"(o), [z] "+s"(z), [be] "=&s"(be), [e] "=&s"(e),
+            [n] "=&s"(n), [zi] "=&s"(zi)
+          : [v] "v"(eL), [end] "s"(end)
+          : "scc");
+      if (be) {  // a block ended: the next one's tables
+        nend++;
+        bs = next_bs(tm, bs);
+        z = 0u;
+        o = 64u;
+      }
+    }
+    if (lane == 0)
+      sst[k] = make_uint4(p0, zb0,
+                          (uint32_t)(nend + (z != 0u ? 1 : 0) - ((zb0 & 0xFFu) != 0u ? 1 : 0)), z);
+    if (k + 1 == min(run_first(u) + K, nslots)) {  // the end of run u
+      if (lane == 0) {
+        S.run_pos[u] = pos;
+        S.run_zb[u] = z | (bs << 8);
+      }
+      u++;
+    }
+  }
+  return pos - pos_in;  // bits decoded (diagnostics)
+}
+
 // One image's scan, decoded by the whole workgroup.  kSlow: the scan has
 // more distinct tables than LDS slots, or long codes outside the LDS
 // sub-table pool (parse_kernel's ent_wide): lookups may go to HBM copies
@@ -1518,7 +1693,16 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
   // and the block scan read the slot records it writes -- a round-4 mask
   // that skipped it left them unwritten, and the write pass then stored
   // descriptors at garbage block indices)
-  const int warm_slots = warm_param & 0xFFFF;
+  const int warm_slots = warm_param & 0xFF;
+  // bits 8-15: the fewest slots a run holds (0: runs = threads).  A small
+  // image spread over every thread gives each run less than its warm-up's
+  // worth of bits, so round 0 decodes mostly warm-up; with a floor of K slots
+  // per run only ceil(slots / K) runs work (the rest idle at the barriers),
+  // and the workgroup's issue cycles scale with the image's bits.
+  const int min_run_slots = (warm_param >> 8) & 0xFF;
+  // bits 26-29: sync rounds after which still-unresolved chains of runs are
+  // re-decoded wave-cooperatively (chain_round below; 0: never)
+  const int chain_after = (warm_param >> 26) & 0xF;
   const int dbg = (warm_param >> 16) & 0xFF;
   uint32_t* win = &S.win[0][tid];
   const ImageDesc dd = desc[img];
@@ -1602,7 +1786,10 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
       tm.cmap |= (uint32_t)c << (3 * b);
     }
     tm.bs_end = 3u * (uint32_t)bpm;
-    if (tid == 0) S.err = kOk;
+    if (tid == 0) {
+      S.err = kOk;
+      S.chain_bits = 0;
+    }
   }
   if (nseg_found < nseg) {
     if (tid == 0) infos[img].status = kErrBadRestart;
@@ -1657,13 +1844,13 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
   auto seg_first_blk = [&](int s) { return ri > 0 ? s * ri * bpm : 0; };
   auto seg_end_blk = [&](int s) { return ri > 0 ? min((s + 1) * ri, nmcu) * bpm : nblocks; };
   int rounds_total = 0;
-  int64_t tph[4] = {0, 0, 0, 0}, dcfix = 0;
+  int64_t tph[4] = {0, 0, 0, 0}, dcfix = 0, chain_ticks = 0;
   int64_t tstamp = wall_clock64();
 
   for (int seg_lo = seg_a; seg_lo < seg_b; seg_lo += seg_per_chunk) {
     const int nsc = min(seg_per_chunk, seg_b - seg_lo);
     const int nslots = nsc * cmax;
-    const int K = (nslots + nruns - 1) / nruns;
+    const int K = max((nslots + nruns - 1) / nruns, min_run_slots);
     const int r0 = min((pc * NT + tid) * K, nslots), r1 = min(r0 + K, nslots);
     auto slot_seg = [&](int k) { return seg_lo + k / cmax; };
     auto slot_j = [&](int k) { return k % cmax; };
@@ -1740,9 +1927,79 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
       S.left_pos = 0;
       S.left_zb = 0xFFFFFFFFu;
     }
+    // ---- chain rounds.  A run whose recorded start state disagrees with its
+    // left neighbour's end state is re-decoded by the sync rounds; when the
+    // guessed trajectories stay out of phase for many runs (high-quality
+    // scans with optimised tables: the block-in-MCU phase is lost for tens of
+    // kbit), the true state walks one run per round, each round one run's
+    // decode long.  A chain round instead decodes each chain serially from its
+    // head (a run to re-decode whose left neighbour is not), through the
+    // following runs' slots -- rewriting their slot records and end states --
+    // until the trajectory meets a recorded slot state or the next head.  One
+    // wave decodes a chain cooperatively: lane l looks up the symbol at bit
+    // offset l of a 64-bit window (the current block's DC and AC tables), and
+    // the wave walks the symbol chain with v_readlane, so a symbol costs a
+    // readlane and a few scalar operations instead of a lane's full step;
+    // a block end or the window's end refills the lookups.  The semantics are
+    // decode_state's, symbol for symbol; the sync round that follows checks
+    // every run again.
+    auto chain_round = [&]() {
+      const int64_t tc0 = wall_clock64();
+      // (wave-uniform in the compiler's eyes too: the chain decode keeps its
+      // state in SGPRs)
+      const int lane = tid & 63, wave = (int)rfl((uint32_t)(tid >> 6));
+      constexpr int kNW = NT / 64;
+      bool redo = false;
+      if ((tid > 0 || S.left_zb != 0xFFFFFFFFu) && r0 < r1 && !slot_known(r0) &&
+          !slot_empty(r0)) {
+        const uint32_t npos = tid > 0 ? S.run_pos[tid - 1] : S.left_pos;
+        const uint32_t nzb = tid > 0 ? S.run_zb[tid - 1] : S.left_zb;
+        if (nzb != 0xFFFFFFFFu) {
+          const uint4 q = sst[r0];
+          redo = npos != q.x || nzb != q.y;
+        }
+      }
+      const uint64_t rm = __ballot(redo);
+      if (lane == 0) S.cmask[wave] = rm;
+      __syncthreads();
+      if (lane == 0) {
+        const uint64_t carry = wave > 0 ? S.cmask[wave - 1] >> 63 : 0ull;
+        S.hmask[wave] = rm & ~((rm << 1) | carry);
+      }
+      __syncthreads();
+      const SlotGeo geo{sg, seg_lo, cmax, nseg_found, N, (uint32_t)clean_len};
+      int ord = 0;  // heads are dealt to the waves in order
+      for (int w = 0; w < kNW; w++) {
+        uint64_t hm = S.hmask[w];
+        hm = (uint64_t)rfl((uint32_t)hm) | (uint64_t)rfl((uint32_t)(hm >> 32)) << 32;
+        while (hm) {
+          const int h = w * 64 + __builtin_ctzll(hm);
+          hm &= hm - 1ull;
+          if (ord++ % kNW != wave) continue;
+          // the next head: where this chain's decode stops at the latest
+          int nh = NT;
+          {
+            uint64_t rest = hm;
+            for (int w2 = w; w2 < kNW && nh == NT; w2++) {
+              if (w2 > w) {
+                rest = S.hmask[w2];
+                rest = (uint64_t)rfl((uint32_t)rest) | (uint64_t)rfl((uint32_t)(rest >> 32)) << 32;
+              }
+              if (rest) nh = w2 * 64 + __builtin_ctzll(rest);
+            }
+          }
+          const uint32_t cb = chain_sweep<NT, kSlow>(S, sst, words, tm, geo, K, pc, nslots, h, nh,
+                                                     lane, wave);
+          if (lane == 0) atomicAdd(&S.chain_bits, cb);
+        }
+      }
+      __syncthreads();
+      chain_ticks += wall_clock64() - tc0;
+    };
     auto sync_rounds = [&]() -> int {
       int rounds = 0;
       for (; !(dbg & 2);) {
+        if (chain_after > 0 && rounds >= chain_after) chain_round();
         if (tid == 0) S.flag = 0;
         __syncthreads();
         bool redo = false;
@@ -2077,6 +2334,8 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
     for (int i = 0; i < 4; i++) infos[img].tphase[i] = tph[i];
     for (int i = 0; i < 4; i++) infos[img].dbg[i] = 0;
     infos[img].dbg[0] = dcfix;  // DC predictor pass (ticks)
+    infos[img].dbg[1] = chain_ticks;  // chain rounds (ticks, inside the sync phase)
+    infos[img].dbg[2] = S.chain_bits;  // bits the chain rounds decoded
   }
 }
 
@@ -2088,7 +2347,7 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
 // pool) runs the LDS-only decode loops; a wide one (parse_kernel's ent_wide)
 // the loops that may read HBM table copies and the canonical fallback.
 template <int NT, int NTAB>
-__global__ void __launch_bounds__(NT) entropy_kernel(const uint8_t* __restrict__ clean,
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT >= 256 ? 4 : 1))) entropy_kernel(const uint8_t* __restrict__ clean,
                                                      const uint32_t* __restrict__ segs,
                                                      const ImageDesc* __restrict__ desc,
                                                      ImageInfo* __restrict__ infos,

@@ -14,6 +14,8 @@ dec = Decoder(0)
 dec.set_param("entropy_threads", threads)
 if os.environ.get("PH_SUB"):
     dec.set_param("sub_bits", int(os.environ["PH_SUB"]))
+if os.environ.get("PH_CHAIN"):
+    dec.set_param("chain_after", int(os.environ["PH_CHAIN"]))
 if os.environ.get("PH_WARM"):
     dec.set_param("warmup_slots", int(os.environ["PH_WARM"]))
 rows = []
@@ -25,9 +27,10 @@ for i in range(64):
     ph = diag["phase_us"]
     tot = sum(ph) + diag["dbg"][0] / 100.0
     s = mixed_spec(i)
-    rows.append((tot, i, len(d), ph, diag["sync_rounds"], s))
+    rows.append((tot, i, len(d), ph, diag["sync_rounds"], s, diag["dbg"]))
 rows.sort(key=lambda r: r[0])
-for tot, i, n, ph, r, s in rows:
+for tot, i, n, ph, r, s, dg in rows:
     print(f"img {i:2d} bytes {n:7d} {s['width']}x{s['height']} q{s['quality']} sub{s['subsampling']} "
           f"opt{int(s['optimize'])} rst{int(s['restart_rows'])} total {tot:7.1f} us phases "
-          f"{[round(x, 1) for x in ph]} rounds {r}", flush=True)
+          f"{[round(x, 1) for x in ph]} rounds {r} chain {dg[1] / 100.0:.1f} us "
+          f"{dg[2]} bits", flush=True)
