@@ -846,6 +846,7 @@ struct EntShared {
   // chain rounds: runs to re-decode, and the chains' heads (bit per run)
   uint64_t cmask[NT / 64], hmask[NT / 64];
   uint32_t chain_bits;  // bits the chain rounds decoded (diagnostics)
+  uint32_t chain_sweeps;  // chains they decoded (diagnostics)
   // the left neighbour of run 0 (a piece's first run: the previous piece's
   // end state once known; zb 0xFFFFFFFF = none) and a piece's hand-off results
   uint32_t left_pos, left_zb;
@@ -1027,6 +1028,32 @@ __device__ __forceinline__ uint32_t lookup(const SH& S, uint32_t t, uint32_t hi,
     if (((e >> 5) & 3) == kKindSlow) e = slow_symbol(S, (int)t, hi, is_dc);
   }
   return e;
+}
+
+// lookup() without the canonical fallback: an entry of kind Slow comes back
+// as it is (the chain walk's lane lookups decode every bit offset of a
+// window, most of them no symbol start, and leave the rare Slow symbol that
+// the walk actually meets to one uniform lookup())
+template <bool SLOW, class SH>
+__device__ __forceinline__ uint32_t lookup_fast(const SH& S, uint32_t t, uint32_t hi,
+                                                uint64_t soff) {
+  if constexpr (SLOW) {
+    if (t >= (uint32_t)SH::kTabs) {
+      const HuffTable& G = S.gtab[S.gslot[t]];
+      uint32_t e = G.lut[hi >> (32 - kLutBits)];
+      if (((e >> 5) & 3) == kKindSub)
+        e = G.sub[((e >> kEntHiShift) << kSubBits) |
+                  ((hi >> (32 - kLutBits - kSubBits)) & ((1u << kSubBits) - 1))];
+      return e;
+    }
+    uint32_t e = S.lut[t][hi >> (32 - kLutBits)];
+    if (((e >> 5) & 3) == kKindSub)
+      e = S.sub[((e >> kEntHiShift) << kSubBits) |
+                ((hi >> (32 - kLutBits - kSubBits)) & ((1u << kSubBits) - 1))];
+    return e;
+  } else {
+    return lookup<false>(S, t, hi, false, soff);
+  }
 }
 
 // State-only decode of every symbol that starts in [d.pos, end): bit
@@ -1532,7 +1559,7 @@ struct SlotGeo {
 // with v_readlane.  (Out of line: the rare path keeps its registers out of
 // the decode loops' budget.)
 template <int NT, bool kSlow, class SH>
-__device__ __forceinline__ uint32_t chain_sweep(SH& S, uint4* sst, const uint32_t* __restrict__ words,
+__device__ __forceinline__ void chain_sweep(SH& S, uint4* sst, const uint32_t* __restrict__ words,
                                          TabMap tm, SlotGeo geo, int K, int pc, int nslots,
                                          int h, int nh, const int lane, const int wave) {
   // every scalar in SGPRs (a value the compiler cannot prove uniform would
@@ -1568,8 +1595,12 @@ __device__ __forceinline__ uint32_t chain_sweep(SH& S, uint4* sst, const uint32_
   const uint32_t zb_in = __builtin_amdgcn_readfirstlane(h > 0 ? S.run_zb[h - 1] : S.left_zb);
   uint32_t z = zb_in & 0xFFu, bs = zb_in >> 8;
   uint32_t cbit = 0xFFFFFFFFu;  // first bit of the staged chunk (none yet)
-  uint32_t eL = 0;              // lane l: the entry of the symbol at window bit l
-  uint32_t o = 64;              // pos's bit in the window (>= 64: refill)
+  // lane l, for the symbol at window bit l: the window bit of the next
+  // symbol (nx) and the coefficient-index advance (zi); the walk's
+  // dependency chain is one v_readlane of nx per symbol
+  uint32_t nx = 0, zi = 0;
+  uint32_t wb = 0;  // the window's first bit
+  uint32_t o = 64;  // pos's bit in the window (>= 64: refill)
   // lane lookups of the window starting at pos: the AC table of block-in-MCU
   // bs, but lane 0 takes the DC table when the block's DC symbol is next
   // (z == 0): a window is refilled at every block start
@@ -1578,12 +1609,21 @@ __device__ __forceinline__ uint32_t chain_sweep(SH& S, uint4* sst, const uint32_
       cbit = pos & ~31u;
       const uint32_t w0 = cbit >> 5;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      // (one word in flight per lane at a time: this rare path must not
-      // raise the kernel's register count)
+      // (four words in flight per lane: this rare path must not raise the
+      // kernel's register count)
 #pragma unroll 1
-      for (int i = 0; i < kWinWords; i++) {
-        const uint32_t wi = w0 + (uint32_t)(i * 64 + lane);
-        cw[i * 64 + lane] = wi < nwords + 2u ? __builtin_bswap32(words[wi]) : 0u;
+      for (int i = 0; i < kWinWords; i += 4) {
+        uint32_t q[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t wi = w0 + (uint32_t)((i + j) * 64 + lane);
+          q[j] = words[min(wi, nwords + 1u)];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t wi = w0 + (uint32_t)((i + j) * 64 + lane);
+          cw[(i + j) * 64 + lane] = wi < nwords + 2u ? __builtin_bswap32(q[j]) : 0u;
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
@@ -1591,7 +1631,14 @@ __device__ __forceinline__ uint32_t chain_sweep(SH& S, uint4* sst, const uint32_
     const uint64_t pr = ((uint64_t)cw[r >> 5] << 32) | cw[(r >> 5) + 1];
     const uint32_t hi = (uint32_t)((pr << (r & 31u)) >> 32);
     const bool dc = lane == 0 && z == 0u;
-    eL = lookup<kSlow>(S, __builtin_amdgcn_ubfe(dc ? tm.dmap : tm.amap, bs, 3), hi, dc, tm.soff);
+    const uint32_t e =
+        lookup_fast<kSlow>(S, __builtin_amdgcn_ubfe(dc ? tm.dmap : tm.amap, bs, 3), hi, tm.soff);
+    // a Slow entry (a code the LDS tables do not resolve): nx = 128 + l makes
+    // the walk stop there with o >= 128, and the symbol takes lookup()
+    const bool slow = ((e >> 5) & 3u) == kKindSlow;
+    nx = slow ? 128u + (uint32_t)lane : (uint32_t)lane + (e & 31u);
+    zi = slow ? 0u : __builtin_amdgcn_ubfe(e, 12, 7);
+    wb = pos;
     o = 0;
   };
   pos = rfl(pos);
@@ -1622,33 +1669,48 @@ __device__ __forceinline__ uint32_t chain_sweep(SH& S, uint4* sst, const uint32_
     while (pos < end) {
       if (o >= 64u) fill();
       // symbols until a block ends, the slot ends or the window runs out:
-      // the entry at the window bit o of lane o (one v_readlane), the
-      // position, window bit and coefficient index advanced in scalar code
-      uint32_t be, e, n, zi;
+      // o <- nx[o] (one v_readlane on the chain), z += zi[o] beside it
+      const uint32_t lim = rfl(min(end - wb, 64u));
+      uint32_t be, t;
       asm volatile(
           "s_nop 4\n\t"  // (o may come from a VALU write: lane-select hazard)
           "s_mov_b32 %[be], 0\n"
           "1:\n\t"
-          "v_readlane_b32 %[e], %[v], %[o]\n\t"
-          "s_and_b32 %[n], %[e], 31\n\t"
-          "s_bfe_u32 %[zi], %[e], 0x7000c\n\t"
-          "s_add_u32 %[pos], %[pos], %[n]\n\t"
-          "s_add_u32 %[o], %[o], %[n]\n\t"
-          "s_add_u32 %[z], %[z], %[zi]\n\t"
+          "v_readlane_b32 %[t], %[zi], %[o]\n\t"
+          "v_readlane_b32 %[o], %[nx], %[o]\n\t"
+          "s_add_u32 %[z], %[z], %[t]\n\t"
           "s_cmp_gt_u32 %[z], 63\n\t"
           "s_cbranch_scc1 3f\n\t"
-          "s_cmp_ge_u32 %[pos], %[end]\n\t"
-          "s_cbranch_scc1 2f\n\t"
-          "s_cmp_lt_u32 %[o], 64\n\t"
+          "s_cmp_lt_u32 %[o], %[lim]\n\t"
           "s_cbranch_scc1 1b\n\t"
           "s_branch 2f\n"
           "3:\n\t"
           "s_mov_b32 %[be], 1\n"
           "2:"
-          : [pos] "+s"(pos), [o] "+s"(o), [z] "+s"(z), [be] "=&s"(be), [e] "=&s"(e),
-            [n] "=&s"(n), [zi] "=&s"(zi)
-          : [v] "v"(eL), [end] "s"(end)
+          : [o] "+s"(o), [z] "+s"(z), [be] "=&s"(be), [t] "=&s"(t)
+          : [nx] "v"(nx), [zi] "v"(zi), [lim] "s"(lim)
           : "scc");
+      if (o >= 128u) {  // a Slow symbol at window bit o - 128: the full lookup
+        pos = wb + (o - 128u);
+        const uint32_t r = pos - cbit;
+        const uint64_t pr = ((uint64_t)cw[r >> 5] << 32) | cw[(r >> 5) + 1];
+        const uint32_t hi = (uint32_t)((pr << (r & 31u)) >> 32);
+        const bool isdc = z == 0u;
+        const uint32_t e = rfl(lookup<kSlow>(
+            S, __builtin_amdgcn_ubfe(isdc ? tm.dmap : tm.amap, bs, 3), hi, isdc, tm.soff));
+        pos += e & 31u;
+        const uint32_t zn = z + __builtin_amdgcn_ubfe(e, 12, 7);
+        if (zn >= 64u) {
+          nend++;
+          bs = next_bs(tm, bs);
+          z = 0u;
+        } else {
+          z = zn;
+        }
+        o = 64u;  // refill at the next symbol
+        continue;
+      }
+      pos = wb + o;
       if (be) {  // a block ended: the next one's tables
         nend++;
         bs = next_bs(tm, bs);
@@ -1667,7 +1729,10 @@ __device__ __forceinline__ uint32_t chain_sweep(SH& S, uint4* sst, const uint32_
       u++;
     }
   }
-  return pos - pos_in;  // bits decoded (diagnostics)
+  if (lane == 0) {
+    atomicAdd(&S.chain_bits, pos - pos_in);
+    atomicAdd(&S.chain_sweeps, 1u);
+  }
 }
 
 // One image's scan, decoded by the whole workgroup.  kSlow: the scan has
@@ -1789,6 +1854,7 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
     if (tid == 0) {
       S.err = kOk;
       S.chain_bits = 0;
+      S.chain_sweeps = 0;
     }
   }
   if (nseg_found < nseg) {
@@ -1988,9 +2054,7 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
               if (rest) nh = w2 * 64 + __builtin_ctzll(rest);
             }
           }
-          const uint32_t cb = chain_sweep<NT, kSlow>(S, sst, words, tm, geo, K, pc, nslots, h, nh,
-                                                     lane, wave);
-          if (lane == 0) atomicAdd(&S.chain_bits, cb);
+          chain_sweep<NT, kSlow>(S, sst, words, tm, geo, K, pc, nslots, h, nh, lane, wave);
         }
       }
       __syncthreads();
@@ -2334,8 +2398,9 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
     for (int i = 0; i < 4; i++) infos[img].tphase[i] = tph[i];
     for (int i = 0; i < 4; i++) infos[img].dbg[i] = 0;
     infos[img].dbg[0] = dcfix;  // DC predictor pass (ticks)
-    infos[img].dbg[1] = chain_ticks;  // chain rounds (ticks, inside the sync phase)
-    infos[img].dbg[2] = S.chain_bits;  // bits the chain rounds decoded
+    // chain rounds (ticks, inside the sync phase) | chains decoded << 24
+    infos[img].dbg[1] = chain_ticks | ((int64_t)S.chain_sweeps << 24);
+    infos[img].dbg[2] = S.chain_bits;  // bits they decoded (summed over the chains)
   }
 }
 

@@ -32,5 +32,5 @@ rows.sort(key=lambda r: r[0])
 for tot, i, n, ph, r, s, dg in rows:
     print(f"img {i:2d} bytes {n:7d} {s['width']}x{s['height']} q{s['quality']} sub{s['subsampling']} "
           f"opt{int(s['optimize'])} rst{int(s['restart_rows'])} total {tot:7.1f} us phases "
-          f"{[round(x, 1) for x in ph]} rounds {r} chain {dg[1] / 100.0:.1f} us "
-          f"{dg[2]} bits", flush=True)
+          f"{[round(x, 1) for x in ph]} rounds {r} chain {(dg[1] & 0xFFFFFF) / 100.0:.1f} us "
+          f"in {dg[1] >> 24} chains, {dg[2]} bits", flush=True)
