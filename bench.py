@@ -63,7 +63,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # committed rocprofv3 --pmc passes of this same command (tools/pmc_round.sh:
 # tools/pmc_traffic.py, tools/pmc_issue.py): counters cannot be read from
 # inside the timed process.
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05", "final")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r06", "final")
 PMC_TRAFFIC = os.path.join(PROFILE_DIR, "traffic.json")
 PMC_ISSUE = os.path.join(PROFILE_DIR, "issue.json")
 # rocprofv3 --kernel-trace --stats of this command (tools/profile_round.sh)

@@ -1,6 +1,6 @@
 """The bench line's roofline fields follow from the committed profile set.
 
-bench.py prices the dominant kernel from `profiles/r05/final/`: the
+bench.py prices the dominant kernel from `profiles/r06/final/`: the
 rocprofv3 kernel-trace average, the kernel-trace busy time and the PMC
 traffic / issue records. These CPU tests read the same files through
 bench.py's own helpers and recompute the committed bench line's `kernel_ms`,
@@ -14,7 +14,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FINAL = os.path.join(ROOT, "profiles", "r05", "final")
+FINAL = os.path.join(ROOT, "profiles", "r06", "final")
 
 
 @pytest.fixture(scope="module")
