@@ -321,7 +321,8 @@ const char* spdl_hj_stage_name(int32_t i);
  * whose pieces would have waited is re-decoded in one workgroup).
  * "chain_after" (ABI 6: entropy sync rounds after which runs still out of
  * step with their left neighbour are re-decoded chain by chain by whole
- * waves; default 2, 0 = never; byte-identical outputs), "min_run_slots"
+ * waves; default -1 = 1 with 512+ entropy threads, 2 with fewer; 0 =
+ * never; byte-identical outputs), "min_run_slots"
  * (ABI 6: the fewest slots an entropy run decodes; default 0 = one run per
  * thread; byte-identical outputs),
  * "profile_stages" (ABI 6: bitmask of the stages, by spdl_hj_stage_name

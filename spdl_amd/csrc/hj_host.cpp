@@ -864,11 +864,13 @@ struct spdl_hj_ctx {
   // entropy runs hold at least this many slots (0: one run per thread)
   int min_run_slots = 0;
   // entropy sync rounds after which unresolved chains are re-decoded by
-  // whole waves (chain rounds; 0 = never).  r06: the mixed set's slowest
-  // image (q94, optimised tables, 11 sync rounds) 1.02 -> 0.63 ms alone,
-  // one-lane mixed entropy 0.90 -> 0.71 ms; uniform batches unchanged; 2
-  // beat 1 and 3 on that image (profiles/r06/chain/)
-  int chain_after = 2;
+  // whole waves (chain rounds; 0 = never; -1 = by workgroup size: 1 with
+  // 512+ threads, 2 with 256).  r06: the mixed set's slowest image (q94,
+  // optimised tables, 11 sync rounds) 1.02 -> 0.63 ms alone, one-lane mixed
+  // entropy 0.90 -> 0.69 ms; at one lane 1 also takes the uniform batch's
+  // entropy 0.450 -> 0.434 ms (318 k -> 325 k img/s); at four lanes 2 and 1
+  // measure the same (profiles/r06/ab/warm_chain.txt)
+  int chain_after = -1;
   // s_setprio of the entropy waves (0-3; A/B knob)
   int entropy_prio = 0;
   // parse_kernel workgroup size (its marker walk is one thread's)
@@ -1144,7 +1146,9 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
                         static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
                         static_cast<uint32_t*>(W.recs.p), work, chain,
                         ctx->sub_bits,
-                        warm | (ctx->min_run_slots << 8) | (ctx->chain_after << 26) |
+                        warm | (ctx->min_run_slots << 8) |
+                            ((ctx->chain_after >= 0 ? ctx->chain_after : (ent_threads >= 512 ? 1 : 2))
+                             << 26) |
                             ((((ctx->debug_mask >> 12) & 0xF) | (((ctx->debug_mask >> 19) & 1) << 4))
                              << 16) |
                             (ctx->entropy_prio << 24),
@@ -1988,7 +1992,7 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "chain_after")) {  // entropy chain rounds after this many sync rounds
-    if (value < 0 || value > 15) return SPDL_HJ_ERR_INVALID_ARG;
+    if (value < -1 || value > 15) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->chain_after = (int)value;
     return SPDL_HJ_OK;
   }
@@ -2096,7 +2100,7 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"sws_prepass", ctx->plans.pre_mode()},
       {"entropy_prio", ctx->entropy_prio},
       {"min_run_slots", ctx->min_run_slots},
-      {"chain_after", ctx->chain_after},
+      {"chain_after", ctx->chain_after >= 0 ? ctx->chain_after : (ent >= 512 ? 1 : 2)},
       {"parse_threads", ctx->parse_threads},
       {"sws_cols", ctx->plans.max_cols()},
       {"hw_queues", ctx->hw_queues},

@@ -33,7 +33,8 @@ def _ref(oracle, d: bytes):
 
 
 def _decode(decoder, datas, params):
-    prev = {k: decoder.get_param(k) for k in params}
+    # ("chain_after" goes back to -1, automatic: get_param reports the value in effect)
+    prev = {k: (-1 if k == "chain_after" else decoder.get_param(k)) for k in params}
     for k, v in params.items():
         decoder.set_param(k, v)
     try:
@@ -81,7 +82,7 @@ def test_chain_rounds_cases_and_pieces(decoder, oracle, chain_after, piece_kb):
 def test_chain_rounds_planes(decoder, oracle, chain_after):
     """The coefficient path itself (planes) of the mixed set's slowest images."""
     datas = _mixed()
-    prev = decoder.get_param("chain_after")
+    prev = -1  # (automatic)
     decoder.set_param("chain_after", chain_after)
     try:
         for i in (3, 33, 26, 27):
