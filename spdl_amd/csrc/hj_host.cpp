@@ -811,6 +811,8 @@ struct Workspace {
   // image, host-bytes entry points): created on first use
   hipStream_t side = nullptr;
   hipEvent_t ev_parsed = nullptr, ev_ms = nullptr;
+  hipStream_t last_st = nullptr;  // the stream the workspace's last batch ran on
+  bool used = false;
 };
 
 struct spdl_hj_ctx {
@@ -877,6 +879,10 @@ struct spdl_hj_ctx {
   int parse_threads = 64;  // (r05 A/B: 64 +1 % over 256 at four lanes)
   int entropy_lds_pad = 0;  // extra (unused) dynamic LDS per entropy workgroup: CU packing
   PlanCache plans;          // swscale plans per distinct geometry
+  // skip the event waits that stream order already implies: the workspace's
+  // previous batch on the same stream, and a caller stream with nothing
+  // pending (r06 A/B, profiles/r06/ab/lean_waits.txt: +0.5-1 %)
+  int lean_waits = 1;
   // piece hand-off wait bound (us of polling with nothing arriving), and the
   // images re-decoded in one workgroup after a wait gave up
   int64_t handoff_wait_us = 2000000;
@@ -1044,8 +1050,10 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   }
   Workspace& W = ctx->ws[slot.ticket % ctx->lanes];
   // the previous batch may still be using the workspace (async call, maybe on
-  // another stream)
-  HJ_HIP(hipStreamWaitEvent(st, W.done, 0));
+  // another stream; on the same stream, stream order already covers it)
+  if (!(ctx->lean_waits && W.used && W.last_st == st)) HJ_HIP(hipStreamWaitEvent(st, W.done, 0));
+  W.last_st = st;
+  W.used = true;
   HJ_HIP(W.clean.ensure((size_t)max_end + 512));
   HJ_HIP(W.segs.ensure((size_t)L.total_segs * 4 + 64));
   HJ_HIP(W.dschunks.ensure((size_t)L.total_ds * sizeof(DsChunk) + 64));
@@ -1279,8 +1287,11 @@ int exec_stream(spdl_hj_ctx* ctx, Slot& slot, hipStream_t st, hipStream_t* xs, c
     return SPDL_HJ_OK;
   }
   Workspace& W = ctx->ws[slot.ticket % ctx->lanes];
-  HJ_HIP(hipEventRecord(slot.submitted, st));
-  HJ_HIP(hipStreamWaitEvent(W.stream, slot.submitted, 0));
+  // (a caller stream with nothing pending orders nothing: no cross-queue wait)
+  if (!(ctx->lean_waits && hipStreamQuery(st) == hipSuccess)) {
+    HJ_HIP(hipEventRecord(slot.submitted, st));
+    HJ_HIP(hipStreamWaitEvent(W.stream, slot.submitted, 0));
+  }
   *xs = W.stream;
   return SPDL_HJ_OK;
 }
@@ -2062,6 +2073,10 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     ctx->output_path = (int)value;
     return SPDL_HJ_OK;
   }
+  if (!strcmp(name, "lean_waits")) {
+    ctx->lean_waits = value != 0;
+    return SPDL_HJ_OK;
+  }
   if (!strcmp(name, "profile_stages")) {  // bitmask over spdl_hj_stage_name indices
     if (value < 0 || value >= (1 << kStages)) return SPDL_HJ_ERR_INVALID_ARG;
     ctx->profile_stages = (uint32_t)value;
@@ -2114,6 +2129,7 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"device", ctx->device},
       {"handoff_wait_us", ctx->handoff_wait_us},
       {"profile_stages", ctx->profile_stages},
+      {"lean_waits", ctx->lean_waits},
       {"handoff_retries", ctx->handoff_retries},
   };
   for (const auto& t : tab)
