@@ -578,6 +578,10 @@ struct Layout {
   // side stream beside destuff + entropy (only the host-bytes entry points
   // see the headers; elsewhere it runs after entropy on the lane's stream)
   bool ms_side = false;
+  // the entry point knows every image's scan structure (host probes, or the
+  // caller's ABI-5 image_info): a batch without multi-scan images may skip
+  // the multi-scan launch
+  bool ms_known = false;
   // images decoded by several entropy workgroups (hand-offs): their probes,
   // for a one-workgroup re-decode should a hand-off give up
   std::vector<std::pair<int, spdl_hj_image_info>> multi;
@@ -883,6 +887,9 @@ struct spdl_hj_ctx {
   // previous batch on the same stream, and a caller stream with nothing
   // pending (r06 A/B, profiles/r06/ab/lean_waits.txt: +0.5-1 %)
   int lean_waits = 1;
+  // skip the multi-scan launch of a batch known to hold no multi-scan image
+  // (A/B knob; r05: 1 % slower, the empty launch staggered the lanes)
+  int ms_skip_empty = 0;
   // piece hand-off wait bound (us of polling with nothing arriving), and the
   // images re-decoded in one workgroup after a wait gave up
   int64_t handoff_wait_us = 2000000;
@@ -1170,7 +1177,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   if (ms_side) {
     side_join.w = nullptr;
     HJ_HIP(hipStreamWaitEvent(st, W.ev_ms, 0));
-  } else if (!(ctx->debug_mask & 0x10000))
+  } else if (!(ctx->debug_mask & 0x10000) && !(ctx->ms_skip_empty && L.ms_known && !L.ms_side))
     HJ_HIP(launch_multiscan(d_bytes, static_cast<uint8_t*>(W.clean.p), desc, infos,
                             static_cast<uint32_t*>(W.ents.p),
                             static_cast<uint2*>(W.bdesc.p), n, st));
@@ -1500,6 +1507,7 @@ int spdl_hj_decode_batch(spdl_hj_ctx* ctx, const uint8_t* const* data, const siz
                         errlen, &ctx->plans);
   if (rc) return rc;
   L.ms_side = prog;
+  L.ms_known = true;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
   if (rc) return rc;
@@ -1532,6 +1540,7 @@ int spdl_hj_decode_batch_device(spdl_hj_ctx* ctx, const uint8_t* dev_data, size_
   if (rc) return rc;
   // the caller's probe says which files take the multi-scan path (ABI 5)
   for (int i = 0; i < n; i++) L.ms_side = L.ms_side || infos[i].multiscan != 0;
+  L.ms_known = true;
   Slot* s = nullptr;
   rc = acquire_slot(ctx, &s, err, errlen);
   if (rc) return rc;
@@ -1676,6 +1685,7 @@ int spdl_hj_decode_staged(spdl_hj_ctx* ctx, int64_t ticket, size_t len, const in
     return rc;
   }
   L.ms_side = prog;
+  L.ms_known = true;
   memset(static_cast<uint8_t*>(s->pin_in.p) + len, 0, 512);  // tail read slack
   hipStream_t xs;
   rc = exec_stream(ctx, *s, st, &xs, err, errlen);
@@ -2073,6 +2083,10 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     ctx->output_path = (int)value;
     return SPDL_HJ_OK;
   }
+  if (!strcmp(name, "ms_skip_empty")) {
+    ctx->ms_skip_empty = value != 0;
+    return SPDL_HJ_OK;
+  }
   if (!strcmp(name, "lean_waits")) {
     ctx->lean_waits = value != 0;
     return SPDL_HJ_OK;
@@ -2130,6 +2144,7 @@ int spdl_hj_get_param(spdl_hj_ctx* ctx, const char* name, int64_t* value) {
       {"handoff_wait_us", ctx->handoff_wait_us},
       {"profile_stages", ctx->profile_stages},
       {"lean_waits", ctx->lean_waits},
+      {"ms_skip_empty", ctx->ms_skip_empty},
       {"handoff_retries", ctx->handoff_retries},
   };
   for (const auto& t : tab)
