@@ -32,6 +32,9 @@
 
 namespace hj {
 
+// a wave-uniform value into an SGPR
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
 // ---------------------------------------------------------------------------
 // parse_kernel
 // ---------------------------------------------------------------------------
@@ -49,6 +52,9 @@ struct ParseScratch {
   int32_t dqt_off[4], dqt_pq[4];
   int32_t dht_off[8], dht_n[8];
   int32_t qtsel[kMaxComp];
+  // the SOF's component ids and quantiser selectors, the SOS's component
+  // order (LDS: as private arrays indexed at run time they lived in scratch)
+  int32_t comp_id[kMaxComp], comp_tq[kMaxComp], order[kMaxComp];
 };
 
 // Header bytes: the first kHdrBytes of the file are staged in LDS by the
@@ -58,18 +64,29 @@ constexpr int kHdrBytes = 4096;
 
 typedef __attribute__((address_space(3))) const uint8_t lds_u8;  // an LDS byte
 
+// a header byte past the LDS window (rare): out of line, so the compiler
+// cannot speculate the HBM load beside every LDS read of the serial walk
+// (it did: each byte of the marker walk waited for an HBM load it then threw
+// away -- 31 of the parse kernel's 47 us for a bench image, r06)
+__device__ __forceinline__ uint8_t bytes_far(const uint8_t* g, int i) { return g[i]; }
+
 struct Bytes {
   const uint8_t* g;  // file in HBM
   lds_u8* l;         // its first nl bytes in LDS (typed so: a generic pointer
                      // would make every header read a flat load)
   int nl;
-  __device__ uint8_t operator[](int i) const { return i < nl ? l[i] : g[i]; }
+  __device__ uint8_t operator[](int i) const {
+    if (__builtin_expect(i < nl, 1)) return l[i];
+    return bytes_far(g, i);
+  }
 };
 
+// (the Bytes by value: a pointer to the walk's local Bytes put it in scratch
+// memory, and every header byte read first loaded its fields from there)
 struct BPtr {
-  const Bytes* b;
+  Bytes b;
   int o;
-  __device__ uint8_t operator[](int k) const { return (*b)[o + k]; }
+  __device__ uint8_t operator[](int k) const { return b[o + k]; }
   __device__ BPtr operator+(int k) const { return BPtr{b, o + k}; }
   __device__ BPtr& operator+=(int k) {
     o += k;
@@ -83,8 +100,8 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
   ImageInfo& in = s.info;
   if (size < 4 || d[0] != 0xFF || d[1] != 0xD8) return kErrNotJpeg;
   int have_sof = 0, prog = 0;
-  int comp_id[kMaxComp] = {};
-  int comp_tq[kMaxComp] = {};
+  int32_t* comp_id = s.comp_id;  // (zeroed with the scratch)
+  int32_t* comp_tq = s.comp_tq;
   int adobe = -1;
   int pos = 2;
   for (;;) {
@@ -95,9 +112,9 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
     if (m == 0xD8 || m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
     if (m == 0xD9) return kErrBadHeader;
     if (pos + 2 > size) return kErrBadHeader;
-    int len = be16(BPtr{&d, pos});
+    int len = be16(BPtr{d, pos});
     if (len < 2 || pos + len > size) return kErrBadHeader;
-    BPtr p{&d, pos + 2};
+    BPtr p{d, pos + 2};
     int n = len - 2;
     pos += len;
     if (m == 0xDB) {
@@ -174,7 +191,8 @@ __device__ static int parse_headers(const Bytes& d, int size, ParseScratch& s) {
       in.multiscan = prog || ns != in.ncomp;
       in.progressive = prog;
       if (n < 1 + 2 * ns + 3) return kErrBadHeader;
-      int order[kMaxComp] = {};
+      int32_t* order = s.order;
+      for (int i = 0; i < kMaxComp; i++) order[i] = 0;
       for (int i = 0; i < ns; i++) {
         int cs = p[1 + 2 * i], c = -1;
         for (int k = 0; k < in.ncomp; k++)
@@ -261,18 +279,37 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
   __shared__ int st;
   __shared__ __attribute__((aligned(16))) uint8_t hdr[kHdrBytes];
   const int img = blockIdx.x, tid = threadIdx.x;
-  if (host_desc) {
+#if HJ_PARSE_PROF  // phase timers (variant builds): ImageInfo::sdiag[40..46]
+  int64_t pt[8];
+  int npt = 0;
+  pt[npt++] = wall_clock64();
+#define HJ_PT() (pt[npt++] = wall_clock64())
+#else
+#define HJ_PT() ((void)0)
+#endif
+  // the descriptor in LDS (a private copy, indexed at run time, lived in
+  // scratch memory)
+  __shared__ __attribute__((aligned(16))) ImageDesc sdd;
+  {
     static_assert(sizeof(ImageDesc) % 8 == 0, "descriptor copied in 8-byte words");
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(host_desc + img);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>((host_desc ? host_desc : desc) + img);
     uint64_t* dst = reinterpret_cast<uint64_t*>(desc + img);
-    for (int i = tid; i < (int)(sizeof(ImageDesc) / 8); i += blockDim.x) dst[i] = src[i];
+    uint64_t* sdst = reinterpret_cast<uint64_t*>(&sdd);
+    for (int i = tid; i < (int)(sizeof(ImageDesc) / 8); i += blockDim.x) {
+      const uint64_t v = src[i];
+      if (host_desc) dst[i] = v;
+      sdst[i] = v;
+    }
+  }
+  if (host_desc) {
     for (int64_t i = (int64_t)img * blockDim.x + tid; i < ntab16;
          i += (int64_t)gridDim.x * blockDim.x)
       tables[i] = host_tables[i];
     for (int i = img * blockDim.x + tid; i < nwork; i += gridDim.x * blockDim.x)
       work[i] = host_work[i];
   }
-  const ImageDesc dd = (host_desc ? host_desc : desc)[img];
+  __syncthreads();
+  const ImageDesc& dd = sdd;
   // the flat grids' dispatch maps: this image's destuff-chunk and IDCT
   // workgroups (written whatever the status: those kernels look it up)
   for (int i = tid; i < dd.ds_cap; i += blockDim.x) ds_map[dd.ds_wg0 + i] = (uint32_t)img;
@@ -294,6 +331,7 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
   for (int i = tid; i < nh / 16; i += blockDim.x)
     reinterpret_cast<uint4*>(hdr)[i] = reinterpret_cast<const uint4*>(bytes + dd.in_off)[i];
   __syncthreads();
+  HJ_PT();
   if (tid == 0) {
     const Bytes file{bytes + dd.in_off, (lds_u8*)hdr, nh};
     int rc = parse_headers(file, (int)dd.in_size, s);
@@ -313,6 +351,7 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     st = rc;
   }
   __syncthreads();
+  HJ_PT();
   // canonical-code decode arrays (T.81 F.2.2.3 / libjpeg jdhuff.c), one
   // thread per table slot
   if (tid < 8 && st == kOk && s.have[tid]) {
@@ -335,6 +374,7 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     }
   }
   __syncthreads();
+  HJ_PT();
   if (st != kOk) {
     if (tid == 0) infos[img] = s.info;
     return;
@@ -355,6 +395,7 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     }
   }
   __syncthreads();
+  HJ_PT();
   // the image's quantisation tables by component
   for (int i = tid; i < s.info.ncomp * 64; i += blockDim.x)
     s.info.qt[i / 64][i % 64] = s.qt[s.qtsel[i / 64]][i % 64];
@@ -422,6 +463,11 @@ __global__ void __launch_bounds__(256, 8) parse_kernel(const uint8_t* __restrict
     s.info.ent_wide = !(ns <= 4 && (subs << kSubBits) <= kSubPool && !slow);
   }
   __syncthreads();
+  HJ_PT();
+#if HJ_PARSE_PROF
+  if (tid == 0)
+    for (int i = 1; i < npt && i < 8; i++) s.info.sdiag[39 + i] = (int32_t)(pt[i] - pt[0]);
+#endif
   static_assert(sizeof(ImageInfo) % 4 == 0, "ImageInfo copied in words");
   {  // the parse result out, a word per thread
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&s.info);
@@ -1527,9 +1573,6 @@ __device__ void chain_dc(SH& S, const uint64_t* chain, int p, int lane, int64_t 
 
 // Slot geometry of one chunk of restart segments (entropy_image's slot_*
 // lambdas, for code outside it)
-// a wave-uniform value into an SGPR
-__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
 struct SlotGeo {
   const uint32_t* sg;  // segment start bytes
   int seg_lo, cmax, nseg_found;
