@@ -93,16 +93,21 @@ const char* status_str(int s) {
 
 inline int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
+// A grow-only device buffer.  Given a stream, a growth is stream-ordered
+// (hipFreeAsync / hipMallocAsync on it, after the work it already holds):
+// hipFree synchronises the whole device, so a workspace that grew while a
+// trainer's kernels ran on another stream used to wait for all of them (a
+// decode beside a 0.46 s GEMM loop took 0.46 s; tests/test_gpu_pieces.py).
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
-  hipError_t ensure(size_t n) {
+  hipError_t ensure(size_t n, hipStream_t st = nullptr, bool async = false) {
     if (n <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
+    if (p) (void)(async ? hipFreeAsync(p, st) : hipFree(p));
     p = nullptr;
     cap = 0;
     size_t want = n + n / 4 + 4096;
-    hipError_t e = hipMalloc(&p, want);
+    hipError_t e = async ? hipMallocAsync(&p, want, st) : hipMalloc(&p, want);
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -113,14 +118,22 @@ struct DevBuf {
   }
 };
 
+// A grow-only pinned host buffer.  hipHostFree synchronises the whole
+// device, so a buffer outgrown while the context runs is not freed then --
+// that stalled a decode behind a trainer's kernels on another stream
+// (tests/test_gpu_pieces.py: a 0.48 s GEMM loop) -- but kept until release();
+// growth doubles, so the kept ones total less than the live buffer.
 struct PinBuf {
   void* p = nullptr;
   void* dev = nullptr;  // the same pages as the device sees them (kernels read / write them)
   size_t cap = 0;
+  std::vector<void*> old;  // outgrown buffers, freed by release()
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
-    release();
-    size_t want = n + n / 4 + 4096;
+    if (p) old.push_back(p);
+    p = dev = nullptr;
+    const size_t want = std::max(2 * cap, n + n / 4 + 4096);
+    cap = 0;
     hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
     if (e != hipSuccess) {
       p = nullptr;
@@ -128,7 +141,8 @@ struct PinBuf {
     }
     e = hipHostGetDevicePointer(&dev, p, 0);
     if (e != hipSuccess) {
-      release();
+      (void)hipHostFree(p);
+      p = dev = nullptr;
       return e;
     }
     cap = want;
@@ -136,6 +150,8 @@ struct PinBuf {
   }
   void release() {
     if (p) (void)hipHostFree(p);
+    for (void* q : old) (void)hipHostFree(q);
+    old.clear();
     p = nullptr;
     dev = nullptr;
     cap = 0;
@@ -787,6 +803,7 @@ struct Slot {
   // A batch with multi-piece images: what re-decoding one of them in one
   // workgroup needs, should a piece hand-off give up (kErrHandoff)
   struct Retry {
+    int64_t ticket = 0;              // the batch's (its lane's workspace)
     const uint8_t* bytes = nullptr;  // the batch's bytes in HBM
     size_t len = 0;
     spdl_hj_output out{};
@@ -823,7 +840,10 @@ struct spdl_hj_ctx {
   int device = 0;
   Workspace ws[kMaxLanes];
   int lanes = 1;
-  Slot slots[kSlots];
+  // the ring, and a spare slot outside it for the one-workgroup re-decode of
+  // an image whose piece hand-off gave up (it must not take a ring slot a
+  // caller's un-waited ticket may still hold)
+  Slot slots[kSlots + 1];
   int64_t next_ticket = 1;
   int64_t last_ticket = 0;
   int lanes_ready = 0;                // workspaces [0, lanes_ready) have their event / stream
@@ -1005,8 +1025,8 @@ int collect_status(spdl_hj_ctx* ctx, Slot& s, int32_t* status, char* err, size_t
   std::vector<int32_t> fixed;
   if (handoff && !s.retry.idx.empty()) {
     // re-decode each image whose hand-off gave up in one workgroup (its
-    // output lands where the batch's would have); the statuses are copied
-    // first: the re-decode may take this very ring slot
+    // output lands where the batch's would have; the spare slot, statuses
+    // copied first all the same)
     fixed.assign(stv, stv + s.n);
     Slot::Retry r = std::move(s.retry);
     s.retry = Slot::Retry{};
@@ -1061,15 +1081,15 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   if (!(ctx->lean_waits && W.used && W.last_st == st)) HJ_HIP(hipStreamWaitEvent(st, W.done, 0));
   W.last_st = st;
   W.used = true;
-  HJ_HIP(W.clean.ensure((size_t)max_end + 512));
-  HJ_HIP(W.segs.ensure((size_t)L.total_segs * 4 + 64));
-  HJ_HIP(W.dschunks.ensure((size_t)L.total_ds * sizeof(DsChunk) + 64));
+  HJ_HIP(W.clean.ensure((size_t)max_end + 512, st, true));
+  HJ_HIP(W.segs.ensure((size_t)L.total_segs * 4 + 64, st, true));
+  HJ_HIP(W.dschunks.ensure((size_t)L.total_ds * sizeof(DsChunk) + 64, st, true));
   const int nwork = (int)L.work.size();
   const size_t desc_bytes = sizeof(ImageDesc) * n + sizeof(uint32_t) * nwork;  // + work list
-  HJ_HIP(W.desc.ensure(desc_bytes));
-  HJ_HIP(W.chain.ensure((size_t)(kChainHead + L.chain_granules) * 8 + 64));
-  HJ_HIP(W.maps.ensure((size_t)(L.ds_wgs + L.idct_wgs + L.hs_wgs + L.sws_wgs) * 4 + 64));
-  HJ_HIP(W.hbuf.ensure((size_t)L.total_hbuf * 2 + 64));
+  HJ_HIP(W.desc.ensure(desc_bytes, st, true));
+  HJ_HIP(W.chain.ensure((size_t)(kChainHead + L.chain_granules) * 8 + 64, st, true));
+  HJ_HIP(W.maps.ensure((size_t)(L.ds_wgs + L.idct_wgs + L.hs_wgs + L.sws_wgs) * 4 + 64, st, true));
+  HJ_HIP(W.hbuf.ensure((size_t)L.total_hbuf * 2 + 64, st, true));
   auto* ds_map = static_cast<uint32_t*>(W.maps.p);
   auto* idct_map = ds_map + L.ds_wgs;
   auto* hs_map = idct_map + L.idct_wgs;
@@ -1083,13 +1103,13 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   const bool ds_flat = use_flat(L.ds_wgs, L.max_chunks);
   const bool idct_flat = use_flat(L.idct_wgs, (L.max_blocks + kIdctThreads - 1) / kIdctThreads);
   const bool sws_flat = use_flat(L.sws_wgs, (int64_t)L.sws_bands * L.sws_chunks);
-  HJ_HIP(W.info.ensure(sizeof(ImageInfo) * n));
-  HJ_HIP(W.luts.ensure(sizeof(HuffTable) * 8 * n));
-  HJ_HIP(W.ents.ensure((size_t)L.total_blocks * 256 + 256));
-  HJ_HIP(W.bdesc.ensure((size_t)L.total_blocks * 8 + 64));
-  HJ_HIP(W.planes.ensure((size_t)L.total_planes + 256));
-  HJ_HIP(W.recs.ensure((size_t)L.total_recs * 4 + 256));
-  HJ_HIP(W.wts.ensure(L.tables.size() * 4 + 256));
+  HJ_HIP(W.info.ensure(sizeof(ImageInfo) * n, st, true));
+  HJ_HIP(W.luts.ensure(sizeof(HuffTable) * 8 * n, st, true));
+  HJ_HIP(W.ents.ensure((size_t)L.total_blocks * 256 + 256, st, true));
+  HJ_HIP(W.bdesc.ensure((size_t)L.total_blocks * 8 + 64, st, true));
+  HJ_HIP(W.planes.ensure((size_t)L.total_planes + 256, st, true));
+  HJ_HIP(W.recs.ensure((size_t)L.total_recs * 4 + 256, st, true));
+  HJ_HIP(W.wts.ensure(L.tables.size() * 4 + 256, st, true));
   HJ_HIP(slot.pin_desc.ensure(desc_bytes));
   HJ_HIP(slot.pin_status.ensure(sizeof(int32_t) * n));
   slot.n = n;
@@ -1267,6 +1287,7 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
       R.size.push_back(L.desc[m.first].in_size);
       R.info.push_back(m.second);
     }
+    R.ticket = slot.ticket;
     R.bytes = d_bytes;
     R.len = bytes_len;
     R.out = *out;
@@ -1294,8 +1315,12 @@ int exec_stream(spdl_hj_ctx* ctx, Slot& slot, hipStream_t st, hipStream_t* xs, c
     return SPDL_HJ_OK;
   }
   Workspace& W = ctx->ws[slot.ticket % ctx->lanes];
-  // (a caller stream with nothing pending orders nothing: no cross-queue wait)
-  if (!(ctx->lean_waits && hipStreamQuery(st) == hipSuccess)) {
+  // (a caller stream with nothing pending orders nothing: no cross-queue wait.
+  // Not asked of the null / per-thread default streams: a query of the
+  // legacy null stream waits for the device's other blocking streams -- a
+  // test with a GEMM loop on a torch side stream saw every decode wait for it)
+  const bool special = st == nullptr || st == hipStreamPerThread;
+  if (!(ctx->lean_waits && !special && hipStreamQuery(st) == hipSuccess)) {
     HJ_HIP(hipEventRecord(slot.submitted, st));
     HJ_HIP(hipStreamWaitEvent(W.stream, slot.submitted, 0));
   }
@@ -1314,23 +1339,29 @@ int retry_image(spdl_hj_ctx* ctx, const Slot::Retry& r, int k) {
   int rc = build_layout(&r.off[k], &r.size[k], &r.info[k], 1, &r.out, ctx->sub_bits, 0, L, &st1,
                         err, errlen, &ctx->plans);
   if (rc) return rc;
-  Slot* s = nullptr;
-  rc = acquire_slot(ctx, &s, err, errlen);
-  if (rc) return rc;
+  // the spare slot, on the failed batch's lane (its workspace is free: the
+  // batch has finished); the caller's last ticket is left as it was
+  Slot* s = &ctx->slots[kSlots];
+  if (s->ticket && hipEventSynchronize(s->done) != hipSuccess) return SPDL_HJ_ERR_HIP;
+  s->ticket = r.ticket;
+  s->pending = false;
+  const int64_t last = ctx->last_ticket;
   hipStream_t xs;
   rc = exec_stream(ctx, *s, nullptr, &xs, err, errlen);
   if (rc) return rc;
   ctx->handoff_retries++;
   rc = run_pipeline(ctx, *s, r.bytes, r.len, L, 1, &r.out, r.out_dev + (size_t)r.idx[k] * r.img_bytes,
                     r.img_bytes, xs, 1, &st1, err, errlen, false);
+  ctx->last_ticket = last;
   return rc ? rc : st1;
 }
 
 // H2D of the slot's staged bytes on the copy stream; `st` waits for it.
 int stage_h2d(spdl_hj_ctx* ctx, Slot& s, size_t total, hipStream_t st, char* err, size_t errlen) {
-  HJ_HIP(s.bytes.ensure(total + 512));
   // (created on first use: device-resident batches never take its queue)
   if (!ctx->copy) HJ_HIP(hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking));
+  // (the slot's previous batch has finished: acquire_slot waited for it)
+  HJ_HIP(s.bytes.ensure(total + 512, ctx->copy, true));
   mark(ctx, s, 0, ctx->copy);
   HJ_HIP(hipMemcpyAsync(s.bytes.p, s.pin_in.p, total, hipMemcpyHostToDevice, ctx->copy));
   HJ_HIP(hipEventRecord(s.h2d_done, ctx->copy));
@@ -1423,11 +1454,11 @@ spdl_hj_ctx* spdl_hj_create(int device, char* err, size_t errlen) {
   c->device = device;
   if (const char* q = getenv("GPU_MAX_HW_QUEUES")) c->hw_queues = atoi(q) > 0 ? atoi(q) : 4;
   bool ok = ensure_lanes(c, 1);
-  for (int i = 0; ok && i < kSlots; i++)
+  for (int i = 0; ok && i <= kSlots; i++)
     ok = hipEventCreateWithFlags(&c->slots[i].h2d_done, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->slots[i].done, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->slots[i].submitted, hipEventDisableTiming) == hipSuccess;
-  for (int i = 0; ok && i < kSlots; i++)
+  for (int i = 0; ok && i <= kSlots; i++)
     for (int k = 0; ok && k <= kStages; k++) ok = hipEventCreate(&c->slots[i].ev[k]) == hipSuccess;
   if (!ok) {
     set_err(err, errlen, "hipEventCreate / hipStreamCreate failed");
