@@ -197,7 +197,11 @@ int64_t spdl_hj_last_ticket(spdl_hj_ctx* ctx);
 int spdl_hj_wait(spdl_hj_ctx* ctx, int64_t ticket, int32_t* status, int32_t n, char* err,
                  size_t errlen);
 
-/* Make `stream` wait (on the device, no host block) for batch `ticket`. */
+/* Make `stream` wait (on the device, no host block) for batch `ticket`.
+ * The per-image statuses -- and the re-decode of an image whose piece
+ * hand-off gave up (SPDL_HJ_ERR_HANDOFF), which rewrites its output slot --
+ * come only from spdl_hj_wait: work queued on `stream` may see such an
+ * image's output before spdl_hj_wait has re-decoded it. */
 int spdl_hj_stream_wait(spdl_hj_ctx* ctx, int64_t ticket, void* stream, char* err,
                         size_t errlen);
 
@@ -327,7 +331,18 @@ const char* spdl_hj_stage_name(int32_t i);
  * thread; byte-identical outputs),
  * "profile_stages" (ABI 6: bitmask of the stages, by spdl_hj_stage_name
  * index, whose HIP events are recorded while profiling; default all; stages
- * outside it report -1).
+ * outside it report -1), "lean_waits" (ABI 6: 1, the default, skips the
+ * cross-stream event waits stream order already implies -- a workspace's
+ * previous batch on the same stream, a caller stream with nothing pending;
+ * 0 = always wait), "xcd_order" (ABI 6: XCD-aware tile order, bit 0 the
+ * swscale kernel, bit 1 the IDCT kernel; default 1; byte-identical outputs).
+ * A/B knobs, byte-identical outputs: "entropy_prio" (0-3, s_setprio of the
+ * entropy waves; default 0), "parse_threads" (64/128/256; default 64),
+ * "sws_cols" (16-256 output columns per swscale workgroup; default 256),
+ * "entropy_lds_pad" (extra LDS bytes per entropy workgroup; default 0),
+ * "ms_skip_empty" (1: skip the multi-scan launch of a batch known to hold
+ * no multi-scan image; default 0), "host_staging" (1, the default: kernels
+ * move descriptors / statuses through mapped pinned memory; 0: DMA copies).
  * Read-only (spdl_hj_get_param): "handoff_retries", images re-decoded after a
  * hand-off gave up, since the context was created.
  * Builds with -DHJ_ABLATIONS=1 also take "debug_mask" (timing ablations that

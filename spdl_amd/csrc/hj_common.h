@@ -272,6 +272,7 @@ struct BatchParams {
   int32_t out_w, out_h;  // full-res mode: common size
   int32_t sub_bits;      // Huffman subsequence size (bits, multiple of 32)
   int32_t debug_mask;    // diagnostics: skip kernel phases (timing ablations only)
+  int32_t xcd_order;     // XCD-aware tile order ("xcd_order"): bit 0 sws_kernel, bit 1 idct_kernel
   float mean[3], std[3];
   // ff_yuv2rgb_c_init_tables coefficients (hj_sws.h SwsCsc)
   int32_t crv, cbu, cgu, cgv;

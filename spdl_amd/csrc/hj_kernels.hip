@@ -4593,20 +4593,39 @@ __device__ __forceinline__ void idct_block(const uint32_t* b32, int32_t (&px)[64
   }
 }
 
+// XCD-aware workgroup order: workgroups b and b + 8 share an XCD (observed
+// round-robin dispatch, MI355X_MICROARCH.md -- speed only, never
+// correctness), so the grid's linear index b is taken as tile
+// (b % 8) * Q + b / 8: each XCD gets a contiguous range of tiles in dispatch
+// order (a tail of fewer than 8 keeps its place).  (bx, by, bz) in and out.
+__device__ __forceinline__ void xcd_order(uint32_t& bx, uint32_t& by, uint32_t& bz) {
+  const uint32_t n_wg = gridDim.x * gridDim.y * gridDim.z, full = n_wg & ~7u;
+  uint32_t lin = bx + gridDim.x * (by + gridDim.y * bz);
+  if (lin < full) lin = (lin & 7u) * (full >> 3) + (lin >> 3);
+  bx = lin % gridDim.x;
+  by = (lin / gridDim.x) % gridDim.y;
+  bz = lin / (gridDim.x * gridDim.y);
+}
+
 template <int IDCT>
 __global__ void __launch_bounds__(kIdctThreads) idct_kernel(const uint32_t* __restrict__ ents,
                                                             const uint2* __restrict__ bdesc,
                                                             const ImageDesc* __restrict__ desc,
                                                             const ImageInfo* __restrict__ infos,
                                                             uint8_t* __restrict__ planes,
-                                                            const uint32_t* __restrict__ idct_map) {
+                                                            const uint32_t* __restrict__ idct_map,
+                                                            const int xcd) {
   __shared__ __attribute__((aligned(16))) uint32_t sblk[kBlkWords + 1][kIdctThreads];
   __shared__ uint32_t sq[kMaxComp][64];
   // (tile, image) grid, or a flat grid over every image's block tiles
-  // (idct_map: workgroup -> image) when the batch's sizes differ widely
+  // (idct_map: workgroup -> image) when the batch's sizes differ widely;
+  // xcd: XCD-aware order ("xcd_order" bit 1: neighbouring tiles of one plane
+  // row share their edge lines in one L2)
+  uint32_t gx = blockIdx.x, gy = blockIdx.y, gz = blockIdx.z;
+  if (xcd) xcd_order(gx, gy, gz);
   const bool flat = idct_map != nullptr;
-  const int img = flat ? (int)idct_map[blockIdx.x] : (int)blockIdx.y;
-  const int tile = flat ? (int)blockIdx.x - desc[img].idct_wg0 : (int)blockIdx.x;
+  const int img = flat ? (int)idct_map[gx] : (int)gy;
+  const int tile = flat ? (int)gx - desc[img].idct_wg0 : (int)gx;
   const int j = tile * kIdctThreads + threadIdx.x;
   const ImageInfo& in = infos[img];
   if (in.status != kOk || tile * kIdctThreads >= in.nblocks) return;
@@ -5018,12 +5037,15 @@ __global__ void __launch_bounds__(256) sws_kernel(const uint8_t* __restrict__ pl
   // (band, chunk, image) grid, or a flat grid over every image's own tiles
   // (sws_map: workgroup -> image) when the batch's plans differ widely
   const bool flat = sws_map != nullptr;
-  const int img = flat ? (int)sws_map[blockIdx.x] : (int)blockIdx.z, tid = threadIdx.x,
-            nt = blockDim.x;
+  // XCD-aware order ("xcd_order" bit 0): neighbouring bands of one image,
+  // whose source rows overlap, run on one XCD at about the same time
+  uint32_t bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (p.xcd_order & 1) xcd_order(bx, by, bz);
+  const int img = flat ? (int)sws_map[bx] : (int)bz, tid = threadIdx.x, nt = blockDim.x;
   const ImageDesc& dd = desc[img];
-  const int t = flat ? (int)blockIdx.x - dd.sws_wg0 : (int)(blockIdx.x * dd.sws_chunks + blockIdx.y);
-  const int band = flat ? t / dd.sws_chunks : (int)blockIdx.x;
-  const int chunk = flat ? t - band * dd.sws_chunks : (int)blockIdx.y;
+  const int t = flat ? (int)bx - dd.sws_wg0 : (int)(bx * dd.sws_chunks + by);
+  const int band = flat ? t / dd.sws_chunks : (int)bx;
+  const int chunk = flat ? t - band * dd.sws_chunks : (int)by;
   const ImageInfo& in = infos[img];
   // the image's final status, straight into the slot's pinned status array
   if (host_status && t == 0 && tid == 0) host_status[img] = in.status;
@@ -5648,20 +5670,20 @@ hipError_t launch_entropy(const uint8_t* clean, const uint32_t* segs, const Imag
 }
 hipError_t launch_idct(const uint32_t* ents, const uint2* bdesc, const ImageDesc* desc,
                        const ImageInfo* infos, uint8_t* planes, int idct, const uint32_t* idct_map,
-                       int idct_wgs, int max_blocks, int n, hipStream_t st) {
+                       int idct_wgs, int max_blocks, int n, int xcd, hipStream_t st) {
   // flat: every image's tiles, no empty workgroups; idct_map null: (max
   // tiles, image)
   const dim3 grid = idct_map ? dim3(idct_wgs)
                              : dim3((max_blocks + kIdctThreads - 1) / kIdctThreads, n);
   if (idct == 2)  // timing ablation (debug_mask 0x800): no transform, wrong output
     hipLaunchKernelGGL(idct_kernel<2>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
-                       planes, idct_map);
+                       planes, idct_map, xcd);
   else if (idct == 1)
     hipLaunchKernelGGL(idct_kernel<1>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
-                       planes, idct_map);
+                       planes, idct_map, xcd);
   else
     hipLaunchKernelGGL(idct_kernel<0>, grid, dim3(kIdctThreads), 0, st, ents, bdesc, desc, infos,
-                       planes, idct_map);
+                       planes, idct_map, xcd);
   return hipGetLastError();
 }
 hipError_t launch_csc(const uint8_t* planes, const ImageDesc* desc, const ImageInfo* infos,

@@ -1,6 +1,7 @@
 """Tuning knobs that change launch shapes but must not change a byte
 (ADVICE r05): swscale tile width (`sws_cols`), parse_kernel workgroup size
-(`parse_threads`) and the entropy waves' priority (`entropy_prio`), each
+(`parse_threads`), the entropy waves' priority (`entropy_prio`) and the
+XCD-aware tile order of swscale / IDCT (`xcd_order`, round 6), each
 bit-exact vs the oracle on a few resize cases in one batch.
 """
 
@@ -23,7 +24,7 @@ SPECS = {
 
 @pytest.mark.parametrize("knob,value", [("sws_cols", 16), ("sws_cols", 64),
                                         ("parse_threads", 128), ("parse_threads", 256),
-                                        ("entropy_prio", 3)])
+                                        ("entropy_prio", 3), ("xcd_order", 0), ("xcd_order", 2), ("xcd_order", 3)])
 @pytest.mark.parametrize("sk", list(SPECS))
 def test_knob_bit_exact(decoder, oracle, knob, value, sk):
     kw = SPECS[sk]

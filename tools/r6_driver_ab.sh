@@ -4,6 +4,7 @@
 # (env: SPDL_AMD_LIB=path or empty).  One summary line per run.
 mkdir -p gpurun_out/r6ab
 OUT=${OUT:-gpurun_out/r6ab/summary.txt}
+mkdir -p "$(dirname "$OUT")"
 : > "$OUT"
 IFS=';' read -ra VS <<< "$VARIANTS"
 for rep in $(seq 1 ${REPS:-3}); do
