@@ -892,6 +892,9 @@ struct EntShared {
   // chain rounds: runs to re-decode, and the chains' heads (bit per run)
   uint64_t cmask[NT / 64], hmask[NT / 64];
   uint32_t chain_bits;  // bits the chain rounds decoded (diagnostics)
+#if HJ_OWN_CHECK
+  uint32_t own_viol;    // write-pass descriptor stores outside the storing run's scan range
+#endif
   uint32_t chain_sweeps;  // chains they decoded (diagnostics)
   // the left neighbour of run 0 (a piece's first run: the previous piece's
   // end state once known; zb 0xFFFFFFFF = none) and a piece's hand-off results
@@ -1203,6 +1206,9 @@ __device__ __forceinline__ int sym_value(uint32_t e, uint32_t hi, uint32_t nbits
   return ((int32_t)e >> kEntHiShift) + (int)(raw - neg);
 }
 
+#ifndef HJ_DESC_PAIRS
+#define HJ_DESC_PAIRS 0
+#endif
 struct BlockOut {
   uint32_t* ents;
   uint2* bdesc;
@@ -1213,6 +1219,14 @@ struct BlockOut {
   int dcv;          // its DC difference
   bool open;        // a block of this run is being decoded
   uint32_t pk[4];   // the last four entries (a shift register: pk[3] the newest)
+#if HJ_DESC_PAIRS
+  uint2 held;       // the descriptor of block hblk (the low half of a 16-byte pair), not stored yet
+  int hblk;         // -1: none held
+#endif
+#if HJ_OWN_CHECK
+  int lo, hi;       // the run's blocks by the block scan, [lo, hi)
+  uint32_t viol;    // descriptor stores outside them
+#endif
 #if HJ_ABLATIONS
   bool no_list, no_desc;  // store-site ablations (write-traffic accounting)
 #endif
@@ -1243,9 +1257,44 @@ __device__ __forceinline__ void close_block(BlockOut& o, int blk) {
 #if HJ_ABLATIONS
   if (o.no_desc) blk = -1;
 #endif
-  if ((uint32_t)blk < o.nblk)
-    o.bdesc[blk] = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
+  if ((uint32_t)blk < o.nblk) {
+#if HJ_OWN_CHECK
+    o.viol += (blk < o.lo || blk >= o.hi) ? 1u : 0u;
+#endif
+    const uint2 dv = make_uint2(o.bstart, (o.cur - o.bstart) | ((uint32_t)o.dcv << 16));
+#if HJ_DESC_PAIRS
+    // descriptors leave in 16-byte pairs (the even and odd block of the
+    // 16-byte aligned grid) when a run closes both: half the partial-line
+    // writes.  (Only a held block pairs: an image's first block at an odd
+    // position never does.)
+    uint2* p = o.bdesc + blk;
+    const bool hi = ((uintptr_t)p & 8u) != 0;
+    if (hi && o.hblk >= 0 && o.hblk == blk - 1) {
+      *reinterpret_cast<uint4*>(p - 1) = make_uint4(o.held.x, o.held.y, dv.x, dv.y);
+      o.hblk = -1;
+    } else {
+      if (o.hblk >= 0) o.bdesc[o.hblk] = o.held;
+      if (hi) {
+        *p = dv;
+        o.hblk = -1;
+      } else {
+        o.held = dv;
+        o.hblk = blk;
+      }
+    }
+#else
+    o.bdesc[blk] = dv;
+#endif
+  }
   o.open = false;
+}
+
+// a descriptor still held for pairing, out (the run's end)
+__device__ __forceinline__ void flush_desc(BlockOut& o) {
+#if HJ_DESC_PAIRS
+  if (o.hblk >= 0) o.bdesc[o.hblk] = o.held;
+  o.hblk = -1;
+#endif
 }
 
 // the run's last r = cur & 3 entries, pk[4 - r .. 3], to the group at cur & ~3
@@ -1898,6 +1947,9 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
       S.err = kOk;
       S.chain_bits = 0;
       S.chain_sweeps = 0;
+#if HJ_OWN_CHECK
+      S.own_viol = 0;
+#endif
     }
   }
   if (nseg_found < nseg) {
@@ -2296,6 +2348,15 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
       o.bstart = o.cur;
       o.dcv = 0;
       o.open = false;
+#if HJ_DESC_PAIRS
+      o.hblk = -1;
+      o.held = make_uint2(0u, 0u);
+#endif
+#if HJ_OWN_CHECK
+      o.lo = b0;
+      o.hi = b1;
+      o.viol = 0u;
+#endif
 #pragma unroll
       for (uint32_t i = 0; i < 4; i++) o.pk[i] = 0u;
       Dec d;
@@ -2334,6 +2395,10 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
         k = k2 + 1;
       }
       flush_tail(o);
+      flush_desc(o);
+#if HJ_OWN_CHECK
+      if (o.viol) atomicAdd(&S.own_viol, o.viol);
+#endif
       if (rc != kOk) atomicCAS(&S.err, kOk, rc);
     }
     __syncthreads();
@@ -2444,6 +2509,9 @@ __device__ __forceinline__ void entropy_image(EntShared<NT, NTAB>& S, const int 
     // chain rounds (ticks, inside the sync phase) | chains decoded << 24
     infos[img].dbg[1] = chain_ticks | ((int64_t)S.chain_sweeps << 24);
     infos[img].dbg[2] = S.chain_bits;  // bits they decoded (summed over the chains)
+#if HJ_OWN_CHECK
+    infos[img].dbg[3] = S.own_viol;
+#endif
   }
 }
 
