@@ -340,9 +340,8 @@ const char* spdl_hj_stage_name(int32_t i);
  * entropy waves; default 0), "parse_threads" (64/128/256; default 64),
  * "sws_cols" (16-256 output columns per swscale workgroup; default 256),
  * "entropy_lds_pad" (extra LDS bytes per entropy workgroup; default 0),
- * "ms_skip_empty" (a batch known to hold no multi-scan image: 0, the
- * default, launches the multi-scan kernel over every image, 1 not at all,
- * 2 as one workgroup), "host_staging" (1, the default: kernels
+ * "ms_skip_empty" (1: skip the multi-scan launch of a batch known to hold
+ * no multi-scan image; default 0), "host_staging" (1, the default: kernels
  * move descriptors / statuses through mapped pinned memory; 0: DMA copies).
  * Read-only (spdl_hj_get_param): "handoff_retries", images re-decoded after a
  * hand-off gave up, since the context was created.

@@ -1202,10 +1202,10 @@ int run_pipeline(spdl_hj_ctx* ctx, Slot& slot, const uint8_t* d_bytes, size_t by
   if (ms_side) {
     side_join.w = nullptr;
     HJ_HIP(hipStreamWaitEvent(st, W.ev_ms, 0));
-  } else if (!(ctx->debug_mask & 0x10000) && !(ctx->ms_skip_empty == 1 && L.ms_known && !L.ms_side))
+  } else if (!(ctx->debug_mask & 0x10000) && !(ctx->ms_skip_empty && L.ms_known && !L.ms_side))
     HJ_HIP(launch_multiscan(d_bytes, static_cast<uint8_t*>(W.clean.p), desc, infos,
-                            static_cast<uint32_t*>(W.ents.p), static_cast<uint2*>(W.bdesc.p),
-                            ctx->ms_skip_empty == 2 && L.ms_known && !L.ms_side ? 1 : n, st));
+                            static_cast<uint32_t*>(W.ents.p),
+                            static_cast<uint2*>(W.bdesc.p), n, st));
   // full resolution u8 through swscale's unscaled converter: IDCT and
   // conversion in one kernel (output_path 1: the generic sws_kernel, 2:
   // separate IDCT + rgb_unscaled_kernel)
@@ -2120,9 +2120,8 @@ int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value) {
     ctx->output_path = (int)value;
     return SPDL_HJ_OK;
   }
-  if (!strcmp(name, "ms_skip_empty")) {  // 1: no launch, 2: a one-workgroup launch
-    if (value < 0 || value > 2) return SPDL_HJ_ERR_INVALID_ARG;
-    ctx->ms_skip_empty = (int)value;
+  if (!strcmp(name, "ms_skip_empty")) {
+    ctx->ms_skip_empty = value != 0;
     return SPDL_HJ_OK;
   }
   if (!strcmp(name, "xcd_order")) {

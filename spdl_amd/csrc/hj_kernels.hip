@@ -4476,12 +4476,9 @@ __global__ void __launch_bounds__(256) multiscan_kernel(const uint8_t* __restric
   }
 }
 
-// (grid: the images [0, grid) are looked at -- n, or fewer when the host knows
-// the rest hold no multi-scan image)
 hipError_t launch_multiscan(const uint8_t* bytes, uint8_t* clean, const ImageDesc* desc,
-                            ImageInfo* infos, uint32_t* ents, uint2* bdesc, int grid,
-                            hipStream_t st) {
-  hipLaunchKernelGGL(multiscan_kernel, dim3(grid), dim3(256), 0, st, bytes, clean, desc, infos, ents,
+                            ImageInfo* infos, uint32_t* ents, uint2* bdesc, int n, hipStream_t st) {
+  hipLaunchKernelGGL(multiscan_kernel, dim3(n), dim3(256), 0, st, bytes, clean, desc, infos, ents,
                      bdesc);
   return hipGetLastError();
 }

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Multi-scan launch of a batch known to hold no multi-scan image (round 6,
 # "ms_skip_empty": 0 = the full 256-workgroup launch, 1 = no launch, 2 = one
-# workgroup): knob parity, then the driver's command and 200-step runs.
+# workgroup -- the build of commit a33d1dc only): knob parity, then the
+# driver's command and 200-step runs.
 set -o pipefail
 mkdir -p gpurun_out/r6ms
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
