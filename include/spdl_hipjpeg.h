@@ -344,7 +344,10 @@ const char* spdl_hj_stage_name(int32_t i);
  * no multi-scan image; default 0), "host_staging" (1, the default: kernels
  * move descriptors / statuses through mapped pinned memory; 0: DMA copies).
  * Read-only (spdl_hj_get_param): "handoff_retries", images re-decoded after a
- * hand-off gave up, since the context was created.
+ * hand-off gave up, since the context was created; "streams", the HIP
+ * streams a batch holding a progressive image may use (one per lane, a
+ * multi-scan side stream per lane when the hardware queues allow, the copy
+ * stream).
  * Builds with -DHJ_ABLATIONS=1 also take "debug_mask" (timing ablations that
  * skip kernel phases; outputs wrong); release builds reject it. */
 int spdl_hj_set_param(spdl_hj_ctx* ctx, const char* name, int64_t value);

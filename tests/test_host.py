@@ -235,3 +235,27 @@ def test_release_build_rejects_debug_mask():
     src = open(os.path.join(ROOT, "spdl_amd", "csrc", "hj_host.cpp")).read()
     i = src.index('"debug_mask"')
     assert "#if HJ_ABLATIONS" in src[src.rindex("\n#", 0, i) - 40: i]
+
+
+def test_every_knob_is_documented_in_the_header():
+    """Every name spdl_hj_set_param accepts (release builds) and every name
+    spdl_hj_get_param reports is documented in include/spdl_hipjpeg.h's knob
+    text, and the header documents no knob the library does not take."""
+    src = open(os.path.join(ROOT, "spdl_amd", "csrc", "hj_host.cpp")).read()
+    s0 = src.index("int spdl_hj_set_param(")
+    s1 = src.index("int spdl_hj_get_param(")
+    setter = src[s0:s1]
+    # (release builds: the HJ_ABLATIONS-only names are not part of the ABI)
+    setter = re.sub(r"#if HJ_ABLATIONS.*?#endif", "", setter, flags=re.S)
+    set_names = set(re.findall(r'strcmp\(name, "([a-z0-9_]+)"\)', setter))
+    getter = src[s1:src.index("\n}\n", s1)]
+    get_names = set(re.findall(r'\{"([a-z0-9_]+)",', getter))
+    hdr = open(os.path.join(ROOT, "include", "spdl_hipjpeg.h")).read()
+    h0 = hdr.index("/* Tuning knobs:")
+    doc = hdr[h0:hdr.index("int spdl_hj_get_param(", h0)]
+    doc_names = set(re.findall(r'"([a-z][a-z0-9_]*)"', doc))
+    assert set_names, "no knob names found in spdl_hj_set_param"
+    assert not set_names - doc_names, f"undocumented knobs: {sorted(set_names - doc_names)}"
+    assert not get_names - doc_names, f"undocumented values: {sorted(get_names - doc_names)}"
+    extra = doc_names - set_names - get_names - {"debug_mask"}
+    assert not extra, f"documented but not taken: {sorted(extra)}"
